@@ -1,0 +1,292 @@
+"""Host-side problem data for the batched relaxation path.
+
+``LinProblem`` is the flat form of a Minotaur ``Relaxation`` with linear rows
+that the engine loads once per batch (``OsiLPEngine::load``,
+src/interfaces/OsiLPEngine.cpp:390-498, builds the same row-major CSR):
+
+* rows in constraint-index order, terms inside a row in ascending column
+  order (the reference's ``VariableGroup`` is a ``std::map`` ordered by
+  variable id, src/base/Types.h:496 + Types.cpp:30-34, and ids follow
+  creation order = column index, Problem.cpp:1854-1856);
+* column bounds / types (reference ``VariableType`` numerics, Types.h:83-89);
+* a linear objective (dense ``obj``) plus constant, minimisation.
+
+Node boxes (``lb``/``ub`` per node) are the per-node data; everything here is
+shared across the batch.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+BINARY, INTEGER, CONTINUOUS = 0, 1, 4
+
+
+@dataclass
+class LinProblem:
+    name: str
+    n: int
+    m: int
+    rowptr: np.ndarray   # int32 [m+1]
+    colidx: np.ndarray   # int32 [nnz]
+    val: np.ndarray      # f64 [nnz]
+    rlo: np.ndarray      # f64 [m]
+    rhi: np.ndarray      # f64 [m]
+    vlb: np.ndarray      # f64 [n] root box
+    vub: np.ndarray      # f64 [n]
+    vtype: np.ndarray    # int32 [n]
+    obj: np.ndarray      # f64 [n] dense linear objective (minimise)
+    obj_const: float = 0.0
+
+    # ------------------------------------------------------------------
+    @property
+    def nnz(self) -> int:
+        return int(self.rowptr[-1])
+
+    def csc_pattern(self):
+        """Column -> rows pattern (rows ascending) used by ``changeBFlag_``
+        (LinearHandler.cpp:1229-1234 marks every row holding the column)."""
+        counts = np.bincount(self.colidx, minlength=self.n)
+        colptr = np.zeros(self.n + 1, dtype=np.int32)
+        np.cumsum(counts, out=colptr[1:])
+        rowidx = np.empty(self.nnz, dtype=np.int32)
+        fill = colptr[:-1].copy()
+        for i in range(self.m):
+            for k in range(self.rowptr[i], self.rowptr[i + 1]):
+                j = self.colidx[k]
+                rowidx[fill[j]] = i
+                fill[j] += 1
+        return colptr, rowidx
+
+    def obj_sparse(self):
+        idx = np.nonzero(self.obj)[0].astype(np.int32)
+        return idx, self.obj[idx].astype(np.float64)
+
+    def cons_bad(self) -> int:
+        """``checkBounds_`` second loop (LinearHandler.cpp:350-357)."""
+        return int(np.any(self.rlo > self.rhi + 1e-8))
+
+    def dense(self) -> np.ndarray:
+        A = np.zeros((self.m, self.n))
+        for i in range(self.m):
+            s, e = self.rowptr[i], self.rowptr[i + 1]
+            A[i, self.colidx[s:e]] = self.val[s:e]
+        return A
+
+    def validate(self):
+        assert self.rowptr.dtype == np.int32 and self.colidx.dtype == np.int32
+        assert self.rowptr.shape == (self.m + 1,) and self.rowptr[0] == 0
+        for i in range(self.m):
+            c = self.colidx[self.rowptr[i]:self.rowptr[i + 1]]
+            assert np.all(np.diff(c) > 0), f"row {i} not strictly ascending"
+        assert np.all((self.colidx >= 0) & (self.colidx < self.n))
+        for a in (self.val, self.rlo, self.rhi, self.vlb, self.vub, self.obj):
+            assert a.dtype == np.float64
+        return self
+
+    # ------------------------------------------------------------------
+    def save(self, path: str):
+        np.savez_compressed(path, name=self.name, n=self.n, m=self.m,
+                            rowptr=self.rowptr, colidx=self.colidx, val=self.val,
+                            rlo=self.rlo, rhi=self.rhi, vlb=self.vlb, vub=self.vub,
+                            vtype=self.vtype, obj=self.obj,
+                            obj_const=self.obj_const)
+
+    @staticmethod
+    def load(path: str) -> "LinProblem":
+        z = np.load(path, allow_pickle=False)
+        return LinProblem(name=str(z['name']), n=int(z['n']), m=int(z['m']),
+                          rowptr=z['rowptr'].astype(np.int32),
+                          colidx=z['colidx'].astype(np.int32),
+                          val=z['val'].astype(np.float64),
+                          rlo=z['rlo'].astype(np.float64),
+                          rhi=z['rhi'].astype(np.float64),
+                          vlb=z['vlb'].astype(np.float64),
+                          vub=z['vub'].astype(np.float64),
+                          vtype=z['vtype'].astype(np.int32),
+                          obj=z['obj'].astype(np.float64),
+                          obj_const=float(z['obj_const'])).validate()
+
+
+def from_rows(name, n, rows, rlo, rhi, vlb, vub, vtype, obj, obj_const=0.0):
+    """Build a LinProblem from per-row ``[(col, coef), ...]`` lists.  Terms are
+    sorted by column and |coef| <= 1e-9 dropped (``LinearFunction::addTerm``
+    keeps only |a| > tol_ = 1e-9, LinearFunction.cpp:22,89-95)."""
+    rowptr = [0]
+    colidx, val = [], []
+    for r in rows:
+        d = {}
+        for j, a in r:
+            d[int(j)] = d.get(int(j), 0.0) + float(a)
+        for j in sorted(d):
+            if abs(d[j]) > 1e-9:
+                colidx.append(j)
+                val.append(d[j])
+        rowptr.append(len(colidx))
+    return LinProblem(name=name, n=int(n), m=len(rows),
+                      rowptr=np.asarray(rowptr, dtype=np.int32),
+                      colidx=np.asarray(colidx, dtype=np.int32),
+                      val=np.asarray(val, dtype=np.float64),
+                      rlo=np.asarray(rlo, dtype=np.float64),
+                      rhi=np.asarray(rhi, dtype=np.float64),
+                      vlb=np.asarray(vlb, dtype=np.float64),
+                      vub=np.asarray(vub, dtype=np.float64),
+                      vtype=np.asarray(vtype, dtype=np.int32),
+                      obj=np.asarray(obj, dtype=np.float64),
+                      obj_const=float(obj_const)).validate()
+
+
+def from_nl_linear(model, name=None) -> LinProblem:
+    """Linear part of an ``.nl`` model: every row without a nonlinear
+    expression ("tls4-lin" for tls4.nl)."""
+    keep = model.linear_rows()
+    obj = np.zeros(model.n)
+    for j, a in model.obj_grad:
+        obj[j] += a
+    if model.obj_sense == 1:
+        obj = -obj
+    return from_rows(name or (model.name + "-lin"), model.n,
+                     [model.rows[i] for i in keep],
+                     model.con_lb[keep], model.con_ub[keep],
+                     model.var_lb, model.var_ub, model.var_type, obj,
+                     model.obj_const)
+
+
+def knapsack_oa(f=9, N=64, a=None, b=None, points=(1.0, 8.0, 32.0, 64.0)):
+    """Outer-approximation LP of the knapsack example
+    (examples/knapsack/knapsack.cpp:68-114, data main.f:12-32):
+    min sum a_i x_i^{b_i}, sum x_i <= N, x_i integer in [1, N].
+    Columns: x_1..x_f (Integer), eta_1..eta_f (Continuous); rows: the
+    capacity row, then for each term one tangent row per point t:
+    eta_i - f_i'(t) x_i >= f_i(t) - f_i'(t) t  (the terms are convex for
+    a > 0, b < 0, x > 0, so tangents under-estimate)."""
+    if a is None:
+        a = [1.0, 2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0, 9.0][:f]
+    if b is None:
+        b = [-1.0, -2.0, -1.5, -1.7, -1.2, -1.7, -1.4, -1.2, -1.5][:f]
+    if len(a) < f:
+        rng = np.random.default_rng(1234 + f)
+        a = list(a) + list(rng.uniform(1.0, 9.0, f - len(a)))
+        b = list(b) + list(rng.uniform(-2.0, -1.0, f - len(b)))
+    n = 2 * f
+    rows, rlo, rhi = [], [], []
+    rows.append([(i, 1.0) for i in range(f)])
+    rlo.append(-math.inf)
+    rhi.append(float(N))
+    for i in range(f):
+        for t in points:
+            if t > N:
+                continue
+            fv = a[i] * t ** b[i]
+            g = a[i] * b[i] * t ** (b[i] - 1.0)
+            rows.append([(i, -g), (f + i, 1.0)])
+            rlo.append(fv - g * t)
+            rhi.append(math.inf)
+    vlb = [1.0] * f + [-math.inf] * f
+    vub = [float(N)] * f + [math.inf] * f
+    vtype = [INTEGER] * f + [CONTINUOUS] * f
+    obj = [0.0] * f + [1.0] * f
+    return from_rows(f"knapsack-oa-f{f}-N{N}", n, rows, rlo, rhi, vlb, vub,
+                     vtype, obj)
+
+
+def random_boxes(p: LinProblem, B: int, seed: int, max_depth: int = 20,
+                 root_lb=None, root_ub=None):
+    """Seeded node boxes by random branching from the root:
+    each node gets a depth d in [1, max_depth]; each of the d steps picks a
+    random integer column that is not fixed yet and either fixes a binary to
+    0/1 or splits an integer at its midpoint (down: ub=floor(mid), up:
+    lb=ceil(mid)).  Returns (lb[B,n], ub[B,n])."""
+    rng = np.random.default_rng(seed)
+    lb0 = p.vlb if root_lb is None else root_lb
+    ub0 = p.vub if root_ub is None else root_ub
+    ints = np.nonzero((p.vtype == BINARY) | (p.vtype == INTEGER))[0]
+    LB = np.tile(lb0, (B, 1)).astype(np.float64)
+    UB = np.tile(ub0, (B, 1)).astype(np.float64)
+    for bi in range(B):
+        d = int(rng.integers(1, max_depth + 1))
+        for _ in range(d):
+            free = ints[UB[bi, ints] - LB[bi, ints] >= 1.0]
+            if free.size == 0:
+                break
+            j = int(free[rng.integers(0, free.size)])
+            lo, hi = LB[bi, j], UB[bi, j]
+            if not (math.isfinite(lo) and math.isfinite(hi)):
+                lo = lo if math.isfinite(lo) else -1e3
+                hi = hi if math.isfinite(hi) else 1e3
+            split = math.floor(0.5 * (lo + hi))   # down: ub=split, up: lb=split+1
+            if rng.integers(0, 2) == 0:
+                UB[bi, j] = split
+            else:
+                LB[bi, j] = split + 1.0
+    return LB, UB
+
+
+def random_problem(seed: int, n: int = 40, m: int = 30, density: float = 0.15,
+                   inf_frac: float = 0.15, int_frac: float = 0.5,
+                   eq_frac: float = 0.1):
+    """Synthetic edge-case generator: ragged rows (including empty and dense
+    ones), infinite column bounds (exercising getSingLfBnds_), one-sided and
+    two-sided rows, equality rows, tiny (|a|<=1e-8) and large coefficients,
+    and a mix of binary / integer / continuous columns."""
+    rng = np.random.default_rng(seed)
+    vtype = np.full(n, CONTINUOUS, dtype=np.int32)
+    r = rng.random(n)
+    vtype[r < int_frac] = INTEGER
+    vtype[r < int_frac * 0.5] = BINARY
+    vlb = np.where(vtype == BINARY, 0.0, np.round(rng.uniform(-20, 5, n)))
+    vub = np.where(vtype == BINARY, 1.0, vlb + np.round(rng.uniform(1, 40, n)))
+    cont = vtype == CONTINUOUS
+    vlb = np.where(cont, rng.uniform(-20, 5, n), vlb)
+    vub = np.where(cont, vlb + rng.uniform(0.5, 40, n), vub)
+    infl = (rng.random(n) < inf_frac) & (vtype != BINARY)
+    infu = (rng.random(n) < inf_frac) & (vtype != BINARY)
+    vlb[infl] = -math.inf
+    vub[infu] = math.inf
+    rows, rlo, rhi = [], [], []
+    for i in range(m):
+        if i == 0:
+            k = 0
+        elif i == 1:
+            k = n
+        else:
+            k = max(1, rng.binomial(n, density))
+        cols = rng.choice(n, size=k, replace=False) if k else []
+        terms = []
+        for j in cols:
+            u = rng.random()
+            if u < 0.03:
+                c = float(rng.choice([-1, 1]) * 5e-9)  # ignored by updates
+            elif u < 0.08:
+                c = float(rng.choice([-1, 1]) * rng.uniform(50, 500))
+            else:
+                c = float(np.round(rng.uniform(-5, 5), 3)) or 1.0
+            terms.append((int(j), c))
+        rows.append(terms)
+        # feasible-ish sides around the activity at a random interior point
+        x = np.where(np.isfinite(vlb) & np.isfinite(vub),
+                     rng.uniform(0, 1, n) * (np.where(np.isfinite(vub), vub, 0) -
+                                             np.where(np.isfinite(vlb), vlb, 0)) +
+                     np.where(np.isfinite(vlb), vlb, 0),
+                     np.where(np.isfinite(vlb), vlb, np.where(np.isfinite(vub), vub, 0.0)))
+        act = sum(c * x[j] for j, c in terms)
+        kind = rng.random()
+        slack = float(rng.uniform(0, 10))
+        if kind < eq_frac:
+            rlo.append(act)
+            rhi.append(act)
+        elif kind < 0.45:
+            rlo.append(-math.inf)
+            rhi.append(act + slack)
+        elif kind < 0.8:
+            rlo.append(act - slack)
+            rhi.append(math.inf)
+        else:
+            rlo.append(act - slack)
+            rhi.append(act + slack)
+    obj = np.round(rng.uniform(-3, 3, n), 2)
+    obj[rng.random(n) < 0.3] = 0.0
+    return from_rows(f"random-{seed}", n, rows, rlo, rhi, vlb, vub, vtype, obj,
+                     obj_const=float(np.round(rng.uniform(-5, 5), 2)))

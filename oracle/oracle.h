@@ -1,0 +1,46 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (see oracle/README.md).
+ * CPU restatements of the reference algorithms on the hot path.  Loaded only
+ * by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+ */
+#ifndef MGPU_ORACLE_H
+#define MGPU_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_OBJ_LOOP_CAP 100000L
+
+/* Shared (per batch) linear problem: CSR rows in ascending column order
+ * (the reference's VariableGroup order, Types.cpp:30-34), the column->rows
+ * pattern used by changeBFlag_, and the linear objective. */
+typedef struct {
+  int n, m;
+  const int *rowptr, *colidx;
+  const double *val;
+  const double *rlo, *rhi;
+  const int *colptr, *rowidx;
+  const int *vtype;        /* Types.h:83-89 numerics */
+  int nobj;
+  const int *objidx;
+  const double *objval;
+  int cons_bad;            /* some row has lb > ub + 1e-8 (checkBounds_) */
+} orc_lin_problem;
+
+int orc_linear_fbbt_node(const orc_lin_problem *P, double *lb, double *ub,
+                         int has_inc, double inc_ub, unsigned char *flag,
+                         int mod_cap, int *mod_var, int *mod_lu,
+                         double *mod_val, int *nmods_out);
+
+int orc_linear_fbbt_batch(const orc_lin_problem *P, int B,
+                          const double *lb_in, const double *ub_in,
+                          double *lb_out, double *ub_out, int has_inc,
+                          double inc_ub, int *infeas, int *nmods,
+                          unsigned char *flag_scratch, int mod_cap,
+                          int *mod_var, int *mod_lu, double *mod_val);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

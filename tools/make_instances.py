@@ -1,0 +1,31 @@
+"""Convert the reference's test instances into the committed LinProblem
+fixtures under minotaur_amd/instances/ (run in the container that has
+/root/reference; the GPU box only reads the .npz files).
+
+  tls4_lin.npz     — linear rows of test_instances/tls4.nl
+  knapsack9.npz    — OA-LP of examples/knapsack (config 3)
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
+from minotaur_amd.nl import read_nl            # noqa: E402
+from minotaur_amd.problem import from_nl_linear, knapsack_oa  # noqa: E402
+
+REF = os.environ.get('MINOTAUR_REF', '/root/reference')
+OUT = os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd', 'instances')
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    tls4 = from_nl_linear(read_nl(os.path.join(REF, 'test_instances', 'tls4.nl')),
+                          name='tls4-lin')
+    tls4.save(os.path.join(OUT, 'tls4_lin.npz'))
+    print('tls4-lin', tls4.n, tls4.m, tls4.nnz)
+    ks = knapsack_oa()
+    ks.save(os.path.join(OUT, 'knapsack9.npz'))
+    print('knapsack9', ks.n, ks.m, ks.nnz)
+
+
+if __name__ == '__main__':
+    main()
