@@ -1,0 +1,114 @@
+/*
+ * mgpu.h — C ABI of the MI355X (gfx950) relaxation-solving and
+ * bound-tightening engine for Minotaur's branch-and-bound.
+ *
+ * This is the drop-in boundary.  A host C++ plugin that keeps
+ * Minotaur's src/base plugin surface unchanged calls only these entry points:
+ *
+ *   HipLPEngine : LPEngine   (replaces OsiLPEngine, src/interfaces/OsiLPEngine.cpp)
+ *   batched FBBT handler     (replaces LinearHandler::presolveNode,
+ *                             src/base/LinearHandler.cpp:1592-1603)
+ *
+ * (INTEGRATION.md shows both subclasses and the EngineFactory registration.)
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no exceptions cross the ABI; every
+ *     function returns MGPU_OK (0) or a negative MGPU_ERR_* code and records
+ *     a message retrievable with mgpu_last_error().
+ *   - Variable types use the reference's VariableType numerics
+ *     (src/base/Types.h:83-89): 0 Binary, 1 Integer, 2 ImplBin, 3 ImplInt,
+ *     4 Continuous.
+ *   - LP status values ARE the reference's EngineStatus numerics
+ *     (src/base/Types.h:152-166).
+ *   - Missing bounds are IEEE +-infinity; |b| >= 1e20 counts as infinite in
+ *     FBBT exactly as in LinearHandler.cpp:58,71.
+ *   - Node boxes are row-major [batch][n] f64.
+ *   - Functions suffixed _dev take DEVICE pointers (hipMalloc'ed or torch
+ *     CUDA tensors) and are asynchronous on the context's stream; the others
+ *     take host pointers and return after the results are in host memory.
+ *   - One context per host thread (the reference engine is not thread-safe
+ *     either: OsiLPEngine, and QGPar.cpp:712-715 clones one per thread).
+ */
+#ifndef MGPU_H
+#define MGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGPU_OK 0
+#define MGPU_ERR_ARG (-1)     /* bad argument (null pointer, size) */
+#define MGPU_ERR_HIP (-2)     /* HIP runtime error (maps to EngineError) */
+#define MGPU_ERR_STATE (-3)   /* call out of order (e.g. no problem loaded) */
+#define MGPU_ERR_NOMEM (-4)   /* device allocation failed */
+
+/* EngineStatus numerics (src/base/Types.h:152-166). */
+#define MGPU_PROVEN_OPTIMAL 0
+#define MGPU_PROVEN_INFEASIBLE 2
+#define MGPU_PROVEN_UNBOUNDED 4
+#define MGPU_PROVEN_OBJECTIVE_CUTOFF 5
+#define MGPU_ENGINE_ITERATION_LIMIT 6
+#define MGPU_ENGINE_ERROR 11
+#define MGPU_ENGINE_UNKNOWN_STATUS 12
+
+typedef struct mgpu_ctx mgpu_ctx;
+
+/* Context lifetime.  `device` is the HIP device ordinal (one process per
+ * GPU: pass LOCAL_RANK).  Replaces the OsiLPEngine constructor
+ * (OsiLPEngine.cpp:95-137) and emptyCopy() (:289-291). */
+int mgpu_create(int device, mgpu_ctx **out);
+int mgpu_destroy(mgpu_ctx *ctx);
+const char *mgpu_last_error(const mgpu_ctx *ctx);
+/* Use an existing hipStream_t (e.g. torch.cuda.current_stream()); NULL =
+ * the context's own stream. */
+int mgpu_set_stream(mgpu_ctx *ctx, void *hip_stream);
+void *mgpu_get_stream(mgpu_ctx *ctx);
+int mgpu_sync(mgpu_ctx *ctx);
+
+/* Load the batch-shared relaxation: row-major CSR with columns ascending
+ * inside each row (the reference's VariableGroup order), row bounds, root
+ * column bounds and types, and a linear objective to MINIMISE plus constant.
+ * Replaces OsiLPEngine::load (OsiLPEngine.cpp:390-498). */
+int mgpu_load_lp(mgpu_ctx *ctx, int n, int m, const int32_t *rowptr,
+                 const int32_t *colidx, const double *val,
+                 const double *rowlb, const double *rowub,
+                 const double *collb, const double *colub,
+                 const int32_t *coltype, const double *obj, double objoff);
+
+/* Batched node FBBT over linear rows: for every node box b, the exact
+ * result of LinearHandler::presolveNode (LinearHandler.cpp:1592-1653) on the
+ * loaded rows with that box.
+ *   incumbent   : best known objective value, +INFINITY if none (the
+ *                 reference then skips varBndsFromObj_, :1636-1640).
+ *   lb/ub_out   : tightened boxes [batch][n] (may alias lb/ub_in).
+ *   infeasible  : [batch] presolveNode's return value (1 = infeasible).
+ *   nmods       : [batch] number of VarBoundMods the reference appends to
+ *                 r_mods.
+ *   mod_cap>0   : also write the mod log in push order, [batch][mod_cap]
+ *                 (var index, 0 Lower / 1 Upper, new value); entries past
+ *                 mod_cap are dropped but still counted in nmods. */
+int mgpu_fbbt(mgpu_ctx *ctx, int batch, const double *lb_in,
+              const double *ub_in, double incumbent, double *lb_out,
+              double *ub_out, int32_t *infeasible, int32_t *nmods,
+              int mod_cap, int32_t *mod_var, int32_t *mod_lu,
+              double *mod_val);
+int mgpu_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in,
+                  const double *d_ub_in, double incumbent, double *d_lb_out,
+                  double *d_ub_out, int32_t *d_infeasible, int32_t *d_nmods,
+                  int mod_cap, int32_t *d_mod_var, int32_t *d_mod_lu,
+                  double *d_mod_val);
+
+/* Which FBBT kernel variant the next call uses: 0 auto, 1 node bounds in
+ * LDS, 2 node bounds in a global scratch (large n). For tests/benchmarks. */
+int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
+
+/* Device-side timing of the last launch of the named kernel family
+ * ("fbbt", "lp"), measured with hipEvents on the context stream. */
+double mgpu_last_kernel_ms(mgpu_ctx *ctx, const char *which);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGPU_H */

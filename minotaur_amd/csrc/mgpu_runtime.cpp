@@ -1,0 +1,335 @@
+// Host runtime behind the C ABI (include/mgpu.h): one context per host
+// thread and device, the batch-shared relaxation resident in HBM, grow-only
+// device workspaces, and synchronous host-pointer wrappers around the
+// asynchronous device-pointer entry points.
+//
+// Reference counterparts: OsiLPEngine (src/interfaces/OsiLPEngine.cpp) for
+// the context/problem lifetime (load :390-498, clear :264-275), and
+// LinearHandler::presolveNode (src/base/LinearHandler.cpp:1592-1603) for
+// mgpu_fbbt.  No exception crosses the ABI; HIP failures become
+// MGPU_ERR_HIP, which the engine adapter maps to EngineError.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mgpu.h"
+#include "mgpu_internal.h"
+
+using namespace mgpu;
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t want) {
+    if (want <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct mgpu_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool loaded = false;
+  DevLP lp{};
+  // problem storage
+  DevBuf rowptr, terms, rlo, rhi, colptr, rowidx, vtype, obj, collb, colub, objd;
+  std::vector<Term> h_terms;
+  // workspaces
+  DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_inf, io_nmods, io_mv, io_ml, io_mval;
+  DevBuf scratch, flag_scratch;
+  int fbbt_variant = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_fbbt_ms = 0.0, last_lp_ms = 0.0;
+};
+
+namespace {
+
+int fail(mgpu_ctx *c, int code, const char *fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(c, expr)                                                          \
+  do {                                                                           \
+    hipError_t e_ = (expr);                                                      \
+    if (e_ != hipSuccess)                                                        \
+      return fail((c), e_ == hipErrorOutOfMemory ? MGPU_ERR_NOMEM : MGPU_ERR_HIP, \
+                  "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,      \
+                  __LINE__);                                                     \
+  } while (0)
+
+template <class T>
+hipError_t upload(DevBuf &b, const T *src, size_t count) {
+  hipError_t e = b.ensure(count * sizeof(T) > 0 ? count * sizeof(T) : 16);
+  if (e != hipSuccess || count == 0) return e;
+  return hipMemcpy(b.p, src, count * sizeof(T), hipMemcpyHostToDevice);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgpu_create(int device, mgpu_ctx **out) {
+  if (!out) return MGPU_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MGPU_ERR_HIP;
+  if (device < 0 || device >= ndev) return MGPU_ERR_ARG;
+  mgpu_ctx *c = new mgpu_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return MGPU_ERR_HIP;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return MGPU_OK;
+}
+
+int mgpu_destroy(mgpu_ctx *c) {
+  if (!c) return MGPU_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (DevBuf *b : {&c->rowptr, &c->terms, &c->rlo, &c->rhi, &c->colptr, &c->rowidx,
+                    &c->vtype, &c->obj, &c->collb, &c->colub, &c->objd, &c->io_lb_in,
+                    &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
+                    &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch})
+    b->release();
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return MGPU_OK;
+}
+
+const char *mgpu_last_error(const mgpu_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int mgpu_set_stream(mgpu_ctx *c, void *s) {
+  if (!c) return MGPU_ERR_ARG;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return MGPU_OK;
+}
+
+void *mgpu_get_stream(mgpu_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int mgpu_sync(mgpu_ctx *c) {
+  if (!c) return MGPU_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MGPU_OK;
+}
+
+int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t *colidx,
+                 const double *val, const double *rowlb, const double *rowub,
+                 const double *collb, const double *colub, const int32_t *coltype,
+                 const double *obj, double objoff) {
+  if (!c) return MGPU_ERR_ARG;
+  if (n <= 0 || m < 0 || !rowptr || (m > 0 && (!rowlb || !rowub)) || !collb || !colub ||
+      !coltype || !obj)
+    return fail(c, MGPU_ERR_ARG, "mgpu_load_lp: bad argument");
+  const int nnz = rowptr[m];
+  if (rowptr[0] != 0 || nnz < 0 || (nnz > 0 && (!colidx || !val)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_load_lp: bad CSR");
+  for (int i = 0; i < m; ++i) {
+    if (rowptr[i + 1] < rowptr[i]) return fail(c, MGPU_ERR_ARG, "rowptr not monotone at %d", i);
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+      if (colidx[k] < 0 || colidx[k] >= n)
+        return fail(c, MGPU_ERR_ARG, "column index out of range in row %d", i);
+      if (k > rowptr[i] && colidx[k] <= colidx[k - 1])
+        return fail(c, MGPU_ERR_ARG, "row %d columns not strictly ascending", i);
+    }
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // CSR terms, packed
+  c->h_terms.resize(nnz > 0 ? nnz : 1);
+  for (int k = 0; k < nnz; ++k) c->h_terms[k] = Term{val[k], colidx[k], 0};
+  // column -> rows pattern
+  std::vector<int32_t> colptr(n + 1, 0), rowidx(nnz > 0 ? nnz : 1);
+  for (int k = 0; k < nnz; ++k) colptr[colidx[k] + 1]++;
+  for (int j = 0; j < n; ++j) colptr[j + 1] += colptr[j];
+  {
+    std::vector<int32_t> fill(colptr.begin(), colptr.end() - 1);
+    for (int i = 0; i < m; ++i)
+      for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) rowidx[fill[colidx[k]]++] = i;
+  }
+  std::vector<uint8_t> vt(n);
+  for (int j = 0; j < n; ++j) vt[j] = (uint8_t)coltype[j];
+  std::vector<Term> objt;
+  for (int j = 0; j < n; ++j)
+    if (obj[j] != 0.0) objt.push_back(Term{obj[j], j, 0});
+  int cons_bad = 0;
+  for (int i = 0; i < m; ++i)
+    if (rowlb[i] > rowub[i] + kETol) cons_bad = 1;
+
+  HIPCHK(c, upload(c->rowptr, rowptr, (size_t)m + 1));
+  HIPCHK(c, upload(c->terms, c->h_terms.data(), (size_t)(nnz > 0 ? nnz : 1)));
+  HIPCHK(c, upload(c->rlo, rowlb, (size_t)m));
+  HIPCHK(c, upload(c->rhi, rowub, (size_t)m));
+  HIPCHK(c, upload(c->colptr, colptr.data(), (size_t)n + 1));
+  HIPCHK(c, upload(c->rowidx, rowidx.data(), rowidx.size()));
+  HIPCHK(c, upload(c->vtype, vt.data(), (size_t)n));
+  HIPCHK(c, upload(c->obj, objt.empty() ? c->h_terms.data() : objt.data(),
+                   objt.empty() ? (size_t)0 : objt.size()));
+  HIPCHK(c, upload(c->collb, collb, (size_t)n));
+  HIPCHK(c, upload(c->colub, colub, (size_t)n));
+  HIPCHK(c, upload(c->objd, obj, (size_t)n));
+
+  DevLP &lp = c->lp;
+  lp.n = n;
+  lp.m = m;
+  lp.nnz = nnz;
+  lp.nobj = (int)objt.size();
+  lp.cons_bad = cons_bad;
+  lp.rowptr = c->rowptr.as<int32_t>();
+  lp.terms = c->terms.as<Term>();
+  lp.rlo = c->rlo.as<double>();
+  lp.rhi = c->rhi.as<double>();
+  lp.colptr = c->colptr.as<int32_t>();
+  lp.rowidx = c->rowidx.as<int32_t>();
+  lp.vtype = c->vtype.as<uint8_t>();
+  lp.obj = c->obj.as<Term>();
+  lp.collb = c->collb.as<double>();
+  lp.colub = c->colub.as<double>();
+  lp.objd = c->objd.as<double>();
+  lp.objoff = objoff;
+  c->loaded = true;
+  return MGPU_OK;
+}
+
+int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
+  if (!c || variant < 0 || variant > 2) return MGPU_ERR_ARG;
+  c->fbbt_variant = variant;
+  return MGPU_OK;
+}
+
+double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
+  if (!c || !which) return -1.0;
+  if (!strcmp(which, "fbbt")) return c->last_fbbt_ms;
+  if (!strcmp(which, "lp")) return c->last_lp_ms;
+  return -1.0;
+}
+
+int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
+                  double incumbent, double *lb_out, double *ub_out, int32_t *infeas,
+                  int32_t *nmods, int mod_cap, int32_t *mod_var, int32_t *mod_lu,
+                  double *mod_val) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_fbbt: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb_in || !ub_in || !lb_out || !ub_out || !infeas || !nmods)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_fbbt: bad argument");
+  if (mod_cap > 0 && (!mod_var || !mod_lu || !mod_val))
+    return fail(c, MGPU_ERR_ARG, "mgpu_fbbt: mod_cap > 0 needs mod buffers");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  FbbtIO io{};
+  io.lb_in = lb_in;
+  io.ub_in = ub_in;
+  io.lb_out = lb_out;
+  io.ub_out = ub_out;
+  io.infeas = infeas;
+  io.nmods = nmods;
+  io.mod_cap = mod_cap > 0 ? mod_cap : 0;
+  io.mod_var = mod_cap > 0 ? mod_var : nullptr;
+  io.mod_lu = mod_cap > 0 ? mod_lu : nullptr;
+  io.mod_val = mod_cap > 0 ? mod_val : nullptr;
+  io.batch = batch;
+  // LinearHandler.cpp:1636-1640: only with an incumbent, against
+  // (best value - objective constant).
+  io.has_inc = std::isfinite(incumbent) ? 1 : 0;
+  io.inc_ub = io.has_inc ? incumbent - c->lp.objoff : 0.0;
+  const int waves = (batch + kLanes - 1) / kLanes;
+  const bool fits = fbbt_lds_bytes(c->lp.n, c->lp.m) <= 160 * 1024;
+  if (c->fbbt_variant == 2 || (c->fbbt_variant == 0 && !fits)) {
+    HIPCHK(c, c->scratch.ensure((size_t)waves * 2 * c->lp.n * kLanes * sizeof(double)));
+    HIPCHK(c, c->flag_scratch.ensure((size_t)waves * (c->lp.m > 0 ? c->lp.m : 1) * kLanes));
+    io.scratch = c->scratch.as<double>();
+    io.flag_scratch = c->flag_scratch.as<uint8_t>();
+  } else if (c->fbbt_variant == 1 && !fits) {
+    return fail(c, MGPU_ERR_ARG, "LDS variant needs %zu B > 160 KiB",
+                fbbt_lds_bytes(c->lp.n, c->lp.m));
+  }
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, launch_fbbt_linear(c->lp, io, c->fbbt_variant, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  return MGPU_OK;
+}
+
+int mgpu_fbbt(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
+              double incumbent, double *lb_out, double *ub_out, int32_t *infeas,
+              int32_t *nmods, int mod_cap, int32_t *mod_var, int32_t *mod_lu,
+              double *mod_val) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_fbbt: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb_in || !ub_in || !lb_out || !ub_out || !infeas || !nmods)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_fbbt: bad argument");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t nb = (size_t)batch * c->lp.n * sizeof(double);
+  const int cap = mod_cap > 0 ? mod_cap : 0;
+  HIPCHK(c, c->io_lb_in.ensure(nb));
+  HIPCHK(c, c->io_ub_in.ensure(nb));
+  HIPCHK(c, c->io_lb_out.ensure(nb));
+  HIPCHK(c, c->io_ub_out.ensure(nb));
+  HIPCHK(c, c->io_inf.ensure((size_t)batch * 4));
+  HIPCHK(c, c->io_nmods.ensure((size_t)batch * 4));
+  if (cap) {
+    HIPCHK(c, c->io_mv.ensure((size_t)batch * cap * 4));
+    HIPCHK(c, c->io_ml.ensure((size_t)batch * cap * 4));
+    HIPCHK(c, c->io_mval.ensure((size_t)batch * cap * 8));
+  }
+  HIPCHK(c, hipMemcpyAsync(c->io_lb_in.p, lb_in, nb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->io_ub_in.p, ub_in, nb, hipMemcpyHostToDevice, c->stream));
+  int rc = mgpu_fbbt_dev(c, batch, c->io_lb_in.as<double>(), c->io_ub_in.as<double>(),
+                         incumbent, c->io_lb_out.as<double>(), c->io_ub_out.as<double>(),
+                         c->io_inf.as<int32_t>(), c->io_nmods.as<int32_t>(), cap,
+                         c->io_mv.as<int32_t>(), c->io_ml.as<int32_t>(),
+                         c->io_mval.as<double>());
+  if (rc != MGPU_OK) return rc;
+  HIPCHK(c, hipMemcpyAsync(lb_out, c->io_lb_out.p, nb, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(ub_out, c->io_ub_out.p, nb, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(infeas, c->io_inf.p, (size_t)batch * 4, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipMemcpyAsync(nmods, c->io_nmods.p, (size_t)batch * 4, hipMemcpyDeviceToHost,
+                           c->stream));
+  if (cap && mod_var && mod_lu && mod_val) {
+    HIPCHK(c, hipMemcpyAsync(mod_var, c->io_mv.p, (size_t)batch * cap * 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(mod_lu, c->io_ml.p, (size_t)batch * cap * 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(mod_val, c->io_mval.p, (size_t)batch * cap * 8,
+                             hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_fbbt_ms = ms;
+  return MGPU_OK;
+}
+
+}  // extern "C"

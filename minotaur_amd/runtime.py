@@ -1,0 +1,167 @@
+"""ctypes binding of the C ABI in include/mgpu.h (libmgpu.so, built in-tree).
+
+The product path has no CPU fallback: if ``libmgpu.so`` is missing or no HIP
+device is visible, every call raises ``MgpuError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libmgpu.so')
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_D = ctypes.c_double
+
+# Every entry point declared in include/mgpu.h (checked by the CPU tests).
+EXPORTS = [
+    'mgpu_create', 'mgpu_destroy', 'mgpu_last_error', 'mgpu_set_stream',
+    'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
+    'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms',
+]
+
+_lib = None
+
+
+class MgpuError(RuntimeError):
+    pass
+
+
+def load_library():
+    """Load libmgpu.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MgpuError(f"{LIB_PATH} not built: run __graft_entry__.build() "
+                        "(there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.mgpu_create.argtypes = [_I, ctypes.POINTER(_P)]
+    lib.mgpu_destroy.argtypes = [_P]
+    lib.mgpu_last_error.argtypes = [_P]
+    lib.mgpu_last_error.restype = ctypes.c_char_p
+    lib.mgpu_set_stream.argtypes = [_P, _P]
+    lib.mgpu_get_stream.argtypes = [_P]
+    lib.mgpu_get_stream.restype = _P
+    lib.mgpu_sync.argtypes = [_P]
+    lib.mgpu_load_lp.argtypes = [_P, _I, _I] + [_P] * 10 + [_D]
+    lib.mgpu_fbbt.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
+    lib.mgpu_fbbt_dev.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
+    lib.mgpu_set_fbbt_variant.argtypes = [_P, _I]
+    lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
+    lib.mgpu_last_kernel_ms.restype = _D
+    for name in EXPORTS:
+        getattr(lib, name).restype = getattr(lib, name).restype or _I
+    _lib = lib
+    return lib
+
+
+def _np(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _hp(a):
+    return None if a is None else a.ctypes.data_as(_P)
+
+
+def _dp(t):
+    """Device pointer of a torch CUDA tensor (or None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class FbbtOut:
+    def __init__(self, lb, ub, infeasible, nmods, mod_var=None, mod_lu=None,
+                 mod_val=None):
+        self.lb, self.ub, self.infeasible, self.nmods = lb, ub, infeasible, nmods
+        self.mod_var, self.mod_lu, self.mod_val = mod_var, mod_lu, mod_val
+
+
+class Context:
+    """One engine context on one device (one per host thread)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = _P()
+        rc = self.lib.mgpu_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise MgpuError(f"mgpu_create(device={device}) failed rc={rc} "
+                            "(no HIP device visible?)")
+        self.h = h
+        self.device = device
+        self.problem = None
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.mgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.lib.mgpu_last_error(self.h)
+            raise MgpuError(f"{what} failed rc={rc}: {msg.decode() if msg else ''}")
+
+    def set_stream(self, stream_ptr):
+        self._chk(self.lib.mgpu_set_stream(self.h, _P(stream_ptr)), 'mgpu_set_stream')
+
+    def sync(self):
+        self._chk(self.lib.mgpu_sync(self.h), 'mgpu_sync')
+
+    def set_fbbt_variant(self, v: int):
+        self._chk(self.lib.mgpu_set_fbbt_variant(self.h, int(v)), 'mgpu_set_fbbt_variant')
+
+    def last_kernel_ms(self, which: str) -> float:
+        return float(self.lib.mgpu_last_kernel_ms(self.h, which.encode()))
+
+    # -- problem -----------------------------------------------------------
+    def load(self, p):
+        """mgpu_load_lp: OsiLPEngine::load equivalent for a LinProblem."""
+        self._keep = [_np(p.rowptr, np.int32), _np(p.colidx, np.int32),
+                      _np(p.val, np.float64), _np(p.rlo, np.float64),
+                      _np(p.rhi, np.float64), _np(p.vlb, np.float64),
+                      _np(p.vub, np.float64), _np(p.vtype, np.int32),
+                      _np(p.obj, np.float64)]
+        k = self._keep
+        self._chk(self.lib.mgpu_load_lp(self.h, p.n, p.m, *[_hp(a) for a in k],
+                                        float(p.obj_const)), 'mgpu_load_lp')
+        self.problem = p
+
+    # -- FBBT --------------------------------------------------------------
+    def fbbt(self, lb, ub, incumbent=math.inf, mod_cap=0) -> FbbtOut:
+        """Host arrays [B,n] in, tightened boxes out (synchronous)."""
+        lb = _np(lb, np.float64)
+        ub = _np(ub, np.float64)
+        B = lb.shape[0]
+        olb = np.empty_like(lb)
+        oub = np.empty_like(ub)
+        inf = np.zeros(B, dtype=np.int32)
+        nm = np.zeros(B, dtype=np.int32)
+        mv = ml = mval = None
+        if mod_cap > 0:
+            mv = np.full((B, mod_cap), -1, dtype=np.int32)
+            ml = np.full((B, mod_cap), -1, dtype=np.int32)
+            mval = np.zeros((B, mod_cap))
+        self._chk(self.lib.mgpu_fbbt(self.h, B, _hp(lb), _hp(ub), float(incumbent),
+                                     _hp(olb), _hp(oub), _hp(inf), _hp(nm), int(mod_cap),
+                                     _hp(mv), _hp(ml), _hp(mval)), 'mgpu_fbbt')
+        return FbbtOut(olb, oub, inf, nm, mv, ml, mval)
+
+    def fbbt_dev(self, lb, ub, lb_out, ub_out, infeasible, nmods,
+                 incumbent=math.inf, mod_var=None, mod_lu=None, mod_val=None):
+        """Torch CUDA tensors in/out, asynchronous on the context stream."""
+        B = int(lb.shape[0])
+        cap = int(mod_var.shape[1]) if mod_var is not None else 0
+        self._chk(self.lib.mgpu_fbbt_dev(self.h, B, _dp(lb), _dp(ub), float(incumbent),
+                                         _dp(lb_out), _dp(ub_out), _dp(infeasible),
+                                         _dp(nmods), cap, _dp(mod_var), _dp(mod_lu),
+                                         _dp(mod_val)), 'mgpu_fbbt_dev')

@@ -34,9 +34,19 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(_P)
 
 
+def build_oracle():
+    """(Re)build liboracle.so from oracle/*.c (gcc; a second or two)."""
+    import subprocess
+    subprocess.run(['make', '-s', '-C', HERE, 'oracle'], check=True)
+
+
 def lib():
     global _lib
     if _lib is None:
+        srcs = [os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(('.c', '.h'))]
+        if (not os.path.exists(LIB_ORACLE) or
+                os.path.getmtime(LIB_ORACLE) < max(os.path.getmtime(s) for s in srcs)):
+            build_oracle()
         _lib = ctypes.CDLL(LIB_ORACLE)
         _lib.orc_linear_fbbt.restype = _I
         _lib.orc_linear_fbbt.argtypes = [_I, _I] + [_P] * 8 + [_I, _P, _P, _I, _I,

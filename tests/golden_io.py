@@ -1,0 +1,45 @@
+"""Load the committed golden fixtures (tests/golden/*.npz)."""
+import glob
+import math
+import os
+
+import numpy as np
+
+from minotaur_amd.problem import LinProblem
+
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def cases(prefix='fbbt_'):
+    return sorted(os.path.basename(p)[len(prefix):-4]
+                  for p in glob.glob(os.path.join(GOLDEN, prefix + '*.npz')))
+
+
+def load_fbbt(name):
+    z = np.load(os.path.join(GOLDEN, f'fbbt_{name}.npz'), allow_pickle=False)
+    p = LinProblem(name=str(z['name']), n=int(z['n']), m=int(z['m']),
+                   rowptr=z['rowptr'].astype(np.int32), colidx=z['colidx'].astype(np.int32),
+                   val=z['val'], rlo=z['rlo'], rhi=z['rhi'], vlb=z['vlb'], vub=z['vub'],
+                   vtype=z['vtype'].astype(np.int32), obj=z['obj'],
+                   obj_const=float(z['obj_const'])).validate()
+    inc = float(z['incumbent'])
+    g = {k: z[k] for k in ('lb_in', 'ub_in', 'lb_out', 'ub_out', 'infeas', 'nmods',
+                           'mod_var', 'mod_lu', 'mod_val')}
+    g['incumbent'] = None if math.isnan(inc) else inc
+    g['mod_cap'] = g['mod_var'].shape[1]
+    return p, g
+
+
+def bits_equal(a, b):
+    """Bit-exact f64 comparison (NaN payloads included)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+def assert_mods_equal(nmods, mv, ml, mval, g, cap):
+    for b in range(len(nmods)):
+        k = min(int(nmods[b]), cap)
+        assert np.array_equal(mv[b, :k], g['mod_var'][b, :k].astype(np.int32)), b
+        assert np.array_equal(ml[b, :k], g['mod_lu'][b, :k].astype(np.int32)), b
+        assert bits_equal(mval[b, :k], g['mod_val'][b, :k]), b

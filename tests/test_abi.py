@@ -1,0 +1,44 @@
+"""CPU: the C-ABI library builds, loads, and exports every entry point that
+include/mgpu.h declares (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+from minotaur_amd import build, runtime
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, 'include', 'mgpu.h')).read()
+    hdr = re.sub(r'/\*.*?\*/', '', hdr, flags=re.S)
+    return sorted(set(re.findall(r'\b(mgpu_[a-z_]+)\s*\(', hdr)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert 'mgpu_fbbt' in syms and 'mgpu_load_lp' in syms and 'mgpu_create' in syms
+    assert set(syms) == set(runtime.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    path = build.build()
+    lib = ctypes.CDLL(path)
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+
+
+def test_no_cpu_fallback_without_device():
+    """Creating a context with no visible HIP device must fail loudly."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    lib = runtime.load_library()
+    h = ctypes.c_void_p()
+    assert lib.mgpu_create(0, ctypes.byref(h)) != 0
+    try:
+        runtime.Context(0)
+    except runtime.MgpuError:
+        pass
+    else:
+        raise AssertionError("Context() succeeded without a GPU")

@@ -1,0 +1,123 @@
+"""GPU parity of K1 (batched node FBBT) through the C ABI.
+
+Bar: bit-exact f64 bounds, identical infeasibility verdicts, identical mod
+counts and mod logs, against (a) the committed golden vectors produced by
+the reference's own LinearHandler::presolveNode and (b) the C oracle on
+larger seeded batches.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+from golden_io import assert_mods_equal, bits_equal, cases, load_fbbt
+from minotaur_amd.problem import LinProblem, random_boxes, random_problem
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from minotaur_amd.runtime import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _inc(g):
+    return math.inf if g['incumbent'] is None else g['incumbent']
+
+
+@pytest.mark.parametrize('variant', [1, 2])
+@pytest.mark.parametrize('name', cases())
+def test_fbbt_matches_reference_golden(ctx, name, variant):
+    p, g = load_fbbt(name)
+    ctx.load(p)
+    ctx.set_fbbt_variant(variant)
+    try:
+        r = ctx.fbbt(g['lb_in'], g['ub_in'], _inc(g), mod_cap=g['mod_cap'])
+    finally:
+        ctx.set_fbbt_variant(0)
+    assert bits_equal(r.lb, g['lb_out'])
+    assert bits_equal(r.ub, g['ub_out'])
+    assert np.array_equal(r.infeasible, g['infeas'])
+    assert np.array_equal(r.nmods, g['nmods'])
+    assert_mods_equal(r.nmods, r.mod_var, r.mod_lu, r.mod_val, g, g['mod_cap'])
+
+
+def _tls4():
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    return LinProblem.load(os.path.join(here, '..', 'minotaur_amd', 'instances',
+                                        'tls4_lin.npz'))
+
+
+@pytest.mark.parametrize('inc', [math.inf, 20.0])
+def test_fbbt_large_batch_vs_oracle(ctx, inc):
+    """Ragged last wave (B not a multiple of 64) and many waves."""
+    p = _tls4()
+    LB, UB = random_boxes(p, 20001, 424242)
+    ctx.load(p)
+    r = ctx.fbbt(LB, UB, inc)
+    o = oracle.linear_fbbt(p, LB, UB, None if math.isinf(inc) else inc, nthreads=8)
+    assert bits_equal(r.lb, o.lb) and bits_equal(r.ub, o.ub)
+    assert np.array_equal(r.infeasible, o.infeas)
+    assert np.array_equal(r.nmods, o.nmods)
+
+
+def test_fbbt_global_variant_large_problem(ctx):
+    """n=400 does not fit LDS: the global-scratch kernel runs automatically."""
+    p = random_problem(77, n=400, m=300, density=0.02)
+    LB, UB = random_boxes(p, 300, 5)
+    ctx.load(p)
+    r = ctx.fbbt(LB, UB, 0.0, mod_cap=64)
+    o = oracle.linear_fbbt(p, LB, UB, 0.0, 64)
+    assert bits_equal(r.lb, o.lb) and bits_equal(r.ub, o.ub)
+    assert np.array_equal(r.infeasible, o.infeas)
+    assert np.array_equal(r.nmods, o.nmods)
+    assert np.array_equal(r.mod_var, o.mod_var)
+
+
+def test_fbbt_device_pointers_and_aliasing(ctx):
+    import torch
+    p = _tls4()
+    LB, UB = random_boxes(p, 1000, 99)
+    ctx.load(p)
+    host = ctx.fbbt(LB, UB, 20.0)
+    dev = torch.device('cuda', 0)
+    lb = torch.from_numpy(LB).to(dev)
+    ub = torch.from_numpy(UB).to(dev)
+    inf = torch.zeros(1000, dtype=torch.int32, device=dev)
+    nm = torch.zeros(1000, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx.fbbt_dev(lb, ub, lb, ub, inf, nm, 20.0)     # in place (aliased)
+    ctx.sync()
+    assert bits_equal(lb.cpu().numpy(), host.lb)
+    assert bits_equal(ub.cpu().numpy(), host.ub)
+    assert np.array_equal(inf.cpu().numpy(), host.infeasible)
+    assert np.array_equal(nm.cpu().numpy(), host.nmods)
+
+
+def test_fbbt_empty_and_single(ctx):
+    p = _tls4()
+    ctx.load(p)
+    r = ctx.fbbt(np.zeros((0, p.n)), np.zeros((0, p.n)))
+    assert r.lb.shape == (0, p.n)
+    r = ctx.fbbt(p.vlb[None], p.vub[None])
+    o = oracle.linear_fbbt(p, p.vlb[None], p.vub[None])
+    assert bits_equal(r.lb, o.lb) and bits_equal(r.ub, o.ub)
+
+
+def test_errors_are_reported_not_thrown(ctx):
+    from minotaur_amd.runtime import Context, MgpuError
+    c = Context(0)
+    with pytest.raises(MgpuError, match='no problem loaded'):
+        c.fbbt(np.zeros((1, 3)), np.ones((1, 3)))
+    p = _tls4()
+    bad = LinProblem(**{**p.__dict__})
+    bad.colidx = p.colidx.copy()
+    bad.colidx[1] = bad.colidx[0]          # not strictly ascending
+    with pytest.raises(MgpuError, match='ascending'):
+        c.load(bad)
+    c.close()
