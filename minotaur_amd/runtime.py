@@ -49,7 +49,7 @@ def load_library():
     lib.mgpu_get_stream.argtypes = [_P]
     lib.mgpu_get_stream.restype = _P
     lib.mgpu_sync.argtypes = [_P]
-    lib.mgpu_load_lp.argtypes = [_P, _I, _I] + [_P] * 10 + [_D]
+    lib.mgpu_load_lp.argtypes = [_P, _I, _I] + [_P] * 9 + [_D]
     lib.mgpu_fbbt.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
     lib.mgpu_fbbt_dev.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
     lib.mgpu_set_fbbt_variant.argtypes = [_P, _I]

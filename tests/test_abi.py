@@ -42,3 +42,19 @@ def test_no_cpu_fallback_without_device():
         pass
     else:
         raise AssertionError("Context() succeeded without a GPU")
+
+
+def _header_arity():
+    hdr = open(os.path.join(ROOT, 'include', 'mgpu.h')).read()
+    hdr = re.sub(r'/\*.*?\*/', '', hdr, flags=re.S)
+    out = {}
+    for name, args in re.findall(r'\b(mgpu_[a-z_]+)\s*\(([^)]*)\)\s*;', hdr):
+        args = args.strip()
+        out[name] = 0 if args in ('', 'void') else len(args.split(','))
+    return out
+
+
+def test_ctypes_signatures_match_header():
+    lib = runtime.load_library()
+    for name, nargs in _header_arity().items():
+        assert len(getattr(lib, name).argtypes) == nargs, name
