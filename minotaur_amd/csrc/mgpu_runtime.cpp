@@ -231,7 +231,13 @@ int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
 
 double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
   if (!c || !which) return -1.0;
-  if (!strcmp(which, "fbbt")) return c->last_fbbt_ms;
+  if (!strcmp(which, "fbbt")) {
+    float ms = 0.f;
+    if (hipEventSynchronize(c->ev1) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess)
+      c->last_fbbt_ms = ms;
+    return c->last_fbbt_ms;
+  }
   if (!strcmp(which, "lp")) return c->last_lp_ms;
   return -1.0;
 }
@@ -327,8 +333,6 @@ int mgpu_fbbt(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
                              hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_fbbt_ms = ms;
   return MGPU_OK;
 }
 
