@@ -11,14 +11,18 @@
 //  * FBBT inside a node is Gauss-Seidel: rows in index order, bounds updated
 //    in place, order-dependent f64 sums.  Bit-exactness forbids splitting a
 //    row sum, so parallelism is across nodes only.
-//  * Every node shares the same rows, so the row/term loops are wave-uniform:
-//    CSR terms are read with scalar (SMEM) loads and broadcast to all lanes;
-//    only the comparisons/updates diverge (EXEC-masked).
+//  * Every node shares the same rows, so row/term loops are wave-uniform.
+//    Row and term records are fetched 64 at a time with one coalesced vector
+//    load (lane t holds record t) and broadcast with v_readlane into SGPRs;
+//    the inner loops issue only LDS reads and VALU (scalar-memory loads
+//    would share lgkmcnt with the LDS reads and serialise every term).
 //  * The node's bounds live in LDS as [var][lane] f64 with a 65-element
 //    stride: term j of a row is one conflict-free ds_read_b64 per bound for
-//    the whole wave.  Row flags (Constraint::BFlag) are bytes [row][lane].
-//  * Problems whose bounds do not fit the 160 KiB LDS use the same code on a
-//    global [var][lane] scratch (coalesced 512-B wave accesses, L2-resident).
+//    the whole wave.  Row flags (Constraint::BFlag) are a per-lane 64-bit
+//    mask in VGPRs when m <= 64 (changeBFlag_ = OR of the column's row
+//    mask), else bytes [row][lane].
+//  * Problems whose bounds do not fit the 160 KiB LDS run the same code on a
+//    global [var][lane] scratch (coalesced 512-B wave accesses).
 //  * Compiled with -ffp-contract=off: no fused multiply-add, as the
 //    reference's x86-64 build (no FMA without -march).
 #include "mgpu_internal.h"
@@ -26,25 +30,102 @@
 namespace mgpu {
 namespace {
 
+// ---- wave-uniform broadcast ------------------------------------------------
+__device__ __forceinline__ int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ double rld(double v, int k) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), k);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ uint64_t rlu64(uint64_t v, int k) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffffu), k);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(v >> 32), k);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Per-lane slice of a chunk of up to 64 term records.
+struct TermChunk {
+  double a;
+  uint64_t cmask;
+  int j, cs, ce, isint;
+};
+
+__device__ __forceinline__ TermChunk load_terms(const TermRec *base, int cnt, int lane) {
+  TermChunk c{0.0, 0ull, 0, 0, 0, 0};
+  if (lane < cnt) {
+    const TermRec r = base[lane];
+    c.a = r.a;
+    c.cmask = r.cmask;
+    c.j = r.j;
+    c.cs = r.cs;
+    c.ce = r.ce;
+    c.isint = r.isint;
+  }
+  return c;
+}
+
+struct Term1 {  // one term, every field wave-uniform
+  double a;
+  uint64_t cmask;
+  int j, cs, ce, isint;
+};
+
+// Calls f(Term1) for every term of a term list, in order.  Chunk 0 (the
+// first 64 terms) comes from `pre`, which the caller loaded with the FULL
+// wave active (v_readlane reads lanes regardless of EXEC, so the source
+// VGPR must have been written by every lane); longer lists read the rest
+// straight from memory with wave-uniform addresses, which is correct under
+// any EXEC mask.
+template <class F>
+__device__ __forceinline__ void for_terms(const TermRec *base, int nt, const TermChunk &pre,
+                                          F &&f) {
+  const int cnt = nt < kLanes ? nt : kLanes;
+#pragma unroll 4
+  for (int k = 0; k < cnt; ++k)
+    f(Term1{rld(pre.a, k), rlu64(pre.cmask, k), rl(pre.j, k), rl(pre.cs, k), rl(pre.ce, k),
+            rl(pre.isint, k)});
+  for (int k = kLanes; k < nt; ++k) {
+    const TermRec r = base[k];
+    f(Term1{r.a, r.cmask, r.j, r.cs, r.ce, r.isint});
+  }
+}
+
+// ---- per-lane node view ----------------------------------------------------
+template <bool kBitFlags>
 struct NodeView {
   double *lb;
   double *ub;
-  uint8_t *flag;
-  int stride;  // elements between consecutive variables (same lane)
+  uint8_t *flag;     // byte flags [row][lane] (m > 64)
+  uint64_t bits;     // bit flags (m <= 64)
+  int stride;        // elements between consecutive variables (same lane)
   int lane;
+  const int32_t *rowidx;
   __device__ __forceinline__ double &L(int j) const { return lb[j * stride + lane]; }
   __device__ __forceinline__ double &U(int j) const { return ub[j * stride + lane]; }
-  __device__ __forceinline__ uint8_t &F(int r) const { return flag[r * kLanes + lane]; }
+  __device__ __forceinline__ bool flagged(int r) const {
+    if constexpr (kBitFlags) return (bits >> r) & 1ull;
+    else return flag[r * kLanes + lane] != 0;
+  }
+  __device__ __forceinline__ void clear(int r) {
+    if constexpr (kBitFlags) bits &= ~(1ull << r);
+    else flag[r * kLanes + lane] = 0;
+  }
+  // changeBFlag_ (LinearHandler.cpp:1229-1234): flag every row holding the
+  // column of term k of chunk ch.
+  __device__ __forceinline__ void change_bflag(const Term1 &t) {
+    if constexpr (kBitFlags) {
+      bits |= t.cmask;
+    } else {
+      for (int q = t.cs; q < t.ce; ++q) flag[rowidx[q] * kLanes + lane] = 1;
+    }
+  }
 };
 
 struct NodeState {
   int nmods;
   unsigned nintmods;
 };
-
-__device__ __forceinline__ bool is_int_type(uint8_t t) {
-  return t == kBinary || t == kInteger;
-}
 
 struct ModLog {
   int32_t *var, *lu;
@@ -60,42 +141,35 @@ struct ModLog {
   }
 };
 
-// changeBFlag_: every row holding column j is flagged (LinearHandler.cpp:1229).
-__device__ __forceinline__ void change_bflag(const DevLP &lp, const NodeView &v, int j) {
-  const int k0 = lp.colptr[j], k1 = lp.colptr[j + 1];
-  for (int k = k0; k < k1; ++k) v.F(lp.rowidx[k]) = 1;
-}
-
 // getLfBnds_ (LinearHandler.cpp:1237-1258): ascending-column f64 sums.
-__device__ __forceinline__ void lf_bnds(const Term *t, int nt, const NodeView &v,
-                                        double &lo, double &up) {
+template <class V>
+__device__ __forceinline__ void lf_bnds(const TermRec *base, int nt, const TermChunk &pre,
+                                        const V &v, double &lo, double &up) {
   double l = 0.0, u = 0.0;
-  for (int k = 0; k < nt; ++k) {
-    const double c = t[k].a;
-    const int j = t[k].j;
-    const double vl = v.L(j), vu = v.U(j);
-    if (c > 0) {
-      l += c * vl;
-      u += c * vu;
+  for_terms(base, nt, pre, [&](const Term1 &t) {
+    const double vl = v.L(t.j), vu = v.U(t.j);
+    if (t.a > 0) {
+      l += t.a * vl;
+      u += t.a * vu;
     } else {
-      l += c * vu;
-      u += c * vl;
+      l += t.a * vu;
+      u += t.a * vl;
     }
-  }
+  });
   lo = l;
   up = u;
 }
 
 // getSingLfBnds_ (LinearHandler.cpp:1261-1319): sums that skip a single
 // infinite term; a second infinite term makes the side infinite.
-__device__ void sing_lf_bnds(const Term *t, int nt, const NodeView &v, double &lo,
-                             double &up) {
+template <class V>
+__device__ void sing_lf_bnds(const TermRec *base, int nt, const TermChunk &pre, const V &v,
+                             double &lo, double &up) {
   double l = 0.0, u = 0.0;
   bool lo_sing = false, up_sing = false, lo_fin = true, up_fin = true;
-  for (int k = 0; k < nt; ++k) {
-    const double c = t[k].a;
-    const int j = t[k].j;
-    const double vl = v.L(j), vu = v.U(j);
+  for_terms(base, nt, pre, [&](const Term1 &t) {
+    const double c = t.a;
+    const double vl = v.L(t.j), vu = v.U(t.j);
     if (c > kETol) {
       if (vu < kInfty && up_fin) {
         u += c * vu;
@@ -127,18 +201,19 @@ __device__ void sing_lf_bnds(const Term *t, int nt, const NodeView &v, double &l
         up_sing = true;
       }
     }
-  }
+  });
   lo = l;
   up = u;
 }
 
 // updateLfBoundsFromLb_ (LinearHandler.cpp:1048-1134).
-__device__ void upd_from_lb(const DevLP &lp, const Term *t, int nt, const NodeView &v,
+template <class V>
+__device__ void upd_from_lb(const TermRec *base, int nt, const TermChunk &pre, V &v,
                             NodeState &s, const ModLog &log, double lb, double uu,
                             bool is_sing, bool &changed, bool count_int) {
-  for (int k = 0; k < nt; ++k) {
-    const double c = t[k].a;
-    const int j = t[k].j;
+  for_terms(base, nt, pre, [&](const Term1 &t) {
+    const double c = t.a;
+    const int j = t.j;
     double vlb = v.L(j), vub = v.U(j);
     if (c > kETol && (!is_sing || vub >= kInfty)) {
       if (vub >= kInfty) vub = 0.;
@@ -146,10 +221,10 @@ __device__ void upd_from_lb(const DevLP &lp, const Term *t, int nt, const NodeVi
       if (nlb > vlb + kETol) {
         const double cur_ub = v.U(j);
         if (nlb > cur_ub - kETol) nlb = cur_ub;
-        change_bflag(lp, v, j);
+        v.change_bflag(t);
         v.L(j) = nlb;
         log.push(s, j, 0, nlb);
-        if (count_int && is_int_type(lp.vtype[j])) s.nintmods++;
+        if (count_int && t.isint) s.nintmods++;
         changed = true;
       }
     } else if (c < -kETol && (!is_sing || vlb <= -kInfty)) {
@@ -158,23 +233,24 @@ __device__ void upd_from_lb(const DevLP &lp, const Term *t, int nt, const NodeVi
       if (nub < vub - kETol) {
         const double cur_lb = v.L(j);
         if (nub < cur_lb + kETol) nub = cur_lb;
-        change_bflag(lp, v, j);
+        v.change_bflag(t);
         v.U(j) = nub;
         log.push(s, j, 1, nub);
-        if (count_int && is_int_type(lp.vtype[j])) s.nintmods++;
+        if (count_int && t.isint) s.nintmods++;
         changed = true;
       }
     }
-  }
+  });
 }
 
 // updateLfBoundsFromUb_ (LinearHandler.cpp:1137-1226).
-__device__ void upd_from_ub(const DevLP &lp, const Term *t, int nt, const NodeView &v,
+template <class V>
+__device__ void upd_from_ub(const TermRec *base, int nt, const TermChunk &pre, V &v,
                             NodeState &s, const ModLog &log, double ub, double ll,
                             bool is_sing, bool &changed, bool count_int) {
-  for (int k = 0; k < nt; ++k) {
-    const double c = t[k].a;
-    const int j = t[k].j;
+  for_terms(base, nt, pre, [&](const Term1 &t) {
+    const double c = t.a;
+    const int j = t.j;
     double vlb = v.L(j), vub = v.U(j);
     if (c > kETol && (!is_sing || vlb <= -kInfty)) {
       if (vlb <= -kInfty) vlb = 0.;
@@ -182,10 +258,10 @@ __device__ void upd_from_ub(const DevLP &lp, const Term *t, int nt, const NodeVi
       if (nub < vub - kETol) {
         const double cur_lb = v.L(j);
         if (nub < cur_lb + kETol) nub = cur_lb;
-        change_bflag(lp, v, j);
+        v.change_bflag(t);
         v.U(j) = nub;
         log.push(s, j, 1, nub);
-        if (count_int && is_int_type(lp.vtype[j])) s.nintmods++;
+        if (count_int && t.isint) s.nintmods++;
         changed = true;
       }
     } else if (c < -kETol && (!is_sing || vub >= kInfty)) {
@@ -194,46 +270,44 @@ __device__ void upd_from_ub(const DevLP &lp, const Term *t, int nt, const NodeVi
       if (nlb > vlb + kETol) {
         const double cur_ub = v.U(j);
         if (nlb > cur_ub - kETol) nlb = cur_ub;
-        change_bflag(lp, v, j);
+        v.change_bflag(t);
         v.L(j) = nlb;
         log.push(s, j, 0, nlb);
-        if (count_int && is_int_type(lp.vtype[j])) s.nintmods++;
+        if (count_int && t.isint) s.nintmods++;
         changed = true;
       }
     }
-  }
+  });
 }
 
 // linBndTighten_ in node mode (LinearHandler.cpp:952-1045).  Returns true if
 // the row proves the node infeasible.
-__device__ bool lin_bnd_tighten(const DevLP &lp, int r, const NodeView &v, NodeState &s,
-                                const ModLog &log, bool &changed) {
-  const int k0 = lp.rowptr[r];
-  const int nt = lp.rowptr[r + 1] - k0;
-  const Term *t = lp.terms + k0;
-  const double lb = lp.rlo[r], ub = lp.rhi[r];
+template <class V>
+__device__ bool lin_bnd_tighten(const TermRec *base, int nt, const TermChunk &pre, double lb,
+                                double ub, V &v, NodeState &s, const ModLog &log,
+                                bool &changed) {
   double ll, uu, sing_ll = -INFINITY, sing_uu = INFINITY;
   changed = false;
-  lf_bnds(t, nt, v, ll, uu);
-  if (ll < -kInfty || uu > kInfty) sing_lf_bnds(t, nt, v, sing_ll, sing_uu);
+  lf_bnds(base, nt, pre, v, ll, uu);
+  if (ll < -kInfty || uu > kInfty) sing_lf_bnds(base, nt, pre, v, sing_ll, sing_uu);
   if (ll > ub + kETol) return true;
   if (uu < lb - kETol) return true;
   if (lb > -kInfty) {
     if (uu < kInfty) {
-      upd_from_lb(lp, t, nt, v, s, log, lb, uu, false, changed, true);
+      upd_from_lb(base, nt, pre, v, s, log, lb, uu, false, changed, true);
     } else if (sing_uu < kInfty) {
-      upd_from_lb(lp, t, nt, v, s, log, lb, sing_uu, true, changed, true);
+      upd_from_lb(base, nt, pre, v, s, log, lb, sing_uu, true, changed, true);
     }
   }
   if (changed) {
-    lf_bnds(t, nt, v, ll, uu);
-    if (ll < -kInfty || uu > kInfty) sing_lf_bnds(t, nt, v, sing_ll, sing_uu);
+    lf_bnds(base, nt, pre, v, ll, uu);
+    if (ll < -kInfty || uu > kInfty) sing_lf_bnds(base, nt, pre, v, sing_ll, sing_uu);
   }
   if (ub < kInfty) {
     if (ll > -kInfty) {
-      upd_from_ub(lp, t, nt, v, s, log, ub, ll, false, changed, true);
+      upd_from_ub(base, nt, pre, v, s, log, ub, ll, false, changed, true);
     } else if (sing_ll > -kInfty) {
-      upd_from_ub(lp, t, nt, v, s, log, ub, sing_ll, true, changed, true);
+      upd_from_ub(base, nt, pre, v, s, log, ub, sing_ll, true, changed, true);
     }
   }
   return false;
@@ -242,58 +316,68 @@ __device__ bool lin_bnd_tighten(const DevLP &lp, int r, const NodeView &v, NodeS
 // varBndsFromObj_ (LinearHandler.cpp:544-597).  The reference loops until no
 // change; the 100000 cap is a safety net never reached on real data (the
 // oracle uses the same cap).
-__device__ void bnds_from_obj(const DevLP &lp, const NodeView &v, NodeState &s,
+template <class V>
+__device__ void bnds_from_obj(const DevLP &lp, const TermChunk &pre, V &v, NodeState &s,
                               const ModLog &log, double ub, bool &changed) {
   bool tch = true;
   long guard = 0;
   while (tch) {
     double ll, uu, sing_ll = INFINITY, sing_uu = INFINITY;
     tch = false;
-    lf_bnds(lp.obj, lp.nobj, v, ll, uu);
-    if (ll < -kInfty || uu > kInfty) sing_lf_bnds(lp.obj, lp.nobj, v, sing_ll, sing_uu);
+    lf_bnds(lp.orec, lp.nobj, pre, v, ll, uu);
+    if (ll < -kInfty || uu > kInfty) sing_lf_bnds(lp.orec, lp.nobj, pre, v, sing_ll, sing_uu);
     if (ll > ub + kETol) return;  // SolvedInfeasible, ignored by the caller
     if (ll > -kInfty) {
-      upd_from_ub(lp, lp.obj, lp.nobj, v, s, log, ub, ll, false, tch, false);
+      upd_from_ub(lp.orec, lp.nobj, pre, v, s, log, ub, ll, false, tch, false);
     } else if (sing_ll > -kInfty) {
-      upd_from_ub(lp, lp.obj, lp.nobj, v, s, log, ub, sing_ll, true, tch, false);
+      upd_from_ub(lp.orec, lp.nobj, pre, v, s, log, ub, sing_ll, true, tch, false);
     }
     if (tch) changed = true;
     if (++guard > 100000L) break;
   }
 }
 
-// tightenInts_ in node mode (LinearHandler.cpp:415-490).
-__device__ void tighten_ints(const DevLP &lp, const NodeView &v, NodeState &s,
-                             const ModLog &log, bool &changed) {
-  for (int j = 0; j < lp.n; ++j) {
-    if (!is_int_type(lp.vtype[j])) continue;
-    const double l = v.L(j), u = v.U(j);
-    if (l > -kInfty && fabs(l - floor(l + 0.5)) > kIntTol) {
-      const double nv = ceil(l);
-      change_bflag(lp, v, j);
-      v.L(j) = nv;
-      log.push(s, j, 0, nv);
-      changed = true;
-    }
-    if (u < kInfty && fabs(u - floor(u + 0.5)) > kIntTol) {
-      const double nv = floor(u);
-      v.U(j) = nv;
-      change_bflag(lp, v, j);
-      log.push(s, j, 1, nv);
-      changed = true;
+// tightenInts_ in node mode (LinearHandler.cpp:415-490), over the list of
+// Binary/Integer columns in ascending order.
+template <class V>
+__device__ void tighten_ints(const DevLP &lp, V &v, NodeState &s, const ModLog &log,
+                             bool act, bool &changed) {
+  // called with the full wave active: `act` predicates this lane's updates
+  for (int c0 = 0; c0 < lp.nint; c0 += kLanes) {
+    const int cnt = lp.nint - c0 < kLanes ? lp.nint - c0 : kLanes;
+    const TermChunk ch = load_terms(lp.irec + c0, cnt, v.lane);
+#pragma unroll 2
+    for (int k = 0; k < cnt; ++k) {
+      const Term1 t{0.0, rlu64(ch.cmask, k), rl(ch.j, k), rl(ch.cs, k), rl(ch.ce, k), 1};
+      const int j = t.j;
+      const double l = v.L(j), u = v.U(j);
+      if (act && l > -kInfty && fabs(l - floor(l + 0.5)) > kIntTol) {
+        const double nv = ceil(l);
+        v.change_bflag(t);
+        v.L(j) = nv;
+        log.push(s, j, 0, nv);
+        changed = true;
+      }
+      if (act && u < kInfty && fabs(u - floor(u + 0.5)) > kIntTol) {
+        const double nv = floor(u);
+        v.U(j) = nv;
+        v.change_bflag(t);
+        log.push(s, j, 1, nv);
+        changed = true;
+      }
     }
   }
 }
 
-// checkBounds_ (LinearHandler.cpp:328-359).
-__device__ bool check_bounds(const DevLP &lp, const NodeView &v) {
-  for (int j = 0; j < lp.n; ++j) {
-    if (v.L(j) > v.U(j) + kETol) return true;
-  }
-  return lp.cons_bad != 0;
+// checkBounds_ (LinearHandler.cpp:328-359); branch-free over the columns.
+template <class V>
+__device__ bool check_bounds(const DevLP &lp, const V &v) {
+  bool bad = false;
+  for (int j = 0; j < lp.n; ++j) bad |= v.L(j) > v.U(j) + kETol;
+  return bad || lp.cons_bad != 0;
 }
 
-template <bool kLds>
+template <bool kLds, bool kBitFlags>
 __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x;
@@ -301,8 +385,10 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   const int nb = min(kLanes, io.batch - b0);
   const int n = lp.n, m = lp.m;
 
-  NodeView v;
+  NodeView<kBitFlags> v;
   v.lane = lane;
+  v.rowidx = lp.rowidx;
+  v.bits = 0ull;
   if constexpr (kLds) {
     v.stride = kLdsStride;
     v.lb = lds;
@@ -326,7 +412,11 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
     }
   }
   // simplePresolve: every constraint's BFlag set (LinearHandler.cpp:1618-1622)
-  for (int r = 0; r < m; ++r) v.F(r) = 1;
+  if constexpr (kBitFlags) {
+    v.bits = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+  } else {
+    for (int r = 0; r < m; ++r) v.flag[r * kLanes + lane] = 1;
+  }
   __syncthreads();
 
   const bool live = lane < nb;
@@ -342,6 +432,8 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   // simplePresolve sweep loop (LinearHandler.cpp:1624-1644).  The status
   // returns of varBndsFromCons_/varBndsFromObj_ are ignored (:1630, :1637);
   // only checkBounds_ ends the loop as infeasible.
+  // objective terms for varBndsFromObj_, loaded once with the full wave
+  const TermChunk opre = load_terms(lp.orec, lp.nobj < kLanes ? lp.nobj : kLanes, lane);
   bool changed = live;
   bool infeas = false;
   unsigned iters = 1;
@@ -356,24 +448,32 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
     // varBndsFromCons_: one pass over the rows in index order; a row that
     // proves infeasibility ends this lane's pass (early return, :527-529).
     bool cons_on = go;
-    for (int r = 0; r < m; ++r) {
-      const bool mine = cons_on && v.F(r) != 0;
-      if (!__any(mine)) continue;
-      if (mine) {
-        bool tch;
-        v.F(r) = 0;
-        if (lin_bnd_tighten(lp, r, v, s, log, tch)) {
-          cons_on = false;
-        } else if (tch) {
-          changed = true;
+    for (int r0 = 0; r0 < m; r0 += kLanes) {
+      const int rcnt = m - r0 < kLanes ? m - r0 : kLanes;
+      RowRec rr{0.0, 0.0, 0, 0, 0, 0};
+      if (lane < rcnt) rr = lp.rows[r0 + lane];
+      for (int q = 0; q < rcnt; ++q) {
+        const int r = r0 + q;
+        const bool mine = cons_on && v.flagged(r);
+        if (!__any(mine)) continue;
+        // full wave active here: load the row's first 64 terms for broadcast
+        const int k0 = rl(rr.k0, q), nt = rl(rr.nt, q);
+        const TermChunk pre = load_terms(lp.trec + k0, nt < kLanes ? nt : kLanes, lane);
+        if (mine) {
+          const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
+          bool tch;
+          v.clear(r);
+          if (lin_bnd_tighten(lp.trec + k0, nt, pre, rlo, rhi, v, s, log, tch)) {
+            cons_on = false;
+          } else if (tch) {
+            changed = true;
+          }
         }
       }
     }
-    if (go && io.has_inc && lp.nobj > 0) bnds_from_obj(lp, v, s, log, io.inc_ub, changed);
-    if (go) {
-      tighten_ints(lp, v, s, log, changed);
-      infeas = check_bounds(lp, v);
-    }
+    if (go && io.has_inc && lp.nobj > 0) bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
+    tighten_ints(lp, v, s, log, go, changed);
+    if (go) infeas = check_bounds(lp, v);
   }
   if (live) {
     io.infeas[b0 + lane] = infeas ? 1 : 0;
@@ -390,36 +490,44 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   }
 }
 
-}  // namespace
-
-size_t fbbt_lds_bytes(int n, int m) {
-  return (size_t)2 * n * kLdsStride * sizeof(double) + (size_t)m * kLanes;
-}
-
-hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
-                              hipStream_t stream) {
-  if (io.batch <= 0) return hipSuccess;
+template <bool kLds, bool kBits>
+hipError_t launch_variant(const DevLP &lp, const FbbtIO &io, size_t lds, hipStream_t stream) {
   const int waves = (io.batch + kLanes - 1) / kLanes;
-  const size_t lds = fbbt_lds_bytes(lp.n, lp.m);
-  const bool use_lds = variant == 1 || (variant == 0 && lds <= 160 * 1024);
-  if (use_lds) {
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if constexpr (kLds) {
     static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted in
     if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute((const void *)fbbt_linear_kernel<true>,
+      hipError_t e = hipFuncSetAttribute((const void *)fbbt_linear_kernel<kLds, kBits>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024);
       if (e != hipSuccess) return e;
       attr_set = true;
     }
-    hipLaunchKernelGGL(fbbt_linear_kernel<true>, dim3(waves), dim3(kLanes), lds, stream,
-                       lp, io);
-  } else {
-    if (io.scratch == nullptr || io.flag_scratch == nullptr) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(fbbt_linear_kernel<false>, dim3(waves), dim3(kLanes), 0, stream,
-                       lp, io);
   }
+  hipLaunchKernelGGL((fbbt_linear_kernel<kLds, kBits>), dim3(waves), dim3(kLanes),
+                     kLds ? lds : 0, stream, lp, io);
   return hipGetLastError();
+}
+
+}  // namespace
+
+size_t fbbt_lds_bytes(int n, int m) {
+  return (size_t)2 * n * kLdsStride * sizeof(double) + (m > 64 ? (size_t)m * kLanes : 0);
+}
+
+hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
+                              hipStream_t stream) {
+  if (io.batch <= 0) return hipSuccess;
+  const size_t lds = fbbt_lds_bytes(lp.n, lp.m);
+  const bool use_lds = variant == 1 || (variant == 0 && lds <= 160 * 1024);
+  const bool bits = lp.m <= 64;
+  if (use_lds) {
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    return bits ? launch_variant<true, true>(lp, io, lds, stream)
+                : launch_variant<true, false>(lp, io, lds, stream);
+  }
+  if (io.scratch == nullptr || (!bits && io.flag_scratch == nullptr)) return hipErrorInvalidValue;
+  return bits ? launch_variant<false, true>(lp, io, 0, stream)
+              : launch_variant<false, false>(lp, io, 0, stream);
 }
 
 }  // namespace mgpu

@@ -24,6 +24,23 @@ struct alignas(16) Term {
   int32_t pad;
 };
 
+// Wave-uniform row/term records for the FBBT kernel.  A wave loads up to 64
+// of them with ONE coalesced vector load (lane t holds record t) and
+// broadcasts record k with v_readlane into SGPRs: no scalar-memory loads in
+// the inner loops (SMEM and LDS share lgkmcnt, so mixing them serialises).
+struct alignas(16) RowRec {   // 32 B
+  double lo, hi;              // row bounds
+  int32_t k0, nt;             // first term, term count
+  int32_t pad0, pad1;
+};
+struct alignas(16) TermRec {  // 32 B
+  double a;                   // coefficient (0 for the integer-column list)
+  uint64_t cmask;             // rows holding column j (bitmask, m <= 64)
+  int32_t j;                  // column
+  int32_t cs, ce;             // CSC range of column j (m > 64)
+  int32_t isint;              // column is Binary/Integer
+};
+
 // Batch-shared linear relaxation, resident in HBM after mgpu_load_lp.
 struct DevLP {
   int n, m, nnz, nobj;
@@ -38,6 +55,11 @@ struct DevLP {
   const double *collb, *colub;  // [n] root box
   const double *objd;           // [n] dense objective
   double objoff;
+  const RowRec *rows;           // [m]
+  const TermRec *trec;          // [nnz] row terms
+  const TermRec *orec;          // [nobj] objective terms
+  const TermRec *irec;          // [nint] integer columns (tightenInts_)
+  int nint;
 };
 
 // Output/optional mod-log arguments of one FBBT launch.

@@ -51,6 +51,7 @@ struct mgpu_ctx {
   DevLP lp{};
   // problem storage
   DevBuf rowptr, terms, rlo, rhi, colptr, rowidx, vtype, obj, collb, colub, objd;
+  DevBuf rows, trec, orec, irec;
   std::vector<Term> h_terms;
   // workspaces
   DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_inf, io_nmods, io_mv, io_ml, io_mval;
@@ -118,7 +119,8 @@ int mgpu_destroy(mgpu_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->rowptr, &c->terms, &c->rlo, &c->rhi, &c->colptr, &c->rowidx,
-                    &c->vtype, &c->obj, &c->collb, &c->colub, &c->objd, &c->io_lb_in,
+                    &c->vtype, &c->obj, &c->collb, &c->colub, &c->objd, &c->rows,
+                    &c->trec, &c->orec, &c->irec, &c->io_lb_in,
                     &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
                     &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch})
     b->release();
@@ -187,6 +189,31 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   int cons_bad = 0;
   for (int i = 0; i < m; ++i)
     if (rowlb[i] > rowub[i] + kETol) cons_bad = 1;
+  // wave-uniform records for the FBBT kernel
+  std::vector<uint64_t> cmask(n, 0ull);
+  if (m <= 64)
+    for (int i = 0; i < m; ++i)
+      for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) cmask[colidx[k]] |= 1ull << i;
+  auto mkrec = [&](double a, int j) {
+    TermRec r;
+    r.a = a;
+    r.cmask = cmask[j];
+    r.j = j;
+    r.cs = colptr[j];
+    r.ce = colptr[j + 1];
+    r.isint = (vt[j] == kBinary || vt[j] == kInteger) ? 1 : 0;
+    return r;
+  };
+  std::vector<RowRec> rrec(m > 0 ? m : 1);
+  for (int i = 0; i < m; ++i) rrec[i] = RowRec{rowlb[i], rowub[i], rowptr[i], rowptr[i + 1] - rowptr[i], 0, 0};
+  std::vector<TermRec> trec(nnz > 0 ? nnz : 1), orec, irec;
+  for (int i = 0; i < m; ++i)
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) trec[k] = mkrec(val[k], colidx[k]);
+  for (const Term &t : objt) orec.push_back(mkrec(t.a, t.j));
+  for (int j = 0; j < n; ++j)
+    if (vt[j] == kBinary || vt[j] == kInteger) irec.push_back(mkrec(0.0, j));
+  if (orec.empty()) orec.push_back(TermRec{});
+  if (irec.empty()) irec.push_back(TermRec{});
 
   HIPCHK(c, upload(c->rowptr, rowptr, (size_t)m + 1));
   HIPCHK(c, upload(c->terms, c->h_terms.data(), (size_t)(nnz > 0 ? nnz : 1)));
@@ -200,6 +227,10 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   HIPCHK(c, upload(c->collb, collb, (size_t)n));
   HIPCHK(c, upload(c->colub, colub, (size_t)n));
   HIPCHK(c, upload(c->objd, obj, (size_t)n));
+  HIPCHK(c, upload(c->rows, rrec.data(), rrec.size()));
+  HIPCHK(c, upload(c->trec, trec.data(), trec.size()));
+  HIPCHK(c, upload(c->orec, orec.data(), orec.size()));
+  HIPCHK(c, upload(c->irec, irec.data(), irec.size()));
 
   DevLP &lp = c->lp;
   lp.n = n;
@@ -219,6 +250,12 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   lp.colub = c->colub.as<double>();
   lp.objd = c->objd.as<double>();
   lp.objoff = objoff;
+  lp.rows = c->rows.as<RowRec>();
+  lp.trec = c->trec.as<TermRec>();
+  lp.orec = c->orec.as<TermRec>();
+  lp.irec = c->irec.as<TermRec>();
+  lp.nint = 0;
+  for (int j = 0; j < n; ++j) lp.nint += (vt[j] == kBinary || vt[j] == kInteger) ? 1 : 0;
   c->loaded = true;
   return MGPU_OK;
 }
@@ -275,6 +312,7 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   if (c->fbbt_variant == 2 || (c->fbbt_variant == 0 && !fits)) {
     HIPCHK(c, c->scratch.ensure((size_t)waves * 2 * c->lp.n * kLanes * sizeof(double)));
     HIPCHK(c, c->flag_scratch.ensure((size_t)waves * (c->lp.m > 0 ? c->lp.m : 1) * kLanes));
+    // (byte flags are only used when m > 64; bit flags live in VGPRs)
     io.scratch = c->scratch.as<double>();
     io.flag_scratch = c->flag_scratch.as<uint8_t>();
   } else if (c->fbbt_variant == 1 && !fits) {

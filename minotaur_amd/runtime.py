@@ -40,6 +40,13 @@ def load_library():
     if not os.path.exists(LIB_PATH):
         raise MgpuError(f"{LIB_PATH} not built: run __graft_entry__.build() "
                         "(there is no CPU fallback)")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7.  If
+    # torch is importable, load it first so libmgpu.so binds to that same
+    # runtime (same soname) and device pointers / streams are shared.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     lib.mgpu_create.argtypes = [_I, ctypes.POINTER(_P)]
     lib.mgpu_destroy.argtypes = [_P]
