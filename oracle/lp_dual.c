@@ -1,0 +1,489 @@
+/*
+ * ORACLE / CPU BASELINE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Bounded dual simplex with an explicit dense basis inverse: the CPU
+ * restatement of what OsiLPEngine::solve asks Clp for
+ * (src/interfaces/OsiLPEngine.cpp:571-652: resolve() = dual simplex from the
+ * loaded warm basis, OsiDoDualInResolve hint :579-583, iteration limit
+ * :561-569, status map :592-627).  Clp 1.17.9 itself is not vendored and
+ * cannot be built here; this file restates the published
+ * algorithm (textbook bounded dual simplex with Dantzig pricing, Harris
+ * two-pass ratio test and artificial bounds for free columns), the same
+ * algorithm the HIP kernel K3 runs.  Objective/status parity is pinned
+ * against scipy's HiGHS and the AMPLOsiUT known answers
+ * (src/testing/AMPLOsiUT.cpp:46-120).
+ *
+ * Problem: min c'x  s.t.  rlo <= A x <= rhi,  lb <= x <= ub.
+ * Internally [A  -I] z = 0 with z = (x, r), r the row activities, so the
+ * slack basis is B = -I.  Columns n..n+m-1 are the logicals.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+#define P_TOL 1e-7      /* primal feasibility (Clp default primal tolerance) */
+#define D_TOL 1e-7      /* dual feasibility   (Clp default dual tolerance)   */
+#define PIV_TOL 1e-9    /* smallest acceptable |alpha_rq| in the ratio test  */
+#define ART_BOUND 1e7   /* first artificial box for free / half-free columns */
+#define INF_B 1e30
+
+enum { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
+
+typedef struct {
+  const orc_lp *P;
+  int N;               /* n + m */
+  const double *lb, *ub;  /* structural node box */
+  double *blo, *bhi;   /* working bounds of all N columns (may be artificial) */
+  unsigned char *art;  /* 1 if the current bound of column j is artificial */
+  double *z, *d;       /* values and reduced costs of all N columns */
+  double *binv;        /* m x m row-major */
+  int *head;           /* basic column of each row */
+  signed char *st;
+  double *rho, *alpha_r, *alpha_q, *w;
+} lpw;
+
+static double bnd_lo(const orc_lp *P, const double *lb, int j) {
+  return j < P->n ? lb[j] : P->rlo[j - P->n];
+}
+static double bnd_hi(const orc_lp *P, const double *ub, int j) {
+  return j < P->n ? ub[j] : P->rhi[j - P->n];
+}
+
+/* alpha_r[j] = rho' a_j for column j of [A -I]. */
+static double col_dot(const orc_lp *P, const double *v, int j) {
+  if (j >= P->n) return -v[j - P->n];
+  double s = 0.0;
+  for (int k = P->colptr[j]; k < P->colptr[j + 1]; ++k) s += P->cval[k] * v[P->rowidx[k]];
+  return s;
+}
+
+/* out = B^{-1} a_j */
+static void ftran_col(const lpw *W, int j, double *out) {
+  const orc_lp *P = W->P;
+  int m = P->m;
+  if (j >= P->n) {
+    int i0 = j - P->n;
+    for (int i = 0; i < m; ++i) out[i] = -W->binv[i * m + i0];
+    return;
+  }
+  for (int i = 0; i < m; ++i) out[i] = 0.0;
+  for (int k = P->colptr[j]; k < P->colptr[j + 1]; ++k) {
+    int r = P->rowidx[k];
+    double a = P->cval[k];
+    for (int i = 0; i < m; ++i) out[i] += W->binv[i * m + r] * a;
+  }
+}
+
+/* Artificial bounds of a column whose true bound is infinite: a box of
+ * half-width art_bound anchored at the finite side (or at 0). */
+static double art_lo(double tlo_, double thi_, double art_bound) {
+  (void) tlo_;
+  return (thi_ < INF_B ? thi_ : 0.0) - art_bound;
+}
+static double art_hi(double tlo_, double thi_, double art_bound) {
+  (void) thi_;
+  return (tlo_ > -INF_B ? tlo_ : 0.0) + art_bound;
+}
+
+/* Choose the status of a nonbasic column from its reduced cost so the basis
+ * is dual feasible; use an artificial bound when the needed side is
+ * infinite. */
+static void place_nonbasic(lpw *W, int j, double art_bound) {
+  double lo = W->blo[j], hi = W->bhi[j], dj = W->d[j];
+  int lo_f = lo > -INF_B, hi_f = hi < INF_B;
+  if (lo_f && hi_f && lo == hi) { W->st[j] = ST_LB; W->z[j] = lo; return; }
+  if (dj > D_TOL) {
+    if (!lo_f) { W->blo[j] = art_lo(lo, hi, art_bound); W->art[j] |= 1; }
+    W->st[j] = ST_LB; W->z[j] = W->blo[j];
+  } else if (dj < -D_TOL) {
+    if (!hi_f) { W->bhi[j] = art_hi(lo, hi, art_bound); W->art[j] |= 2; }
+    W->st[j] = ST_UB; W->z[j] = W->bhi[j];
+  } else {
+    if (lo_f) { W->st[j] = ST_LB; W->z[j] = lo; }
+    else if (hi_f) { W->st[j] = ST_UB; W->z[j] = hi; }
+    else { W->st[j] = ST_FREE; W->z[j] = 0.0; }
+  }
+}
+
+/* Widen every artificial bound to the new half-width (nonbasic columns keep
+ * their status and move with their bound). */
+static void grow_art(lpw *W, double art_bound) {
+  for (int j = 0; j < W->N; ++j) {
+    if (!W->art[j] || W->st[j] == ST_BASIC) continue;
+    double tl = bnd_lo(W->P, W->lb, j), th = bnd_hi(W->P, W->ub, j);
+    if (W->art[j] & 1) W->blo[j] = art_lo(tl, th, art_bound);
+    if (W->art[j] & 2) W->bhi[j] = art_hi(tl, th, art_bound);
+    if (W->st[j] == ST_LB) W->z[j] = W->blo[j];
+    if (W->st[j] == ST_UB) W->z[j] = W->bhi[j];
+  }
+}
+
+static void compute_duals(lpw *W) {
+  const orc_lp *P = W->P;
+  int m = P->m, N = W->N;
+  /* y = c_B' B^{-1}; reuse rho as y */
+  double *y = W->rho;
+  for (int k = 0; k < m; ++k) y[k] = 0.0;
+  for (int i = 0; i < m; ++i) {
+    int h = W->head[i];
+    double cb = h < P->n ? P->c[h] : 0.0;
+    if (cb != 0.0)
+      for (int k = 0; k < m; ++k) y[k] += cb * W->binv[i * m + k];
+  }
+  for (int j = 0; j < N; ++j) {
+    if (W->st[j] == ST_BASIC) { W->d[j] = 0.0; continue; }
+    double cj = j < P->n ? P->c[j] : 0.0;
+    W->d[j] = cj - col_dot(P, y, j);
+  }
+}
+
+static void compute_primals(lpw *W) {
+  const orc_lp *P = W->P;
+  int m = P->m, N = W->N;
+  double *w = W->w;
+  for (int i = 0; i < m; ++i) w[i] = 0.0;
+  for (int j = 0; j < N; ++j) {
+    if (W->st[j] == ST_BASIC) continue;
+    double zj = W->z[j];
+    if (zj == 0.0) continue;
+    if (j >= P->n) {
+      w[j - P->n] -= zj;
+    } else {
+      for (int k = P->colptr[j]; k < P->colptr[j + 1]; ++k) w[P->rowidx[k]] += P->cval[k] * zj;
+    }
+  }
+  for (int i = 0; i < m; ++i) {
+    double s = 0.0;
+    for (int k = 0; k < m; ++k) s += W->binv[i * m + k] * w[k];
+    W->z[W->head[i]] = -s;
+  }
+}
+
+/* Gauss-Jordan inverse of the basis matrix (used when no inverse is
+ * supplied with a warm basis).  Returns 0 if singular. */
+static int invert_basis(lpw *W) {
+  const orc_lp *P = W->P;
+  int m = P->m;
+  double *Bm = (double *) calloc((size_t) m * m, sizeof(double));
+  double *I = W->binv;
+  for (int i = 0; i < m; ++i) {
+    int h = W->head[i];
+    if (h >= P->n) {
+      Bm[(h - P->n) * m + i] = -1.0;
+    } else {
+      for (int k = P->colptr[h]; k < P->colptr[h + 1]; ++k) Bm[P->rowidx[k] * m + i] = P->cval[k];
+    }
+  }
+  for (int i = 0; i < m * m; ++i) I[i] = 0.0;
+  for (int i = 0; i < m; ++i) I[i * m + i] = 1.0;
+  for (int c = 0; c < m; ++c) {
+    int piv = -1;
+    double best = 0.0;
+    for (int r = c; r < m; ++r)
+      if (fabs(Bm[r * m + c]) > best) { best = fabs(Bm[r * m + c]); piv = r; }
+    if (piv < 0 || best < 1e-12) { free(Bm); return 0; }
+    if (piv != c) {
+      for (int k = 0; k < m; ++k) {
+        double t = Bm[c * m + k]; Bm[c * m + k] = Bm[piv * m + k]; Bm[piv * m + k] = t;
+        t = I[c * m + k]; I[c * m + k] = I[piv * m + k]; I[piv * m + k] = t;
+      }
+    }
+    double inv = 1.0 / Bm[c * m + c];
+    for (int k = 0; k < m; ++k) { Bm[c * m + k] *= inv; I[c * m + k] *= inv; }
+    for (int r = 0; r < m; ++r) {
+      if (r == c) continue;
+      double f = Bm[r * m + c];
+      if (f == 0.0) continue;
+      for (int k = 0; k < m; ++k) { Bm[r * m + k] -= f * Bm[c * m + k]; I[r * m + k] -= f * I[c * m + k]; }
+    }
+  }
+  free(Bm);
+  /* rows of B^{-1} are indexed by basis position: B^{-1} = (B)^-1 where
+   * column i of B is the column of head[i]; I now holds B^{-1} with row i
+   * <-> basis position i. */
+  return 1;
+}
+
+/*
+ * Solve one LP.  ws_head/ws_st/ws_binv: warm start in/out (NULL = slack
+ * basis).  Returns an EngineStatus numeric (Types.h:152-166).
+ */
+int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
+                     int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
+                     int have_ws, int have_binv, int iter_limit, double *obj_out,
+                     double *x_out, double *y_out, int *iters_out)
+{
+  int n = P->n, m = P->m, N = n + m;
+  lpw W;
+  int status = 12, iters = 0, fresh = 1;
+  double art_bound = ART_BOUND;
+  memset(&W, 0, sizeof W);
+  W.P = P; W.N = N; W.lb = lb; W.ub = ub;
+  W.blo = (double *) malloc(sizeof(double) * N);
+  W.bhi = (double *) malloc(sizeof(double) * N);
+  W.art = (unsigned char *) calloc((size_t) N, 1);
+  W.z = (double *) calloc((size_t) N, sizeof(double));
+  W.d = (double *) calloc((size_t) N, sizeof(double));
+  W.binv = (double *) malloc(sizeof(double) * (size_t) m * m + 8);
+  W.head = (int *) malloc(sizeof(int) * (size_t) m + 4);
+  W.st = (signed char *) malloc((size_t) N);
+  W.rho = (double *) malloc(sizeof(double) * (size_t) m + 8);
+  W.w = (double *) malloc(sizeof(double) * (size_t) m + 8);
+  W.alpha_r = (double *) malloc(sizeof(double) * (size_t) N);
+  W.alpha_q = (double *) malloc(sizeof(double) * (size_t) m + 8);
+
+  for (int j = 0; j < N; ++j) {
+    W.blo[j] = bnd_lo(P, lb, j);
+    W.bhi[j] = bnd_hi(P, ub, j);
+    if (W.blo[j] < -INF_B) W.blo[j] = -INFINITY;
+    if (W.bhi[j] > INF_B) W.bhi[j] = INFINITY;
+  }
+  /* quick primal-infeasibility check of the box itself */
+  for (int j = 0; j < N; ++j) {
+    if (W.blo[j] > W.bhi[j] + P_TOL) { status = 2; goto done; }
+  }
+  if (have_ws) {
+    memcpy(W.head, ws_head, sizeof(int) * (size_t) m);
+    for (int j = 0; j < N; ++j) W.st[j] = ST_LB;
+    for (int i = 0; i < m; ++i) W.st[W.head[i]] = ST_BASIC;
+    for (int j = 0; j < N; ++j) if (W.st[j] != ST_BASIC) W.st[j] = ws_st[j] == ST_BASIC ? ST_LB : ws_st[j];
+    if (have_binv) {
+      memcpy(W.binv, ws_binv, sizeof(double) * (size_t) m * m);
+    } else if (!invert_basis(&W)) {
+      have_ws = 0;
+    }
+  }
+  if (!have_ws) {
+    for (int i = 0; i < m; ++i) W.head[i] = n + i;
+    for (int j = 0; j < N; ++j) W.st[j] = ST_LB;
+    for (int i = 0; i < m; ++i) W.st[n + i] = ST_BASIC;
+    for (int i = 0; i < m * m; ++i) W.binv[i] = 0.0;
+    for (int i = 0; i < m; ++i) W.binv[i * m + i] = -1.0;
+  }
+  if (have_ws && have_binv && ws_d) {
+    /* reduced costs depend only on the basis: reuse the parent's */
+    for (int j = 0; j < N; ++j) W.d[j] = W.st[j] == ST_BASIC ? 0.0 : ws_d[j];
+  } else {
+    compute_duals(&W);
+  }
+  /* nonbasic placement: keep the warm status when dual feasible */
+  for (int j = 0; j < N; ++j) {
+    if (W.st[j] == ST_BASIC) continue;
+    double lo = W.blo[j], hi = W.bhi[j], dj = W.d[j];
+    int keep = 0;
+    if (have_ws) {
+      if (W.st[j] == ST_LB && lo > -INF_B && dj >= -D_TOL) { W.z[j] = lo; keep = 1; }
+      else if (W.st[j] == ST_UB && hi < INF_B && dj <= D_TOL) { W.z[j] = hi; keep = 1; }
+      else if (lo == hi && lo > -INF_B) { W.st[j] = ST_LB; W.z[j] = lo; keep = 1; }
+    }
+    if (!keep) place_nonbasic(&W, j, art_bound);
+  }
+  compute_primals(&W);
+
+  for (;;) {
+    /* ---- pricing: most infeasible basic row (Dantzig) ---- */
+    int r = -1;
+    double best = 0.0, delta = 0.0;
+    for (int i = 0; i < m; ++i) {
+      int h = W.head[i];
+      double v = W.z[h], inf = 0.0;
+      if (v < W.blo[h] - P_TOL) inf = v - W.blo[h];
+      else if (v > W.bhi[h] + P_TOL) inf = v - W.bhi[h];
+      if (fabs(inf) > best) { best = fabs(inf); r = i; delta = inf; }
+    }
+    if (r < 0 && !fresh) {
+      /* confirm against freshly recomputed primal values */
+      compute_primals(&W);
+      fresh = 1;
+      continue;
+    }
+    if (r < 0) {
+      /* optimal for the (possibly artificially boxed) LP */
+      int grow = 0;
+      for (int j = 0; j < N; ++j) {
+        if (W.st[j] == ST_BASIC || !W.art[j]) continue;
+        if ((W.st[j] == ST_LB && (W.art[j] & 1)) || (W.st[j] == ST_UB && (W.art[j] & 2))) grow = 1;
+      }
+      if (!grow) { status = 0; break; }
+      if (art_bound >= 1e13) { status = 4; break; }   /* ProvenUnbounded */
+      art_bound *= 1e3;
+      grow_art(&W, art_bound);
+      compute_primals(&W);
+      fresh = 1;
+      continue;
+    }
+    if (iters >= iter_limit) { status = 6; break; }   /* EngineIterationLimit */
+    /* ---- row r of B^{-1}, pivot row ---- */
+    for (int k = 0; k < m; ++k) W.rho[k] = W.binv[r * m + k];
+    double sigma = delta > 0 ? 1.0 : -1.0;
+    /* ---- Harris two-pass ratio test ---- */
+    double tmax = INFINITY;
+    for (int j = 0; j < N; ++j) {
+      W.alpha_r[j] = 0.0;
+      if (W.st[j] == ST_BASIC) continue;
+      if (W.blo[j] == W.bhi[j]) continue;             /* fixed: never enters */
+      double a = col_dot(P, W.rho, j);
+      W.alpha_r[j] = a;
+      double at = sigma * a;
+      double dj = W.d[j];
+      if (W.st[j] == ST_LB && at > PIV_TOL) {
+        double t = (fmax(dj, 0.0) + D_TOL) / at;
+        if (t < tmax) tmax = t;
+      } else if (W.st[j] == ST_UB && at < -PIV_TOL) {
+        double t = (fmin(dj, 0.0) - D_TOL) / at;
+        if (t < tmax) tmax = t;
+      } else if (W.st[j] == ST_FREE && fabs(at) > PIV_TOL) {
+        double t = D_TOL / fabs(at);
+        if (t < tmax) tmax = t;
+      }
+    }
+    if (tmax == INFINITY) {                             /* dual unbounded */
+      int boxed = 0;
+      for (int j = 0; j < N; ++j) if (W.st[j] != ST_BASIC && W.art[j]) boxed = 1;
+      if (!boxed || art_bound >= 1e13) { status = 2; break; }
+      art_bound *= 1e3;          /* the artificial box may be what is infeasible */
+      grow_art(&W, art_bound);
+      compute_primals(&W);
+      fresh = 1;
+      continue;
+    }
+    int q = -1;
+    double qa = 0.0;
+    for (int j = 0; j < N; ++j) {
+      if (W.st[j] == ST_BASIC || W.blo[j] == W.bhi[j]) continue;
+      double at = sigma * W.alpha_r[j], dj = W.d[j], t;
+      if (W.st[j] == ST_LB && at > PIV_TOL) t = fmax(dj, 0.0) / at;
+      else if (W.st[j] == ST_UB && at < -PIV_TOL) t = fmin(dj, 0.0) / at;
+      else if (W.st[j] == ST_FREE && fabs(at) > PIV_TOL) t = 0.0;
+      else continue;
+      if (t <= tmax && fabs(at) > qa) { qa = fabs(at); q = j; }
+    }
+    if (q < 0) { status = 2; break; }
+    /* ---- column q, steps ---- */
+    ftran_col(&W, q, W.alpha_q);
+    double arq = W.alpha_q[r];
+    double theta_d = W.d[q] / W.alpha_r[q];
+    /* keep the step sign consistent with the leaving direction */
+    if (sigma * theta_d < 0) theta_d = 0.0;
+    double theta_p = delta / arq;
+    int p = W.head[r];
+    /* duals */
+    for (int j = 0; j < N; ++j) {
+      if (W.st[j] == ST_BASIC) continue;
+      W.d[j] -= theta_d * W.alpha_r[j];
+    }
+    W.d[q] = 0.0;
+    W.d[p] = -theta_d;
+    /* primals */
+    for (int i = 0; i < m; ++i) W.z[W.head[i]] -= theta_p * W.alpha_q[i];
+    double zq = W.z[q] + theta_p;
+    /* leaving variable to its violated bound */
+    if (delta < 0) { W.st[p] = ST_LB; W.z[p] = W.blo[p]; }
+    else { W.st[p] = ST_UB; W.z[p] = W.bhi[p]; }
+    /* basis */
+    W.head[r] = q;
+    W.st[q] = ST_BASIC;
+    W.z[q] = zq;
+    if (W.art[q]) {   /* basic columns keep their true (infinite) bounds */
+      W.blo[q] = bnd_lo(P, lb, q) < -INF_B ? -INFINITY : bnd_lo(P, lb, q);
+      W.bhi[q] = bnd_hi(P, ub, q) > INF_B ? INFINITY : bnd_hi(P, ub, q);
+      W.art[q] = 0;
+    }
+    {
+      double inv = 1.0 / arq;
+      double *br = W.binv + (size_t) r * m;
+      for (int k = 0; k < m; ++k) br[k] *= inv;
+      for (int i = 0; i < m; ++i) {
+        if (i == r) continue;
+        double f = W.alpha_q[i];
+        if (f == 0.0) continue;
+        double *bi = W.binv + (size_t) i * m;
+        for (int k = 0; k < m; ++k) bi[k] -= f * br[k];
+      }
+    }
+    ++iters;
+    fresh = 0;
+    /* periodic refresh of primal values against drift */
+    if (iters % 64 == 0) { compute_primals(&W); fresh = 1; }
+  }
+done:
+  if (status == 0 || status == 6) {
+    double obj = 0.0;
+    for (int j = 0; j < n; ++j) obj += P->c[j] * W.z[j];
+    if (obj_out) *obj_out = obj;
+    if (x_out) for (int j = 0; j < n; ++j) x_out[j] = W.z[j];
+    if (y_out) {
+      compute_duals(&W);
+      for (int i = 0; i < m; ++i) y_out[i] = W.rho[i];
+    }
+  } else if (obj_out) {
+    *obj_out = status == 2 ? INFINITY : -INFINITY;
+  }
+  if (ws_head && (status == 0 || status == 6)) {
+    memcpy(ws_head, W.head, sizeof(int) * (size_t) m);
+    if (ws_st) for (int j = 0; j < N; ++j) ws_st[j] = W.st[j];
+    if (ws_binv) memcpy(ws_binv, W.binv, sizeof(double) * (size_t) m * m);
+    if (ws_d) memcpy(ws_d, W.d, sizeof(double) * (size_t) N);
+  }
+  if (iters_out) *iters_out = iters;
+  free(W.blo); free(W.bhi); free(W.art); free(W.z); free(W.d); free(W.binv);
+  free(W.head); free(W.st); free(W.rho); free(W.w); free(W.alpha_r); free(W.alpha_q);
+  return status;
+}
+
+/* Batch entry for ctypes: one LP per node box, optional shared warm start
+ * (head/st/binv of e.g. the root optimum), OpenMP over nodes. */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+int orc_dual_simplex_batch(int n, int m, const int *colptr, const int *rowidx,
+                           const double *cval, const double *c, const double *rlo,
+                           const double *rhi, int B, const double *lb, const double *ub,
+                           const int *ws_head, const signed char *ws_st,
+                           const double *ws_binv, const double *ws_d, int iter_limit, int *status,
+                           double *obj, double *x, int *iters, int nthreads)
+{
+  orc_lp P;
+  P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cval; P.c = c;
+  P.rlo = rlo; P.rhi = rhi;
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+  {
+    int *h = (int *) malloc(sizeof(int) * (size_t) (m + 1));
+    signed char *s = (signed char *) malloc((size_t) (n + m + 1));
+    double *bi = (double *) malloc(sizeof(double) * (size_t) m * m + 8);
+    double *dd = (double *) malloc(sizeof(double) * (size_t) (n + m) + 8);
+#pragma omp for schedule(dynamic, 16)
+    for (int b = 0; b < B; ++b) {
+      int have = ws_head != 0;
+      if (have) {
+        memcpy(h, ws_head, sizeof(int) * (size_t) m);
+        memcpy(s, ws_st, (size_t) (n + m));
+        if (ws_binv) memcpy(bi, ws_binv, sizeof(double) * (size_t) m * m);
+        if (ws_d) memcpy(dd, ws_d, sizeof(double) * (size_t) (n + m));
+      }
+      status[b] = orc_dual_simplex(&P, lb + (size_t) b * n, ub + (size_t) b * n, h, s, bi,
+                                   ws_d ? dd : 0, have, have && ws_binv != 0 && ws_d != 0,
+                                   iter_limit, obj + b, x ? x + (size_t) b * n : 0, 0,
+                                   iters + b);
+    }
+    free(h); free(s); free(bi); free(dd);
+  }
+  return 0;
+}
+
+/* Root solve that also returns the optimal warm start (head, st, binv). */
+int orc_dual_simplex_root(int n, int m, const int *colptr, const int *rowidx,
+                          const double *cval, const double *c, const double *rlo,
+                          const double *rhi, const double *lb, const double *ub,
+                          int iter_limit, int *head, signed char *st, double *binv,
+                          double *dred, double *obj, double *x, double *y, int *iters)
+{
+  orc_lp P;
+  P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cval; P.c = c;
+  P.rlo = rlo; P.rhi = rhi;
+  return orc_dual_simplex(&P, lb, ub, head, st, binv, dred, 0, 0, iter_limit, obj, x, y,
+                          iters);
+}

@@ -40,6 +40,20 @@ int orc_linear_fbbt_batch(const orc_lin_problem *P, int B,
                           unsigned char *flag_scratch, int mod_cap,
                           int *mod_var, int *mod_lu, double *mod_val);
 
+/* LP for the dual simplex restatement: CSC of A. */
+typedef struct {
+  int n, m;
+  const int *colptr, *rowidx;
+  const double *cval;
+  const double *c;
+  const double *rlo, *rhi;
+} orc_lp;
+
+int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
+                     int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
+                     int have_ws, int have_binv, int iter_limit, double *obj_out,
+                     double *x_out, double *y_out, int *iters_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -144,3 +144,115 @@ def ref_linear_fbbt(p, lb, ub, incumbent=None, mod_cap=0):
                               _ptr(olb), _ptr(oub), _ptr(infeas), _ptr(nmods),
                               mod_cap, _ptr(mv), _ptr(ml), _ptr(mval), _ptr(secs))
     return FbbtResult(olb, oub, infeas, nmods, mv, ml, mval, float(secs[0]))
+
+
+# ---------------------------------------------------------------------------
+# LP: bounded dual simplex restatement (liboracle) and scipy HiGHS
+# ---------------------------------------------------------------------------
+def lp_csc(p):
+    """CSC of the constraint matrix (rows ascending inside each column)."""
+    colptr, rowidx = p.csc_pattern()
+    cval = np.empty(p.nnz)
+    fill = colptr[:-1].copy()
+    for i in range(p.m):
+        for k in range(p.rowptr[i], p.rowptr[i + 1]):
+            j = p.colidx[k]
+            cval[fill[j]] = p.val[k]
+            fill[j] += 1
+    return colptr, rowidx, cval
+
+
+class WarmStart:
+    """Optimal basis of an LP: basic column per row, status of every column
+    (0 at lb, 1 at ub, 2 free, 3 basic) and the dense basis inverse."""
+
+    def __init__(self, head, st, binv, d):
+        self.head, self.st, self.binv, self.d = head, st, binv, d
+
+
+def _lp_sig(l):
+    l.orc_dual_simplex_batch.restype = _I
+    l.orc_dual_simplex_batch.argtypes = [_I, _I] + [_P] * 6 + [_I, _P, _P, _P, _P, _P, _P,
+                                         _I, _P, _P, _P, _P, _I]
+    l.orc_dual_simplex_root.restype = _I
+    l.orc_dual_simplex_root.argtypes = [_I, _I] + [_P] * 8 + [_I] + [_P] * 8
+
+
+def dual_simplex(p, LB, UB, ws=None, iter_limit=10000, nthreads=1, want_x=False):
+    """Per-node LP solves; returns (status[B], obj[B] incl. constant, iters[B], x)."""
+    l = lib()
+    _lp_sig(l)
+    LB = np.ascontiguousarray(LB, dtype=np.float64)
+    UB = np.ascontiguousarray(UB, dtype=np.float64)
+    B = LB.shape[0]
+    colptr, rowidx, cval = lp_csc(p)
+    st = np.zeros(B, dtype=np.int32)
+    obj = np.zeros(B)
+    it = np.zeros(B, dtype=np.int32)
+    x = np.zeros((B, p.n)) if want_x else None
+    h = s = bi = dd = None
+    if ws is not None:
+        h = np.ascontiguousarray(ws.head, dtype=np.int32)
+        s = np.ascontiguousarray(ws.st, dtype=np.int8)
+        bi = np.ascontiguousarray(ws.binv, dtype=np.float64)
+        dd = np.ascontiguousarray(ws.d, dtype=np.float64)
+    l.orc_dual_simplex_batch(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj),
+                             _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(h),
+                             _ptr(s), _ptr(bi), _ptr(dd), iter_limit, _ptr(st), _ptr(obj), _ptr(x),
+                             _ptr(it), nthreads)
+    obj = obj + p.obj_const
+    return st, obj, it, x
+
+
+def dual_simplex_root(p, lb=None, ub=None, iter_limit=100000):
+    l = lib()
+    _lp_sig(l)
+    lb = np.ascontiguousarray(p.vlb if lb is None else lb, dtype=np.float64)
+    ub = np.ascontiguousarray(p.vub if ub is None else ub, dtype=np.float64)
+    colptr, rowidx, cval = lp_csc(p)
+    head = np.zeros(p.m, dtype=np.int32)
+    st = np.zeros(p.n + p.m, dtype=np.int8)
+    binv = np.zeros((p.m, p.m))
+    dred = np.zeros(p.n + p.m)
+    obj = np.zeros(1)
+    x = np.zeros(p.n)
+    y = np.zeros(p.m)
+    it = np.zeros(1, dtype=np.int32)
+    status = l.orc_dual_simplex_root(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval),
+                                     _ptr(p.obj), _ptr(p.rlo), _ptr(p.rhi), _ptr(lb), _ptr(ub),
+                                     iter_limit, _ptr(head), _ptr(st), _ptr(binv), _ptr(dred),
+                                     _ptr(obj), _ptr(x), _ptr(y), _ptr(it))
+    return (status, float(obj[0]) + p.obj_const, x, y, int(it[0]),
+            WarmStart(head, st, binv, dred))
+
+
+def highs(p, lb=None, ub=None):
+    """scipy HiGHS: (EngineStatus numeric, objective incl. constant)."""
+    from scipy.optimize import linprog
+    from scipy.sparse import csr_matrix
+    lb = p.vlb if lb is None else lb
+    ub = p.vub if ub is None else ub
+    A = csr_matrix((p.val, p.colidx, p.rowptr), shape=(p.m, p.n))
+    fin_hi = np.isfinite(p.rhi)
+    fin_lo = np.isfinite(p.rlo)
+    eq = fin_hi & fin_lo & (p.rlo == p.rhi)
+    ub_rows = fin_hi & ~eq
+    lo_rows = fin_lo & ~eq
+    import scipy.sparse as sp
+    A_ub = sp.vstack([A[ub_rows], -A[lo_rows]]) if (ub_rows.any() or lo_rows.any()) else None
+    b_ub = np.concatenate([p.rhi[ub_rows], -p.rlo[lo_rows]]) if A_ub is not None else None
+    A_eq = A[eq] if eq.any() else None
+    b_eq = p.rlo[eq] if eq.any() else None
+    bounds = [(None if not np.isfinite(a) else a, None if not np.isfinite(b) else b)
+              for a, b in zip(lb, ub)]
+    if np.any(np.asarray(lb) > np.asarray(ub)):
+        return 2, math.inf
+    r = linprog(p.obj, A_ub=A_ub, b_ub=b_ub, A_eq=A_eq, b_eq=b_eq, bounds=bounds,
+                method='highs')
+    if r.status == 0:
+        return 0, float(r.fun) + p.obj_const
+    if r.status == 2:
+        return 2, math.inf
+    if r.status == 3:
+        return 4, -math.inf
+    return 12, math.nan
