@@ -100,6 +100,38 @@ int mgpu_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in,
                   int mod_cap, int32_t *d_mod_var, int32_t *d_mod_lu,
                   double *d_mod_val);
 
+/* Batched LP relaxation solves: for every node box b, what
+ * OsiLPEngine::solve (OsiLPEngine.cpp:571-652) returns for the loaded rows
+ * with that box — a bounded dual simplex from the warm basis.
+ *   skip        : [batch] or NULL; nonzero = node already pruned (e.g. by
+ *                 FBBT): not solved, status 12 (EngineUnknownStatus).
+ *   ws_*        : warm start (basic column per row [m], column status
+ *                 [n+m] 0 lb/1 ub/2 free/3 basic, reduced costs [n+m], basis
+ *                 inverse [m][m] row-major); ws_shared=1 means one basis for
+ *                 all nodes (e.g. the root optimum), else [batch] of each.
+ *                 ws_head == NULL: slack basis.  Replaces
+ *                 getWarmStartCopy/loadFromWarmStart (:375-384, :500-505).
+ *   iter_limit  : <= 0 means none; hitting it gives status 6
+ *                 (EngineIterationLimit, :561-569).
+ *   status/obj/iters : [batch]; obj includes the objective constant and is
+ *                 +INF for infeasible nodes.
+ *   x           : [batch][n] primal solution, or NULL.
+ *   wo_*        : [batch] warm starts out (children's warm start), or NULL.
+ * Current limit: m <= 64 rows (basis inverse rows held one per lane). */
+int mgpu_lp_solve(mgpu_ctx *ctx, int batch, const double *lb, const double *ub,
+                  const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,
+                  const double *ws_d, const double *ws_binv, int ws_shared,
+                  int iter_limit, int32_t *status, double *obj, int32_t *iters,
+                  double *x, int32_t *wo_head, int8_t *wo_st, double *wo_d,
+                  double *wo_binv);
+int mgpu_lp_solve_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double *d_ub,
+                      const int32_t *d_skip, const int32_t *d_ws_head,
+                      const int8_t *d_ws_st, const double *d_ws_d,
+                      const double *d_ws_binv, int ws_shared, int iter_limit,
+                      int32_t *d_status, double *d_obj, int32_t *d_iters, double *d_x,
+                      int32_t *d_wo_head, int8_t *d_wo_st, double *d_wo_d,
+                      double *d_wo_binv);
+
 /* Which FBBT kernel variant the next call uses: 0 auto, 1 node bounds in
  * LDS, 2 node bounds in a global scratch (large n). For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);

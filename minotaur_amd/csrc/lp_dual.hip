@@ -1,0 +1,531 @@
+// K3 — batched bounded dual simplex, gfx950.
+//
+// Replaces OsiLPEngine::solve -> Clp resolve() (src/interfaces/
+// OsiLPEngine.cpp:571-652): dual simplex from the loaded warm basis
+// (OsiDoDualInResolve, :579-583), iteration limit (:561-569) and the status
+// map (:592-627) onto EngineStatus numerics (src/base/Types.h:152-166).
+// The arithmetic restates oracle/lp_dual.c step for step (same pricing,
+// Harris two-pass ratio test, tie-breaks and update order), so the GPU and
+// the CPU restatement follow the same pivot sequence.
+//
+// Mapping (MI355X-first): ONE NODE PER WAVE64, kLpWaves nodes per
+// workgroup.
+//  * The dense basis inverse lives in VGPRs: lane i holds row i of B^{-1}
+//    (64 f64 = 128 VGPRs, fully unrolled, never spilled); basic values,
+//    bounds and the basic column index of row i are lane-i registers.
+//  * Products with a vector distributed one element per lane (B^{-1} a_q,
+//    B^{-1} w) broadcast the vector with v_readlane: no LDS traffic.
+//  * The constraint matrix is staged once per workgroup into LDS in both
+//    CSC (pivot row rho'A) and CSR (primal recompute) and shared by the
+//    waves; per-column state (reduced costs, values, working bounds, pivot
+//    row, status) is a per-wave LDS slice, swept lane-strided.
+//  * Reductions (pricing arg-max, ratio-test min / arg-max) are xor
+//    butterflies with deterministic lowest-index tie-breaks.
+//  * Pivots: B^{-1} row r is published to LDS once and read back as a
+//    broadcast for both the pivot row and the rank-1 update.
+#include "mgpu_internal.h"
+#include "wave.h"
+
+namespace mgpu {
+namespace {
+
+constexpr double kPTol = 1e-7;    // primal feasibility (Clp default)
+constexpr double kDTol = 1e-7;    // dual feasibility (Clp default)
+constexpr double kPivTol = 1e-9;  // smallest |alpha_rq| allowed to pivot
+constexpr double kArt0 = 1e7;     // first artificial box half-width
+constexpr double kInfB = 1e30;    // |bound| >= this is infinite in the LP
+
+constexpr int kUnknownStatus = 12;  // EngineUnknownStatus: node not solved
+
+enum : int8_t { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
+
+__host__ __device__ constexpr size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
+
+__host__ __device__ inline size_t shared_a_bytes(int n, int m, int nnz) {
+  return al16((size_t)(n + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
+         al16((size_t)(m + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8);
+}
+__host__ __device__ inline size_t wave_bytes(int N) {
+  return 5 * al16((size_t)N * 8) + 2 * al16((size_t)N) + 2 * 64 * 8;
+}
+
+__device__ __forceinline__ double art_lo(double thi, double ab) {
+  return (thi < kInfB ? thi : 0.0) - ab;
+}
+__device__ __forceinline__ double art_hi(double tlo, double ab) {
+  return (tlo > -kInfB ? tlo : 0.0) + ab;
+}
+
+struct Ctx {
+  // shared matrix
+  const int *colptr, *rowidx, *rowptr, *ccol;
+  const double *cval, *rval;
+  // per-wave column state
+  double *d, *z, *blo, *bhi, *al, *rho, *aq;
+  int8_t *st, *art;
+  // problem
+  int n, m, N;
+  const double *nlb, *nub, *rlo, *rhi, *c;
+  int lane;
+  __device__ __forceinline__ double tlo(int j) const {
+    const double v = j < n ? nlb[j] : rlo[j - n];
+    return v < -kInfB ? -INFINITY : v;
+  }
+  __device__ __forceinline__ double thi(int j) const {
+    const double v = j < n ? nub[j] : rhi[j - n];
+    return v > kInfB ? INFINITY : v;
+  }
+};
+
+// oracle place_nonbasic
+__device__ __forceinline__ void place_nonbasic(const Ctx &C, int j, double ab) {
+  const double lo = C.blo[j], hi = C.bhi[j], dj = C.d[j];
+  const bool lo_f = lo > -kInfB, hi_f = hi < kInfB;
+  if (lo_f && hi_f && lo == hi) {
+    C.st[j] = ST_LB;
+    C.z[j] = lo;
+    return;
+  }
+  if (dj > kDTol) {
+    if (!lo_f) {
+      C.blo[j] = art_lo(hi, ab);
+      C.art[j] |= 1;
+    }
+    C.st[j] = ST_LB;
+    C.z[j] = C.blo[j];
+  } else if (dj < -kDTol) {
+    if (!hi_f) {
+      C.bhi[j] = art_hi(lo, ab);
+      C.art[j] |= 2;
+    }
+    C.st[j] = ST_UB;
+    C.z[j] = C.bhi[j];
+  } else {
+    if (lo_f) {
+      C.st[j] = ST_LB;
+      C.z[j] = lo;
+    } else if (hi_f) {
+      C.st[j] = ST_UB;
+      C.z[j] = hi;
+    } else {
+      C.st[j] = ST_FREE;
+      C.z[j] = 0.0;
+    }
+  }
+}
+
+// oracle grow_art
+__device__ __forceinline__ void grow_art(const Ctx &C, double ab) {
+  for (int j = C.lane; j < C.N; j += 64) {
+    const int8_t a = C.art[j];
+    if (!a || C.st[j] == ST_BASIC) continue;
+    if (a & 1) C.blo[j] = art_lo(C.thi(j), ab);
+    if (a & 2) C.bhi[j] = art_hi(C.tlo(j), ab);
+    if (C.st[j] == ST_LB) C.z[j] = C.blo[j];
+    if (C.st[j] == ST_UB) C.z[j] = C.bhi[j];
+  }
+}
+
+// oracle compute_primals: z_B = -B^{-1} (N z_N); lane k forms w_k from CSR
+// row k in column order, then lane i takes row i of B^{-1} times w.
+__device__ __forceinline__ double compute_primals(const Ctx &C, const double (&binv)[kLpMaxM]) {
+  wave_sync();
+  double w = 0.0;
+  const int k = C.lane;
+  if (k < C.m) {
+    for (int t = C.rowptr[k]; t < C.rowptr[k + 1]; ++t) {
+      const int j = C.ccol[t];
+      if (C.st[j] == ST_BASIC) continue;
+      const double zj = C.z[j];
+      if (zj == 0.0) continue;
+      w += C.rval[t] * zj;
+    }
+    const int jl = C.n + k;
+    if (C.st[jl] != ST_BASIC) {
+      const double zl = C.z[jl];
+      if (zl != 0.0) w -= zl;
+    }
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int q = 0; q < kLpMaxM; ++q) s += binv[q] * rld(w, q);
+  return -s;
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+  // ---- stage the constraint matrix (CSC + CSR) once per workgroup ----
+  unsigned char *p = smem;
+  int *s_colptr = (int *)p;      p += al16((size_t)(n + 1) * 4);
+  int *s_rowidx = (int *)p;      p += al16((size_t)nnz * 4);
+  double *s_cval = (double *)p;  p += al16((size_t)nnz * 8);
+  int *s_rowptr = (int *)p;      p += al16((size_t)(m + 1) * 4);
+  int *s_ccol = (int *)p;        p += al16((size_t)nnz * 4);
+  double *s_rval = (double *)p;  p += al16((size_t)nnz * 8);
+  for (int t = threadIdx.x; t <= n; t += 64 * W) s_colptr[t] = lp.colptr[t];
+  for (int t = threadIdx.x; t <= m; t += 64 * W) s_rowptr[t] = lp.rowptr[t];
+  for (int t = threadIdx.x; t < nnz; t += 64 * W) {
+    s_rowidx[t] = lp.rowidx[t];
+    s_cval[t] = lp.cval[t];
+    s_ccol[t] = lp.ccol[t];
+    s_rval[t] = lp.rval[t];
+  }
+  __syncthreads();
+
+  const int b = blockIdx.x * W + wave;
+  if (b >= io.batch) return;  // no workgroup barrier below this point
+
+  unsigned char *wp = p + (size_t)wave * wave_bytes(N);
+  Ctx C;
+  C.colptr = s_colptr; C.rowidx = s_rowidx; C.cval = s_cval;
+  C.rowptr = s_rowptr; C.ccol = s_ccol; C.rval = s_rval;
+  C.d = (double *)wp;   wp += al16((size_t)N * 8);
+  C.z = (double *)wp;   wp += al16((size_t)N * 8);
+  C.blo = (double *)wp; wp += al16((size_t)N * 8);
+  C.bhi = (double *)wp; wp += al16((size_t)N * 8);
+  C.al = (double *)wp;  wp += al16((size_t)N * 8);
+  C.st = (int8_t *)wp;  wp += al16((size_t)N);
+  C.art = (int8_t *)wp; wp += al16((size_t)N);
+  C.rho = (double *)wp; wp += 64 * 8;
+  C.aq = (double *)wp;
+  C.n = n; C.m = m; C.N = N;
+  C.nlb = io.lb + (size_t)b * n;
+  C.nub = io.ub + (size_t)b * n;
+  C.rlo = lp.rlo; C.rhi = lp.rhi; C.c = lp.objd;
+  C.lane = lane;
+
+  if (io.skip != nullptr && io.skip[b] != 0) {  // pruned by FBBT: not solved
+    if (lane == 0) {
+      io.status[b] = kUnknownStatus;
+      io.obj[b] = INFINITY;
+      io.iters[b] = 0;
+    }
+    return;
+  }
+
+  // ---- working bounds; an empty box is infeasible before any pivot ----
+  bool bad = false;
+  for (int j = lane; j < N; j += 64) {
+    C.blo[j] = C.tlo(j);
+    C.bhi[j] = C.thi(j);
+    C.art[j] = 0;
+    bad |= C.blo[j] > C.bhi[j] + kPTol;
+  }
+  if (__any(bad)) {
+    if (lane == 0) {
+      io.status[b] = 2;
+      io.obj[b] = INFINITY;
+      io.iters[b] = 0;
+    }
+    return;
+  }
+
+  // ---- basis: warm start (parent / root optimum) or slack basis ----
+  const bool warm = io.ws.head != nullptr;
+  double binv[kLpMaxM];
+  int h = -1;
+  if (warm) {
+    const int32_t *wh = io.ws.head + (size_t)b * io.ws.s_head;
+    const int8_t *wst = io.ws.st + (size_t)b * io.ws.s_st;
+    const double *wd = io.ws.d + (size_t)b * io.ws.s_d;
+    const double *wb = io.ws.binv + (size_t)b * io.ws.s_binv;
+    for (int j = lane; j < N; j += 64) {
+      const int8_t s = wst[j];
+      C.st[j] = s == ST_BASIC ? ST_LB : s;
+    }
+    if (lane < m) h = wh[lane];
+    wave_sync();
+    if (lane < m) C.st[h] = ST_BASIC;
+    wave_sync();
+    for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
+#pragma unroll
+    for (int k = 0; k < kLpMaxM; ++k)
+      binv[k] = (lane < m && k < m) ? wb[(size_t)lane * m + k] : 0.0;
+  } else {
+    if (lane < m) h = n + lane;
+    for (int j = lane; j < N; j += 64) {
+      C.st[j] = j >= n ? ST_BASIC : ST_LB;
+      C.d[j] = j < n ? C.c[j] : 0.0;  // y = 0 for the slack basis
+    }
+#pragma unroll
+    for (int k = 0; k < kLpMaxM; ++k) binv[k] = (k == lane && lane < m) ? -1.0 : 0.0;
+  }
+  wave_sync();
+  double art_bound = kArt0;
+  for (int j = lane; j < N; j += 64) {
+    if (C.st[j] == ST_BASIC) continue;
+    const double lo = C.blo[j], hi = C.bhi[j], dj = C.d[j];
+    bool keep = false;
+    if (warm) {
+      const int8_t s = C.st[j];
+      if (s == ST_LB && lo > -kInfB && dj >= -kDTol) {
+        C.z[j] = lo;
+        keep = true;
+      } else if (s == ST_UB && hi < kInfB && dj <= kDTol) {
+        C.z[j] = hi;
+        keep = true;
+      } else if (lo == hi && lo > -kInfB) {
+        C.st[j] = ST_LB;
+        C.z[j] = lo;
+        keep = true;
+      }
+    }
+    if (!keep) place_nonbasic(C, j, art_bound);
+  }
+  wave_sync();
+  double lbB = 0.0, ubB = 0.0;
+  if (lane < m) {
+    lbB = C.blo[h];
+    ubB = C.bhi[h];
+  }
+  double zB = compute_primals(C, binv);
+
+  int status = kUnknownStatus, iters = 0;
+  bool fresh = true;
+  for (;;) {
+    // ---- pricing: most infeasible basic row (Dantzig), lowest row on ties
+    double inf = 0.0;
+    if (lane < m) {
+      if (zB < lbB - kPTol) inf = zB - lbB;
+      else if (zB > ubB + kPTol) inf = zB - ubB;
+    }
+    double best = fabs(inf);
+    int r = best > 0.0 ? lane : INT_MAX;
+    wave_argmax(best, r);
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (best == 0.0) {
+      if (!fresh) {
+        zB = compute_primals(C, binv);
+        fresh = true;
+        continue;
+      }
+      bool grow = false;
+      for (int j = lane; j < N; j += 64) {
+        const int8_t a = C.art[j], s = C.st[j];
+        if (s == ST_BASIC || !a) continue;
+        if ((s == ST_LB && (a & 1)) || (s == ST_UB && (a & 2))) grow = true;
+      }
+      if (!__any(grow)) {
+        status = 0;
+        break;
+      }
+      if (art_bound >= 1e13) {
+        status = 4;
+        break;
+      }
+      art_bound *= 1e3;
+      grow_art(C, art_bound);
+      zB = compute_primals(C, binv);
+      fresh = true;
+      continue;
+    }
+    if (iters >= io.iter_limit) {
+      status = 6;
+      break;
+    }
+    const double delta = rld(inf, r);
+
+    // ---- row r of B^{-1} to LDS (read back as a broadcast) ----
+    if (lane == r) {
+#pragma unroll
+      for (int k = 0; k < kLpMaxM; k += 2) {
+        double2 v;
+        v.x = binv[k];
+        v.y = binv[k + 1];
+        *reinterpret_cast<double2 *>(C.rho + k) = v;
+      }
+    }
+    wave_sync();
+    const double sigma = delta > 0 ? 1.0 : -1.0;
+
+    // ---- pivot row and Harris pass 1 ----
+    double tmax = INFINITY;
+    for (int j = lane; j < N; j += 64) {
+      const int8_t s = C.st[j];
+      double a = 0.0;
+      if (s != ST_BASIC && C.blo[j] != C.bhi[j]) {
+        if (j >= n) {
+          a = -C.rho[j - n];
+        } else {
+          for (int t = C.colptr[j]; t < C.colptr[j + 1]; ++t) a += C.cval[t] * C.rho[C.rowidx[t]];
+        }
+        const double at = sigma * a, dj = C.d[j];
+        if (s == ST_LB && at > kPivTol) {
+          const double t = (fmax(dj, 0.0) + kDTol) / at;
+          if (t < tmax) tmax = t;
+        } else if (s == ST_UB && at < -kPivTol) {
+          const double t = (fmin(dj, 0.0) - kDTol) / at;
+          if (t < tmax) tmax = t;
+        } else if (s == ST_FREE && fabs(at) > kPivTol) {
+          const double t = kDTol / fabs(at);
+          if (t < tmax) tmax = t;
+        }
+      }
+      C.al[j] = a;
+    }
+    tmax = wave_min(tmax);
+    if (tmax == INFINITY) {  // dual unbounded
+      bool boxed = false;
+      for (int j = lane; j < N; j += 64) boxed |= C.st[j] != ST_BASIC && C.art[j] != 0;
+      if (!__any(boxed) || art_bound >= 1e13) {
+        status = 2;
+        break;
+      }
+      art_bound *= 1e3;
+      grow_art(C, art_bound);
+      zB = compute_primals(C, binv);
+      fresh = true;
+      continue;
+    }
+    // ---- Harris pass 2: largest |alpha| among ratios <= tmax ----
+    double qa = 0.0;
+    int q = INT_MAX;
+    for (int j = lane; j < N; j += 64) {
+      const int8_t s = C.st[j];
+      if (s == ST_BASIC || C.blo[j] == C.bhi[j]) continue;
+      const double at = sigma * C.al[j], dj = C.d[j];
+      double t;
+      if (s == ST_LB && at > kPivTol) t = fmax(dj, 0.0) / at;
+      else if (s == ST_UB && at < -kPivTol) t = fmin(dj, 0.0) / at;
+      else if (s == ST_FREE && fabs(at) > kPivTol) t = 0.0;
+      else continue;
+      if (t <= tmax && fabs(at) > qa) {
+        qa = fabs(at);
+        q = j;
+      }
+    }
+    wave_argmax(qa, q);
+    q = __builtin_amdgcn_readfirstlane(q);
+    if (qa == 0.0) {
+      status = 2;
+      break;
+    }
+
+    // ---- column q: alpha_q = B^{-1} a_q (a_q one element per lane) ----
+    double aqk;
+    if (q < n) {
+      C.aq[lane] = 0.0;
+      wave_sync();
+      const int cs = C.colptr[q], deg = C.colptr[q + 1] - cs;
+      for (int t = lane; t < deg; t += 64) C.aq[C.rowidx[cs + t]] = C.cval[cs + t];
+      wave_sync();
+      aqk = C.aq[lane];
+    } else {
+      aqk = lane == q - n ? -1.0 : 0.0;
+    }
+    double alq = 0.0;
+#pragma unroll
+    for (int k = 0; k < kLpMaxM; ++k) alq += binv[k] * rld(aqk, k);
+    const double arq = rld(alq, r);
+
+    // ---- steps ----
+    double theta_d = C.d[q] / C.al[q];
+    if (sigma * theta_d < 0) theta_d = 0.0;
+    const double theta_p = delta / arq;
+    const int pl = rl(h, r);
+    for (int j = lane; j < N; j += 64) {
+      if (C.st[j] == ST_BASIC) continue;
+      C.d[j] -= theta_d * C.al[j];
+    }
+    const double zq = C.z[q] + theta_p;
+    const int8_t art_q = C.art[q];
+    const double bloq = C.blo[q], bhiq = C.bhi[q];
+    const double bound_p = delta < 0 ? C.blo[pl] : C.bhi[pl];
+    wave_sync();
+    if (lane == 0) {
+      C.d[q] = 0.0;
+      C.d[pl] = -theta_d;
+      C.st[pl] = delta < 0 ? ST_LB : ST_UB;
+      C.z[pl] = bound_p;
+      C.st[q] = ST_BASIC;
+      C.z[q] = zq;
+      if (art_q) {  // basic columns keep their true (infinite) bounds
+        C.blo[q] = C.tlo(q);
+        C.bhi[q] = C.thi(q);
+        C.art[q] = 0;
+      }
+    }
+    if (lane < m) zB -= theta_p * alq;
+    if (lane == r) {
+      h = q;
+      zB = zq;
+      lbB = art_q ? C.tlo(q) : bloq;
+      ubB = art_q ? C.thi(q) : bhiq;
+    }
+    // ---- rank-1 update of B^{-1} ----
+    const double inv = 1.0 / arq;
+#pragma unroll
+    for (int k = 0; k < kLpMaxM; ++k) {
+      const double nr = C.rho[k] * inv;
+      binv[k] = lane == r ? nr : binv[k] - alq * nr;
+    }
+    ++iters;
+    fresh = false;
+    if (iters % 64 == 0) {
+      zB = compute_primals(C, binv);
+      fresh = true;
+    }
+  }
+
+  // ---- outputs ----
+  wave_sync();
+  if (status == 0 || status == 6) {
+    if (lane < m) C.z[h] = zB;
+    wave_sync();
+    double s = 0.0;
+    for (int j = lane; j < n; j += 64) s += C.c[j] * C.z[j];
+    s = wave_sum(s);
+    if (lane == 0) io.obj[b] = s + lp.objoff;
+    if (io.x != nullptr)
+      for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = C.z[j];
+    if (io.wo_head != nullptr) {
+      if (lane < m) io.wo_head[(size_t)b * m + lane] = h;
+      for (int j = lane; j < N; j += 64) {
+        io.wo_st[(size_t)b * N + j] = C.st[j];
+        io.wo_d[(size_t)b * N + j] = C.d[j];
+      }
+      if (lane < m) {
+        double *dst = io.wo_binv + (size_t)b * m * m + (size_t)lane * m;
+#pragma unroll
+        for (int k = 0; k < kLpMaxM; ++k)
+          if (k < m) dst[k] = binv[k];
+      }
+    }
+  } else if (lane == 0) {
+    io.obj[b] = status == 2 ? INFINITY : -INFINITY;
+  }
+  if (lane == 0) {
+    io.status[b] = status;
+    io.iters[b] = iters;
+  }
+}
+
+}  // namespace
+
+size_t lp_lds_bytes(int n, int m, int nnz) {
+  return shared_a_bytes(n, m, nnz) + (size_t)kLpWaves * wave_bytes(n + m);
+}
+
+hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, hipStream_t stream) {
+  if (io.batch <= 0) return hipSuccess;
+  if (lp.m > kLpMaxM) return hipErrorInvalidValue;
+  const size_t lds = lp_lds_bytes(lp.n, lp.m, lp.nnz);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void *)lp_dual_kernel<kLpWaves>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int blocks = (io.batch + kLpWaves - 1) / kLpWaves;
+  hipLaunchKernelGGL(lp_dual_kernel<kLpWaves>, dim3(blocks), dim3(64 * kLpWaves), lds, stream,
+                     lp, io);
+  return hipGetLastError();
+}
+
+}  // namespace mgpu

@@ -60,7 +60,43 @@ struct DevLP {
   const TermRec *orec;          // [nobj] objective terms
   const TermRec *irec;          // [nint] integer columns (tightenInts_)
   int nint;
+  const double *cval;           // [nnz] CSC values (column order of colptr/rowidx)
+  const int32_t *ccol;          // [nnz] CSR column indices
+  const double *rval;           // [nnz] CSR values
 };
+
+// Warm start of the LP kernel (one basis per node, or one shared basis when
+// the strides are 0): basic column per row, status of every column
+// (0 at lb, 1 at ub, 2 free, 3 basic), reduced costs, dense basis inverse.
+struct LpWarm {
+  const int32_t *head;
+  const int8_t *st;
+  const double *d;
+  const double *binv;
+  long s_head, s_st, s_d, s_binv;   // per-node strides in elements (0 = shared)
+};
+
+struct LpIO {
+  int batch;
+  const double *lb, *ub;        // [B][n] node boxes
+  const int32_t *skip;          // [B] nonzero = node already infeasible (FBBT)
+  LpWarm ws;                    // ws.head == nullptr: slack basis
+  int iter_limit;
+  int32_t *status;              // [B] EngineStatus numerics
+  double *obj;                  // [B] objective incl. constant
+  int32_t *iters;               // [B]
+  double *x;                    // [B][n] primal (optional)
+  int32_t *wo_head;             // [B][m]  warm start out (optional)
+  int8_t *wo_st;                // [B][n+m]
+  double *wo_d;                 // [B][n+m]
+  double *wo_binv;              // [B][m][m]
+};
+
+constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
+constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
+
+size_t lp_lds_bytes(int n, int m, int nnz);
+hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, hipStream_t stream);
 
 // Output/optional mod-log arguments of one FBBT launch.
 struct FbbtIO {

@@ -51,13 +51,16 @@ struct mgpu_ctx {
   DevLP lp{};
   // problem storage
   DevBuf rowptr, terms, rlo, rhi, colptr, rowidx, vtype, obj, collb, colub, objd;
-  DevBuf rows, trec, orec, irec;
+  DevBuf rows, trec, orec, irec, cval, ccol, rval;
+  // LP workspaces (host-pointer path)
+  DevBuf lp_lb, lp_ub, lp_skip, lp_wh, lp_wst, lp_wd, lp_wb, lp_st, lp_obj, lp_it, lp_x,
+      lp_oh, lp_ost, lp_od, lp_ob;
   std::vector<Term> h_terms;
   // workspaces
   DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_inf, io_nmods, io_mv, io_ml, io_mval;
   DevBuf scratch, flag_scratch;
   int fbbt_variant = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   double last_fbbt_ms = 0.0, last_lp_ms = 0.0;
 };
 
@@ -105,7 +108,8 @@ int mgpu_create(int device, mgpu_ctx **out) {
   c->device = device;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess) {
     delete c;
     return MGPU_ERR_HIP;
   }
@@ -120,12 +124,17 @@ int mgpu_destroy(mgpu_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->rowptr, &c->terms, &c->rlo, &c->rhi, &c->colptr, &c->rowidx,
                     &c->vtype, &c->obj, &c->collb, &c->colub, &c->objd, &c->rows,
-                    &c->trec, &c->orec, &c->irec, &c->io_lb_in,
+                    &c->trec, &c->orec, &c->irec, &c->cval, &c->ccol, &c->rval,
+                    &c->lp_lb, &c->lp_ub, &c->lp_skip, &c->lp_wh, &c->lp_wst, &c->lp_wd,
+                    &c->lp_wb, &c->lp_st, &c->lp_obj, &c->lp_it, &c->lp_x, &c->lp_oh,
+                    &c->lp_ost, &c->lp_od, &c->lp_ob, &c->io_lb_in,
                     &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
                     &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch})
     b->release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  if (c->ev3) (void)hipEventDestroy(c->ev3);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return MGPU_OK;
@@ -176,10 +185,14 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   std::vector<int32_t> colptr(n + 1, 0), rowidx(nnz > 0 ? nnz : 1);
   for (int k = 0; k < nnz; ++k) colptr[colidx[k] + 1]++;
   for (int j = 0; j < n; ++j) colptr[j + 1] += colptr[j];
+  std::vector<double> cvalv(nnz > 0 ? nnz : 1);
   {
     std::vector<int32_t> fill(colptr.begin(), colptr.end() - 1);
     for (int i = 0; i < m; ++i)
-      for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) rowidx[fill[colidx[k]]++] = i;
+      for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        cvalv[fill[colidx[k]]] = val[k];
+        rowidx[fill[colidx[k]]++] = i;
+      }
   }
   std::vector<uint8_t> vt(n);
   for (int j = 0; j < n; ++j) vt[j] = (uint8_t)coltype[j];
@@ -231,6 +244,9 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   HIPCHK(c, upload(c->trec, trec.data(), trec.size()));
   HIPCHK(c, upload(c->orec, orec.data(), orec.size()));
   HIPCHK(c, upload(c->irec, irec.data(), irec.size()));
+  HIPCHK(c, upload(c->cval, cvalv.data(), cvalv.size()));
+  HIPCHK(c, upload(c->ccol, nnz > 0 ? colidx : rowptr, (size_t)(nnz > 0 ? nnz : 1)));
+  HIPCHK(c, upload(c->rval, nnz > 0 ? val : cvalv.data(), (size_t)(nnz > 0 ? nnz : 1)));
 
   DevLP &lp = c->lp;
   lp.n = n;
@@ -254,6 +270,9 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   lp.trec = c->trec.as<TermRec>();
   lp.orec = c->orec.as<TermRec>();
   lp.irec = c->irec.as<TermRec>();
+  lp.cval = c->cval.as<double>();
+  lp.ccol = c->ccol.as<int32_t>();
+  lp.rval = c->rval.as<double>();
   lp.nint = 0;
   for (int j = 0; j < n; ++j) lp.nint += (vt[j] == kBinary || vt[j] == kInteger) ? 1 : 0;
   c->loaded = true;
@@ -275,7 +294,13 @@ double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
       c->last_fbbt_ms = ms;
     return c->last_fbbt_ms;
   }
-  if (!strcmp(which, "lp")) return c->last_lp_ms;
+  if (!strcmp(which, "lp")) {
+    float ms = 0.f;
+    if (hipEventSynchronize(c->ev3) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev2, c->ev3) == hipSuccess)
+      c->last_lp_ms = ms;
+    return c->last_lp_ms;
+  }
   return -1.0;
 }
 
@@ -371,6 +396,116 @@ int mgpu_fbbt(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
                              hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MGPU_OK;
+}
+
+int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                      const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,
+                      const double *ws_d, const double *ws_binv, int ws_shared, int iter_limit,
+                      int32_t *status, double *obj, int32_t *iters, double *x,
+                      int32_t *wo_head, int8_t *wo_st, double *wo_d, double *wo_binv) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb || !ub || !status || !obj || !iters)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: bad argument");
+  if (ws_head && (!ws_st || !ws_d || !ws_binv))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: warm start needs head, st, d and binv");
+  if (wo_head && (!wo_st || !wo_d || !wo_binv))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: warm-start output needs all four arrays");
+  if (c->lp.m > kLpMaxM)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: m=%d rows > %d not supported yet", c->lp.m,
+                kLpMaxM);
+  if (lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: problem too large for the LDS kernel");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = c->lp.n, m = c->lp.m, N = n + m;
+  LpIO io{};
+  io.batch = batch;
+  io.lb = lb;
+  io.ub = ub;
+  io.skip = skip;
+  io.ws.head = ws_head;
+  io.ws.st = ws_st;
+  io.ws.d = ws_d;
+  io.ws.binv = ws_binv;
+  io.ws.s_head = ws_shared ? 0 : m;
+  io.ws.s_st = ws_shared ? 0 : N;
+  io.ws.s_d = ws_shared ? 0 : N;
+  io.ws.s_binv = ws_shared ? 0 : (long)m * m;
+  io.iter_limit = iter_limit > 0 ? iter_limit : 0x7fffffff;
+  io.status = status;
+  io.obj = obj;
+  io.iters = iters;
+  io.x = x;
+  io.wo_head = wo_head;
+  io.wo_st = wo_st;
+  io.wo_d = wo_d;
+  io.wo_binv = wo_binv;
+  HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+  HIPCHK(c, launch_lp_dual(c->lp, io, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+  return MGPU_OK;
+}
+
+int mgpu_lp_solve(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                  const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,
+                  const double *ws_d, const double *ws_binv, int ws_shared, int iter_limit,
+                  int32_t *status, double *obj, int32_t *iters, double *x, int32_t *wo_head,
+                  int8_t *wo_st, double *wo_d, double *wo_binv) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb || !ub || !status || !obj || !iters)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: bad argument");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = c->lp.n, m = c->lp.m, N = n + m;
+  const size_t B = (size_t)batch, wsB = ws_shared ? 1 : B;
+  hipStream_t s = c->stream;
+  auto h2d = [&](DevBuf &d, const void *src, size_t bytes) -> hipError_t {
+    hipError_t e = d.ensure(bytes > 0 ? bytes : 16);
+    if (e != hipSuccess || !src) return e;
+    return hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, s);
+  };
+  HIPCHK(c, h2d(c->lp_lb, lb, B * n * 8));
+  HIPCHK(c, h2d(c->lp_ub, ub, B * n * 8));
+  if (skip) HIPCHK(c, h2d(c->lp_skip, skip, B * 4));
+  if (ws_head) {
+    HIPCHK(c, h2d(c->lp_wh, ws_head, wsB * m * 4));
+    HIPCHK(c, h2d(c->lp_wst, ws_st, wsB * N));
+    HIPCHK(c, h2d(c->lp_wd, ws_d, wsB * N * 8));
+    HIPCHK(c, h2d(c->lp_wb, ws_binv, wsB * m * m * 8));
+  }
+  HIPCHK(c, c->lp_st.ensure(B * 4));
+  HIPCHK(c, c->lp_obj.ensure(B * 8));
+  HIPCHK(c, c->lp_it.ensure(B * 4));
+  if (x) HIPCHK(c, c->lp_x.ensure(B * n * 8));
+  if (wo_head) {
+    HIPCHK(c, c->lp_oh.ensure(B * m * 4 + 16));
+    HIPCHK(c, c->lp_ost.ensure(B * N + 16));
+    HIPCHK(c, c->lp_od.ensure(B * N * 8 + 16));
+    HIPCHK(c, c->lp_ob.ensure(B * m * m * 8 + 16));
+  }
+  int rc = mgpu_lp_solve_dev(
+      c, batch, c->lp_lb.as<double>(), c->lp_ub.as<double>(),
+      skip ? c->lp_skip.as<int32_t>() : nullptr, ws_head ? c->lp_wh.as<int32_t>() : nullptr,
+      ws_head ? c->lp_wst.as<int8_t>() : nullptr, ws_head ? c->lp_wd.as<double>() : nullptr,
+      ws_head ? c->lp_wb.as<double>() : nullptr, ws_shared, iter_limit, c->lp_st.as<int32_t>(),
+      c->lp_obj.as<double>(), c->lp_it.as<int32_t>(), x ? c->lp_x.as<double>() : nullptr,
+      wo_head ? c->lp_oh.as<int32_t>() : nullptr, wo_head ? c->lp_ost.as<int8_t>() : nullptr,
+      wo_head ? c->lp_od.as<double>() : nullptr, wo_head ? c->lp_ob.as<double>() : nullptr);
+  if (rc != MGPU_OK) return rc;
+  HIPCHK(c, hipMemcpyAsync(status, c->lp_st.p, B * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(obj, c->lp_obj.p, B * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(iters, c->lp_it.p, B * 4, hipMemcpyDeviceToHost, s));
+  if (x) HIPCHK(c, hipMemcpyAsync(x, c->lp_x.p, B * n * 8, hipMemcpyDeviceToHost, s));
+  if (wo_head) {
+    HIPCHK(c, hipMemcpyAsync(wo_head, c->lp_oh.p, B * m * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(wo_st, c->lp_ost.p, B * N, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(wo_d, c->lp_od.p, B * N * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(wo_binv, c->lp_ob.p, B * m * m * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(c, hipStreamSynchronize(s));
   return MGPU_OK;
 }
 

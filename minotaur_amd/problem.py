@@ -246,6 +246,12 @@ def random_problem(seed: int, n: int = 40, m: int = 30, density: float = 0.15,
     vlb[infl] = -math.inf
     vub[infu] = math.inf
     rows, rlo, rhi = [], [], []
+    # one interior point shared by all rows, so the root box is feasible
+    x = np.where(np.isfinite(vlb) & np.isfinite(vub),
+                 rng.uniform(0, 1, n) * (np.where(np.isfinite(vub), vub, 0) -
+                                         np.where(np.isfinite(vlb), vlb, 0)) +
+                 np.where(np.isfinite(vlb), vlb, 0),
+                 np.where(np.isfinite(vlb), vlb, np.where(np.isfinite(vub), vub, 0.0)))
     for i in range(m):
         if i == 0:
             k = 0
@@ -265,12 +271,6 @@ def random_problem(seed: int, n: int = 40, m: int = 30, density: float = 0.15,
                 c = float(np.round(rng.uniform(-5, 5), 3)) or 1.0
             terms.append((int(j), c))
         rows.append(terms)
-        # feasible-ish sides around the activity at a random interior point
-        x = np.where(np.isfinite(vlb) & np.isfinite(vub),
-                     rng.uniform(0, 1, n) * (np.where(np.isfinite(vub), vub, 0) -
-                                             np.where(np.isfinite(vlb), vlb, 0)) +
-                     np.where(np.isfinite(vlb), vlb, 0),
-                     np.where(np.isfinite(vlb), vlb, np.where(np.isfinite(vub), vub, 0.0)))
         act = sum(c * x[j] for j, c in terms)
         kind = rng.random()
         slack = float(rng.uniform(0, 10))

@@ -22,7 +22,7 @@ _D = ctypes.c_double
 EXPORTS = [
     'mgpu_create', 'mgpu_destroy', 'mgpu_last_error', 'mgpu_set_stream',
     'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
-    'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms',
+    'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
 ]
 
 _lib = None
@@ -60,6 +60,8 @@ def load_library():
     lib.mgpu_fbbt.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
     lib.mgpu_fbbt_dev.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
     lib.mgpu_set_fbbt_variant.argtypes = [_P, _I]
+    lib.mgpu_lp_solve.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
+    lib.mgpu_lp_solve_dev.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -86,6 +88,23 @@ class FbbtOut:
                  mod_val=None):
         self.lb, self.ub, self.infeasible, self.nmods = lb, ub, infeasible, nmods
         self.mod_var, self.mod_lu, self.mod_val = mod_var, mod_lu, mod_val
+
+
+class WarmStart:
+    """LP basis (getWarmStartCopy equivalent): basic column per row [m],
+    column status [n+m] (0 lb, 1 ub, 2 free, 3 basic), reduced costs [n+m]
+    and the dense basis inverse [m, m].  Leading batch axis when per node."""
+
+    def __init__(self, head, st, d, binv):
+        self.head, self.st, self.d, self.binv = head, st, d, binv
+
+    def node(self, b):
+        return WarmStart(self.head[b], self.st[b], self.d[b], self.binv[b])
+
+
+class LpOut:
+    def __init__(self, status, obj, iters, x=None, ws=None):
+        self.status, self.obj, self.iters, self.x, self.ws = status, obj, iters, x, ws
 
 
 class Context:
@@ -172,3 +191,57 @@ class Context:
                                          _dp(lb_out), _dp(ub_out), _dp(infeasible),
                                          _dp(nmods), cap, _dp(mod_var), _dp(mod_lu),
                                          _dp(mod_val)), 'mgpu_fbbt_dev')
+
+    # -- LP ------------------------------------------------------------------
+    def lp_solve(self, lb, ub, ws=None, skip=None, iter_limit=0, want_x=False,
+                 want_ws=False) -> LpOut:
+        """Host arrays [B,n] in; per-node status/objective/iterations out.
+        ``ws``: a WarmStart shared by all nodes (1-D arrays) or per node
+        (leading batch axis); None = slack basis."""
+        p = self.problem
+        lb = _np(lb, np.float64)
+        ub = _np(ub, np.float64)
+        B = lb.shape[0]
+        n, m = p.n, p.m
+        st = np.zeros(B, dtype=np.int32)
+        obj = np.zeros(B)
+        it = np.zeros(B, dtype=np.int32)
+        x = np.zeros((B, n)) if want_x else None
+        wo = None
+        if want_ws:
+            wo = WarmStart(np.zeros((B, m), np.int32), np.zeros((B, n + m), np.int8),
+                           np.zeros((B, n + m)), np.zeros((B, m, m)))
+        wh = wst = wd = wb = None
+        shared = 1
+        if ws is not None:
+            wh = _np(ws.head, np.int32)
+            wst = _np(ws.st, np.int8)
+            wd = _np(ws.d, np.float64)
+            wb = _np(ws.binv, np.float64)
+            shared = 1 if wh.ndim == 1 else 0
+        sk = None if skip is None else _np(skip, np.int32)
+        self._chk(self.lib.mgpu_lp_solve(
+            self.h, B, _hp(lb), _hp(ub), _hp(sk), _hp(wh), _hp(wst), _hp(wd), _hp(wb), shared,
+            int(iter_limit), _hp(st), _hp(obj), _hp(it), _hp(x),
+            _hp(wo.head) if wo else None, _hp(wo.st) if wo else None,
+            _hp(wo.d) if wo else None, _hp(wo.binv) if wo else None), 'mgpu_lp_solve')
+        return LpOut(st, obj, it, x, wo)
+
+    def lp_solve_dev(self, lb, ub, status, obj, iters, ws=None, skip=None, iter_limit=0,
+                     x=None, wo=None):
+        """Torch CUDA tensors; ``ws``/``wo`` are WarmStart of CUDA tensors."""
+        B = int(lb.shape[0])
+        shared = 1 if (ws is None or ws.head.dim() == 1) else 0
+        self._chk(self.lib.mgpu_lp_solve_dev(
+            self.h, B, _dp(lb), _dp(ub), _dp(skip),
+            _dp(ws.head) if ws else None, _dp(ws.st) if ws else None,
+            _dp(ws.d) if ws else None, _dp(ws.binv) if ws else None, shared, int(iter_limit),
+            _dp(status), _dp(obj), _dp(iters), _dp(x),
+            _dp(wo.head) if wo else None, _dp(wo.st) if wo else None,
+            _dp(wo.d) if wo else None, _dp(wo.binv) if wo else None), 'mgpu_lp_solve_dev')
+
+    def root_solve(self, iter_limit=0):
+        """Solve the root LP from the slack basis; returns (LpOut, WarmStart)."""
+        p = self.problem
+        r = self.lp_solve(p.vlb[None], p.vub[None], None, None, iter_limit, True, True)
+        return r, r.ws.node(0)

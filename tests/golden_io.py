@@ -43,3 +43,28 @@ def assert_mods_equal(nmods, mv, ml, mval, g, cap):
         assert np.array_equal(mv[b, :k], g['mod_var'][b, :k].astype(np.int32)), b
         assert np.array_equal(ml[b, :k], g['mod_lu'][b, :k].astype(np.int32)), b
         assert bits_equal(mval[b, :k], g['mod_val'][b, :k]), b
+
+
+def load_lp(name):
+    z = np.load(os.path.join(GOLDEN, f'lp_{name}.npz'), allow_pickle=False)
+    p = LinProblem(name=str(z['name']), n=int(z['n']), m=int(z['m']),
+                   rowptr=z['rowptr'].astype(np.int32), colidx=z['colidx'].astype(np.int32),
+                   val=z['val'], rlo=z['rlo'], rhi=z['rhi'], vlb=z['vlb'], vub=z['vub'],
+                   vtype=z['vtype'].astype(np.int32), obj=z['obj_c'],
+                   obj_const=float(z['obj_const'])).validate()
+    return p, {k: z[k] for k in ('lb', 'ub', 'status', 'obj')}
+
+
+OBJ_TOL = 1e-6   # north star: relaxation objectives within 1e-6
+
+
+def assert_lp_matches(status, obj, g, mask=None):
+    """Status identical; objective within 1e-6 (relative for |obj| > 1) of the
+    golden HiGHS value.  HiGHS 'unknown' entries (status 12) are skipped."""
+    ok = g['status'] != 12
+    if mask is not None:
+        ok &= mask
+    assert np.array_equal(np.asarray(status)[ok], g['status'][ok])
+    opt = ok & (g['status'] == 0)
+    err = np.abs(np.asarray(obj)[opt] - g['obj'][opt]) / np.maximum(1.0, np.abs(g['obj'][opt]))
+    assert err.size == 0 or err.max() <= OBJ_TOL, err.max()
