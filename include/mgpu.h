@@ -132,6 +132,20 @@ int mgpu_lp_solve_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double
                       int32_t *d_wo_head, int8_t *d_wo_st, double *d_wo_d,
                       double *d_wo_binv);
 
+/* Node decision after the relaxation solve (device pointers, async): the
+ * EngineStatus switch of PCBProcessor::shouldPrune_ (PCBProcessor.cpp:400-523)
+ * plus IntVarHandler::isFeasible (IntVarHandler.cpp:54-84).
+ *   decision[b]: 0 branch, 1 infeasible (FBBT or LP), 2 pruned by bound,
+ *                3 integer feasible (incumbent candidate), 4 engine problem.
+ *   cand_obj[b]: objective when decision 3, else +INF (min = new incumbent).
+ * Tolerances are the reference options solAbs_tol, solRel_tol,
+ * obj_cut_off, int_tol (Environment.cpp:486,509-528: 1e-6, 1e-6, +INF, 1e-6). */
+int mgpu_node_decide_dev(mgpu_ctx *ctx, int batch, const int32_t *d_fbbt_infeas,
+                         const int32_t *d_status, const double *d_obj, const double *d_x,
+                         double incumbent, double abs_tol, double rel_tol, double cutoff,
+                         double int_tol, int32_t *d_decision, double *d_inf_meas,
+                         double *d_cand_obj);
+
 /* Which FBBT kernel variant the next call uses: 0 auto, 1 node bounds in
  * LDS, 2 node bounds in a global scratch (large n). For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);

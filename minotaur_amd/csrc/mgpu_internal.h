@@ -95,6 +95,23 @@ struct LpIO {
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
 
+struct DecideIO {
+  int batch;
+  const int32_t *fbbt_infeas;   // [B] or null
+  const int32_t *status;        // [B] LP status
+  const double *obj;            // [B]
+  const double *x;              // [B][n]
+  double incumbent;             // best known objective (+inf if none)
+  double abs_tol, rel_tol;      // solAbs_tol / solRel_tol (1e-6)
+  double cutoff;                // obj_cut_off (+inf)
+  double int_tol;               // int_tol (1e-6)
+  int32_t *decision;            // [B]
+  double *inf_meas;             // [B] or null
+  double *cand_obj;             // [B] or null: obj if integer feasible else +inf
+};
+
+hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t stream);
+
 size_t lp_lds_bytes(int n, int m, int nnz);
 hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, hipStream_t stream);
 

@@ -509,4 +509,33 @@ int mgpu_lp_solve(mgpu_ctx *c, int batch, const double *lb, const double *ub,
   return MGPU_OK;
 }
 
+int mgpu_node_decide_dev(mgpu_ctx *c, int batch, const int32_t *fbbt_infeas,
+                         const int32_t *status, const double *obj, const double *x,
+                         double incumbent, double abs_tol, double rel_tol, double cutoff,
+                         double int_tol, int32_t *decision, double *inf_meas,
+                         double *cand_obj) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_node_decide: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!status || !obj || !x || !decision)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_node_decide: bad argument");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  DecideIO io{};
+  io.batch = batch;
+  io.fbbt_infeas = fbbt_infeas;
+  io.status = status;
+  io.obj = obj;
+  io.x = x;
+  io.incumbent = incumbent;
+  io.abs_tol = abs_tol;
+  io.rel_tol = rel_tol;
+  io.cutoff = cutoff;
+  io.int_tol = int_tol;
+  io.decision = decision;
+  io.inf_meas = inf_meas;
+  io.cand_obj = cand_obj;
+  HIPCHK(c, launch_node_decide(c->lp, io, c->stream));
+  return MGPU_OK;
+}
+
 }  // extern "C"

@@ -1,0 +1,74 @@
+// Node decision after the relaxation solve, batched: the engine-status
+// switch of PCBProcessor::shouldPrune_ (src/base/PCBProcessor.cpp:400-523)
+// and the integrality test of IntVarHandler::isFeasible
+// (src/base/IntVarHandler.cpp:54-84), one wave per node.
+//
+// decision codes (mgpu.h): 0 continue/branch, 1 infeasible (FBBT or LP),
+// 2 pruned by bound (NodeHitUb), 3 integer feasible (new incumbent
+// candidate), 4 engine problem (unbounded / unknown).
+#include "mgpu_internal.h"
+#include "wave.h"
+
+namespace mgpu {
+namespace {
+
+constexpr int kNodesPerBlock = 4;
+
+__global__ __launch_bounds__(64 * kNodesPerBlock) void node_decide_kernel(DevLP lp,
+                                                                           DecideIO io) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * kNodesPerBlock + (threadIdx.x >> 6);
+  if (b >= io.batch) return;
+  const int st = io.status[b];
+  const double solval = io.obj[b];
+  int dec;
+  double inf_meas = 0.0;
+  if (io.fbbt_infeas != nullptr && io.fbbt_infeas[b] != 0) {
+    dec = 1;  // presolveNode reported infeasible: pruned before the solve
+  } else if (st == 2 || st == 3) {
+    dec = 1;  // ProvenInfeasible / ProvenLocalInfeasible
+  } else if (st == 0 || st == 1 || st == 6) {
+    // ProvenOptimal / ProvenLocalOptimal / EngineIterationLimit
+    const double cut = io.incumbent;
+    if (solval >= cut - io.abs_tol || solval >= cut - fabs(cut) * io.rel_tol ||
+        solval >= io.cutoff) {
+      dec = 2;
+    } else {
+      // IntVarHandler::isFeasible over Binary/Integer columns
+      const double *x = io.x + (size_t)b * lp.n;
+      bool frac = false;
+      double meas = 0.0;
+      for (int j = lane; j < lp.n; j += 64) {
+        const uint8_t t = lp.vtype[j];
+        if (t != kBinary && t != kInteger) continue;
+        const double v = x[j];
+        const double f = fabs(v - floor(v + 0.5));
+        if (f > io.int_tol) {
+          frac = true;
+          meas += f;
+        }
+      }
+      inf_meas = wave_sum(meas);
+      dec = __any(frac) ? 0 : 3;
+    }
+  } else {
+    dec = 4;
+  }
+  if (lane == 0) {
+    io.decision[b] = dec;
+    if (io.inf_meas != nullptr) io.inf_meas[b] = inf_meas;
+    if (io.cand_obj != nullptr) io.cand_obj[b] = dec == 3 ? solval : INFINITY;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t stream) {
+  if (io.batch <= 0) return hipSuccess;
+  const int blocks = (io.batch + kNodesPerBlock - 1) / kNodesPerBlock;
+  hipLaunchKernelGGL(node_decide_kernel, dim3(blocks), dim3(64 * kNodesPerBlock), 0, stream,
+                     lp, io);
+  return hipGetLastError();
+}
+
+}  // namespace mgpu

@@ -197,30 +197,35 @@ def random_boxes(p: LinProblem, B: int, seed: int, max_depth: int = 20,
     """Seeded node boxes by random branching from the root:
     each node gets a depth d in [1, max_depth]; each of the d steps picks a
     random integer column that is not fixed yet and either fixes a binary to
-    0/1 or splits an integer at its midpoint (down: ub=floor(mid), up:
-    lb=ceil(mid)).  Returns (lb[B,n], ub[B,n])."""
+    0/1 or splits an integer (down: ub=floor(mid), up: lb=floor(mid)+1).
+    Vectorised over nodes.  Returns (lb[B,n], ub[B,n])."""
     rng = np.random.default_rng(seed)
     lb0 = p.vlb if root_lb is None else root_lb
     ub0 = p.vub if root_ub is None else root_ub
     ints = np.nonzero((p.vtype == BINARY) | (p.vtype == INTEGER))[0]
-    LB = np.tile(lb0, (B, 1)).astype(np.float64)
-    UB = np.tile(ub0, (B, 1)).astype(np.float64)
-    for bi in range(B):
-        d = int(rng.integers(1, max_depth + 1))
-        for _ in range(d):
-            free = ints[UB[bi, ints] - LB[bi, ints] >= 1.0]
-            if free.size == 0:
-                break
-            j = int(free[rng.integers(0, free.size)])
-            lo, hi = LB[bi, j], UB[bi, j]
-            if not (math.isfinite(lo) and math.isfinite(hi)):
-                lo = lo if math.isfinite(lo) else -1e3
-                hi = hi if math.isfinite(hi) else 1e3
-            split = math.floor(0.5 * (lo + hi))   # down: ub=split, up: lb=split+1
-            if rng.integers(0, 2) == 0:
-                UB[bi, j] = split
-            else:
-                LB[bi, j] = split + 1.0
+    LB = np.tile(np.asarray(lb0, dtype=np.float64), (B, 1))
+    UB = np.tile(np.asarray(ub0, dtype=np.float64), (B, 1))
+    if ints.size == 0 or B == 0:
+        return LB, UB
+    depth = rng.integers(1, max_depth + 1, size=B)
+    rows = np.arange(B)
+    for step in range(max_depth):
+        lo = LB[:, ints]
+        hi = UB[:, ints]
+        free = (hi - lo) >= 1.0
+        keys = rng.random((B, ints.size))
+        keys[~free] = 2.0
+        pick = np.argmin(keys, axis=1)
+        act = (depth > step) & free[rows, pick]
+        j = ints[pick]
+        l = np.where(np.isfinite(LB[rows, j]), LB[rows, j], -1e3)
+        h = np.where(np.isfinite(UB[rows, j]), UB[rows, j], 1e3)
+        split = np.floor(0.5 * (l + h))
+        down = rng.integers(0, 2, size=B) == 0
+        sel = act & down
+        UB[rows[sel], j[sel]] = split[sel]
+        sel = act & ~down
+        LB[rows[sel], j[sel]] = split[sel] + 1.0
     return LB, UB
 
 

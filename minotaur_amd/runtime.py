@@ -23,6 +23,7 @@ EXPORTS = [
     'mgpu_create', 'mgpu_destroy', 'mgpu_last_error', 'mgpu_set_stream',
     'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
     'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
+    'mgpu_node_decide_dev',
 ]
 
 _lib = None
@@ -62,6 +63,7 @@ def load_library():
     lib.mgpu_set_fbbt_variant.argtypes = [_P, _I]
     lib.mgpu_lp_solve.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_lp_solve_dev.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
+    lib.mgpu_node_decide_dev.argtypes = [_P, _I] + [_P] * 4 + [_D] * 5 + [_P] * 3
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -245,3 +247,13 @@ class Context:
         p = self.problem
         r = self.lp_solve(p.vlb[None], p.vub[None], None, None, iter_limit, True, True)
         return r, r.ws.node(0)
+
+    # -- node decision -------------------------------------------------------
+    def node_decide_dev(self, status, obj, x, decision, incumbent=math.inf, fbbt_infeas=None,
+                        inf_meas=None, cand_obj=None, abs_tol=1e-6, rel_tol=1e-6,
+                        cutoff=math.inf, int_tol=1e-6):
+        B = int(status.shape[0])
+        self._chk(self.lib.mgpu_node_decide_dev(
+            self.h, B, _dp(fbbt_infeas), _dp(status), _dp(obj), _dp(x), float(incumbent),
+            float(abs_tol), float(rel_tol), float(cutoff), float(int_tol), _dp(decision),
+            _dp(inf_meas), _dp(cand_obj)), 'mgpu_node_decide_dev')
