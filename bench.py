@@ -125,7 +125,10 @@ def main():
     ctx.load(p)
     root, ws_h = ctx.root_solve()
     assert root.status[0] == 0, "root LP not optimal"
-    stream = torch.cuda.current_stream(dev)
+    # one dedicated stream for the engine AND the torch glue (the legacy null
+    # stream would not order against the engine's non-blocking stream)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ws = WarmStart(*(torch.from_numpy(np.ascontiguousarray(a)).to(dev)
                      for a in (ws_h.head, ws_h.st, ws_h.d, ws_h.binv)))

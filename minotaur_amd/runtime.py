@@ -140,6 +140,11 @@ class Context:
             raise MgpuError(f"{what} failed rc={rc}: {msg.decode() if msg else ''}")
 
     def set_stream(self, stream_ptr):
+        """Run on an existing hipStream_t (e.g. torch.cuda.Stream().cuda_stream).
+        0 is refused: the legacy null stream would not be ordered against
+        work the engine queues on its own non-blocking stream."""
+        if not stream_ptr:
+            raise MgpuError("set_stream(0): pass a real stream (torch.cuda.Stream())")
         self._chk(self.lib.mgpu_set_stream(self.h, _P(stream_ptr)), 'mgpu_set_stream')
 
     def sync(self):
