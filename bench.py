@@ -51,6 +51,25 @@ def lp_flops(p, pivots, solves):
     return pivots * per_pivot + solves * per_solve
 
 
+def pmc_traffic(kernel, batch):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes of this same bench at the same batch)."""
+    import glob
+    key = {'fbbt': 'fbbt_linear_kernel', 'lp_dual': 'lp_dual_kernel'}[kernel]
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        args = d.get("bench_args", "").split()
+        b = int(args[args.index('--batch') + 1]) if '--batch' in args else 65536
+        k = d.get("kernels", {}).get(key)
+        if b == batch and k and k.get("hbm_bytes_per_launch"):
+            return k["hbm_bytes_per_launch"], os.path.basename(f)
+    return None, None
+
+
 def cpu_baseline(p, LB, UB, budget_s):
     """Rank 0, N=1: the same node boxes on ONE host core — FBBT with the
     reference's own LinearHandler (oracle/_ref, prebuilt) when present else
@@ -106,12 +125,11 @@ def main():
 
     import torch
     import torch.distributed as dist
+    from minotaur_amd import dist as mdist
     from minotaur_amd.problem import LinProblem, random_boxes
     from minotaur_amd.runtime import Context, WarmStart
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    rank, world, local = mdist.env_ranks()
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
@@ -119,7 +137,7 @@ def main():
 
     p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_lin.npz'))
     B = args.batch
-    LB, UB = random_boxes(p, B, 20261015 + rank)
+    LB, UB = random_boxes(p, B, mdist.shard_seed(20261015, rank))
 
     ctx = Context(local)
     ctx.load(p)
@@ -154,22 +172,24 @@ def main():
         ctx.fbbt_dev(lb0, ub0, lb1, ub1, infeas, nmods, inc)
         ctx.lp_solve_dev(lb1, ub1, status, obj, iters, ws=ws, skip=infeas, x=x)
         ctx.node_decide_dev(status, obj, x, decision, inc, fbbt_infeas=infeas, cand_obj=cand)
-        best = cand.min().reshape(1)
-        if world > 1:
-            dist.all_reduce(best, op=dist.ReduceOp.MIN)
-        if acc is not None:
-            acc["solved"] += (status != 12).sum()
-            acc["pivots"] += iters.sum()
+        best = mdist.allreduce_incumbent(cand.min().reshape(1))
+        acc["solved"] += (status != 12).sum()
+        acc["pivots"] += iters.sum()
         b = float(best.item())          # one host sync per step
         state["incumbent"] = min(inc, b)
-        if acc is not None:
-            acc["fbbt_ms"].append(ctx.last_kernel_ms('fbbt'))
-            acc["lp_ms"].append(ctx.last_kernel_ms('lp'))
+        acc["fbbt_ms"].append(ctx.last_kernel_ms('fbbt'))
+        acc["lp_ms"].append(ctx.last_kernel_ms('lp'))
 
-    for _ in range(args.warmup):
-        step(None)
-    acc = {"solved": torch.zeros((), dtype=torch.int64, device=dev),
-           "pivots": torch.zeros((), dtype=torch.int64, device=dev), "fbbt_ms": [], "lp_ms": []}
+    def new_acc():
+        return {"solved": torch.zeros((), dtype=torch.int64, device=dev),
+                "pivots": torch.zeros((), dtype=torch.int64, device=dev),
+                "fbbt_ms": [], "lp_ms": []}
+
+    # warm-up runs the exact timed step (also loads torch's lazily-loaded
+    # reduction kernels, which otherwise land in the first timed step)
+    for _ in range(max(1, args.warmup)):
+        step(new_acc())
+    acc = new_acc()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -182,9 +202,8 @@ def main():
     elapsed = time.perf_counter() - t0
     tot = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     cnt = torch.stack([acc["solved"].double(), acc["pivots"].double()])
-    if world > 1:
-        dist.all_reduce(tot, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    mdist.allreduce_max(tot)
+    mdist.allreduce_sum(cnt)
     elapsed = float(tot.item())
     solved, pivots = (float(v) for v in cnt.tolist())
     nodes = float(B) * world * args.steps
@@ -209,9 +228,12 @@ def main():
             k["frac"] = k["achieved"] / k["peak"]
         dom = "lp_dual" if lp_ms >= fbbt_ms else "fbbt"
         kd = kernels[dom]
+        traffic, tsrc = pmc_traffic(dom, B)
         roofline = {"kernel": dom, "bound": "hbm" if dom == "fbbt" else "mfma",
                     "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
-                    "frac": kd["frac"], "traffic": None}
+                    "frac": kd["frac"], "traffic": traffic}
+        if tsrc:
+            roofline["traffic_source"] = f"profiles/{tsrc} (PMC, bytes per launch)"
         if dom == "lp_dual":
             roofline["note"] = ("FP64 VALU kernel (no MFMA: per-node rank-1 updates); peak = "
                                 "MI355X FP64 dense rate 78.6 TF/s")

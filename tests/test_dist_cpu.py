@@ -1,0 +1,74 @@
+"""CPU, world_size 2 over gloo: the multi-GPU semantics of bench.py /
+minotaur_amd.dist — disjoint per-rank node shards, incumbent all-reduce MIN,
+stop-flag OR, statistics SUM — with the node processing done by the CPU
+oracles as stand-ins for the GPU kernels (this test exercises the
+collectives, not the kernels)."""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import oracle
+    from minotaur_amd import dist as mdist
+    from minotaur_amd.problem import LinProblem, random_boxes
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'knapsack9.npz'))
+    r, w, _ = mdist.env_ranks()
+    assert (r, w) == (rank, world)
+    LB, UB = random_boxes(p, 64, mdist.shard_seed(7, rank))
+    f = oracle.linear_fbbt(p, LB, UB)
+    keep = f.infeas == 0
+    _, _, _, _, _, ws = oracle.dual_simplex_root(p)
+    st, obj, it, x = oracle.dual_simplex(p, f.lb[keep], f.ub[keep], ws, want_x=True)
+    frac = np.abs(x - np.floor(x + 0.5))[:, :9].max(axis=1) > 1e-6
+    cand = np.where((st == 0) & ~frac, obj, math.inf)
+    local_best = float(cand.min()) if cand.size else math.inf
+    best = mdist.allreduce_incumbent(torch.tensor([local_best], dtype=torch.float64))
+    stop = mdist.allreduce_stop(torch.tensor([1 if rank == 1 else 0], dtype=torch.int32))
+    cnt = mdist.allreduce_sum(torch.tensor([float(keep.sum()), 64.0], dtype=torch.float64))
+    allb = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(allb, torch.tensor([local_best], dtype=torch.float64))
+    out[rank] = (float(best.item()), int(stop.item()), cnt.tolist(),
+                 [float(t.item()) for t in allb], LB[:4].tobytes())
+    dist.destroy_process_group()
+
+
+def test_two_rank_incumbent_and_stats():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    b0, s0, c0, allb0, lb0 = out[0]
+    b1, s1, c1, allb1, lb1 = out[1]
+    assert b0 == b1 == min(allb0)           # MIN over ranks, identical everywhere
+    assert s0 == s1 == 1                    # OR of stop flags
+    assert c0 == c1 and c0[1] == 128.0      # SUM of counters
+    assert lb0 != lb1                       # disjoint shards (different seeds)
+
+
+def test_round_robin_deal_covers_all():
+    from minotaur_amd.dist import deal_round_robin
+    items = sorted(sum((deal_round_robin(10, r, 4) for r in range(4)), []))
+    assert items == list(range(10))
