@@ -107,7 +107,8 @@ int mgpu_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in,
  *                 FBBT): not solved, status 12 (EngineUnknownStatus).
  *   ws_*        : warm start (basic column per row [m], column status
  *                 [n+m] 0 lb/1 ub/2 free/3 basic, reduced costs [n+m], basis
- *                 inverse [m][m] row-major); ws_shared=1 means one basis for
+ *                 inverse [m][m] COLUMN-major, i.e. binv[k*m+i] = (B^-1)_ik,
+ *                 so lane i's row loads coalesce); ws_shared=1: one basis for
  *                 all nodes (e.g. the root optimum), else [batch] of each.
  *                 ws_head == NULL: slack basis.  Replaces
  *                 getWarmStartCopy/loadFromWarmStart (:375-384, :500-505).

@@ -206,78 +206,102 @@ __device__ void sing_lf_bnds(const TermRec *base, int nt, const TermChunk &pre, 
   up = u;
 }
 
-// updateLfBoundsFromLb_ (LinearHandler.cpp:1048-1134).
-template <class V>
-__device__ void upd_from_lb(const TermRec *base, int nt, const TermChunk &pre, V &v,
-                            NodeState &s, const ModLog &log, double lb, double uu,
-                            bool is_sing, bool &changed, bool count_int) {
-  for_terms(base, nt, pre, [&](const Term1 &t) {
-    const double c = t.a;
-    const int j = t.j;
-    double vlb = v.L(j), vub = v.U(j);
-    if (c > kETol && (!is_sing || vub >= kInfty)) {
-      if (vub >= kInfty) vub = 0.;
-      double nlb = (lb - uu) / c + vub;
-      if (nlb > vlb + kETol) {
-        const double cur_ub = v.U(j);
-        if (nlb > cur_ub - kETol) nlb = cur_ub;
-        v.change_bflag(t);
-        v.L(j) = nlb;
-        log.push(s, j, 0, nlb);
-        if (count_int && t.isint) s.nintmods++;
-        changed = true;
-      }
-    } else if (c < -kETol && (!is_sing || vlb <= -kInfty)) {
-      if (vlb <= -kInfty) vlb = 0.;
-      double nub = (lb - uu) / c + vlb;
-      if (nub < vub - kETol) {
-        const double cur_lb = v.L(j);
-        if (nub < cur_lb + kETol) nub = cur_lb;
-        v.change_bflag(t);
-        v.U(j) = nub;
-        log.push(s, j, 1, nub);
-        if (count_int && t.isint) s.nintmods++;
-        changed = true;
-      }
-    }
-  });
+// Term k of a list: from the preloaded chunk (k < 64, v_readlane) or from
+// memory (uniform address).
+__device__ __forceinline__ Term1 term_at(const TermRec *base, const TermChunk &pre, int k) {
+  if (k < kLanes)
+    return Term1{rld(pre.a, k), rlu64(pre.cmask, k), rl(pre.j, k), rl(pre.cs, k),
+                 rl(pre.ce, k), rl(pre.isint, k)};
+  const TermRec r = base[k];
+  return Term1{r.a, r.cmask, r.j, r.cs, r.ce, r.isint};
 }
 
-// updateLfBoundsFromUb_ (LinearHandler.cpp:1137-1226).
+// updateLfBoundsFromLb_ (LinearHandler.cpp:1048-1134) when from_lb, with
+// diff = lb - uu; updateLfBoundsFromUb_ (:1137-1226) otherwise, with
+// diff = ub - ll.  A term with coef > 0 (from_lb) / coef < 0 (from_ub)
+// raises its column's lower bound, the other sign lowers the upper bound.
+//
+// Terms are taken four at a time: phase A computes the four candidate
+// bounds (four independent f64 divisions in flight), phase B applies them
+// in term order.  This is exactly the reference's sequential loop because
+// each term of a row is a different column and a term only reads and writes
+// its own column's bounds; the order-dependent effects (mod log, nintmods)
+// are produced in phase B in term order.
 template <class V>
-__device__ void upd_from_ub(const TermRec *base, int nt, const TermChunk &pre, V &v,
-                            NodeState &s, const ModLog &log, double ub, double ll,
-                            bool is_sing, bool &changed, bool count_int) {
-  for_terms(base, nt, pre, [&](const Term1 &t) {
-    const double c = t.a;
-    const int j = t.j;
-    double vlb = v.L(j), vub = v.U(j);
-    if (c > kETol && (!is_sing || vlb <= -kInfty)) {
-      if (vlb <= -kInfty) vlb = 0.;
-      double nub = (ub - ll) / c + vlb;
-      if (nub < vub - kETol) {
-        const double cur_lb = v.L(j);
-        if (nub < cur_lb + kETol) nub = cur_lb;
-        v.change_bflag(t);
-        v.U(j) = nub;
-        log.push(s, j, 1, nub);
-        if (count_int && t.isint) s.nintmods++;
-        changed = true;
+__device__ void upd_side(const TermRec *base, int nt, const TermChunk &pre, V &v,
+                         NodeState &s, const ModLog &log, double diff, bool from_lb,
+                         bool is_sing, bool &changed, bool count_int) {
+  for (int k0 = 0; k0 < nt; k0 += 4) {
+    Term1 t[4];
+    double cand[4], cur[4];
+    bool hit[4], low[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      hit[u] = false;
+      low[u] = false;
+      cand[u] = 0.0;
+      cur[u] = 0.0;
+      if (k0 + u < nt) {
+        t[u] = term_at(base, pre, k0 + u);
+        const double c = t[u].a;
+        if (c > kETol || c < -kETol) {
+          const int j = t[u].j;
+          const double vl = v.L(j), vu = v.U(j);
+          low[u] = from_lb ? c > 0 : c < 0;
+          if (low[u]) {
+            // new lower bound: diff/c + (vub, or 0 for a singleton infinity)
+            const bool ok = !is_sing || vu >= kInfty;
+            const double nb = diff / c + (vu >= kInfty ? 0. : vu);
+            hit[u] = ok && nb > vl + kETol;
+            cand[u] = nb;
+            cur[u] = vu;          // var->getUb() for the clamp
+          } else {
+            const bool ok = !is_sing || vl <= -kInfty;
+            const double nb = diff / c + (vl <= -kInfty ? 0. : vl);
+            hit[u] = ok && nb < vu - kETol;
+            cand[u] = nb;
+            cur[u] = vl;          // var->getLb() for the clamp
+          }
+        }
       }
-    } else if (c < -kETol && (!is_sing || vub >= kInfty)) {
-      if (vub >= kInfty) vub = 0.;
-      double nlb = (ub - ll) / c + vub;
-      if (nlb > vlb + kETol) {
-        const double cur_ub = v.U(j);
-        if (nlb > cur_ub - kETol) nlb = cur_ub;
-        v.change_bflag(t);
-        v.L(j) = nlb;
-        log.push(s, j, 0, nlb);
-        if (count_int && t.isint) s.nintmods++;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (hit[u]) {
+        const int j = t[u].j;
+        double nb = cand[u];
+        if (low[u]) {
+          if (nb > cur[u] - kETol) nb = cur[u];
+          v.change_bflag(t[u]);
+          v.L(j) = nb;
+          log.push(s, j, 0, nb);
+        } else {
+          if (nb < cur[u] + kETol) nb = cur[u];
+          v.change_bflag(t[u]);
+          v.U(j) = nb;
+          log.push(s, j, 1, nb);
+        }
+        if (count_int && t[u].isint) s.nintmods++;
         changed = true;
       }
     }
-  });
+  }
+}
+
+template <class V>
+__device__ __forceinline__ void upd_from_lb(const TermRec *base, int nt, const TermChunk &pre,
+                                            V &v, NodeState &s, const ModLog &log, double lb,
+                                            double uu, bool is_sing, bool &changed,
+                                            bool count_int) {
+  upd_side(base, nt, pre, v, s, log, lb - uu, true, is_sing, changed, count_int);
+}
+
+template <class V>
+__device__ __forceinline__ void upd_from_ub(const TermRec *base, int nt, const TermChunk &pre,
+                                            V &v, NodeState &s, const ModLog &log, double ub,
+                                            double ll, bool is_sing, bool &changed,
+                                            bool count_int) {
+  upd_side(base, nt, pre, v, s, log, ub - ll, false, is_sing, changed, count_int);
 }
 
 // linBndTighten_ in node mode (LinearHandler.cpp:952-1045).  Returns true if

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
 #pragma unroll
     for (int k = 0; k < kLpMaxM; ++k)
-      binv[k] = (lane < m && k < m) ? wb[(size_t)lane * m + k] : 0.0;
+      binv[k] = (lane < m && k < m) ? wb[(size_t)k * m + lane] : 0.0;  // column-major: coalesced
   } else {
     if (lane < m) h = n + lane;
     for (int j = lane; j < N; j += 64) {
@@ -489,10 +489,10 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         io.wo_d[(size_t)b * N + j] = C.d[j];
       }
       if (lane < m) {
-        double *dst = io.wo_binv + (size_t)b * m * m + (size_t)lane * m;
+        double *dst = io.wo_binv + (size_t)b * m * m + lane;
 #pragma unroll
         for (int k = 0; k < kLpMaxM; ++k)
-          if (k < m) dst[k] = binv[k];
+          if (k < m) dst[(size_t)k * m] = binv[k];   // column-major: coalesced
       }
     }
   } else if (lane == 0) {

@@ -95,7 +95,12 @@ class FbbtOut:
 class WarmStart:
     """LP basis (getWarmStartCopy equivalent): basic column per row [m],
     column status [n+m] (0 lb, 1 ub, 2 free, 3 basic), reduced costs [n+m]
-    and the dense basis inverse [m, m].  Leading batch axis when per node."""
+    and the dense basis inverse stored COLUMN-major: binv[k, i] = (B^-1)[i, k]
+    (the ABI layout; ``binv_rows()`` gives (B^-1) itself).  Leading batch
+    axis when per node."""
+
+    def binv_rows(self):
+        return np.swapaxes(np.asarray(self.binv), -1, -2)
 
     def __init__(self, head, st, d, binv):
         self.head, self.st, self.d, self.binv = head, st, d, binv

@@ -51,6 +51,10 @@ def test_lp_warm_from_root(ctx, name):
     root, ws = ctx.root_solve()
     rs, robj, x, y, it, ows = oracle.dual_simplex_root(p)
     assert root.status[0] == rs and root.iters[0] == it and abs(root.obj[0] - robj) < 1e-9
+    # same optimal basis as the oracle (binv is column-major in the ABI)
+    assert np.array_equal(ws.head, ows.head) and np.array_equal(ws.st, ows.st)
+    assert np.allclose(ws.binv_rows(), ows.binv, rtol=1e-9, atol=1e-12)
+    assert np.allclose(ws.d, ows.d, rtol=1e-9, atol=1e-12)
     r = ctx.lp_solve(g['lb'], g['ub'], ws)
     assert_lp_matches(r.status, r.obj, g)
     st, obj, its, _ = oracle.dual_simplex(p, g['lb'], g['ub'], ows)
