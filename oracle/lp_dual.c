@@ -409,6 +409,14 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
     if (iters % 64 == 0) { compute_primals(&W); fresh = 1; }
   }
 done:
+  /* warm start out: the maintained reduced costs (reduced costs of fixed
+   * nonbasic columns are not maintained: they can never enter) */
+  if (ws_head && (status == 0 || status == 6)) {
+    memcpy(ws_head, W.head, sizeof(int) * (size_t) m);
+    if (ws_st) for (int j = 0; j < N; ++j) ws_st[j] = W.st[j];
+    if (ws_binv) memcpy(ws_binv, W.binv, sizeof(double) * (size_t) m * m);
+    if (ws_d) memcpy(ws_d, W.d, sizeof(double) * (size_t) N);
+  }
   if (status == 0 || status == 6) {
     double obj = 0.0;
     for (int j = 0; j < n; ++j) obj += P->c[j] * W.z[j];
@@ -420,12 +428,6 @@ done:
     }
   } else if (obj_out) {
     *obj_out = status == 2 ? INFINITY : -INFINITY;
-  }
-  if (ws_head && (status == 0 || status == 6)) {
-    memcpy(ws_head, W.head, sizeof(int) * (size_t) m);
-    if (ws_st) for (int j = 0; j < N; ++j) ws_st[j] = W.st[j];
-    if (ws_binv) memcpy(ws_binv, W.binv, sizeof(double) * (size_t) m * m);
-    if (ws_d) memcpy(ws_d, W.d, sizeof(double) * (size_t) N);
   }
   if (iters_out) *iters_out = iters;
   free(W.blo); free(W.bhi); free(W.art); free(W.z); free(W.d); free(W.binv);
