@@ -67,9 +67,11 @@ int mgpu_set_stream(mgpu_ctx *ctx, void *hip_stream);
 void *mgpu_get_stream(mgpu_ctx *ctx);
 int mgpu_sync(mgpu_ctx *ctx);
 
-/* Load the batch-shared relaxation: row-major CSR with columns ascending
- * inside each row (the reference's VariableGroup order), row bounds, root
- * column bounds and types, and a linear objective to MINIMISE plus constant.
+/* Load the batch-shared relaxation: row-major CSR, row bounds, root column
+ * bounds and types, and a linear objective to MINIMISE plus constant.
+ * Terms inside a row must be given in the order the reference iterates them
+ * (the LinearFunction's VariableGroup, ascending variable id: Types.cpp:30-34)
+ * — FBBT sums in that order; each column at most once per row.
  * Replaces OsiLPEngine::load (OsiLPEngine.cpp:390-498). */
 int mgpu_load_lp(mgpu_ctx *ctx, int n, int m, const int32_t *rowptr,
                  const int32_t *colidx, const double *val,

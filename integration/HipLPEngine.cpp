@@ -1,0 +1,446 @@
+//
+// HipLPEngine — see HipLPEngine.h.  Mirrors OsiLPEngine's behaviour
+// (src/interfaces/OsiLPEngine.cpp) call by call:
+//   load            :390-498  row-major CSR, bounds, objective (x -1 when
+//                             maximising), problem->setEngine(this)
+//   edits           :152-262  set dirty flags; rows re-read lazily
+//   solve           :571-652  resolve from the kept basis; status map;
+//                             solution value + objective constant
+//   warm start      :375-384, :500-505
+//   iteration limit :561-569  (default 10000, ctor :95-137)
+//
+#include "HipLPEngine.h"
+
+#include <cassert>
+#include <cmath>
+#include <cstring>
+#include <iostream>
+
+#include "Constraint.h"
+#include "Environment.h"
+#include "Function.h"
+#include "LinearFunction.h"
+#include "Logger.h"
+#include "Objective.h"
+#include "Problem.h"
+#include "Solution.h"
+#include "Timer.h"
+#include "Variable.h"
+#include "mgpu.h"
+
+using namespace Minotaur;
+
+const std::string HipLPEngine::me_ = "HipLPEngine: ";
+
+void HipLPWarmStart::write(std::ostream &out) const {
+  out << "HipLPWarmStart: " << head.size() << " basic columns" << std::endl;
+}
+
+HipLPEngine::HipLPEngine(EnvPtr env, int device)
+    : env_(env),
+      problem_(0),
+      ctx_(0),
+      device_(device),
+      n_(0),
+      m_(0),
+      bndChanged_(true),
+      consChanged_(true),
+      objChanged_(true),
+      needUpload_(true),
+      wsValid_(false),
+      sol_(0),
+      maxIterLimit_(10000),
+      iterLimit_(10000),
+      lastIters_(0),
+      strBr_(false) {
+  logger_ = env_->getLogger();
+  stats_ = new HipLPStats();
+  std::memset(stats_, 0, sizeof(HipLPStats));
+  timer_ = env_->getNewTimer();
+  status_ = EngineUnknownStatus;
+  if (mgpu_create(device_, &ctx_) != MGPU_OK) {
+    ctx_ = 0;
+    logger_->errStream() << me_ << "no HIP device " << device_ << std::endl;
+  }
+}
+
+HipLPEngine::~HipLPEngine() {
+  if (ctx_) mgpu_destroy(ctx_);
+  delete stats_;
+  delete timer_;
+  if (problem_) {
+    problem_->unsetEngine();
+    problem_ = 0;
+  }
+  delete sol_;
+}
+
+void HipLPEngine::syncRows_() {
+  n_ = (int)problem_->getNumVars();
+  m_ = (int)problem_->getNumCons();
+  rowptr_.assign(1, 0);
+  colidx_.clear();
+  val_.clear();
+  rlo_.resize(m_);
+  rhi_.resize(m_);
+  int i = 0;
+  for (ConstraintConstIterator it = problem_->consBegin(); it != problem_->consEnd();
+       ++it, ++i) {
+    assert((*it)->getFunctionType() == Linear);  // as OsiLPEngine.cpp:420
+    rlo_[i] = (*it)->getLb();
+    rhi_[i] = (*it)->getUb();
+    LinearFunctionPtr lf = (*it)->getLinearFunction();
+    if (lf) {
+      for (VariableGroupConstIterator t = lf->termsBegin(); t != lf->termsEnd(); ++t) {
+        colidx_.push_back((int32_t)t->first->getIndex());
+        val_.push_back(t->second);
+      }
+    }
+    rowptr_.push_back((int32_t)colidx_.size());
+  }
+  clo_.resize(n_);
+  chi_.resize(n_);
+  ctype_.resize(n_);
+  int j = 0;
+  for (VariableConstIterator v = problem_->varsBegin(); v != problem_->varsEnd(); ++v, ++j) {
+    clo_[j] = (*v)->getLb();
+    chi_[j] = (*v)->getUb();
+    ctype_[j] = (int32_t)(*v)->getType();
+  }
+}
+
+void HipLPEngine::load(ProblemPtr problem) {
+  problem_ = problem;
+  syncRows_();
+  double sense = 1.0;
+  LinearFunctionPtr lin = 0;
+  if (problem->getObjective()) {
+    lin = problem->getObjective()->getLinearFunction();
+    if (problem->getObjective()->getObjectiveType() == Maximize) sense = -1.0;
+  }
+  obj_.assign(n_, 0.0);
+  if (lin) {
+    int j = 0;
+    for (VariableConstIterator v = problem->varsBegin(); v != problem->varsEnd(); ++v, ++j)
+      obj_[j] = sense * lin->getWeight(*v);
+  }
+  delete sol_;
+  sol_ = new Solution(1E20, 0, problem_);
+  wsValid_ = false;
+  objChanged_ = bndChanged_ = consChanged_ = needUpload_ = true;
+  problem->setEngine(this);
+}
+
+int HipLPEngine::upload_() {
+  if (!ctx_) return MGPU_ERR_STATE;
+  // the objective constant is added at solve time, as OsiLPEngine does
+  return mgpu_load_lp(ctx_, n_, m_, rowptr_.data(), colidx_.empty() ? 0 : colidx_.data(),
+                      val_.empty() ? 0 : val_.data(), rlo_.data(), rhi_.data(), clo_.data(),
+                      chi_.data(), ctype_.data(), obj_.data(), 0.0);
+}
+
+// Gauss-Jordan inverse of the kept basis after the matrix changed (rows
+// edited / added / removed).  Falls back to the slack basis if singular.
+void HipLPEngine::refactor_() {
+  const int m = m_, n = n_;
+  if ((int)ws_.head.size() != m) {
+    wsValid_ = false;
+    return;
+  }
+  std::vector<double> B((size_t)m * m, 0.0), I((size_t)m * m, 0.0);
+  for (int i = 0; i < m; ++i) {
+    const int h = ws_.head[i];
+    if (h >= n) {
+      B[(size_t)(h - n) * m + i] = -1.0;
+    } else {
+      for (int r = 0; r < m; ++r)
+        for (int k = rowptr_[r]; k < rowptr_[r + 1]; ++k)
+          if (colidx_[k] == h) B[(size_t)r * m + i] = val_[k];
+    }
+    I[(size_t)i * m + i] = 1.0;
+  }
+  for (int c = 0; c < m; ++c) {
+    int piv = -1;
+    double best = 0;
+    for (int r = c; r < m; ++r)
+      if (std::fabs(B[(size_t)r * m + c]) > best) {
+        best = std::fabs(B[(size_t)r * m + c]);
+        piv = r;
+      }
+    if (piv < 0 || best < 1e-12) {
+      wsValid_ = false;
+      return;
+    }
+    for (int k = 0; k < m; ++k) {
+      std::swap(B[(size_t)c * m + k], B[(size_t)piv * m + k]);
+      std::swap(I[(size_t)c * m + k], I[(size_t)piv * m + k]);
+    }
+    const double inv = 1.0 / B[(size_t)c * m + c];
+    for (int k = 0; k < m; ++k) {
+      B[(size_t)c * m + k] *= inv;
+      I[(size_t)c * m + k] *= inv;
+    }
+    for (int r = 0; r < m; ++r) {
+      if (r == c) continue;
+      const double f = B[(size_t)r * m + c];
+      if (f == 0.0) continue;
+      for (int k = 0; k < m; ++k) {
+        B[(size_t)r * m + k] -= f * B[(size_t)c * m + k];
+        I[(size_t)r * m + k] -= f * I[(size_t)c * m + k];
+      }
+    }
+  }
+  ws_.binv.assign((size_t)m * m, 0.0);  // column-major (mgpu.h)
+  for (int i = 0; i < m; ++i)
+    for (int k = 0; k < m; ++k) ws_.binv[(size_t)k * m + i] = I[(size_t)i * m + k];
+  recomputeDuals_();
+}
+
+void HipLPEngine::recomputeDuals_() {
+  const int m = m_, n = n_, N = n_ + m_;
+  std::vector<double> y(m, 0.0);
+  for (int i = 0; i < m; ++i) {
+    const int h = ws_.head[i];
+    const double cb = h < n ? obj_[h] : 0.0;
+    if (cb != 0.0)
+      for (int k = 0; k < m; ++k) y[k] += cb * ws_.binv[(size_t)k * m + i];
+  }
+  ws_.d.assign(N, 0.0);
+  std::vector<double> aty(n, 0.0);
+  for (int r = 0; r < m; ++r)
+    for (int k = rowptr_[r]; k < rowptr_[r + 1]; ++k) aty[colidx_[k]] += val_[k] * y[r];
+  for (int j = 0; j < N; ++j) {
+    if (ws_.st[j] == 3) continue;
+    ws_.d[j] = j < n ? obj_[j] - aty[j] : y[j - n];
+  }
+}
+
+EngineStatus HipLPEngine::solve() {
+  double off = 0;
+  if (problem_->getObjective()) off = problem_->getObjective()->getConstant();
+  timer_->start();
+  stats_->calls += 1;
+  if (needUpload_ || consChanged_ || objChanged_) {
+    if (consChanged_) syncRows_();
+    if (upload_() != MGPU_OK) {
+      status_ = EngineError;
+      sol_->setObjValue(INFINITY);
+      timer_->stop();
+      return status_;
+    }
+    needUpload_ = false;
+    if (wsValid_ && consChanged_) refactor_();
+    else if (wsValid_ && objChanged_) recomputeDuals_();
+  }
+  // current column bounds (edits since the last solve)
+  const int n = n_, m = m_, N = n_ + m_;
+  int32_t st = 0, it = 0;
+  double obj = 0.0;
+  x_.assign(n, 0.0);
+  HipLPWarmStart out;
+  out.head.resize(m);
+  out.st.resize(N);
+  out.d.resize(N);
+  out.binv.resize((size_t)m * m);
+  int rc = mgpu_lp_solve(ctx_, 1, clo_.data(), chi_.data(), 0,
+                         wsValid_ ? ws_.head.data() : 0, wsValid_ ? ws_.st.data() : 0,
+                         wsValid_ ? ws_.d.data() : 0, wsValid_ ? ws_.binv.data() : 0, 1,
+                         iterLimit_, &st, &obj, &it, x_.data(), out.head.data(),
+                         out.st.data(), out.d.data(), out.binv.data());
+  if (rc != MGPU_OK) {
+    logger_->errStream() << me_ << mgpu_last_error(ctx_) << std::endl;
+    status_ = EngineError;
+    sol_->setObjValue(INFINITY);
+  } else {
+    status_ = (EngineStatus)st;
+    if (status_ == ProvenOptimal || status_ == EngineIterationLimit) {
+      ws_ = out;
+      wsValid_ = true;
+      // duals from the final basis: y = c_B B^-1, reduced costs d
+      y_.assign(m, 0.0);
+      for (int i = 0; i < m; ++i) {
+        const int h = ws_.head[i];
+        const double cb = h < n ? obj_[h] : 0.0;
+        if (cb != 0.0)
+          for (int k = 0; k < m; ++k) y_[k] += cb * ws_.binv[(size_t)k * m + i];
+      }
+      rc_.assign(n, 0.0);
+      for (int j = 0; j < n; ++j) rc_[j] = ws_.st[j] == 3 ? 0.0 : ws_.d[j];
+      sol_->setPrimal(x_.data());
+      sol_->setObjValue(obj + off);
+      sol_->setDualOfCons(y_.data());
+      sol_->setDualOfVars(rc_.data());
+    } else if (status_ == ProvenInfeasible) {
+      sol_->setObjValue(INFINITY);
+    } else if (status_ == ProvenUnbounded) {
+      sol_->setObjValue(-INFINITY);
+    } else {
+      sol_->setObjValue(INFINITY);
+    }
+  }
+  lastIters_ = it;
+  stats_->iters += it;
+  stats_->time += timer_->query();
+  if (strBr_) {
+    ++(stats_->strCalls);
+    stats_->strIters += it;
+    stats_->strTime += timer_->query();
+  }
+  timer_->stop();
+  bndChanged_ = consChanged_ = objChanged_ = false;
+  return status_;
+}
+
+void HipLPEngine::addConstraint(ConstraintPtr) {
+  // the new row's logical joins the basis (refactor_ on the next solve)
+  if (wsValid_) {
+    const int N = n_ + m_;
+    ws_.head.push_back(N);
+    ws_.st.push_back(3);
+    ws_.d.push_back(0.0);
+  }
+  consChanged_ = true;
+}
+
+void HipLPEngine::removeCons(std::vector<ConstraintPtr> &delcons) {
+  // basis kept only if every removed row's logical is basic
+  if (wsValid_) {
+    std::vector<char> del(m_, 0);
+    for (ConstraintPtr c : delcons) del[c->getIndex()] = 1;
+    std::vector<int32_t> head;
+    std::vector<int8_t> st;
+    std::vector<int> newidx(m_, -1);
+    int nm = 0;
+    for (int i = 0; i < m_; ++i)
+      if (!del[i]) newidx[i] = nm++;
+    bool ok = true;
+    for (int i = 0; i < m_; ++i) {
+      const int h = ws_.head[i];
+      if (h >= n_ && del[h - n_]) continue;
+      if (h >= n_) head.push_back(n_ + newidx[h - n_]);
+      else head.push_back(h);
+    }
+    if ((int)head.size() != nm) ok = false;
+    for (int j = 0; j < n_; ++j) st.push_back(ws_.st[j]);
+    for (int i = 0; i < m_; ++i)
+      if (!del[i]) st.push_back(ws_.st[n_ + i]);
+    if (ok) {
+      ws_.head = head;
+      ws_.st = st;
+    } else {
+      wsValid_ = false;
+    }
+  }
+  consChanged_ = true;
+}
+
+void HipLPEngine::changeBound(ConstraintPtr cons, BoundType lu, double new_val) {
+  if (Upper == lu) rhi_[cons->getIndex()] = new_val;
+  else rlo_[cons->getIndex()] = new_val;
+  needUpload_ = true;
+  bndChanged_ = true;
+}
+
+void HipLPEngine::changeBound(VariablePtr var, BoundType lu, double new_val) {
+  const int col = var->getIndex();
+  if (lu == Lower) clo_[col] = new_val;
+  else if (lu == Upper) chi_[col] = new_val;
+  bndChanged_ = true;
+}
+
+void HipLPEngine::changeBound(VariablePtr var, double new_lb, double new_ub) {
+  const int col = var->getIndex();
+  clo_[col] = new_lb;
+  chi_[col] = new_ub;
+  bndChanged_ = true;
+}
+
+void HipLPEngine::changeConstraint(ConstraintPtr, LinearFunctionPtr, double, double) {
+  // rows are re-read from problem_ on the next solve (the Problem applies
+  // the edit before forwarding it, Problem.cpp:273-291)
+  consChanged_ = true;
+}
+
+void HipLPEngine::changeConstraint(ConstraintPtr, NonlinearFunctionPtr) {
+  assert(!"Cannot change a nonlinear function in HipLPEngine");
+}
+
+void HipLPEngine::changeObj(FunctionPtr f, double) {
+  LinearFunctionPtr lf = (f) ? f->getLinearFunction() : 0;
+  std::fill(obj_.begin(), obj_.end(), 0.0);
+  if (lf)
+    for (VariableGroupConstIterator it = lf->termsBegin(); it != lf->termsEnd(); ++it)
+      obj_[it->first->getIndex()] = it->second;
+  objChanged_ = true;
+}
+
+void HipLPEngine::negateObj() {
+  // OsiLPEngine::negateObj copies the coefficients without negating them
+  // (OsiLPEngine.cpp:514-522); kept as is.
+  objChanged_ = true;
+}
+
+void HipLPEngine::clear() {
+  wsValid_ = false;
+  needUpload_ = true;
+  if (problem_) {
+    problem_->unsetEngine();
+    problem_ = 0;
+  }
+}
+
+void HipLPEngine::disableStrBrSetup() { strBr_ = false; }
+void HipLPEngine::enableStrBrSetup() { strBr_ = true; }
+
+EnginePtr HipLPEngine::emptyCopy() { return (EnginePtr) new HipLPEngine(env_, device_); }
+
+ConstSolutionPtr HipLPEngine::getSolution() { return sol_; }
+double HipLPEngine::getSolutionValue() { return sol_->getObjValue(); }
+std::string HipLPEngine::getName() const { return "HipLP"; }
+EngineStatus HipLPEngine::getStatus() { return status_; }
+
+ConstWarmStartPtr HipLPEngine::getWarmStart() { return &ws_; }
+
+WarmStartPtr HipLPEngine::getWarmStartCopy() {
+  HipLPWarmStartPtr w = new HipLPWarmStart();
+  if (wsValid_) *w = ws_;
+  return w;
+}
+
+void HipLPEngine::loadFromWarmStart(const WarmStartPtr ws) {
+  const HipLPWarmStart *w = dynamic_cast<const HipLPWarmStart *>(ws);
+  assert(w);
+  if (w && !w->head.empty() && (int)w->head.size() == m_ &&
+      (int)w->st.size() == n_ + m_) {
+    ws_ = *w;
+    wsValid_ = true;
+  }
+}
+
+void HipLPEngine::getBasics(int *index) {
+  for (int i = 0; i < m_ && wsValid_; ++i) index[i] = ws_.head[i];
+}
+
+void HipLPEngine::resetIterationLimit() { iterLimit_ = maxIterLimit_; }
+void HipLPEngine::setIterationLimit(int limit) { iterLimit_ = limit; }
+
+void HipLPEngine::fillStats(std::vector<double> &lpStats) {
+  if (lpStats.size()) {
+    lpStats[0] += stats_->calls;
+    lpStats[1] += stats_->strCalls;
+    lpStats[2] += stats_->time;
+    lpStats[3] += stats_->strTime;
+    lpStats[4] += stats_->iters;
+    lpStats[5] += stats_->strIters;
+  }
+}
+
+void HipLPEngine::writeStats(std::ostream &out) const {
+  std::string me = "HipLP: ";
+  out << me << "total calls            = " << stats_->calls << std::endl
+      << me << "strong branching calls = " << stats_->strCalls << std::endl
+      << me << "total time in solving  = " << stats_->time << std::endl
+      << me << "time in str branching  = " << stats_->strTime << std::endl
+      << me << "total iterations       = " << stats_->iters << std::endl
+      << me << "strong br iterations   = " << stats_->strIters << std::endl;
+}

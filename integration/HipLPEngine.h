@@ -1,0 +1,131 @@
+//
+// HipLPEngine — Minotaur LPEngine backed by the MI355X engine (include/mgpu.h).
+//
+// Drop-in for OsiLPEngine (src/interfaces/OsiLPEngine.{h,cpp}) behind the
+// unchanged src/base plugin surface: Engine (src/base/Engine.h:34-188) and
+// LPEngine (src/base/LPEngine.h:29-74).  Drivers obtain it from
+// EngineFactory::getLPEngine when the option lp_engine is "HipLP"
+// (INTEGRATION.md shows the 3-line factory patch).  One engine = one
+// mgpu context = one host thread (as OsiLPEngine, QGPar.cpp:712-715).
+//
+// This file is written against the reference headers and is compiled only
+// where /root/reference exists (oracle/Makefile target `integ`); it is the
+// binding a Minotaur maintainer adds, not part of the standalone engine.
+//
+#ifndef MINOTAURHIPLPENGINE_H
+#define MINOTAURHIPLPENGINE_H
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "LPEngine.h"
+#include "WarmStart.h"
+
+struct mgpu_ctx;
+
+namespace Minotaur {
+
+class Environment;
+class Problem;
+class Solution;
+class Timer;
+typedef Environment *EnvPtr;
+typedef Problem *ProblemPtr;
+typedef Solution *SolutionPtr;
+
+// Statistics kept like OsiLPStats (OsiLPEngine.h:35-42).
+struct HipLPStats {
+  UInt calls;
+  UInt strCalls;
+  double time;
+  double strTime;
+  UInt iters;
+  UInt strIters;
+};
+
+// Warm start = the engine's basis: basic column per row, column status,
+// reduced costs and the dense basis inverse (column-major).  The reference
+// keeps Clp's CoinWarmStartBasis (OsiLPEngine.cpp:375-384, 500-505).
+class HipLPWarmStart : public WarmStart {
+ public:
+  HipLPWarmStart() {}
+  ~HipLPWarmStart() {}
+  bool hasInfo() { return !head.empty(); }
+  void write(std::ostream &out) const;
+
+  std::vector<int32_t> head;
+  std::vector<int8_t> st;
+  std::vector<double> d;
+  std::vector<double> binv;
+};
+typedef HipLPWarmStart *HipLPWarmStartPtr;
+
+class HipLPEngine : public LPEngine {
+ public:
+  explicit HipLPEngine(EnvPtr env, int device = 0);
+  ~HipLPEngine();
+
+  // Engine interface (Engine.h:44-159)
+  void addConstraint(ConstraintPtr con);
+  void changeBound(ConstraintPtr cons, BoundType lu, double new_val);
+  void changeBound(VariablePtr var, BoundType lu, double new_val);
+  void changeBound(VariablePtr var, double new_lb, double new_ub);
+  void changeConstraint(ConstraintPtr c, LinearFunctionPtr lf, double lb, double ub);
+  void changeConstraint(ConstraintPtr c, NonlinearFunctionPtr nlf);
+  void changeObj(FunctionPtr f, double cb);
+  void clear();
+  void disableStrBrSetup();
+  EnginePtr emptyCopy();
+  void enableStrBrSetup();
+  ConstSolutionPtr getSolution();
+  double getSolutionValue();
+  EngineStatus solve();
+  std::string getName() const;
+  EngineStatus getStatus();
+  ConstWarmStartPtr getWarmStart();
+  WarmStartPtr getWarmStartCopy();
+  void load(ProblemPtr problem);
+  void loadFromWarmStart(const WarmStartPtr ws);
+  void negateObj();
+  void removeCons(std::vector<ConstraintPtr> &delcons);
+  void resetIterationLimit();
+  int setDualObjLimit(double) { return 0; }
+  void setIterationLimit(int limit);
+  void writeStats(std::ostream &out) const;
+  void fillStats(std::vector<double> &lpStats);
+
+  // LPEngine extras used by drivers
+  void getBasics(int *index);
+  int getNumCols() { return n_; }
+  int getNumRows() { return m_; }
+  int getIterationCount() { return lastIters_; }
+
+ private:
+  void syncRows_();            // re-read every row of problem_ (after edits)
+  void refactor_();            // host Gauss-Jordan of the kept basis
+  void recomputeDuals_();      // d = c - A'y, y = c_B B^-1
+  int upload_();
+
+  EnvPtr env_;
+  ProblemPtr problem_;
+  mgpu_ctx *ctx_;
+  int device_;
+  int n_, m_;
+  std::vector<int32_t> rowptr_, colidx_, ctype_;
+  std::vector<double> val_, rlo_, rhi_, clo_, chi_, obj_;
+  bool bndChanged_, consChanged_, objChanged_, needUpload_;
+  HipLPWarmStart ws_;
+  bool wsValid_;
+  SolutionPtr sol_;
+  int maxIterLimit_, iterLimit_, lastIters_;
+  bool strBr_;
+  HipLPStats *stats_;
+  Timer *timer_;
+  std::vector<double> x_, y_, rc_;
+  static const std::string me_;
+};
+typedef HipLPEngine *HipLPEnginePtr;
+
+}  // namespace Minotaur
+#endif

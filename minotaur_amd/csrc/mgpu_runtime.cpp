@@ -171,13 +171,17 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   const int nnz = rowptr[m];
   if (rowptr[0] != 0 || nnz < 0 || (nnz > 0 && (!colidx || !val)))
     return fail(c, MGPU_ERR_ARG, "mgpu_load_lp: bad CSR");
-  for (int i = 0; i < m; ++i) {
-    if (rowptr[i + 1] < rowptr[i]) return fail(c, MGPU_ERR_ARG, "rowptr not monotone at %d", i);
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-      if (colidx[k] < 0 || colidx[k] >= n)
-        return fail(c, MGPU_ERR_ARG, "column index out of range in row %d", i);
-      if (k > rowptr[i] && colidx[k] <= colidx[k - 1])
-        return fail(c, MGPU_ERR_ARG, "row %d columns not strictly ascending", i);
+  {
+    std::vector<int> seen(n, -1);  // a column may appear once per row
+    for (int i = 0; i < m; ++i) {
+      if (rowptr[i + 1] < rowptr[i]) return fail(c, MGPU_ERR_ARG, "rowptr not monotone at %d", i);
+      for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        if (colidx[k] < 0 || colidx[k] >= n)
+          return fail(c, MGPU_ERR_ARG, "column index out of range in row %d", i);
+        if (seen[colidx[k]] == i)
+          return fail(c, MGPU_ERR_ARG, "row %d has duplicate column %d", i, colidx[k]);
+        seen[colidx[k]] = i;
+      }
     }
   }
   HIPCHK(c, hipSetDevice(c->device));

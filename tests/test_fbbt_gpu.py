@@ -121,7 +121,7 @@ def test_errors_are_reported_not_thrown(ctx):
     p = _tls4()
     bad = LinProblem(**{**p.__dict__})
     bad.colidx = p.colidx.copy()
-    bad.colidx[1] = bad.colidx[0]          # not strictly ascending
-    with pytest.raises(MgpuError, match='ascending'):
+    bad.colidx[1] = bad.colidx[0]          # duplicate column in row 0
+    with pytest.raises(MgpuError, match='duplicate'):
         c.load(bad)
     c.close()

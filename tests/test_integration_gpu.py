@@ -1,0 +1,102 @@
+"""GPU: the reference's OWN solver stack with the MI355X engine plugged in
+through the unchanged plugin surface.
+
+oracle/_ref/libminotaur_hip_integ.so = Minotaur src/base (BranchAndBound,
+PCBProcessor, NodeIncRelaxer, ReliabilityBrancher, IntVarHandler,
+LinearHandler, ... compiled from /root/reference) + integration/HipLPEngine
+(LPEngine) + integration/HipLinearHandler (node FBBT) + libmgpu.so.  The
+tests restate AMPLOsiUT (src/testing/AMPLOsiUT.cpp:46-170) and check B&B
+optima against scipy HiGHS MILP.  Skipped where the reference build is
+absent (it is built in the container and travels prebuilt)."""
+import ctypes
+import math
+import os
+
+import numpy as np
+import pytest
+
+from minotaur_amd.problem import LinProblem, knapsack_oa, random_problem
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
+LIB = os.path.join(ROOT, 'oracle', '_ref', 'libminotaur_hip_integ.so')
+P = ctypes.c_void_p
+
+
+@pytest.fixture(scope='module')
+def integ():
+    if not os.path.exists(LIB):
+        pytest.skip("integration library not built (needs /root/reference at build time)")
+    from minotaur_amd import runtime
+    runtime.load_library()          # one HIP runtime in the process (torch's)
+    lib = ctypes.CDLL(LIB, mode=os.RTLD_LAZY | os.RTLD_GLOBAL)
+    lib.integ_lp0.argtypes = [ctypes.c_int, P, P, P]
+    lib.integ_lp_eg0.argtypes = [ctypes.c_int]
+    lib.integ_bnb.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int] + \
+        [P] * 9 + [ctypes.c_double, P, P]
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(P)
+
+
+def test_amplosiut_lp(integ):
+    out = np.zeros(4)
+    st = np.zeros(4, dtype=np.int32)
+    it = np.zeros(1, dtype=np.int32)
+    integ.integ_lp0(0, _p(out), _p(st), _p(it))
+    assert st[0] == 0 and abs(out[0] + 8.42857) < 1e-5          # testOsiLP
+    assert st[1] == 0 and abs(out[1] - 2.0) < 1e-5
+    assert st[2] == 0 and abs(out[2] + 2.0) < 1e-5
+    assert st[3] == 0 and abs(out[3] + 8.42857) < 1e-5 and it[0] == 0   # testOsiWarmStart
+    assert integ.integ_lp_eg0(0) == 2                             # testOsiLP2
+
+
+def _bnb(integ, p, hip_fbbt):
+    res = np.zeros(2)
+    cnt = np.zeros(3, dtype=np.int32)
+    maximize = 0
+    integ.integ_bnb(0, hip_fbbt, p.n, p.m, _p(p.rowptr), _p(p.colidx), _p(p.val), _p(p.rlo),
+                    _p(p.rhi), _p(p.vtype), _p(p.vlb), _p(p.vub), _p(p.obj), float(p.obj_const),
+                    _p(res), _p(cnt))
+    return res, cnt
+
+
+def _milp_opt(p):
+    from scipy.optimize import Bounds, LinearConstraint, milp
+    A = p.dense()
+    integrality = np.isin(p.vtype, (0, 1)).astype(int)
+    r = milp(p.obj, constraints=[LinearConstraint(A, p.rlo, p.rhi)],
+             bounds=Bounds(p.vlb, p.vub), integrality=integrality)
+    return (r.fun + p.obj_const) if r.status == 0 else math.inf
+
+
+def test_amplosiut_bnb_milp(integ):
+    """testOsiBnB: min x4 s.t. 2x0+2x1+2x2+2x3+x4 = 1, binaries -> UB 1."""
+    from minotaur_amd.problem import from_rows
+    p = from_rows('milp', 5, [[(0, 2), (1, 2), (2, 2), (3, 2), (4, 1)]], [1], [1],
+                  [0] * 5, [1] * 5, [0] * 5, [0, 0, 0, 0, 1])
+    for hip in (0, 1):
+        res, cnt = _bnb(integ, p, hip)
+        assert res[0] == 1.0
+
+
+@pytest.mark.parametrize('name', ['knapsack', 'random21', 'random22'])
+def test_bnb_gpu_fbbt_matches_reference_fbbt(integ, name):
+    """Same tree with the reference LinearHandler or HipLinearHandler (bit-
+    exact FBBT), and the optimum of HiGHS' MILP."""
+    if name == 'knapsack':
+        p = knapsack_oa(f=5, N=20)
+    else:
+        p = random_problem(int(name[6:]), n=14, m=10, density=0.3, inf_frac=0.0)
+    r0, c0 = _bnb(integ, p, 0)
+    r1, c1 = _bnb(integ, p, 1)
+    assert r0[0] == r1[0]
+    assert c0[1] == c1[1]            # identical number of LP solves
+    assert c1[2] > 0                 # node FBBT really ran on the GPU
+    opt = _milp_opt(p)
+    if math.isinf(opt):
+        assert math.isinf(r1[0])
+    else:
+        assert abs(r1[0] - opt) <= 1e-6 * max(1.0, abs(opt))
