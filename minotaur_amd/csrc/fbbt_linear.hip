@@ -163,7 +163,7 @@ __device__ __forceinline__ void lf_bnds(const TermRec *base, int nt, const TermC
 // getSingLfBnds_ (LinearHandler.cpp:1261-1319): sums that skip a single
 // infinite term; a second infinite term makes the side infinite.
 template <class V>
-__device__ void sing_lf_bnds(const TermRec *base, int nt, const TermChunk &pre, const V &v,
+__device__ __forceinline__ void sing_lf_bnds(const TermRec *base, int nt, const TermChunk &pre, const V &v,
                              double &lo, double &up) {
   double l = 0.0, u = 0.0;
   bool lo_sing = false, up_sing = false, lo_fin = true, up_fin = true;
@@ -228,7 +228,7 @@ __device__ __forceinline__ Term1 term_at(const TermRec *base, const TermChunk &p
 // its own column's bounds; the order-dependent effects (mod log, nintmods)
 // are produced in phase B in term order.
 template <class V>
-__device__ void upd_side(const TermRec *base, int nt, const TermChunk &pre, V &v,
+__device__ __forceinline__ void upd_side(const TermRec *base, int nt, const TermChunk &pre, V &v,
                          NodeState &s, const ModLog &log, double diff, bool from_lb,
                          bool is_sing, bool &changed, bool count_int) {
   for (int k0 = 0; k0 < nt; k0 += 4) {
@@ -304,10 +304,212 @@ __device__ __forceinline__ void upd_from_ub(const TermRec *base, int nt, const T
   upd_side(base, nt, pre, v, s, log, ub - ll, false, is_sing, changed, count_int);
 }
 
+// ---- register-cached rows ---------------------------------------------------
+// A row of nt <= RC terms is tightened with all of its bounds gathered into
+// registers ONCE (2*RC independent loads in flight), reused by the 4-5 passes
+// of linBndTighten_ and written through on every update.  The passes are
+// straight-line over RC slots; slots >= nt are masked.  Same arithmetic, same
+// order as the generic path (and the reference): sums run over k = 0..nt-1,
+// masked slots contribute nothing and never update.
+template <int RC>
+struct RowCache {
+  double l[RC], u[RC];
+  double a[RC];
+};
+
+template <int RC, class V>
+__device__ __forceinline__ void rc_load(RowCache<RC> &c, const TermChunk &pre, int nt,
+                                        const V &v) {
+#pragma unroll
+  for (int k = 0; k < RC; ++k) {
+    const int kk = k < nt ? k : 0;   // clamped: loads are unconditional
+    const int j = rl(pre.j, kk);
+    c.a[k] = k < nt ? rld(pre.a, kk) : 0.0;
+    c.l[k] = v.L(j);
+    c.u[k] = v.U(j);
+  }
+}
+
+template <int RC>
+__device__ __forceinline__ void rc_lf_bnds(const RowCache<RC> &c, int nt, double &lo,
+                                           double &up) {
+  double l = 0.0, u = 0.0;
+#pragma unroll
+  for (int k = 0; k < RC; ++k) {
+    if (k < nt) {
+      const double a = c.a[k];
+      if (a > 0) {
+        l += a * c.l[k];
+        u += a * c.u[k];
+      } else {
+        l += a * c.u[k];
+        u += a * c.l[k];
+      }
+    }
+  }
+  lo = l;
+  up = u;
+}
+
+template <int RC>
+__device__ __forceinline__ void rc_sing_lf_bnds(const RowCache<RC> &c, int nt, double &lo, double &up) {
+  double l = 0.0, u = 0.0;
+  bool lo_sing = false, up_sing = false, lo_fin = true, up_fin = true;
+#pragma unroll
+  for (int k = 0; k < RC; ++k) {
+    if (k >= nt) continue;
+    const double cc = c.a[k], vl = c.l[k], vu = c.u[k];
+    if (cc > kETol) {
+      if (vu < kInfty && up_fin) {
+        u += cc * vu;
+      } else if (up_sing) {
+        up_sing = false; u = INFINITY; up_fin = false;
+      } else {
+        up_sing = true;
+      }
+      if (vl > -kInfty && lo_fin) {
+        l += cc * vl;
+      } else if (lo_sing) {
+        lo_sing = false; l = -INFINITY; lo_fin = false;
+      } else {
+        lo_sing = true;
+      }
+    } else if (cc < -kETol) {
+      if (vu < kInfty && lo_fin) {
+        l += cc * vu;
+      } else if (lo_sing) {
+        lo_sing = false; l = -INFINITY; lo_fin = false;
+      } else {
+        lo_sing = true;
+      }
+      if (vl > -kInfty && up_fin) {
+        u += cc * vl;
+      } else if (up_sing) {
+        up_sing = false; u = INFINITY; up_fin = false;
+      } else {
+        up_sing = true;
+      }
+    }
+  }
+  lo = l;
+  up = u;
+}
+
+// upd_side on the cache: phase A computes every slot's candidate (RC
+// independent divisions), phase B applies hits in term order.
+template <int RC, class V>
+__device__ __forceinline__ void rc_upd_side(RowCache<RC> &c, int nt, const TermChunk &pre, V &v,
+                            NodeState &s, const ModLog &log, double diff, bool from_lb,
+                            bool is_sing, bool &changed, bool count_int) {
+  double cand[RC];
+  bool hit[RC];
+#pragma unroll
+  for (int k = 0; k < RC; ++k) {
+    const double cc = c.a[k];
+    const double vl = c.l[k], vu = c.u[k];
+    const bool act = k < nt && (cc > kETol || cc < -kETol);
+    const bool low = from_lb ? cc > 0 : cc < 0;
+    const double den = act ? cc : 1.0;
+    if (low) {
+      const bool ok = !is_sing || vu >= kInfty;
+      const double nb = diff / den + (vu >= kInfty ? 0. : vu);
+      hit[k] = act && ok && nb > vl + kETol;
+      cand[k] = nb;
+    } else {
+      const bool ok = !is_sing || vl <= -kInfty;
+      const double nb = diff / den + (vl <= -kInfty ? 0. : vl);
+      hit[k] = act && ok && nb < vu - kETol;
+      cand[k] = nb;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RC; ++k) {
+    if (k < nt && hit[k]) {
+      const Term1 t{c.a[k], rlu64(pre.cmask, k), rl(pre.j, k), rl(pre.cs, k), rl(pre.ce, k),
+                    rl(pre.isint, k)};
+      const bool low = from_lb ? t.a > 0 : t.a < 0;
+      double nb = cand[k];
+      if (low) {
+        if (nb > c.u[k] - kETol) nb = c.u[k];
+        v.change_bflag(t);
+        v.L(t.j) = nb;
+        c.l[k] = nb;
+        log.push(s, t.j, 0, nb);
+      } else {
+        if (nb < c.l[k] + kETol) nb = c.l[k];
+        v.change_bflag(t);
+        v.U(t.j) = nb;
+        c.u[k] = nb;
+        log.push(s, t.j, 1, nb);
+      }
+      if (count_int && t.isint) s.nintmods++;
+      changed = true;
+    }
+  }
+}
+
+// linBndTighten_ (LinearHandler.cpp:952-1045) on a register-cached row.
+template <int RC, class V>
+__device__ __forceinline__ bool rc_lin_bnd_tighten(int nt, const TermChunk &pre, double lb, double ub, V &v,
+                                   NodeState &s, const ModLog &log, bool &changed) {
+  RowCache<RC> c;
+  rc_load<RC>(c, pre, nt, v);
+  double ll, uu, sing_ll = -INFINITY, sing_uu = INFINITY;
+  changed = false;
+  rc_lf_bnds<RC>(c, nt, ll, uu);
+  if (ll < -kInfty || uu > kInfty) rc_sing_lf_bnds<RC>(c, nt, sing_ll, sing_uu);
+  if (ll > ub + kETol) return true;
+  if (uu < lb - kETol) return true;
+  if (lb > -kInfty) {
+    if (uu < kInfty) {
+      rc_upd_side<RC>(c, nt, pre, v, s, log, lb - uu, true, false, changed, true);
+    } else if (sing_uu < kInfty) {
+      rc_upd_side<RC>(c, nt, pre, v, s, log, lb - sing_uu, true, true, changed, true);
+    }
+  }
+  if (changed) {
+    rc_lf_bnds<RC>(c, nt, ll, uu);
+    if (ll < -kInfty || uu > kInfty) rc_sing_lf_bnds<RC>(c, nt, sing_ll, sing_uu);
+  }
+  if (ub < kInfty) {
+    if (ll > -kInfty) {
+      rc_upd_side<RC>(c, nt, pre, v, s, log, ub - ll, false, false, changed, true);
+    } else if (sing_ll > -kInfty) {
+      rc_upd_side<RC>(c, nt, pre, v, s, log, ub - sing_ll, false, true, changed, true);
+    }
+  }
+  return false;
+}
+
+// varBndsFromObj_ (LinearHandler.cpp:544-597) on a register-cached
+// objective (nobj <= RC).
+template <int RC, class V>
+__device__ __forceinline__ void rc_bnds_from_obj(int nobj, const TermChunk &pre, V &v, NodeState &s,
+                                 const ModLog &log, double ub, bool &changed) {
+  RowCache<RC> c;
+  rc_load<RC>(c, pre, nobj, v);
+  bool tch = true;
+  long guard = 0;
+  while (tch) {
+    double ll, uu, sing_ll = INFINITY, sing_uu = INFINITY;
+    tch = false;
+    rc_lf_bnds<RC>(c, nobj, ll, uu);
+    if (ll < -kInfty || uu > kInfty) rc_sing_lf_bnds<RC>(c, nobj, sing_ll, sing_uu);
+    if (ll > ub + kETol) return;
+    if (ll > -kInfty) {
+      rc_upd_side<RC>(c, nobj, pre, v, s, log, ub - ll, false, false, tch, false);
+    } else if (sing_ll > -kInfty) {
+      rc_upd_side<RC>(c, nobj, pre, v, s, log, ub - sing_ll, false, true, tch, false);
+    }
+    if (tch) changed = true;
+    if (++guard > 100000L) break;
+  }
+}
+
 // linBndTighten_ in node mode (LinearHandler.cpp:952-1045).  Returns true if
 // the row proves the node infeasible.
 template <class V>
-__device__ bool lin_bnd_tighten(const TermRec *base, int nt, const TermChunk &pre, double lb,
+__device__ __forceinline__ bool lin_bnd_tighten(const TermRec *base, int nt, const TermChunk &pre, double lb,
                                 double ub, V &v, NodeState &s, const ModLog &log,
                                 bool &changed) {
   double ll, uu, sing_ll = -INFINITY, sing_uu = INFINITY;
@@ -341,7 +543,7 @@ __device__ bool lin_bnd_tighten(const TermRec *base, int nt, const TermChunk &pr
 // change; the 100000 cap is a safety net never reached on real data (the
 // oracle uses the same cap).
 template <class V>
-__device__ void bnds_from_obj(const DevLP &lp, const TermChunk &pre, V &v, NodeState &s,
+__device__ __forceinline__ void bnds_from_obj(const DevLP &lp, const TermChunk &pre, V &v, NodeState &s,
                               const ModLog &log, double ub, bool &changed) {
   bool tch = true;
   long guard = 0;
@@ -364,7 +566,7 @@ __device__ void bnds_from_obj(const DevLP &lp, const TermChunk &pre, V &v, NodeS
 // tightenInts_ in node mode (LinearHandler.cpp:415-490), over the list of
 // Binary/Integer columns in ascending order.
 template <class V>
-__device__ void tighten_ints(const DevLP &lp, V &v, NodeState &s, const ModLog &log,
+__device__ __forceinline__ void tighten_ints(const DevLP &lp, V &v, NodeState &s, const ModLog &log,
                              bool act, bool &changed) {
   // called with the full wave active: `act` predicates this lane's updates
   for (int c0 = 0; c0 < lp.nint; c0 += kLanes) {
@@ -395,7 +597,7 @@ __device__ void tighten_ints(const DevLP &lp, V &v, NodeState &s, const ModLog &
 
 // checkBounds_ (LinearHandler.cpp:328-359); branch-free over the columns.
 template <class V>
-__device__ bool check_bounds(const DevLP &lp, const V &v) {
+__device__ __forceinline__ bool check_bounds(const DevLP &lp, const V &v) {
   bool bad = false;
   for (int j = 0; j < lp.n; ++j) bad |= v.L(j) > v.U(j) + kETol;
   return bad || lp.cons_bad != 0;
@@ -487,7 +689,12 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
           const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
           bool tch;
           v.clear(r);
-          if (lin_bnd_tighten(lp.trec + k0, nt, pre, rlo, rhi, v, s, log, tch)) {
+          bool inf;
+          if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
+          else inf = lin_bnd_tighten(lp.trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
+          if (inf) {
             cons_on = false;
           } else if (tch) {
             changed = true;
@@ -495,7 +702,10 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
         }
       }
     }
-    if (go && io.has_inc && lp.nobj > 0) bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
+    if (go && io.has_inc && lp.nobj > 0) {
+      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
+      else bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
+    }
     tighten_ints(lp, v, s, log, go, changed);
     if (go) infeas = check_bounds(lp, v);
   }
