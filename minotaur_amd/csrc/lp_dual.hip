@@ -398,8 +398,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         q = j;
       }
     }
-    wave_argmax(qa, q);
-    q = __builtin_amdgcn_readfirstlane(q);
+    wave_argmax_dpp(qa, q);
     if (qa == 0.0) {
       status = 2;
       break;

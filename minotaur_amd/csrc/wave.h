@@ -55,4 +55,57 @@ __device__ __forceinline__ void wave_argmax(double &v, int &idx) {
   }
 }
 
+// ---- DPP reductions --------------------------------------------------------
+// Cross-lane moves on the VALU (DPP) instead of ds_bpermute (LDS round trip):
+// quad_perm xor 1 / xor 2, then row_ror 4 / 8 inside each 16-lane row, then
+// the four row results are combined through v_readlane.  The result is wave
+// uniform (in SGPRs).  Exchange patterns only, so any associative,
+// commutative combine gives the same answer in every lane.
+constexpr int kDppXor1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int kDppRor4 = 0x124;  // row_ror:4
+constexpr int kDppRor8 = 0x128;  // row_ror:8
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_i32<CTRL>((int)(b & 0xffffffffLL));
+  const int hi = dpp_i32<CTRL>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ void amax_combine(double &v, int &i, double v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) {
+    v = v2;
+    i = i2;
+  }
+}
+
+// Arg-max over the wave (larger value wins, equal values -> lower index).
+__device__ __forceinline__ void wave_argmax_dpp(double &v, int &idx) {
+  amax_combine(v, idx, dpp_f64<kDppXor1>(v), dpp_i32<kDppXor1>(idx));
+  amax_combine(v, idx, dpp_f64<kDppXor2>(v), dpp_i32<kDppXor2>(idx));
+  amax_combine(v, idx, dpp_f64<kDppRor4>(v), dpp_i32<kDppRor4>(idx));
+  amax_combine(v, idx, dpp_f64<kDppRor8>(v), dpp_i32<kDppRor8>(idx));
+  double r = rld(v, 0);
+  int ri = rl(idx, 0);
+  amax_combine(r, ri, rld(v, 16), rl(idx, 16));
+  amax_combine(r, ri, rld(v, 32), rl(idx, 32));
+  amax_combine(r, ri, rld(v, 48), rl(idx, 48));
+  v = r;
+  idx = ri;
+}
+
+__device__ __forceinline__ double wave_min_dpp(double v) {
+  v = fmin(v, dpp_f64<kDppXor1>(v));
+  v = fmin(v, dpp_f64<kDppXor2>(v));
+  v = fmin(v, dpp_f64<kDppRor4>(v));
+  v = fmin(v, dpp_f64<kDppRor8>(v));
+  return fmin(fmin(rld(v, 0), rld(v, 16)), fmin(rld(v, 32), rld(v, 48)));
+}
+
 }  // namespace mgpu
