@@ -81,7 +81,6 @@ template <class F>
 __device__ __forceinline__ void for_terms(const TermRec *base, int nt, const TermChunk &pre,
                                           F &&f) {
   const int cnt = nt < kLanes ? nt : kLanes;
-#pragma unroll 4
   for (int k = 0; k < cnt; ++k)
     f(Term1{rld(pre.a, k), rlu64(pre.cmask, k), rl(pre.j, k), rl(pre.cs, k), rl(pre.ce, k),
             rl(pre.isint, k)});
@@ -572,7 +571,6 @@ __device__ __forceinline__ void tighten_ints(const DevLP &lp, V &v, NodeState &s
   for (int c0 = 0; c0 < lp.nint; c0 += kLanes) {
     const int cnt = lp.nint - c0 < kLanes ? lp.nint - c0 : kLanes;
     const TermChunk ch = load_terms(lp.irec + c0, cnt, v.lane);
-#pragma unroll 2
     for (int k = 0; k < cnt; ++k) {
       const Term1 t{0.0, rlu64(ch.cmask, k), rl(ch.j, k), rl(ch.cs, k), rl(ch.ce, k), 1};
       const int j = t.j;

@@ -27,6 +27,29 @@
 #include "wave.h"
 
 namespace mgpu {
+
+#ifdef MGPU_STAMPS
+// Diagnostic build only (-DMGPU_STAMPS, tools/lp_stamps.py): s_memtime
+// cycles per section summed over all waves; never compiled into the product.
+__device__ unsigned long long g_lp_stamps[16];
+#define STAMP_DECL unsigned long long st_acc[10] = {0}, st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                              \
+  do {                                                        \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += t_ - st_t;                                   \
+    st_t = t_;                                                \
+  } while (0)
+#define STAMP_FLUSH                                            \
+  if (lane == 0)                                               \
+    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_lp_stamps[i_], st_acc[i_]);
+#else
+#define STAMP_DECL
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#define STAMP_FLUSH
+#endif
+
 namespace {
 
 constexpr double kPTol = 1e-7;    // primal feasibility (Clp default)
@@ -207,6 +230,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     return;
   }
 
+  STAMP_DECL
   // ---- working bounds; an empty box is infeasible before any pivot ----
   bool bad = false;
   for (int j = lane; j < N; j += 64) {
@@ -286,6 +310,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
 
   int status = kUnknownStatus, iters = 0;
   bool fresh = true;
+  STAMP(0);
   for (;;) {
     // ---- pricing: most infeasible basic row (Dantzig), lowest row on ties
     double inf = 0.0;
@@ -328,6 +353,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       break;
     }
     const double delta = rld(inf, r);
+    STAMP(1);
 
     // ---- row r of B^{-1} to LDS (read back as a broadcast) ----
     if (lane == r) {
@@ -342,6 +368,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     wave_sync();
     const double sigma = delta > 0 ? 1.0 : -1.0;
 
+    STAMP(2);
     // ---- pivot row and Harris pass 1 ----
     double tmax = INFINITY;
     for (int j = lane; j < N; j += 64) {
@@ -381,6 +408,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       fresh = true;
       continue;
     }
+    STAMP(3);
     // ---- Harris pass 2: largest |alpha| among ratios <= tmax ----
     double qa = 0.0;
     int q = INT_MAX;
@@ -404,6 +432,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       break;
     }
 
+    STAMP(4);
     // ---- column q: alpha_q = B^{-1} a_q (a_q one element per lane) ----
     double aqk;
     if (q < n) {
@@ -421,6 +450,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     for (int k = 0; k < kLpMaxM; ++k) alq += binv[k] * rld(aqk, k);
     const double arq = rld(alq, r);
 
+    STAMP(5);
     // ---- steps ----
     double theta_d = C.d[q] / C.al[q];
     if (sigma * theta_d < 0) theta_d = 0.0;
@@ -455,6 +485,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       lbB = art_q ? C.tlo(q) : bloq;
       ubB = art_q ? C.thi(q) : bhiq;
     }
+    STAMP(6);
     // ---- rank-1 update of B^{-1} ----
     const double inv = 1.0 / arq;
 #pragma unroll
@@ -462,6 +493,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       const double nr = C.rho[k] * inv;
       binv[k] = lane == r ? nr : binv[k] - alq * nr;
     }
+    STAMP(7);
     ++iters;
     fresh = false;
     if (iters % 64 == 0) {
@@ -471,6 +503,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   }
 
   // ---- outputs ----
+  STAMP(8);
   wave_sync();
   if (status == 0 || status == 6) {
     if (lane < m) C.z[h] = zB;
@@ -501,9 +534,24 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     io.status[b] = status;
     io.iters[b] = iters;
   }
+  STAMP(9);
+  STAMP_FLUSH
 }
 
 }  // namespace
+
+#ifdef MGPU_STAMPS
+extern "C" int mgpu_debug_lp_stamps(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lp_stamps), sizeof(unsigned long long) * 16) !=
+      hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lp_stamps), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 size_t lp_lds_bytes(int n, int m, int nnz) {
   return shared_a_bytes(n, m, nnz) + (size_t)kLpWaves * wave_bytes(n + m);

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libmgpu.so')
+# MGPU_LIB overrides the library (diagnostic builds in tools/ only)
+LIB_PATH = os.environ.get('MGPU_LIB', os.path.join(HERE, 'libmgpu.so'))
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

@@ -1,0 +1,53 @@
+"""Diagnostic: where K3 spends its cycles.  Builds a stamped variant of
+libmgpu (-DMGPU_STAMPS) into /tmp, runs the LP probe workload and prints the
+s_memtime share of each section (see cdna_hip_programming.md §7: read the
+SHARES, not the run time, of a stamped build)."""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
+sys.path.insert(0, ROOT)
+OUT = os.environ.get('STAMP_LIB', os.path.join(ROOT, 'gpurun_out', 'libmgpu_stamps.so'))
+NAMES = ['setup', 'pricing', 'rho_write', 'pass1+min', 'pass2+argmax', 'column_q',
+         'steps/updates', 'binv_update', 'tail', 'outputs']
+
+
+def build():
+    from minotaur_amd import build as b
+    srcs = [os.path.join(b.CSRC, x) for x in b.SOURCES]
+    cmd = [b.HIPCC] + b.FLAGS + ['-DMGPU_STAMPS', '-I', os.path.join(ROOT, 'include'),
+                                 '-o', OUT] + srcs
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    if not os.path.exists(OUT):
+        build()
+    os.environ['MGPU_LIB'] = OUT
+    import numpy as np
+    import torch
+    from minotaur_amd.problem import LinProblem, random_boxes
+    from minotaur_amd.runtime import Context, WarmStart, load_library
+    lib = load_library()
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_lin.npz'))
+    ctx = Context(0)
+    ctx.load(p)
+    root, wsh = ctx.root_solve()
+    B = 65536
+    LB, UB = random_boxes(p, B, 20261015)
+    f = ctx.fbbt(LB, UB)
+    buf = (ctypes.c_ulonglong * 16)()
+    lib.mgpu_debug_lp_stamps(buf, 1)
+    r = ctx.lp_solve(f.lb, f.ub, wsh, skip=f.infeasible)
+    lib.mgpu_debug_lp_stamps(buf, 1)
+    tot = sum(buf[i] for i in range(10))
+    piv = int(r.iters.sum())
+    print(f"pivots {piv}  total wave-cycles {tot:.3e}  per pivot {tot / max(piv, 1):.0f}")
+    for i, nme in enumerate(NAMES):
+        print(f"  {nme:14s} {100.0 * buf[i] / tot:6.2f} %   {buf[i] / max(piv, 1):9.0f} cyc/pivot")
+
+
+if __name__ == '__main__':
+    main()
