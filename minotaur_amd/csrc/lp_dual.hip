@@ -68,6 +68,13 @@ __host__ __device__ inline size_t shared_a_bytes(int n, int m, int nnz) {
   return al16((size_t)(n + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
          al16((size_t)(m + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8);
 }
+// Shared warm start (one basis for every node, e.g. the root optimum)
+// staged once per workgroup: B^-1 (column-major), reduced costs, status,
+// basic columns.
+__host__ __device__ inline size_t shared_ws_bytes(int n, int m) {
+  return al16((size_t)m * m * 8) + al16((size_t)(n + m) * 8) + al16((size_t)(n + m)) +
+         al16((size_t)m * 4);
+}
 __host__ __device__ inline size_t wave_bytes(int N) {
   return 5 * al16((size_t)N * 8) + 2 * al16((size_t)N) + 2 * 64 * 8;
 }
@@ -175,7 +182,7 @@ __device__ __forceinline__ double compute_primals(const Ctx &C, const double (&b
   return -s;
 }
 
-template <int W>
+template <int W, bool kSharedWs>
 __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz;
@@ -196,6 +203,21 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     s_cval[t] = lp.cval[t];
     s_ccol[t] = lp.ccol[t];
     s_rval[t] = lp.rval[t];
+  }
+  double *s_wbinv = nullptr, *s_wd = nullptr;
+  int8_t *s_wst = nullptr;
+  int32_t *s_whead = nullptr;
+  if constexpr (kSharedWs) {
+    s_wbinv = (double *)p;  p += al16((size_t)m * m * 8);
+    s_wd = (double *)p;     p += al16((size_t)N * 8);
+    s_wst = (int8_t *)p;    p += al16((size_t)N);
+    s_whead = (int32_t *)p; p += al16((size_t)m * 4);
+    for (int t = threadIdx.x; t < m * m; t += 64 * W) s_wbinv[t] = io.ws.binv[t];
+    for (int t = threadIdx.x; t < N; t += 64 * W) {
+      s_wd[t] = io.ws.d[t];
+      s_wst[t] = io.ws.st[t];
+    }
+    for (int t = threadIdx.x; t < m; t += 64 * W) s_whead[t] = io.ws.head[t];
   }
   __syncthreads();
 
@@ -253,10 +275,10 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   double binv[kLpMaxM];
   int h = -1;
   if (warm) {
-    const int32_t *wh = io.ws.head + (size_t)b * io.ws.s_head;
-    const int8_t *wst = io.ws.st + (size_t)b * io.ws.s_st;
-    const double *wd = io.ws.d + (size_t)b * io.ws.s_d;
-    const double *wb = io.ws.binv + (size_t)b * io.ws.s_binv;
+    const int32_t *wh = kSharedWs ? s_whead : io.ws.head + (size_t)b * io.ws.s_head;
+    const int8_t *wst = kSharedWs ? s_wst : io.ws.st + (size_t)b * io.ws.s_st;
+    const double *wd = kSharedWs ? s_wd : io.ws.d + (size_t)b * io.ws.s_d;
+    const double *wb = kSharedWs ? s_wbinv : io.ws.binv + (size_t)b * io.ws.s_binv;
     for (int j = lane; j < N; j += 64) {
       const int8_t s = wst[j];
       C.st[j] = s == ST_BASIC ? ST_LB : s;
@@ -557,21 +579,36 @@ size_t lp_lds_bytes(int n, int m, int nnz) {
   return shared_a_bytes(n, m, nnz) + (size_t)kLpWaves * wave_bytes(n + m);
 }
 
+static size_t lp_lds_bytes_shared(int n, int m, int nnz) {
+  return lp_lds_bytes(n, m, nnz) + shared_ws_bytes(n, m);
+}
+
 hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, hipStream_t stream) {
   if (io.batch <= 0) return hipSuccess;
   if (lp.m > kLpMaxM) return hipErrorInvalidValue;
-  const size_t lds = lp_lds_bytes(lp.n, lp.m, lp.nnz);
+  const bool shared = io.ws.head != nullptr && io.ws.s_head == 0 && io.ws.s_st == 0 &&
+                      io.ws.s_d == 0 && io.ws.s_binv == 0 &&
+                      lp_lds_bytes_shared(lp.n, lp.m, lp.nnz) <= 160 * 1024;
+  const size_t lds = shared ? lp_lds_bytes_shared(lp.n, lp.m, lp.nnz)
+                            : lp_lds_bytes(lp.n, lp.m, lp.nnz);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)lp_dual_kernel<kLpWaves>,
+    hipError_t e = hipFuncSetAttribute((const void *)lp_dual_kernel<kLpWaves, false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void *)lp_dual_kernel<kLpWaves, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int blocks = (io.batch + kLpWaves - 1) / kLpWaves;
-  hipLaunchKernelGGL(lp_dual_kernel<kLpWaves>, dim3(blocks), dim3(64 * kLpWaves), lds, stream,
-                     lp, io);
+  if (shared)
+    hipLaunchKernelGGL((lp_dual_kernel<kLpWaves, true>), dim3(blocks), dim3(64 * kLpWaves), lds,
+                       stream, lp, io);
+  else
+    hipLaunchKernelGGL((lp_dual_kernel<kLpWaves, false>), dim3(blocks), dim3(64 * kLpWaves), lds,
+                       stream, lp, io);
   return hipGetLastError();
 }
 
