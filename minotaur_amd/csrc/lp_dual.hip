@@ -186,7 +186,7 @@ template <int W, bool kSharedWs>
 __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
   // ---- stage the constraint matrix (CSC + CSR) once per workgroup ----
   unsigned char *p = smem;
@@ -221,342 +221,349 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   }
   __syncthreads();
 
-  const int b = blockIdx.x * W + wave;
-  if (b >= io.batch) return;  // no workgroup barrier below this point
-
-  unsigned char *wp = p + (size_t)wave * wave_bytes(N);
-  Ctx C;
-  C.colptr = s_colptr; C.rowidx = s_rowidx; C.cval = s_cval;
-  C.rowptr = s_rowptr; C.ccol = s_ccol; C.rval = s_rval;
-  C.d = (double *)wp;   wp += al16((size_t)N * 8);
-  C.z = (double *)wp;   wp += al16((size_t)N * 8);
-  C.blo = (double *)wp; wp += al16((size_t)N * 8);
-  C.bhi = (double *)wp; wp += al16((size_t)N * 8);
-  C.al = (double *)wp;  wp += al16((size_t)N * 8);
-  C.st = (int8_t *)wp;  wp += al16((size_t)N);
-  C.art = (int8_t *)wp; wp += al16((size_t)N);
-  C.rho = (double *)wp; wp += 64 * 8;
-  C.aq = (double *)wp;
-  C.n = n; C.m = m; C.N = N;
-  C.nlb = io.lb + (size_t)b * n;
-  C.nub = io.ub + (size_t)b * n;
-  C.rlo = lp.rlo; C.rhi = lp.rhi; C.c = lp.objd;
-  C.lane = lane;
-
-  if (io.skip != nullptr && io.skip[b] != 0) {  // pruned by FBBT: not solved
-    if (lane == 0) {
-      io.status[b] = kUnknownStatus;
-      io.obj[b] = INFINITY;
-      io.iters[b] = 0;
-    }
-    return;
-  }
-
+  // Persistent waves: the matrix (and a shared warm start) were staged once
+  // for the workgroup; each wave then solves nodes b, b + grid*W, ...
+  // (no workgroup barrier below this point).
   STAMP_DECL
-  // ---- working bounds; an empty box is infeasible before any pivot ----
-  bool bad = false;
-  for (int j = lane; j < N; j += 64) {
-    C.blo[j] = C.tlo(j);
-    C.bhi[j] = C.thi(j);
-    C.art[j] = 0;
-    bad |= C.blo[j] > C.bhi[j] + kPTol;
-  }
-  if (__any(bad)) {
-    if (lane == 0) {
-      io.status[b] = 2;
-      io.obj[b] = INFINITY;
-      io.iters[b] = 0;
-    }
-    return;
-  }
+  for (int b = blockIdx.x * W + wave; b < io.batch; b += gridDim.x * W) {
 
-  // ---- basis: warm start (parent / root optimum) or slack basis ----
-  const bool warm = io.ws.head != nullptr;
-  double binv[kLpMaxM];
-  int h = -1;
-  if (warm) {
-    const int32_t *wh = kSharedWs ? s_whead : io.ws.head + (size_t)b * io.ws.s_head;
-    const int8_t *wst = kSharedWs ? s_wst : io.ws.st + (size_t)b * io.ws.s_st;
-    const double *wd = kSharedWs ? s_wd : io.ws.d + (size_t)b * io.ws.s_d;
-    const double *wb = kSharedWs ? s_wbinv : io.ws.binv + (size_t)b * io.ws.s_binv;
-    for (int j = lane; j < N; j += 64) {
-      const int8_t s = wst[j];
-      C.st[j] = s == ST_BASIC ? ST_LB : s;
-    }
-    if (lane < m) h = wh[lane];
-    wave_sync();
-    if (lane < m) C.st[h] = ST_BASIC;
-    wave_sync();
-    for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
-#pragma unroll
-    for (int k = 0; k < kLpMaxM; ++k)
-      binv[k] = (lane < m && k < m) ? wb[(size_t)k * m + lane] : 0.0;  // column-major: coalesced
-  } else {
-    if (lane < m) h = n + lane;
-    for (int j = lane; j < N; j += 64) {
-      C.st[j] = j >= n ? ST_BASIC : ST_LB;
-      C.d[j] = j < n ? C.c[j] : 0.0;  // y = 0 for the slack basis
-    }
-#pragma unroll
-    for (int k = 0; k < kLpMaxM; ++k) binv[k] = (k == lane && lane < m) ? -1.0 : 0.0;
-  }
-  wave_sync();
-  double art_bound = kArt0;
-  for (int j = lane; j < N; j += 64) {
-    if (C.st[j] == ST_BASIC) continue;
-    const double lo = C.blo[j], hi = C.bhi[j], dj = C.d[j];
-    bool keep = false;
-    if (warm) {
-      const int8_t s = C.st[j];
-      if (s == ST_LB && lo > -kInfB && dj >= -kDTol) {
-        C.z[j] = lo;
-        keep = true;
-      } else if (s == ST_UB && hi < kInfB && dj <= kDTol) {
-        C.z[j] = hi;
-        keep = true;
-      } else if (lo == hi && lo > -kInfB) {
-        C.st[j] = ST_LB;
-        C.z[j] = lo;
-        keep = true;
+    // lane index made opaque per node: otherwise LICM hoists the 64
+    // loop-invariant B^-1 init values / LDS addresses out of the node loop
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    unsigned char *wp = p + (size_t)wave * wave_bytes(N);
+    Ctx C;
+    C.colptr = s_colptr; C.rowidx = s_rowidx; C.cval = s_cval;
+    C.rowptr = s_rowptr; C.ccol = s_ccol; C.rval = s_rval;
+    C.d = (double *)wp;   wp += al16((size_t)N * 8);
+    C.z = (double *)wp;   wp += al16((size_t)N * 8);
+    C.blo = (double *)wp; wp += al16((size_t)N * 8);
+    C.bhi = (double *)wp; wp += al16((size_t)N * 8);
+    C.al = (double *)wp;  wp += al16((size_t)N * 8);
+    C.st = (int8_t *)wp;  wp += al16((size_t)N);
+    C.art = (int8_t *)wp; wp += al16((size_t)N);
+    C.rho = (double *)wp; wp += 64 * 8;
+    C.aq = (double *)wp;
+    C.n = n; C.m = m; C.N = N;
+    C.nlb = io.lb + (size_t)b * n;
+    C.nub = io.ub + (size_t)b * n;
+    C.rlo = lp.rlo; C.rhi = lp.rhi; C.c = lp.objd;
+    C.lane = lane;
+
+    if (io.skip != nullptr && io.skip[b] != 0) {  // pruned by FBBT: not solved
+      if (lane == 0) {
+        io.status[b] = kUnknownStatus;
+        io.obj[b] = INFINITY;
+        io.iters[b] = 0;
       }
+      continue;
     }
-    if (!keep) place_nonbasic(C, j, art_bound);
-  }
-  wave_sync();
-  double lbB = 0.0, ubB = 0.0;
-  if (lane < m) {
-    lbB = C.blo[h];
-    ubB = C.bhi[h];
-  }
-  double zB = compute_primals(C, binv);
 
-  int status = kUnknownStatus, iters = 0;
-  bool fresh = true;
-  STAMP(0);
-  for (;;) {
-    // ---- pricing: most infeasible basic row (Dantzig), lowest row on ties
-    double inf = 0.0;
-    if (lane < m) {
-      if (zB < lbB - kPTol) inf = zB - lbB;
-      else if (zB > ubB + kPTol) inf = zB - ubB;
+    // ---- working bounds; an empty box is infeasible before any pivot ----
+    bool bad = false;
+    for (int j = lane; j < N; j += 64) {
+      C.blo[j] = C.tlo(j);
+      C.bhi[j] = C.thi(j);
+      C.art[j] = 0;
+      bad |= C.blo[j] > C.bhi[j] + kPTol;
     }
-    double best = fabs(inf);
-    int r = best > 0.0 ? lane : INT_MAX;
-    wave_argmax(best, r);
-    r = __builtin_amdgcn_readfirstlane(r);
-    if (best == 0.0) {
-      if (!fresh) {
+    if (__any(bad)) {
+      if (lane == 0) {
+        io.status[b] = 2;
+        io.obj[b] = INFINITY;
+        io.iters[b] = 0;
+      }
+      continue;
+    }
+
+    // ---- basis: warm start (parent / root optimum) or slack basis ----
+    const bool warm = io.ws.head != nullptr;
+    double binv[kLpMaxM];
+    int h = -1;
+    if (warm) {
+      const int32_t *wh = kSharedWs ? s_whead : io.ws.head + (size_t)b * io.ws.s_head;
+      const int8_t *wst = kSharedWs ? s_wst : io.ws.st + (size_t)b * io.ws.s_st;
+      const double *wd = kSharedWs ? s_wd : io.ws.d + (size_t)b * io.ws.s_d;
+      const double *wb = kSharedWs ? s_wbinv : io.ws.binv + (size_t)b * io.ws.s_binv;
+      for (int j = lane; j < N; j += 64) {
+        const int8_t s = wst[j];
+        C.st[j] = s == ST_BASIC ? ST_LB : s;
+      }
+      if (lane < m) h = wh[lane];
+      wave_sync();
+      if (lane < m) C.st[h] = ST_BASIC;
+      wave_sync();
+      for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
+  #pragma unroll
+      for (int k = 0; k < kLpMaxM; ++k)
+        binv[k] = (lane < m && k < m) ? wb[(size_t)k * m + lane] : 0.0;  // column-major: coalesced
+    } else {
+      if (lane < m) h = n + lane;
+      for (int j = lane; j < N; j += 64) {
+        C.st[j] = j >= n ? ST_BASIC : ST_LB;
+        C.d[j] = j < n ? C.c[j] : 0.0;  // y = 0 for the slack basis
+      }
+  #pragma unroll
+      for (int k = 0; k < kLpMaxM; ++k) binv[k] = (k == lane && lane < m) ? -1.0 : 0.0;
+    }
+    wave_sync();
+    double art_bound = kArt0;
+    for (int j = lane; j < N; j += 64) {
+      if (C.st[j] == ST_BASIC) continue;
+      const double lo = C.blo[j], hi = C.bhi[j], dj = C.d[j];
+      bool keep = false;
+      if (warm) {
+        const int8_t s = C.st[j];
+        if (s == ST_LB && lo > -kInfB && dj >= -kDTol) {
+          C.z[j] = lo;
+          keep = true;
+        } else if (s == ST_UB && hi < kInfB && dj <= kDTol) {
+          C.z[j] = hi;
+          keep = true;
+        } else if (lo == hi && lo > -kInfB) {
+          C.st[j] = ST_LB;
+          C.z[j] = lo;
+          keep = true;
+        }
+      }
+      if (!keep) place_nonbasic(C, j, art_bound);
+    }
+    wave_sync();
+    double lbB = 0.0, ubB = 0.0;
+    if (lane < m) {
+      lbB = C.blo[h];
+      ubB = C.bhi[h];
+    }
+    double zB = compute_primals(C, binv);
+
+    int status = kUnknownStatus, iters = 0;
+    bool fresh = true;
+    STAMP(0);
+    for (;;) {
+      // ---- pricing: most infeasible basic row (Dantzig), lowest row on ties
+      double inf = 0.0;
+      if (lane < m) {
+        if (zB < lbB - kPTol) inf = zB - lbB;
+        else if (zB > ubB + kPTol) inf = zB - ubB;
+      }
+      double best = fabs(inf);
+      int r = best > 0.0 ? lane : INT_MAX;
+      wave_argmax(best, r);
+      r = __builtin_amdgcn_readfirstlane(r);
+      if (best == 0.0) {
+        if (!fresh) {
+          zB = compute_primals(C, binv);
+          fresh = true;
+          continue;
+        }
+        bool grow = false;
+        for (int j = lane; j < N; j += 64) {
+          const int8_t a = C.art[j], s = C.st[j];
+          if (s == ST_BASIC || !a) continue;
+          if ((s == ST_LB && (a & 1)) || (s == ST_UB && (a & 2))) grow = true;
+        }
+        if (!__any(grow)) {
+          status = 0;
+          break;
+        }
+        if (art_bound >= 1e13) {
+          status = 4;
+          break;
+        }
+        art_bound *= 1e3;
+        grow_art(C, art_bound);
         zB = compute_primals(C, binv);
         fresh = true;
         continue;
       }
-      bool grow = false;
+      if (iters >= io.iter_limit) {
+        status = 6;
+        break;
+      }
+      const double delta = rld(inf, r);
+      STAMP(1);
+
+      // ---- row r of B^{-1} to LDS (read back as a broadcast) ----
+      if (lane == r) {
+  #pragma unroll
+        for (int k = 0; k < kLpMaxM; k += 2) {
+          double2 v;
+          v.x = binv[k];
+          v.y = binv[k + 1];
+          *reinterpret_cast<double2 *>(C.rho + k) = v;
+        }
+      }
+      wave_sync();
+      const double sigma = delta > 0 ? 1.0 : -1.0;
+
+      STAMP(2);
+      // ---- pivot row and Harris pass 1 ----
+      double tmax = INFINITY;
       for (int j = lane; j < N; j += 64) {
-        const int8_t a = C.art[j], s = C.st[j];
-        if (s == ST_BASIC || !a) continue;
-        if ((s == ST_LB && (a & 1)) || (s == ST_UB && (a & 2))) grow = true;
-      }
-      if (!__any(grow)) {
-        status = 0;
-        break;
-      }
-      if (art_bound >= 1e13) {
-        status = 4;
-        break;
-      }
-      art_bound *= 1e3;
-      grow_art(C, art_bound);
-      zB = compute_primals(C, binv);
-      fresh = true;
-      continue;
-    }
-    if (iters >= io.iter_limit) {
-      status = 6;
-      break;
-    }
-    const double delta = rld(inf, r);
-    STAMP(1);
-
-    // ---- row r of B^{-1} to LDS (read back as a broadcast) ----
-    if (lane == r) {
-#pragma unroll
-      for (int k = 0; k < kLpMaxM; k += 2) {
-        double2 v;
-        v.x = binv[k];
-        v.y = binv[k + 1];
-        *reinterpret_cast<double2 *>(C.rho + k) = v;
-      }
-    }
-    wave_sync();
-    const double sigma = delta > 0 ? 1.0 : -1.0;
-
-    STAMP(2);
-    // ---- pivot row and Harris pass 1 ----
-    double tmax = INFINITY;
-    for (int j = lane; j < N; j += 64) {
-      const int8_t s = C.st[j];
-      double a = 0.0;
-      if (s != ST_BASIC && C.blo[j] != C.bhi[j]) {
-        if (j >= n) {
-          a = -C.rho[j - n];
-        } else {
-          for (int t = C.colptr[j]; t < C.colptr[j + 1]; ++t) a += C.cval[t] * C.rho[C.rowidx[t]];
+        const int8_t s = C.st[j];
+        double a = 0.0;
+        if (s != ST_BASIC && C.blo[j] != C.bhi[j]) {
+          if (j >= n) {
+            a = -C.rho[j - n];
+          } else {
+            for (int t = C.colptr[j]; t < C.colptr[j + 1]; ++t) a += C.cval[t] * C.rho[C.rowidx[t]];
+          }
+          const double at = sigma * a, dj = C.d[j];
+          if (s == ST_LB && at > kPivTol) {
+            const double t = (fmax(dj, 0.0) + kDTol) / at;
+            if (t < tmax) tmax = t;
+          } else if (s == ST_UB && at < -kPivTol) {
+            const double t = (fmin(dj, 0.0) - kDTol) / at;
+            if (t < tmax) tmax = t;
+          } else if (s == ST_FREE && fabs(at) > kPivTol) {
+            const double t = kDTol / fabs(at);
+            if (t < tmax) tmax = t;
+          }
         }
-        const double at = sigma * a, dj = C.d[j];
-        if (s == ST_LB && at > kPivTol) {
-          const double t = (fmax(dj, 0.0) + kDTol) / at;
-          if (t < tmax) tmax = t;
-        } else if (s == ST_UB && at < -kPivTol) {
-          const double t = (fmin(dj, 0.0) - kDTol) / at;
-          if (t < tmax) tmax = t;
-        } else if (s == ST_FREE && fabs(at) > kPivTol) {
-          const double t = kDTol / fabs(at);
-          if (t < tmax) tmax = t;
+        C.al[j] = a;
+      }
+      tmax = wave_min(tmax);
+      if (tmax == INFINITY) {  // dual unbounded
+        bool boxed = false;
+        for (int j = lane; j < N; j += 64) boxed |= C.st[j] != ST_BASIC && C.art[j] != 0;
+        if (!__any(boxed) || art_bound >= 1e13) {
+          status = 2;
+          break;
+        }
+        art_bound *= 1e3;
+        grow_art(C, art_bound);
+        zB = compute_primals(C, binv);
+        fresh = true;
+        continue;
+      }
+      STAMP(3);
+      // ---- Harris pass 2: largest |alpha| among ratios <= tmax ----
+      double qa = 0.0;
+      int q = INT_MAX;
+      for (int j = lane; j < N; j += 64) {
+        const int8_t s = C.st[j];
+        if (s == ST_BASIC || C.blo[j] == C.bhi[j]) continue;
+        const double at = sigma * C.al[j], dj = C.d[j];
+        double t;
+        if (s == ST_LB && at > kPivTol) t = fmax(dj, 0.0) / at;
+        else if (s == ST_UB && at < -kPivTol) t = fmin(dj, 0.0) / at;
+        else if (s == ST_FREE && fabs(at) > kPivTol) t = 0.0;
+        else continue;
+        if (t <= tmax && fabs(at) > qa) {
+          qa = fabs(at);
+          q = j;
         }
       }
-      C.al[j] = a;
-    }
-    tmax = wave_min(tmax);
-    if (tmax == INFINITY) {  // dual unbounded
-      bool boxed = false;
-      for (int j = lane; j < N; j += 64) boxed |= C.st[j] != ST_BASIC && C.art[j] != 0;
-      if (!__any(boxed) || art_bound >= 1e13) {
+      wave_argmax_dpp(qa, q);
+      if (qa == 0.0) {
         status = 2;
         break;
       }
-      art_bound *= 1e3;
-      grow_art(C, art_bound);
-      zB = compute_primals(C, binv);
-      fresh = true;
-      continue;
-    }
-    STAMP(3);
-    // ---- Harris pass 2: largest |alpha| among ratios <= tmax ----
-    double qa = 0.0;
-    int q = INT_MAX;
-    for (int j = lane; j < N; j += 64) {
-      const int8_t s = C.st[j];
-      if (s == ST_BASIC || C.blo[j] == C.bhi[j]) continue;
-      const double at = sigma * C.al[j], dj = C.d[j];
-      double t;
-      if (s == ST_LB && at > kPivTol) t = fmax(dj, 0.0) / at;
-      else if (s == ST_UB && at < -kPivTol) t = fmin(dj, 0.0) / at;
-      else if (s == ST_FREE && fabs(at) > kPivTol) t = 0.0;
-      else continue;
-      if (t <= tmax && fabs(at) > qa) {
-        qa = fabs(at);
-        q = j;
+
+      STAMP(4);
+      // ---- column q: alpha_q = B^{-1} a_q (a_q one element per lane) ----
+      double aqk;
+      if (q < n) {
+        C.aq[lane] = 0.0;
+        wave_sync();
+        const int cs = C.colptr[q], deg = C.colptr[q + 1] - cs;
+        for (int t = lane; t < deg; t += 64) C.aq[C.rowidx[cs + t]] = C.cval[cs + t];
+        wave_sync();
+        aqk = C.aq[lane];
+      } else {
+        aqk = lane == q - n ? -1.0 : 0.0;
       }
-    }
-    wave_argmax_dpp(qa, q);
-    if (qa == 0.0) {
-      status = 2;
-      break;
-    }
+      double alq = 0.0;
+  #pragma unroll
+      for (int k = 0; k < kLpMaxM; ++k) alq += binv[k] * rld(aqk, k);
+      const double arq = rld(alq, r);
 
-    STAMP(4);
-    // ---- column q: alpha_q = B^{-1} a_q (a_q one element per lane) ----
-    double aqk;
-    if (q < n) {
-      C.aq[lane] = 0.0;
-      wave_sync();
-      const int cs = C.colptr[q], deg = C.colptr[q + 1] - cs;
-      for (int t = lane; t < deg; t += 64) C.aq[C.rowidx[cs + t]] = C.cval[cs + t];
-      wave_sync();
-      aqk = C.aq[lane];
-    } else {
-      aqk = lane == q - n ? -1.0 : 0.0;
-    }
-    double alq = 0.0;
-#pragma unroll
-    for (int k = 0; k < kLpMaxM; ++k) alq += binv[k] * rld(aqk, k);
-    const double arq = rld(alq, r);
-
-    STAMP(5);
-    // ---- steps ----
-    double theta_d = C.d[q] / C.al[q];
-    if (sigma * theta_d < 0) theta_d = 0.0;
-    const double theta_p = delta / arq;
-    const int pl = rl(h, r);
-    for (int j = lane; j < N; j += 64) {
-      if (C.st[j] == ST_BASIC) continue;
-      C.d[j] -= theta_d * C.al[j];
-    }
-    const double zq = C.z[q] + theta_p;
-    const int8_t art_q = C.art[q];
-    const double bloq = C.blo[q], bhiq = C.bhi[q];
-    const double bound_p = delta < 0 ? C.blo[pl] : C.bhi[pl];
-    wave_sync();
-    if (lane == 0) {
-      C.d[q] = 0.0;
-      C.d[pl] = -theta_d;
-      C.st[pl] = delta < 0 ? ST_LB : ST_UB;
-      C.z[pl] = bound_p;
-      C.st[q] = ST_BASIC;
-      C.z[q] = zq;
-      if (art_q) {  // basic columns keep their true (infinite) bounds
-        C.blo[q] = C.tlo(q);
-        C.bhi[q] = C.thi(q);
-        C.art[q] = 0;
-      }
-    }
-    if (lane < m) zB -= theta_p * alq;
-    if (lane == r) {
-      h = q;
-      zB = zq;
-      lbB = art_q ? C.tlo(q) : bloq;
-      ubB = art_q ? C.thi(q) : bhiq;
-    }
-    STAMP(6);
-    // ---- rank-1 update of B^{-1} ----
-    const double inv = 1.0 / arq;
-#pragma unroll
-    for (int k = 0; k < kLpMaxM; ++k) {
-      const double nr = C.rho[k] * inv;
-      binv[k] = lane == r ? nr : binv[k] - alq * nr;
-    }
-    STAMP(7);
-    ++iters;
-    fresh = false;
-    if (iters % 64 == 0) {
-      zB = compute_primals(C, binv);
-      fresh = true;
-    }
-  }
-
-  // ---- outputs ----
-  STAMP(8);
-  wave_sync();
-  if (status == 0 || status == 6) {
-    if (lane < m) C.z[h] = zB;
-    wave_sync();
-    double s = 0.0;
-    for (int j = lane; j < n; j += 64) s += C.c[j] * C.z[j];
-    s = wave_sum(s);
-    if (lane == 0) io.obj[b] = s + lp.objoff;
-    if (io.x != nullptr)
-      for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = C.z[j];
-    if (io.wo_head != nullptr) {
-      if (lane < m) io.wo_head[(size_t)b * m + lane] = h;
+      STAMP(5);
+      // ---- steps ----
+      double theta_d = C.d[q] / C.al[q];
+      if (sigma * theta_d < 0) theta_d = 0.0;
+      const double theta_p = delta / arq;
+      const int pl = rl(h, r);
       for (int j = lane; j < N; j += 64) {
-        io.wo_st[(size_t)b * N + j] = C.st[j];
-        io.wo_d[(size_t)b * N + j] = C.d[j];
+        if (C.st[j] == ST_BASIC) continue;
+        C.d[j] -= theta_d * C.al[j];
       }
-      if (lane < m) {
-        double *dst = io.wo_binv + (size_t)b * m * m + lane;
-#pragma unroll
-        for (int k = 0; k < kLpMaxM; ++k)
-          if (k < m) dst[(size_t)k * m] = binv[k];   // column-major: coalesced
+      const double zq = C.z[q] + theta_p;
+      const int8_t art_q = C.art[q];
+      const double bloq = C.blo[q], bhiq = C.bhi[q];
+      const double bound_p = delta < 0 ? C.blo[pl] : C.bhi[pl];
+      wave_sync();
+      if (lane == 0) {
+        C.d[q] = 0.0;
+        C.d[pl] = -theta_d;
+        C.st[pl] = delta < 0 ? ST_LB : ST_UB;
+        C.z[pl] = bound_p;
+        C.st[q] = ST_BASIC;
+        C.z[q] = zq;
+        if (art_q) {  // basic columns keep their true (infinite) bounds
+          C.blo[q] = C.tlo(q);
+          C.bhi[q] = C.thi(q);
+          C.art[q] = 0;
+        }
+      }
+      if (lane < m) zB -= theta_p * alq;
+      if (lane == r) {
+        h = q;
+        zB = zq;
+        lbB = art_q ? C.tlo(q) : bloq;
+        ubB = art_q ? C.thi(q) : bhiq;
+      }
+      STAMP(6);
+      // ---- rank-1 update of B^{-1} ----
+      const double inv = 1.0 / arq;
+  #pragma unroll
+      for (int k = 0; k < kLpMaxM; ++k) {
+        const double nr = C.rho[k] * inv;
+        binv[k] = lane == r ? nr : binv[k] - alq * nr;
+      }
+      STAMP(7);
+      ++iters;
+      fresh = false;
+      if (iters % 64 == 0) {
+        zB = compute_primals(C, binv);
+        fresh = true;
       }
     }
-  } else if (lane == 0) {
-    io.obj[b] = status == 2 ? INFINITY : -INFINITY;
+
+    // ---- outputs ----
+    STAMP(8);
+    wave_sync();
+    if (status == 0 || status == 6) {
+      if (lane < m) C.z[h] = zB;
+      wave_sync();
+      double s = 0.0;
+      for (int j = lane; j < n; j += 64) s += C.c[j] * C.z[j];
+      s = wave_sum(s);
+      if (lane == 0) io.obj[b] = s + lp.objoff;
+      if (io.x != nullptr)
+        for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = C.z[j];
+      if (io.wo_head != nullptr) {
+        if (lane < m) io.wo_head[(size_t)b * m + lane] = h;
+        for (int j = lane; j < N; j += 64) {
+          io.wo_st[(size_t)b * N + j] = C.st[j];
+          io.wo_d[(size_t)b * N + j] = C.d[j];
+        }
+        if (lane < m) {
+          double *dst = io.wo_binv + (size_t)b * m * m + lane;
+  #pragma unroll
+          for (int k = 0; k < kLpMaxM; ++k)
+            if (k < m) dst[(size_t)k * m] = binv[k];   // column-major: coalesced
+        }
+      }
+    } else if (lane == 0) {
+      io.obj[b] = status == 2 ? INFINITY : -INFINITY;
+    }
+    if (lane == 0) {
+      io.status[b] = status;
+      io.iters[b] = iters;
+    }
+    STAMP(9);
   }
-  if (lane == 0) {
-    io.status[b] = status;
-    io.iters[b] = iters;
-  }
-  STAMP(9);
   STAMP_FLUSH
 }
 
@@ -583,7 +590,7 @@ static size_t lp_lds_bytes_shared(int n, int m, int nnz) {
   return lp_lds_bytes(n, m, nnz) + shared_ws_bytes(n, m);
 }
 
-hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, hipStream_t stream) {
+hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, int num_cus, hipStream_t stream) {
   if (io.batch <= 0) return hipSuccess;
   if (lp.m > kLpMaxM) return hipErrorInvalidValue;
   const bool shared = io.ws.head != nullptr && io.ws.s_head == 0 && io.ws.s_st == 0 &&
@@ -602,7 +609,10 @@ hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, hipStream_t stream) {
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int blocks = (io.batch + kLpWaves - 1) / kLpWaves;
+  // persistent grid: two workgroups (8 waves) per CU is the residency the
+  // 214-VGPR / 74-KB LDS budget admits; more nodes loop inside the waves
+  const int want = (io.batch + kLpWaves - 1) / kLpWaves;
+  const int blocks = want < 2 * num_cus ? want : 2 * num_cus;
   if (shared)
     hipLaunchKernelGGL((lp_dual_kernel<kLpWaves, true>), dim3(blocks), dim3(64 * kLpWaves), lds,
                        stream, lp, io);

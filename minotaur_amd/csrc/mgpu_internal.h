@@ -113,7 +113,7 @@ struct DecideIO {
 hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t stream);
 
 size_t lp_lds_bytes(int n, int m, int nnz);
-hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, hipStream_t stream);
+hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, int num_cus, hipStream_t stream);
 
 // Output/optional mod-log arguments of one FBBT launch.
 struct FbbtIO {

@@ -457,7 +457,7 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   io.wo_d = wo_d;
   io.wo_binv = wo_binv;
   HIPCHK(c, hipEventRecord(c->ev2, c->stream));
-  HIPCHK(c, launch_lp_dual(c->lp, io, c->stream));
+  HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
   HIPCHK(c, hipEventRecord(c->ev3, c->stream));
   return MGPU_OK;
 }
