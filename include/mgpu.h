@@ -149,12 +149,67 @@ int mgpu_node_decide_dev(mgpu_ctx *ctx, int batch, const int32_t *d_fbbt_infeas,
                          double int_tol, int32_t *d_decision, double *d_inf_meas,
                          double *d_cand_obj);
 
-/* Which FBBT kernel variant the next call uses: 0 auto, 1 node bounds in
- * LDS, 2 node bounds in a global scratch (large n). For tests/benchmarks. */
+/* Which FBBT kernel variant the next calls use (linear K1 and quadratic
+ * K2): 0 auto, 1 node state in LDS, 2 node state in a global scratch
+ * (large n). For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
 
+/* ---- quadratic node FBBT (K2) ------------------------------------------
+ * Replaces QuadHandler::presolveNode (src/base/QuadHandler.cpp:1204-1269)
+ * for a batch of node boxes over the transformed problem p_ of mglob.
+ *
+ * mgpu_load_quad: the handler's registries and the original quadratic
+ * functions, as QuadHandler::addConstraint (QuadHandler.cpp:127-179) and
+ * tightenQuad_ (:2683-2924) see them.
+ *   nv, vtype[nv]        variables of p_ (original 0..nv0-1, then aux y's)
+ *   sq_x/sq_y[nsq]       y = x^2, strictly ascending x (LinSqrMap order)
+ *   bil_x0/x1/y[nbil]    y = x0*x1, x0 < x1, strictly ascending (x0, x1)
+ *                        (CompareLinBil, LinBil.cpp:51-62)
+ *   ncon, lptr/lvar/lval, qptr/qv1/qv2/qval, clb/cub: the original problem's
+ *     constraints in index order; function c has linear terms
+ *     [lptr[c], lptr[c+1]) (strictly ascending var, |a| > 1e-9) and
+ *     quadratic terms [qptr[c], qptr[c+1]) (v1 <= v2, strictly ascending
+ *     (v1, v2), |a| >= 1e-8), all variables < nv0.  When has_obj, function
+ *     ncon is the objective (constant obj_const, minimised).
+ * A problem is loaded once per context; it may coexist with mgpu_load_lp. */
+int mgpu_load_quad(mgpu_ctx *ctx, int nv0, int nv, const int32_t *vtype, int nsq,
+                   const int32_t *sq_x, const int32_t *sq_y, int nbil, const int32_t *bil_x0,
+                   const int32_t *bil_x1, const int32_t *bil_y, int ncon, const int32_t *lptr,
+                   const int32_t *lvar, const double *lval, const int32_t *qptr,
+                   const int32_t *qv1, const int32_t *qv2, const double *qval,
+                   const double *clb, const double *cub, int has_obj, double obj_const);
+
+/* Secant / McCormick row state of QuadHandler::relax_ (QuadHandler.cpp:
+ * 1549-1592) at box lb/ub [nv] (host pointers).  rows[R], R = 2 nsq +
+ * 12 nbil: per square [a_x, rhs] of  y + a_x x <= rhs, then per bilinear
+ * [a0, a1, rhs] for its four rows  -y + a0 x0 + a1 x1 <= rhs (types 0, 1)
+ * and  y + a0 x0 + a1 x1 <= rhs (types 2, 3).  Returns R in *nrows. */
+int mgpu_quad_rows(mgpu_ctx *ctx, const double *lb, const double *ub, double *rows, int *nrows);
+
+/* One QuadHandler::presolveNode per node box.
+ *   incumbent  best solution value (+INF if none; s_pool->getBestSolutionValue)
+ *   qt         1 when tightenQuad_ runs (first call or doQT_, :1241)
+ *   rows_in    [batch][R], or [R] shared by all nodes when rows_shared
+ *   rows_out   [batch][R] row state after upSqCon_/upBilCon_
+ *   infeas[b]  0 feasible, 1 infeasible (presolveNode returned true),
+ *              2 propagation loop exceeded 100000 passes, 3 a row rebuild
+ *              needed a default bound (|x bound| > 1e12, addDefaultBounds_)
+ *   mod log    r_mods in order: kind 0/1 VarBoundMod lower/upper (v1 = new
+ *              value), 2 VarBoundMod2 (v1 = lb, v2 = ub), 3 LinConMod (idx =
+ *              row: squares 0..nsq-1, then nsq + 4 k + type; v1 = new rhs). */
+int mgpu_quad_fbbt(mgpu_ctx *ctx, int batch, const double *lb_in, const double *ub_in,
+                   double incumbent, int qt, const double *rows_in, int rows_shared,
+                   double *lb_out, double *ub_out, double *rows_out, int32_t *infeas,
+                   int32_t *nmods, int mod_cap, int32_t *mod_kind, int32_t *mod_idx,
+                   double *mod_v1, double *mod_v2);
+int mgpu_quad_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in, const double *d_ub_in,
+                       double incumbent, int qt, const double *d_rows_in, int rows_shared,
+                       double *d_lb_out, double *d_ub_out, double *d_rows_out,
+                       int32_t *d_infeas, int32_t *d_nmods, int mod_cap, int32_t *d_mod_kind,
+                       int32_t *d_mod_idx, double *d_mod_v1, double *d_mod_v2);
+
 /* Device-side timing of the last launch of the named kernel family
- * ("fbbt", "lp"), measured with hipEvents on the context stream. */
+ * ("fbbt", "lp", "quad"), measured with hipEvents on the context stream. */
 double mgpu_last_kernel_ms(mgpu_ctx *ctx, const char *which);
 
 #ifdef __cplusplus

@@ -137,4 +137,48 @@ hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
                               hipStream_t stream);
 size_t fbbt_lds_bytes(int n, int m);
 
+// ---- quadratic node FBBT (K2) ---------------------------------------------
+// One tightenQuad_ term, pre-classified on the host (QuadHandler.cpp:
+// 2361-2427): kind 0 univariate a x^2 + b x (x also linear), 1 product /
+// square coef * v1 * v2, 2 linear coef * v1.
+struct alignas(16) QTermRec {  // 32 B
+  double a, b;
+  int32_t kind, v1, v2, pad;
+};
+// One tightenQuad_ function: terms [t0, t0 + nt) in forward order.
+struct alignas(16) QFunRec {   // 32 B
+  double clb, cub;
+  int32_t t0, nt, is_obj, pad;
+};
+struct DevQuad {
+  int nv, nsq, nbil, maxt;
+  const uint8_t *vtype;          // [nv] Types.h numerics
+  const int32_t *sq;             // [nsq][2]  x, y
+  const int32_t *bil;            // [nbil][3] x0, x1, y
+  // tightenQuad_ programs: [0] without the objective, [1] with it
+  const QFunRec *fun[2];
+  int nfun[2];
+  const QTermRec *term[2];
+  double obj_const;
+};
+struct QuadIO {
+  int batch;
+  const double *lb_in, *ub_in;   // [B][nv]
+  double *lb_out, *ub_out;       // [B][nv]
+  const double *rows_in;         // [B][R] or shared (rows_stride 0)
+  long rows_stride;
+  double *rows_out;              // [B][R]
+  int32_t *infeas, *nmods;       // [B]; infeas 2 = propagation cap hit
+  int32_t *mod_kind, *mod_idx;   // [B][mod_cap] or null
+  double *mod_v1, *mod_v2;
+  int mod_cap;
+  int qt;                        // run tightenQuad_
+  int prog;                      // which program (objective processed or not)
+  double best;                   // incumbent objective value (+inf if none)
+  double *scratch;               // [waves][2 nv + 2 maxt][kLanes]
+};
+hipError_t launch_quad_fbbt(const DevQuad &q, const QuadIO &io, bool use_lds,
+                            hipStream_t stream);
+size_t quad_lds_bytes(const DevQuad &q);
+
 }  // namespace mgpu

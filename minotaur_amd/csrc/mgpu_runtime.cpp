@@ -17,85 +17,8 @@
 #include <string>
 #include <vector>
 
-#include "../../include/mgpu.h"
-#include "mgpu_internal.h"
+#include "ctx.h"
 
-using namespace mgpu;
-
-struct DevBuf {
-  void *p = nullptr;
-  size_t bytes = 0;
-  hipError_t ensure(size_t want) {
-    if (want <= bytes) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) bytes = want;
-    return e;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  template <class T> T *as() const { return static_cast<T *>(p); }
-};
-
-struct mgpu_ctx {
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-  std::string err;
-  bool loaded = false;
-  DevLP lp{};
-  // problem storage
-  DevBuf rowptr, terms, rlo, rhi, colptr, rowidx, vtype, obj, collb, colub, objd;
-  DevBuf rows, trec, orec, irec, cval, ccol, rval;
-  // LP workspaces (host-pointer path)
-  DevBuf lp_lb, lp_ub, lp_skip, lp_wh, lp_wst, lp_wd, lp_wb, lp_st, lp_obj, lp_it, lp_x,
-      lp_oh, lp_ost, lp_od, lp_ob;
-  std::vector<Term> h_terms;
-  // workspaces
-  DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_inf, io_nmods, io_mv, io_ml, io_mval;
-  DevBuf scratch, flag_scratch;
-  int fbbt_variant = 0;
-  int num_cus = 256;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
-  double last_fbbt_ms = 0.0, last_lp_ms = 0.0;
-};
-
-namespace {
-
-int fail(mgpu_ctx *c, int code, const char *fmt, ...) {
-  if (c) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    c->err = buf;
-  }
-  return code;
-}
-
-#define HIPCHK(c, expr)                                                          \
-  do {                                                                           \
-    hipError_t e_ = (expr);                                                      \
-    if (e_ != hipSuccess)                                                        \
-      return fail((c), e_ == hipErrorOutOfMemory ? MGPU_ERR_NOMEM : MGPU_ERR_HIP, \
-                  "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,      \
-                  __LINE__);                                                     \
-  } while (0)
-
-template <class T>
-hipError_t upload(DevBuf &b, const T *src, size_t count) {
-  hipError_t e = b.ensure(count * sizeof(T) > 0 ? count * sizeof(T) : 16);
-  if (e != hipSuccess || count == 0) return e;
-  return hipMemcpy(b.p, src, count * sizeof(T), hipMemcpyHostToDevice);
-}
-
-}  // namespace
 
 extern "C" {
 
@@ -110,7 +33,8 @@ int mgpu_create(int device, mgpu_ctx **out) {
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess) {
+      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess ||
+      hipEventCreate(&c->ev4) != hipSuccess || hipEventCreate(&c->ev5) != hipSuccess) {
     delete c;
     return MGPU_ERR_HIP;
   }
@@ -139,6 +63,9 @@ int mgpu_destroy(mgpu_ctx *c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev2) (void)hipEventDestroy(c->ev2);
   if (c->ev3) (void)hipEventDestroy(c->ev3);
+  if (c->ev4) (void)hipEventDestroy(c->ev4);
+  if (c->ev5) (void)hipEventDestroy(c->ev5);
+  quad_state_free(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return MGPU_OK;
@@ -308,6 +235,13 @@ double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
         hipEventElapsedTime(&ms, c->ev2, c->ev3) == hipSuccess)
       c->last_lp_ms = ms;
     return c->last_lp_ms;
+  }
+  if (!strcmp(which, "quad")) {
+    float ms = 0.f;
+    if (hipEventSynchronize(c->ev5) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev4, c->ev5) == hipSuccess)
+      c->last_quad_ms = ms;
+    return c->last_quad_ms;
   }
   return -1.0;
 }

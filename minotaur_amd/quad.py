@@ -1,0 +1,317 @@
+"""Host-side data for the quadratic node FBBT (K2).
+
+``QuadProblem`` is the flat form of what Minotaur's ``QuadHandler`` sees in
+``mglob``:
+
+* the transformed problem ``p_``: variables ``0..nv0-1`` are the original
+  problem's, ``nv0..nv-1`` the auxiliaries that ``SimpleTransformer`` creates
+  for every distinct product (``newBilVar_``, SimpleTransformer.cpp:178-215;
+  squares and bilinears alike, ``-y + x0*x1 = 0``);
+* the handler's registries: squares ``y = x^2`` in ascending ``x`` (the
+  ``LinSqrMap``, QuadHandler.h:54) and bilinears ``y = x0*x1`` in ascending
+  ``(x0, x1)`` with ``x0 < x1`` (``CompareLinBil``, LinBil.cpp:51-62);
+* the ORIGINAL problem's quadratic constraints and objective, read by
+  ``tightenQuad_`` (QuadHandler.cpp:2683-2924): per function a linear term
+  list (ascending variable) and a quadratic term list (ascending ``(v1, v2)``,
+  ``v1 <= v2``; CompareVariablePair, Types.cpp:56-66).  Function ``ncon`` is
+  the objective when ``has_obj``.
+
+Relaxation row state (one secant per square, four McCormick rows per
+bilinear, all ``<= rhs``; QuadHandler::relax_, QuadHandler.cpp:1549-1592):
+``[a_x, rhs]`` per square (row ``y + a_x x <= rhs``) then ``[a0, a1, rhs] x 4``
+per bilinear (rows ``-y + ..`` for types 0/1, ``+y + ..`` for types 2/3).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .problem import BINARY, CONTINUOUS, INTEGER
+
+LF_TOL = 1e-9   # LinearFunction.cpp:22 / :89-95 — smaller weights are not stored
+QF_TOL = 1e-8   # QuadraticFunction.cpp:36 / :520-528
+
+
+@dataclass
+class QuadProblem:
+    name: str
+    nv0: int
+    vtype: np.ndarray      # int32 [nv]
+    vlb: np.ndarray        # f64 [nv] root box (aux y's included)
+    vub: np.ndarray
+    sq_x: np.ndarray       # int32 [nsq] ascending
+    sq_y: np.ndarray
+    bil_x0: np.ndarray     # int32 [nbil] ascending (x0, x1), x0 < x1
+    bil_x1: np.ndarray
+    bil_y: np.ndarray
+    lptr: np.ndarray       # int32 [nfun+1]  (nfun = ncon + has_obj)
+    lvar: np.ndarray
+    lval: np.ndarray
+    qptr: np.ndarray
+    qv1: np.ndarray
+    qv2: np.ndarray
+    qval: np.ndarray
+    clb: np.ndarray        # f64 [ncon]
+    cub: np.ndarray
+    has_obj: bool = False
+    obj_const: float = 0.0
+    _keep: list = field(default_factory=list, repr=False)
+
+    @property
+    def nv(self) -> int:
+        return int(self.vtype.size)
+
+    @property
+    def nsq(self) -> int:
+        return int(self.sq_x.size)
+
+    @property
+    def nbil(self) -> int:
+        return int(self.bil_x0.size)
+
+    @property
+    def ncon(self) -> int:
+        return int(self.clb.size)
+
+    @property
+    def nrow_state(self) -> int:
+        return 2 * self.nsq + 12 * self.nbil
+
+    def save(self, path):
+        np.savez(path, **{k: getattr(self, k) for k in _ARRAYS},
+                 nv0=self.nv0, has_obj=int(self.has_obj), obj_const=self.obj_const,
+                 name=self.name)
+
+    @staticmethod
+    def load(path) -> 'QuadProblem':
+        z = np.load(path, allow_pickle=False)
+        kw = {k: z[k] for k in _ARRAYS}
+        return QuadProblem(name=str(z['name']), nv0=int(z['nv0']), has_obj=bool(z['has_obj']),
+                           obj_const=float(z['obj_const']), **kw)
+
+
+_ARRAYS = ('vtype', 'vlb', 'vub', 'sq_x', 'sq_y', 'bil_x0', 'bil_x1', 'bil_y', 'lptr',
+           'lvar', 'lval', 'qptr', 'qv1', 'qv2', 'qval', 'clb', 'cub')
+
+
+def _bounds_on_product(l0, u0, l1, u1):
+    """Root-box product bounds (Operations.cpp:122-177, finite boxes)."""
+    c = [l0 * l1, l0 * u1, u0 * l1, u0 * u1]
+    return min(c), max(c)
+
+
+def from_functions(name, vtype, vlb, vub, funcs, clb, cub, obj=None, obj_const=0.0,
+                   aux_bounds='product'):
+    """Builds a QuadProblem from original functions.
+
+    ``funcs[c] = (lin, quad)`` with ``lin = {var: coef}`` and
+    ``quad = {(v1, v2): coef}``; ``obj`` the same for the objective (or None).
+    Aux variables are created (continuous) for every distinct product, squares
+    first then bilinears, each in registry order.  ``aux_bounds``: 'product'
+    gives y the product bounds of the root box (what QuadHandler presolve
+    propagation would set), 'free' leaves y in (-inf, inf)."""
+    nv0 = len(vtype)
+    allf = list(funcs) + ([obj] if obj is not None else [])
+    pairs = set()
+    for lin, quad in allf:
+        for (a, b) in quad:
+            pairs.add((min(a, b), max(a, b)))
+    sq = sorted(a for (a, b) in pairs if a == b)
+    bil = sorted((a, b) for (a, b) in pairs if a != b)
+    vt = list(vtype)
+    lb = list(map(float, vlb))
+    ub = list(map(float, vub))
+    sq_y, bil_y = [], []
+    for x in sq:
+        sq_y.append(len(vt))
+        vt.append(CONTINUOUS)
+        if aux_bounds == 'product':
+            l, u = vlb[x], vub[x]
+            lo = 0.0 if l <= 0.0 <= u else min(l * l, u * u)
+            lb.append(lo)
+            ub.append(max(l * l, u * u))
+        else:
+            lb.append(-np.inf)
+            ub.append(np.inf)
+    for (a, b) in bil:
+        bil_y.append(len(vt))
+        vt.append(CONTINUOUS)
+        if aux_bounds == 'product':
+            lo, hi = _bounds_on_product(vlb[a], vub[a], vlb[b], vub[b])
+            lb.append(lo)
+            ub.append(hi)
+        else:
+            lb.append(-np.inf)
+            ub.append(np.inf)
+    lptr, lvar, lval, qptr, qv1, qv2, qval = [0], [], [], [0], [], [], []
+    for lin, quad in allf:
+        for v in sorted(lin):
+            if abs(lin[v]) > LF_TOL:
+                lvar.append(v)
+                lval.append(float(lin[v]))
+        lptr.append(len(lvar))
+        for (a, b) in sorted((min(a, b), max(a, b)) for (a, b) in quad):
+            w = quad.get((a, b), quad.get((b, a)))
+            if abs(w) >= QF_TOL:
+                qv1.append(a)
+                qv2.append(b)
+                qval.append(float(w))
+        qptr.append(len(qv1))
+    i32 = lambda x: np.asarray(x, dtype=np.int32)
+    f64 = lambda x: np.asarray(x, dtype=np.float64)
+    return QuadProblem(name=name, nv0=nv0, vtype=i32(vt), vlb=f64(lb), vub=f64(ub),
+                       sq_x=i32(sq), sq_y=i32(sq_y),
+                       bil_x0=i32([a for a, _ in bil]), bil_x1=i32([b for _, b in bil]),
+                       bil_y=i32(bil_y), lptr=i32(lptr), lvar=i32(lvar), lval=f64(lval),
+                       qptr=i32(qptr), qv1=i32(qv1), qv2=i32(qv2), qval=f64(qval),
+                       clb=f64(clb), cub=f64(cub), has_obj=obj is not None,
+                       obj_const=float(obj_const))
+
+
+def _eval(lin, quad, x):
+    return (sum(c * x[v] for v, c in lin.items()) +
+            sum(c * x[a] * x[b] for (a, b), c in quad.items()))
+
+
+def random_qcqp(seed: int, nv0: int = 12, ncon: int = 8, with_obj: bool = True,
+                aux_bounds: str = 'product'):
+    """Seeded synthetic QCQP exercising every branch of QuadHandler's node
+    FBBT: univariate terms a x^2 + b x (x also linear), pure squares,
+    bilinears, sign-definite and sign-changing boxes, integer and binary
+    variables, one- and two-sided rows, equalities, rows without a linear
+    part (skipped by tightenQuad_) and purely bilinear rows (type Bilinear,
+    also skipped)."""
+    rng = np.random.default_rng(seed)
+    vtype, vlb, vub = [], [], []
+    for j in range(nv0):
+        r = rng.random()
+        if r < 0.15:
+            vtype.append(BINARY); vlb.append(0.0); vub.append(1.0)
+        elif r < 0.3:
+            vtype.append(INTEGER)
+            l = float(rng.integers(-4, 2)); vlb.append(l); vub.append(l + float(rng.integers(2, 8)))
+        else:
+            vtype.append(CONTINUOUS)
+            kind = rng.integers(0, 4)
+            if kind == 0:      # straddles zero
+                vlb.append(-float(rng.uniform(0.5, 8))); vub.append(float(rng.uniform(0.5, 8)))
+            elif kind == 1:    # nonnegative from 0
+                vlb.append(0.0); vub.append(float(rng.uniform(1, 10)))
+            elif kind == 2:    # strictly positive
+                l = float(rng.uniform(0.25, 3)); vlb.append(l); vub.append(l + float(rng.uniform(0.5, 6)))
+            else:              # strictly negative
+                u = -float(rng.uniform(0.25, 3)); vub.append(u); vlb.append(u - float(rng.uniform(0.5, 6)))
+    xs = np.array([rng.uniform(l, u) if t == CONTINUOUS else float(rng.integers(int(l), int(u) + 1))
+                   for t, l, u in zip(vtype, vlb, vub)])
+    coef = lambda: float(rng.choice([-1, 1]) * rng.uniform(0.5, 3.0))
+    funcs, clb, cub = [], [], []
+    for c in range(ncon):
+        lin, quad = {}, {}
+        style = rng.integers(0, 10)
+        nq = int(rng.integers(1, 4))
+        for _ in range(nq):
+            a = int(rng.integers(0, nv0))
+            if style == 9 or rng.random() < 0.45:
+                b = int(rng.integers(0, nv0))
+                if b == a:
+                    b = (a + 1) % nv0
+                quad[(min(a, b), max(a, b))] = coef()
+            else:
+                quad[(a, a)] = coef()
+                if rng.random() < 0.6 and style != 8:
+                    lin[a] = coef()
+        if style != 8:
+            for _ in range(int(rng.integers(1, 4))):
+                lin[int(rng.integers(0, nv0))] = coef()
+        val = _eval(lin, quad, xs)
+        kind = rng.integers(0, 4)
+        slack = float(rng.uniform(0.0, 2.0))
+        if kind == 0:
+            clb.append(-np.inf); cub.append(val + slack)
+        elif kind == 1:
+            clb.append(val - slack); cub.append(np.inf)
+        elif kind == 2:
+            clb.append(val - slack); cub.append(val + slack)
+        else:
+            clb.append(val); cub.append(val)
+        funcs.append((lin, quad))
+    obj = None
+    if with_obj:
+        lin, quad = {}, {}
+        for _ in range(int(rng.integers(2, 5))):
+            a = int(rng.integers(0, nv0))
+            quad[(a, a)] = float(rng.uniform(0.5, 2.0))
+            lin[a] = coef()
+        for _ in range(int(rng.integers(0, 3))):
+            a, b = rng.integers(0, nv0, size=2)
+            if a != b:
+                quad[(int(min(a, b)), int(max(a, b)))] = coef()
+        obj = (lin, quad)
+    return from_functions(f'qcqp-{seed}', vtype, vlb, vub, funcs, clb, cub, obj=obj,
+                          obj_const=float(rng.uniform(-2, 2)), aux_bounds=aux_bounds)
+
+
+def objective_at(qp: QuadProblem, x) -> float:
+    """Original objective value at x (original variables)."""
+    assert qp.has_obj
+    c = qp.ncon
+    v = qp.obj_const
+    for k in range(qp.lptr[c], qp.lptr[c + 1]):
+        v += qp.lval[k] * x[qp.lvar[k]]
+    for k in range(qp.qptr[c], qp.qptr[c + 1]):
+        v += qp.qval[k] * x[qp.qv1[k]] * x[qp.qv2[k]]
+    return float(v)
+
+
+def random_quad_boxes(qp: QuadProblem, B: int, seed: int, max_depth: int = 8,
+                      edge: bool = False):
+    """Seeded node boxes by random branching on the ORIGINAL variables (glob
+    branches on x; the aux y's keep the root bounds).  Integers split at
+    floor(mid); continuous variables at a random interior point, keeping
+    either side.  ``edge`` adds the interval-arithmetic corner cases of
+    Operations.cpp:122-210: x pinned to [0, 0] or to |x| < 1e-10, aux y
+    bounds shrunk (so y -> x propagation bites) or made infinite."""
+    rng = np.random.default_rng(seed)
+    LB = np.tile(qp.vlb, (B, 1))
+    UB = np.tile(qp.vub, (B, 1))
+    for b in range(B):
+        if edge:
+            for _ in range(int(rng.integers(0, 3))):
+                j = int(rng.integers(0, qp.nv0))
+                if qp.vtype[j] == CONTINUOUS and LB[b, j] <= 0.0 <= UB[b, j]:
+                    if rng.random() < 0.5:
+                        LB[b, j] = UB[b, j] = 0.0
+                    else:
+                        LB[b, j], UB[b, j] = -3e-11, 4e-11
+            for _ in range(int(rng.integers(0, 3))):
+                if qp.nv == qp.nv0:
+                    break
+                j = int(rng.integers(qp.nv0, qp.nv))
+                l, u = LB[b, j], UB[b, j]
+                r = rng.random()
+                if r < 0.2:
+                    LB[b, j], UB[b, j] = -np.inf, np.inf
+                elif np.isfinite(l) and np.isfinite(u):
+                    t0, t1 = np.sort(rng.uniform(0.0, 1.0, size=2))
+                    LB[b, j], UB[b, j] = l + (u - l) * t0, l + (u - l) * t1
+        for _ in range(int(rng.integers(0, max_depth + 1))):
+            j = int(rng.integers(0, qp.nv0))
+            l, u = LB[b, j], UB[b, j]
+            if u - l <= 1e-6:
+                continue
+            if qp.vtype[j] in (BINARY, INTEGER):
+                if u - l < 1.0:
+                    continue
+                m = np.floor(0.5 * (l + u))
+                if rng.random() < 0.5:
+                    UB[b, j] = m
+                else:
+                    LB[b, j] = m + 1.0
+            else:
+                t = l + (u - l) * float(rng.uniform(0.1, 0.9))
+                if rng.random() < 0.5:
+                    UB[b, j] = t
+                else:
+                    LB[b, j] = t
+    return LB, UB

@@ -54,6 +54,33 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
                      int have_ws, int have_binv, int iter_limit, double *obj_out,
                      double *x_out, double *y_out, int *iters_out);
 
+/* Quadratic node FBBT (QuadHandler::presolveNode).  Same layout as the
+ * reference driver's QSpec (oracle/ref/ref_quad.cpp). */
+typedef struct {
+  int nv0, nv;
+  const int *vtype;
+  const double *vlb, *vub;
+  int nsq;
+  const int *sq_x, *sq_y;
+  int nbil;
+  const int *bil_x0, *bil_x1, *bil_y;
+  int ncon;                 /* original quadratic constraints; the objective */
+  const int *lptr, *lvar;   /* is function ncon when has_obj               */
+  const double *lval;
+  const int *qptr, *qv1, *qv2;
+  const double *qval;
+  const double *clb, *cub;
+  int has_obj;
+  double obj_const;
+} orc_qspec;
+
+void orc_quad_rows(const orc_qspec *S, const double *lb, const double *ub, double *rows);
+int orc_quad_fbbt_batch(const orc_qspec *S, int B, const double *lb_in, const double *ub_in,
+                        double best, int qt, const double *rows_in, long rows_stride,
+                        double *lb_out, double *ub_out, int *infeas, int *nmods,
+                        double *rows_out, int mod_cap, int *mod_kind, int *mod_idx,
+                        double *mod_v1, double *mod_v2);
+
 #ifdef __cplusplus
 }
 #endif

@@ -256,3 +256,129 @@ def highs(p, lb=None, ub=None):
     if r.status == 3:
         return 4, -math.inf
     return 12, math.nan
+
+
+# ---------------------------------------------------------------------------
+# Quadratic node FBBT: C restatement (liboracle) and the reference's own
+# QuadHandler::presolveNode (_ref/libref_fbbt.so, oracle/ref/ref_quad.cpp)
+# ---------------------------------------------------------------------------
+class _QSpec(ctypes.Structure):
+    _fields_ = [('nv0', _I), ('nv', _I), ('vtype', _P), ('vlb', _P), ('vub', _P),
+                ('nsq', _I), ('sq_x', _P), ('sq_y', _P),
+                ('nbil', _I), ('bil_x0', _P), ('bil_x1', _P), ('bil_y', _P),
+                ('ncon', _I), ('lptr', _P), ('lvar', _P), ('lval', _P),
+                ('qptr', _P), ('qv1', _P), ('qv2', _P), ('qval', _P),
+                ('clb', _P), ('cub', _P), ('has_obj', _I), ('obj_const', _D)]
+
+
+def qspec(qp):
+    """ctypes view of a minotaur_amd.quad.QuadProblem (arrays stay owned by qp)."""
+    f = {}
+    for k in ('vtype', 'sq_x', 'sq_y', 'bil_x0', 'bil_x1', 'bil_y', 'lptr', 'lvar', 'qptr',
+              'qv1', 'qv2'):
+        a = np.ascontiguousarray(getattr(qp, k), dtype=np.int32)
+        qp._keep.append(a)
+        f[k] = _ptr(a)
+    for k in ('vlb', 'vub', 'lval', 'qval', 'clb', 'cub'):
+        a = np.ascontiguousarray(getattr(qp, k), dtype=np.float64)
+        qp._keep.append(a)
+        f[k] = _ptr(a)
+    return _QSpec(nv0=qp.nv0, nv=qp.nv, nsq=qp.nsq, nbil=qp.nbil, ncon=qp.ncon,
+                  has_obj=int(qp.has_obj), obj_const=float(qp.obj_const), **f)
+
+
+class QuadFbbtResult:
+    def __init__(self, lb, ub, infeas, nmods, rows, kind=None, idx=None, v1=None, v2=None,
+                 seconds=None):
+        self.lb, self.ub, self.infeas, self.nmods, self.rows = lb, ub, infeas, nmods, rows
+        self.kind, self.idx, self.v1, self.v2 = kind, idx, v1, v2
+        self.seconds = seconds
+
+
+def _quad_out(qp, B, mod_cap):
+    olb = np.empty((B, qp.nv))
+    oub = np.empty((B, qp.nv))
+    rows = np.empty((B, qp.nrow_state))
+    infeas = np.zeros(B, dtype=np.int32)
+    nmods = np.zeros(B, dtype=np.int32)
+    kind = idx = v1 = v2 = None
+    if mod_cap > 0:
+        kind = np.full((B, mod_cap), -1, dtype=np.int32)
+        idx = np.full((B, mod_cap), -1, dtype=np.int32)
+        v1 = np.zeros((B, mod_cap))
+        v2 = np.zeros((B, mod_cap))
+    return olb, oub, rows, infeas, nmods, kind, idx, v1, v2
+
+
+def quad_root_rows(qp, lb=None, ub=None):
+    """Secant / McCormick row state of QuadHandler::relax_ at a box (C)."""
+    L = lib()
+    L.orc_quad_rows.restype = None
+    L.orc_quad_rows.argtypes = [ctypes.POINTER(_QSpec), _P, _P, _P]
+    lb = np.ascontiguousarray(qp.vlb if lb is None else lb, dtype=np.float64)
+    ub = np.ascontiguousarray(qp.vub if ub is None else ub, dtype=np.float64)
+    rows = np.empty(qp.nrow_state)
+    s = qspec(qp)
+    L.orc_quad_rows(ctypes.byref(s), _ptr(lb), _ptr(ub), _ptr(rows))
+    return rows
+
+
+def quad_fbbt(qp, lb, ub, incumbent=None, qt=1, rows=None, mod_cap=0):
+    """C restatement of QuadHandler::presolveNode over a batch of boxes.
+    rows: [R] shared or [B, R] per node (default: root rows)."""
+    L = lib()
+    L.orc_quad_fbbt_batch.restype = _I
+    L.orc_quad_fbbt_batch.argtypes = [ctypes.POINTER(_QSpec), _I, _P, _P, _D, _I, _P,
+                                      ctypes.c_long, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P]
+    lb = np.ascontiguousarray(lb, dtype=np.float64)
+    ub = np.ascontiguousarray(ub, dtype=np.float64)
+    B = lb.shape[0]
+    if rows is None:
+        rows = quad_root_rows(qp)
+    rows = np.ascontiguousarray(rows, dtype=np.float64)
+    stride = 0 if rows.ndim == 1 else qp.nrow_state
+    best = math.inf if incumbent is None else float(incumbent)
+    olb, oub, orows, infeas, nmods, kind, idx, v1, v2 = _quad_out(qp, B, mod_cap)
+    s = qspec(qp)
+    r = L.orc_quad_fbbt_batch(ctypes.byref(s), B, _ptr(lb), _ptr(ub), best, int(qt),
+                              _ptr(rows), stride, _ptr(olb), _ptr(oub), _ptr(infeas),
+                              _ptr(nmods), _ptr(orows), mod_cap, _ptr(kind), _ptr(idx),
+                              _ptr(v1), _ptr(v2))
+    if r != 0:
+        raise RuntimeError('orc_quad_fbbt_batch: propagation cap hit')
+    return QuadFbbtResult(olb, oub, infeas, nmods, orows, kind, idx, v1, v2)
+
+
+def ref_quad_root_rows(qp):
+    R = ref_lib()
+    R.ref_quad_root_rows.restype = _I
+    R.ref_quad_root_rows.argtypes = [ctypes.POINTER(_QSpec), _P]
+    rows = np.empty(qp.nrow_state)
+    s = qspec(qp)
+    R.ref_quad_root_rows(ctypes.byref(s), _ptr(rows))
+    return rows
+
+
+def ref_quad_fbbt(qp, lb, ub, incumbent=None, qt=1, rows=None, mod_cap=0):
+    """The reference's own QuadHandler::presolveNode, node by node (shared
+    row state `rows`, default the reference's relax_ rows at the root)."""
+    R = ref_lib()
+    R.ref_quad_fbbt.restype = _I
+    R.ref_quad_fbbt.argtypes = [ctypes.POINTER(_QSpec), _I, _D, _I, _P, _I, _P, _P, _P, _P,
+                                _P, _P, _P, _I, _P, _P, _P, _P, _P]
+    lb = np.ascontiguousarray(lb, dtype=np.float64)
+    ub = np.ascontiguousarray(ub, dtype=np.float64)
+    B = lb.shape[0]
+    if rows is None:
+        rows = ref_quad_root_rows(qp)
+    rows = np.ascontiguousarray(rows, dtype=np.float64)
+    assert rows.ndim == 1
+    olb, oub, orows, infeas, nmods, kind, idx, v1, v2 = _quad_out(qp, B, mod_cap)
+    secs = np.zeros(1)
+    has = 0 if incumbent is None or not math.isfinite(incumbent) else 1
+    s = qspec(qp)
+    R.ref_quad_fbbt(ctypes.byref(s), has, float(incumbent) if has else 0.0, int(qt),
+                    _ptr(rows), B, _ptr(lb), _ptr(ub), _ptr(olb), _ptr(oub), _ptr(infeas),
+                    _ptr(nmods), _ptr(orows), mod_cap, _ptr(kind), _ptr(idx), _ptr(v1),
+                    _ptr(v2), _ptr(secs))
+    return QuadFbbtResult(olb, oub, infeas, nmods, orows, kind, idx, v1, v2, float(secs[0]))

@@ -68,3 +68,33 @@ def assert_lp_matches(status, obj, g, mask=None):
     opt = ok & (g['status'] == 0)
     err = np.abs(np.asarray(obj)[opt] - g['obj'][opt]) / np.maximum(1.0, np.abs(g['obj'][opt]))
     assert err.size == 0 or err.max() <= OBJ_TOL, err.max()
+
+
+def load_quad(name):
+    """QuadProblem + reference outputs of a quad_<name>.npz fixture."""
+    from minotaur_amd.quad import QuadProblem
+    z = np.load(os.path.join(GOLDEN, f'quad_{name}.npz'), allow_pickle=False)
+    qp = QuadProblem.load(os.path.join(GOLDEN, f'quad_{name}.npz'))
+    g = {k: z[k] for k in ('lb_in', 'ub_in', 'rows_in', 'lb_out', 'ub_out', 'rows_out',
+                           'infeas', 'nmods', 'mod_kind', 'mod_idx', 'mod_v1', 'mod_v2')}
+    inc = float(z['incumbent'])
+    g['incumbent'] = None if math.isnan(inc) else inc
+    g['qt'] = int(z['qt'])
+    g['mod_cap'] = g['mod_kind'].shape[1]
+    return qp, g
+
+
+def assert_quad_equal(r_lb, r_ub, r_rows, r_inf, r_nmods, kind, idx, v1, v2, g):
+    """Bit-exact comparison with a reference quad fixture (mod log included)."""
+    assert bits_equal(r_lb, g['lb_out'])
+    assert bits_equal(r_ub, g['ub_out'])
+    assert np.array_equal(np.asarray(r_inf), g['infeas'])
+    assert np.array_equal(np.asarray(r_nmods), g['nmods'])
+    assert bits_equal(r_rows, g['rows_out'])
+    cap = g['mod_cap']
+    for b in range(len(r_nmods)):
+        k = min(int(r_nmods[b]), cap)
+        assert np.array_equal(kind[b, :k], g['mod_kind'][b, :k].astype(np.int32)), b
+        assert np.array_equal(idx[b, :k], g['mod_idx'][b, :k].astype(np.int32)), b
+        assert bits_equal(v1[b, :k], g['mod_v1'][b, :k]), b
+        assert bits_equal(v2[b, :k], g['mod_v2'][b, :k]), b
