@@ -154,6 +154,25 @@ int mgpu_node_decide_dev(mgpu_ctx *ctx, int batch, const int32_t *d_fbbt_infeas,
  * (large n). For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
 
+/* Batched bound LPs: LP b minimises obj_sign[b] * x[obj_col[b]] over the
+ * loaded relaxation on ONE box lb/ub [n] (the relaxation's), warm-started
+ * from one shared basis (head [m], st [n+m], binv [m][m] column-major, as
+ * mgpu_lp_solve; reduced costs are rebuilt for each objective).  This is
+ * the LP work of root OBBT, QuadHandler::tightenLP_ / getBndByLP_
+ * (src/base/QuadHandler.cpp:2218-2297, :2080-2109): the caller loads the
+ * relaxation plus the objective cutoff row (:2236-2246) with mgpu_load_lp.
+ *   obj[b] = obj_sign[b] * x[obj_col[b]] at the optimum (no constant);
+ *   status/iters/x as mgpu_lp_solve. */
+int mgpu_lp_bound(mgpu_ctx *ctx, int batch, const double *lb, const double *ub,
+                  const int32_t *obj_col, const double *obj_sign, const int32_t *ws_head,
+                  const int8_t *ws_st, const double *ws_binv, int iter_limit, int32_t *status,
+                  double *obj, int32_t *iters, double *x);
+int mgpu_lp_bound_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double *d_ub,
+                      const int32_t *d_obj_col, const double *d_obj_sign,
+                      const int32_t *d_ws_head, const int8_t *d_ws_st, const double *d_ws_binv,
+                      int iter_limit, int32_t *d_status, double *d_obj, int32_t *d_iters,
+                      double *d_x);
+
 /* ---- quadratic node FBBT (K2) ------------------------------------------
  * Replaces QuadHandler::presolveNode (src/base/QuadHandler.cpp:1204-1269)
  * for a batch of node boxes over the transformed problem p_ of mglob.

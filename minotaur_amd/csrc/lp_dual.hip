@@ -96,7 +96,12 @@ struct Ctx {
   // problem
   int n, m, N;
   const double *nlb, *nub, *rlo, *rhi, *c;
+  int ocol;        // >= 0: objective is osign * x[ocol] (bound LP), else c
+  double osign;
   int lane;
+  __device__ __forceinline__ double cj(int j) const {
+    return ocol < 0 ? c[j] : (j == ocol ? osign : 0.0);
+  }
   __device__ __forceinline__ double tlo(int j) const {
     const double v = j < n ? nlb[j] : rlo[j - n];
     return v < -kInfB ? -INFINITY : v;
@@ -214,7 +219,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     s_whead = (int32_t *)p; p += al16((size_t)m * 4);
     for (int t = threadIdx.x; t < m * m; t += 64 * W) s_wbinv[t] = io.ws.binv[t];
     for (int t = threadIdx.x; t < N; t += 64 * W) {
-      s_wd[t] = io.ws.d[t];
+      if (io.ws.d != nullptr) s_wd[t] = io.ws.d[t];  // bound LPs rebuild d
       s_wst[t] = io.ws.st[t];
     }
     for (int t = threadIdx.x; t < m; t += 64 * W) s_whead[t] = io.ws.head[t];
@@ -245,9 +250,11 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     C.rho = (double *)wp; wp += 64 * 8;
     C.aq = (double *)wp;
     C.n = n; C.m = m; C.N = N;
-    C.nlb = io.lb + (size_t)b * n;
-    C.nub = io.ub + (size_t)b * n;
+    C.nlb = io.lb + (size_t)b * io.box_stride;
+    C.nub = io.ub + (size_t)b * io.box_stride;
     C.rlo = lp.rlo; C.rhi = lp.rhi; C.c = lp.objd;
+    C.ocol = io.obj_col != nullptr ? io.obj_col[b] : -1;
+    C.osign = io.obj_col != nullptr ? io.obj_sign[b] : 0.0;
     C.lane = lane;
 
     if (io.skip != nullptr && io.skip[b] != 0) {  // pruned by FBBT: not solved
@@ -293,15 +300,44 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       wave_sync();
       if (lane < m) C.st[h] = ST_BASIC;
       wave_sync();
-      for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
   #pragma unroll
       for (int k = 0; k < kLpMaxM; ++k)
         binv[k] = (lane < m && k < m) ? wb[(size_t)k * m + lane] : 0.0;  // column-major: coalesced
+      if (C.ocol < 0) {
+        for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
+      } else {
+        // bound LP: reduced costs of the warm basis for objective osign*x[ocol]
+        // (oracle compute_duals): y = c_B' B^-1 is osign * (row r of B^-1)
+        // when ocol is basic in row r, else 0; d_j = c_j - y' a_j.
+        const uint64_t on = __ballot(lane < m && h == C.ocol);
+        C.rho[lane] = 0.0;
+        wave_sync();
+        if (on != 0ull && lane == __builtin_ctzll(on)) {
+  #pragma unroll
+          for (int k = 0; k < kLpMaxM; ++k)
+            if (k < m) C.rho[k] = 0.0 + C.osign * binv[k];
+        }
+        wave_sync();
+        for (int j = lane; j < N; j += 64) {
+          if (C.st[j] == ST_BASIC) {
+            C.d[j] = 0.0;
+            continue;
+          }
+          double dot;
+          if (j >= n) {
+            dot = -C.rho[j - n];
+          } else {
+            dot = 0.0;
+            for (int t = C.colptr[j]; t < C.colptr[j + 1]; ++t) dot += C.cval[t] * C.rho[C.rowidx[t]];
+          }
+          C.d[j] = C.cj(j) - dot;
+        }
+      }
     } else {
       if (lane < m) h = n + lane;
       for (int j = lane; j < N; j += 64) {
         C.st[j] = j >= n ? ST_BASIC : ST_LB;
-        C.d[j] = j < n ? C.c[j] : 0.0;  // y = 0 for the slack basis
+        C.d[j] = j < n ? C.cj(j) : 0.0;  // y = 0 for the slack basis
       }
   #pragma unroll
       for (int k = 0; k < kLpMaxM; ++k) binv[k] = (k == lane && lane < m) ? -1.0 : 0.0;
@@ -537,9 +573,9 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       if (lane < m) C.z[h] = zB;
       wave_sync();
       double s = 0.0;
-      for (int j = lane; j < n; j += 64) s += C.c[j] * C.z[j];
+      for (int j = lane; j < n; j += 64) s += C.cj(j) * C.z[j];
       s = wave_sum(s);
-      if (lane == 0) io.obj[b] = s + lp.objoff;
+      if (lane == 0) io.obj[b] = C.ocol < 0 ? s + lp.objoff : s;
       if (io.x != nullptr)
         for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = C.z[j];
       if (io.wo_head != nullptr) {

@@ -79,6 +79,9 @@ struct LpWarm {
 struct LpIO {
   int batch;
   const double *lb, *ub;        // [B][n] node boxes
+  long box_stride;              // elements between boxes (n; 0 = one shared box)
+  const int32_t *obj_col;       // [B] or null: LP b minimises obj_sign[b] * x[obj_col[b]]
+  const double *obj_sign;       //   (bound LPs, QuadHandler::tightenLP_)
   const int32_t *skip;          // [B] nonzero = node already infeasible (FBBT)
   LpWarm ws;                    // ws.head == nullptr: slack basis
   int iter_limit;

@@ -372,6 +372,7 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   io.batch = batch;
   io.lb = lb;
   io.ub = ub;
+  io.box_stride = n;
   io.skip = skip;
   io.ws.head = ws_head;
   io.ws.st = ws_st;
@@ -393,6 +394,98 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   HIPCHK(c, hipEventRecord(c->ev2, c->stream));
   HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
   HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+  return MGPU_OK;
+}
+
+int mgpu_lp_bound_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                      const int32_t *obj_col, const double *obj_sign, const int32_t *ws_head,
+                      const int8_t *ws_st, const double *ws_binv, int iter_limit,
+                      int32_t *status, double *obj, int32_t *iters, double *x) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_bound: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb || !ub || !obj_col || !obj_sign || !status || !obj ||
+                                  !iters)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: bad argument");
+  if (ws_head && (!ws_st || !ws_binv))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: warm start needs head, st and binv");
+  if (c->lp.m > kLpMaxM)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: m=%d rows > %d not supported yet", c->lp.m,
+                kLpMaxM);
+  if (lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: problem too large for the LDS kernel");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  LpIO io{};
+  io.batch = batch;
+  io.lb = lb;
+  io.ub = ub;
+  io.box_stride = 0;  // one box (the relaxation's) for every bound LP
+  io.obj_col = obj_col;
+  io.obj_sign = obj_sign;
+  io.ws.head = ws_head;
+  io.ws.st = ws_st;
+  io.ws.d = nullptr;  // reduced costs are rebuilt for each objective
+  io.ws.binv = ws_binv;
+  io.iter_limit = iter_limit > 0 ? iter_limit : 0x7fffffff;
+  io.status = status;
+  io.obj = obj;
+  io.iters = iters;
+  io.x = x;
+  HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+  HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+  return MGPU_OK;
+}
+
+int mgpu_lp_bound(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                  const int32_t *obj_col, const double *obj_sign, const int32_t *ws_head,
+                  const int8_t *ws_st, const double *ws_binv, int iter_limit, int32_t *status,
+                  double *obj, int32_t *iters, double *x) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_bound: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb || !ub || !obj_col || !obj_sign || !status || !obj ||
+                                  !iters)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: bad argument");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = c->lp.n, m = c->lp.m, N = n + m;
+  const size_t nb = (size_t)n * sizeof(double);
+  HIPCHK(c, c->lp_lb.ensure(nb));
+  HIPCHK(c, c->lp_ub.ensure(nb));
+  const size_t sign_off = ((size_t)batch * 4 + 7) & ~(size_t)7;
+  HIPCHK(c, c->lp_skip.ensure(sign_off + (size_t)batch * 8));  // cols, then signs
+  HIPCHK(c, c->lp_st.ensure((size_t)batch * 4));
+  HIPCHK(c, c->lp_obj.ensure((size_t)batch * 8));
+  HIPCHK(c, c->lp_it.ensure((size_t)batch * 4));
+  if (x) HIPCHK(c, c->lp_x.ensure((size_t)batch * nb));
+  int32_t *d_col = c->lp_skip.as<int32_t>();
+  double *d_sign = reinterpret_cast<double *>(c->lp_skip.as<char>() + sign_off);
+  HIPCHK(c, hipMemcpyAsync(c->lp_lb.p, lb, nb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->lp_ub.p, ub, nb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_col, obj_col, (size_t)batch * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_sign, obj_sign, (size_t)batch * 8, hipMemcpyHostToDevice, c->stream));
+  if (ws_head) {
+    HIPCHK(c, c->lp_wh.ensure((size_t)m * 4 + 4));
+    HIPCHK(c, c->lp_wst.ensure((size_t)N));
+    HIPCHK(c, c->lp_wb.ensure((size_t)m * m * 8 + 8));
+    HIPCHK(c, hipMemcpyAsync(c->lp_wh.p, ws_head, (size_t)m * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->lp_wst.p, ws_st, (size_t)N, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->lp_wb.p, ws_binv, (size_t)m * m * 8, hipMemcpyHostToDevice,
+                             c->stream));
+  }
+  int rc = mgpu_lp_bound_dev(c, batch, c->lp_lb.as<double>(), c->lp_ub.as<double>(), d_col,
+                             d_sign, ws_head ? c->lp_wh.as<int32_t>() : nullptr,
+                             ws_head ? c->lp_wst.as<int8_t>() : nullptr,
+                             ws_head ? c->lp_wb.as<double>() : nullptr, iter_limit,
+                             c->lp_st.as<int32_t>(), c->lp_obj.as<double>(),
+                             c->lp_it.as<int32_t>(), x ? c->lp_x.as<double>() : nullptr);
+  if (rc != MGPU_OK) return rc;
+  HIPCHK(c, hipMemcpyAsync(status, c->lp_st.p, (size_t)batch * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(obj, c->lp_obj.p, (size_t)batch * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(iters, c->lp_it.p, (size_t)batch * 4, hipMemcpyDeviceToHost, c->stream));
+  if (x)
+    HIPCHK(c, hipMemcpyAsync(x, c->lp_x.p, (size_t)batch * nb, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return MGPU_OK;
 }
 

@@ -248,8 +248,17 @@ def random_qcqp(seed: int, nv0: int = 12, ncon: int = 8, with_obj: bool = True,
             if a != b:
                 quad[(int(min(a, b)), int(max(a, b)))] = coef()
         obj = (lin, quad)
-    return from_functions(f'qcqp-{seed}', vtype, vlb, vub, funcs, clb, cub, obj=obj,
-                          obj_const=float(rng.uniform(-2, 2)), aux_bounds=aux_bounds)
+    qp = from_functions(f'qcqp-{seed}', vtype, vlb, vub, funcs, clb, cub, obj=obj,
+                        obj_const=float(rng.uniform(-2, 2)), aux_bounds=aux_bounds)
+    # the interior point every row was built around, with y = products
+    xstar = np.zeros(qp.nv)
+    xstar[:nv0] = xs
+    for k in range(qp.nsq):
+        xstar[qp.sq_y[k]] = xs[qp.sq_x[k]] ** 2
+    for k in range(qp.nbil):
+        xstar[qp.bil_y[k]] = xs[qp.bil_x0[k]] * xs[qp.bil_x1[k]]
+    qp.xstar = xstar
+    return qp
 
 
 def objective_at(qp: QuadProblem, x) -> float:

@@ -25,7 +25,7 @@ EXPORTS = [
     'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
     'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
-    'mgpu_quad_fbbt_dev',
+    'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev',
 ]
 
 _lib = None
@@ -72,6 +72,8 @@ def load_library():
     lib.mgpu_quad_fbbt.argtypes = [_P, _I, _P, _P, _D, _I, _P, _I] + [_P] * 5 + [_I] + [_P] * 4
     lib.mgpu_quad_fbbt_dev.argtypes = ([_P, _I, _P, _P, _D, _I, _P, _I] + [_P] * 5 + [_I]
                                        + [_P] * 4)
+    lib.mgpu_lp_bound.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
+    lib.mgpu_lp_bound_dev.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -341,6 +343,37 @@ class Context:
             _dp(status), _dp(obj), _dp(iters), _dp(x),
             _dp(wo.head) if wo else None, _dp(wo.st) if wo else None,
             _dp(wo.d) if wo else None, _dp(wo.binv) if wo else None), 'mgpu_lp_solve_dev')
+
+    def lp_bound(self, cols, signs, lb=None, ub=None, ws=None, iter_limit=0, want_x=False):
+        """Bound LPs min sign_b * x[col_b] on one box (host arrays); ws: the
+        shared warm start (head, st, binv column-major) or None."""
+        p = self.problem
+        cols = _np(cols, np.int32)
+        signs = _np(signs, np.float64)
+        B = cols.shape[0]
+        lb = _np(p.vlb if lb is None else lb, np.float64)
+        ub = _np(p.vub if ub is None else ub, np.float64)
+        st = np.zeros(B, dtype=np.int32)
+        obj = np.zeros(B)
+        it = np.zeros(B, dtype=np.int32)
+        x = np.zeros((B, p.n)) if want_x else None
+        wh = wst = wb = None
+        if ws is not None:
+            wh, wst, wb = _np(ws.head, np.int32), _np(ws.st, np.int8), _np(ws.binv, np.float64)
+        self._chk(self.lib.mgpu_lp_bound(self.h, B, _hp(lb), _hp(ub), _hp(cols), _hp(signs),
+                                         _hp(wh), _hp(wst), _hp(wb), int(iter_limit), _hp(st),
+                                         _hp(obj), _hp(it), _hp(x)), 'mgpu_lp_bound')
+        return LpOut(st, obj, it, x)
+
+    def lp_bound_dev(self, lb, ub, cols, signs, status, obj, iters, ws=None, iter_limit=0,
+                     x=None):
+        """Device-tensor form of lp_bound (asynchronous)."""
+        B = int(cols.shape[0])
+        self._chk(self.lib.mgpu_lp_bound_dev(
+            self.h, B, _dp(lb), _dp(ub), _dp(cols), _dp(signs),
+            _dp(ws.head) if ws is not None else None, _dp(ws.st) if ws is not None else None,
+            _dp(ws.binv) if ws is not None else None, int(iter_limit), _dp(status), _dp(obj),
+            _dp(iters), _dp(x)), 'mgpu_lp_bound_dev')
 
     def root_solve(self, iter_limit=0):
         """Solve the root LP from the slack basis; returns (LpOut, WarmStart)."""

@@ -489,3 +489,41 @@ int orc_dual_simplex_root(int n, int m, const int *colptr, const int *rowidx,
   return orc_dual_simplex(&P, lb, ub, head, st, binv, dred, 0, 0, iter_limit, obj, x, y,
                           iters);
 }
+
+/* Bound LPs (QuadHandler::getBndByLP_, QuadHandler.cpp:2080-2109, inside
+ * tightenLP_ :2218-2297): LP b minimises sign[b] * x[col[b]] over the same
+ * box, warm-started from one basis (head/st/binv row-major); the reduced
+ * costs of each objective are rebuilt from that basis (compute_duals). */
+int orc_lp_bound_batch(int n, int m, const int *colptr, const int *rowidx, const double *cval,
+                       const double *rlo, const double *rhi, const double *lb, const double *ub,
+                       int B, const int *col, const double *sign, const int *ws_head,
+                       const signed char *ws_st, const double *ws_binv, int iter_limit,
+                       int *status, double *obj, double *x, int *iters, int nthreads)
+{
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+  {
+    int *h = (int *) malloc(sizeof(int) * (size_t) (m + 1));
+    signed char *s = (signed char *) malloc((size_t) (n + m + 1));
+    double *bi = (double *) malloc(sizeof(double) * (size_t) m * m + 8);
+    double *c = (double *) calloc((size_t) n + 1, sizeof(double));
+    orc_lp P;
+    P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cval; P.c = c;
+    P.rlo = rlo; P.rhi = rhi;
+#pragma omp for schedule(dynamic, 4)
+    for (int b = 0; b < B; ++b) {
+      const int have = ws_head != 0;
+      if (have) {
+        memcpy(h, ws_head, sizeof(int) * (size_t) m);
+        memcpy(s, ws_st, (size_t) (n + m));
+        memcpy(bi, ws_binv, sizeof(double) * (size_t) m * m);
+      }
+      c[col[b]] = sign[b];
+      status[b] = orc_dual_simplex(&P, lb, ub, h, s, bi, 0, have, have, iter_limit, obj + b,
+                                   x ? x + (size_t) b * n : 0, 0, iters + b);
+      c[col[b]] = 0.0;
+    }
+    free(h); free(s); free(bi); free(c);
+  }
+  return 0;
+}

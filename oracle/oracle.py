@@ -382,3 +382,38 @@ def ref_quad_fbbt(qp, lb, ub, incumbent=None, qt=1, rows=None, mod_cap=0):
                     _ptr(nmods), _ptr(orows), mod_cap, _ptr(kind), _ptr(idx), _ptr(v1),
                     _ptr(v2), _ptr(secs))
     return QuadFbbtResult(olb, oub, infeas, nmods, orows, kind, idx, v1, v2, float(secs[0]))
+
+
+def lp_bound(p, cols, signs, lb=None, ub=None, ws=None, iter_limit=100000, nthreads=1):
+    """C restatement of the bound LPs (min sign_b * x[col_b] on one box,
+    warm-started from ws = oracle WarmStart, binv row-major)."""
+    L = lib()
+    L.orc_lp_bound_batch.restype = _I
+    L.orc_lp_bound_batch.argtypes = [_I, _I] + [_P] * 7 + [_I] + [_P] * 5 + [_I] + [_P] * 4 + [_I]
+    colptr, rowidx, cval = lp_csc(p)
+    lb = np.ascontiguousarray(p.vlb if lb is None else lb, dtype=np.float64)
+    ub = np.ascontiguousarray(p.vub if ub is None else ub, dtype=np.float64)
+    cols = np.ascontiguousarray(cols, dtype=np.int32)
+    signs = np.ascontiguousarray(signs, dtype=np.float64)
+    B = cols.size
+    st = np.zeros(B, dtype=np.int32)
+    obj = np.zeros(B)
+    it = np.zeros(B, dtype=np.int32)
+    x = np.zeros((B, p.n))
+    wh = wst = wb = None
+    if ws is not None:
+        wh = np.ascontiguousarray(ws.head, dtype=np.int32)
+        wst = np.ascontiguousarray(ws.st, dtype=np.int8)
+        wb = np.ascontiguousarray(ws.binv, dtype=np.float64)
+    L.orc_lp_bound_batch(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.rlo),
+                         _ptr(p.rhi), _ptr(lb), _ptr(ub), B, _ptr(cols), _ptr(signs), _ptr(wh),
+                         _ptr(wst), _ptr(wb), iter_limit, _ptr(st), _ptr(obj), _ptr(x), _ptr(it),
+                         nthreads)
+    return st, obj, it, x
+
+
+def highs_obj(p, c, lb=None, ub=None):
+    """scipy HiGHS with objective vector c (no constant)."""
+    import dataclasses
+    q = dataclasses.replace(p, obj=np.asarray(c, dtype=np.float64), obj_const=0.0)
+    return highs(q, lb, ub)
