@@ -173,6 +173,37 @@ int mgpu_lp_bound_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double
                       int iter_limit, int32_t *d_status, double *d_obj, int32_t *d_iters,
                       double *d_x);
 
+/* ---- batched branch-and-bound (the caller of the path) -----------------
+ * Replaces BranchAndBound::solve's node loop (src/base/BranchAndBound.cpp:
+ * 355-526) for the loaded linear relaxation: rounds of up to `batch` open
+ * nodes, each FBBT (LinearHandler::presolveNode) -> LP (warm-started from
+ * the root optimum) -> PCBProcessor::shouldPrune_ / IntVarHandler::
+ * isFeasible -> MaxVioBrancher choice -> IntVarHandler::getBranches, with an
+ * HBM-resident stack of open nodes (depth-first over batches).
+ *   mgpu_bnb_init  : starts a tree at the root box (pool of `capacity`
+ *                    nodes) with a known incumbent value (+INF if none).
+ *   mgpu_bnb_round : one round; `incumbent` may lower the incumbent (e.g.
+ *                    the all-reduced value of other ranks).  stats are
+ *                    cumulative; open == 0 after a round = tree finished.
+ *   mgpu_bnb_best  : incumbent value and solution (x NaN when none found).
+ * decision codes in ndec[] are those of mgpu_node_decide_dev. */
+typedef struct {
+  long long rounds, nodes;      /* rounds run, nodes evaluated            */
+  long long ndec[5];            /* branch, infeasible, pruned, feasible, error */
+  int open;                     /* open nodes after the last round        */
+  int last_batch;               /* nodes evaluated in the last round      */
+  double incumbent;             /* best objective value (+INF if none)    */
+} mgpu_bnb_stats;
+
+int mgpu_bnb_init(mgpu_ctx *ctx, int capacity, const double *root_lb, const double *root_ub,
+                  double incumbent);
+int mgpu_bnb_round(mgpu_ctx *ctx, int batch, double incumbent, mgpu_bnb_stats *stats);
+int mgpu_bnb_best(mgpu_ctx *ctx, double *obj, double *x);
+/* Node-sharded multi-GPU search (MpiBranchAndBound's round-robin deal,
+ * src/base/MpiBranchAndBound.cpp:142-188): keeps open nodes i with
+ * i = rank (mod world), packed in order; *kept = nodes left. */
+int mgpu_bnb_shard(mgpu_ctx *ctx, int rank, int world, int *kept);
+
 /* ---- quadratic node FBBT (K2) ------------------------------------------
  * Replaces QuadHandler::presolveNode (src/base/QuadHandler.cpp:1204-1269)
  * for a batch of node boxes over the transformed problem p_ of mglob.

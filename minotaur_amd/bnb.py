@@ -1,0 +1,62 @@
+"""Batched branch-and-bound drivers over the engine's tree step
+(mgpu_bnb_*, minotaur_amd/csrc/bnb.cpp).
+
+``solve`` runs one tree to completion on one GPU.  ``solve_distributed``
+is the node-sharded multi-GPU form (MpiBranchAndBound analogue):
+every rank runs the same deterministic first rounds, the open nodes are
+then dealt round-robin (rank r keeps nodes r, r + P, ...;
+MpiBranchAndBound.cpp:142-188), each rank searches its share depth-first,
+and the incumbent is all-reduced (MIN, RCCL) after every round; the run
+ends when every rank's pool is empty (all-reduce MAX of the open counts).
+"""
+from __future__ import annotations
+
+import math
+import time
+
+
+def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
+          root_lb=None, root_ub=None):
+    """Tree search on the loaded LinProblem: returns (obj, x, stats, seconds)."""
+    cap = capacity or 64 * batch
+    t0 = time.perf_counter()
+    ctx.bnb_init(cap, root_lb, root_ub, incumbent)
+    st = None
+    for _ in range(max_rounds):
+        st = ctx.bnb_round(batch)
+        if st.open == 0:
+            break
+    obj, x = ctx.bnb_best()
+    return obj, x, st, time.perf_counter() - t0
+
+
+def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
+                      capacity=None, max_rounds=10**9, shard_at=None):
+    """Node-sharded tree search.  Every rank runs the same deterministic
+    rounds until the pool holds at least ``shard_at`` (default 4 * world)
+    open nodes, then keeps nodes i = rank (mod world) (mgpu_bnb_shard) and
+    searches its share; allreduce_min / allreduce_max(float) -> float are
+    the collectives (minotaur_amd/dist.py over RCCL, or gloo in the CPU
+    tests).  Returns (incumbent, x or None, stats, rounds, nodes_this_rank)."""
+    cap = capacity or 64 * batch
+    shard_at = shard_at or 4 * world
+    ctx.bnb_init(cap, None, None, math.inf)
+    inc = math.inf
+    sharded = world == 1
+    st = None
+    rounds = 0
+    shared_nodes = 0
+    while rounds < max_rounds:
+        st = ctx.bnb_round(batch, inc)
+        rounds += 1
+        open_now = st.open
+        if not sharded and (open_now >= shard_at or open_now == 0):
+            shared_nodes = st.nodes          # evaluated identically on every rank
+            open_now = ctx.bnb_shard(rank, world)
+            sharded = True
+        inc = allreduce_min(st.incumbent)
+        if allreduce_max(float(open_now)) == 0.0:
+            break
+    obj, x = ctx.bnb_best()
+    mine = st.nodes - (shared_nodes if rank != 0 else 0)
+    return inc, (x if obj == inc else None), st, rounds, mine

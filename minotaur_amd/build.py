@@ -13,8 +13,8 @@ CSRC = os.path.join(HERE, 'csrc')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 
-SOURCES = ['mgpu_runtime.cpp', 'quad_runtime.cpp', 'fbbt_linear.hip', 'lp_dual.hip',
-           'node_decide.hip', 'quad_fbbt.hip']
+SOURCES = ['mgpu_runtime.cpp', 'quad_runtime.cpp', 'bnb.cpp', 'fbbt_linear.hip',
+           'lp_dual.hip', 'node_decide.hip', 'quad_fbbt.hip', 'bnb.hip']
 # -ffp-contract=off: no fused multiply-add anywhere (bit-exact FBBT sums,
 # SURVEY §7.3); -fno-gpu-rdc keeps one code object per TU.
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off',
@@ -25,15 +25,36 @@ def lib_path():
     return os.path.join(HERE, 'libmgpu.so')
 
 
-def build(verbose=False):
+def build(verbose=False, jobs=None):
+    """Compile every translation unit to an object (in parallel, objects
+    under build/) and link libmgpu.so; no-op when it is up to date."""
+    from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     out = lib_path()
-    newest = max(os.path.getmtime(p) for p in srcs + [os.path.join(CSRC, h) for h in
-                                                        os.listdir(CSRC) if h.endswith('.h')]
-                 + [os.path.join(ROOT, 'include', 'mgpu.h')])
+    headers = ([os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith('.h')]
+               + [os.path.join(ROOT, 'include', 'mgpu.h')])
+    newest_h = max(os.path.getmtime(h) for h in headers)
+    newest = max([newest_h] + [os.path.getmtime(p) for p in srcs])
     if os.path.exists(out) and os.path.getmtime(out) >= newest:
         return out
-    cmd = [HIPCC] + FLAGS + ['-I', os.path.join(ROOT, 'include'), '-o', out] + srcs
+    objdir = os.path.join(HERE, 'build')
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != '-shared'] + ['-I', os.path.join(ROOT, 'include')]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + '.o')
+        if (os.path.exists(obj) and os.path.getmtime(obj) >= max(newest_h, os.path.getmtime(src))):
+            return obj
+        cmd = [HIPCC] + cflags + ['-c', '-o', obj, src]
+        if verbose:
+            print(' '.join(cmd))
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 2) // 2), 8)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    cmd = [HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', out] + objs
     if verbose:
         print(' '.join(cmd))
     subprocess.run(cmd, check=True)

@@ -1,0 +1,260 @@
+// Batched branch-and-bound driver: the caller of the hot
+// path, MI355X-first.  It replaces the node loop of BranchAndBound::solve
+// (src/base/BranchAndBound.cpp:355-526) for linear relaxations: instead of
+// one node at a time through NodeIncRelaxer / PCBProcessor / OsiLPEngine, a
+// round pops B open nodes from an HBM-resident stack and runs them through
+// K1 (LinearHandler::presolveNode), K3 (OsiLPEngine::solve, warm-started
+// from the root basis), the decision kernel (PCBProcessor::shouldPrune_ +
+// IntVarHandler::isFeasible + MaxVioBrancher's choice) and the branching
+// tail (IntVarHandler::getBranches), then reads back one small record.
+//
+// Search order: depth-first over batches (the pool is a stack and the
+// preferred child is pushed last), which keeps the pool at O(depth * B)
+// nodes; the incumbent prunes by bound with the reference tolerances
+// (solAbs_tol / solRel_tol 1e-6, Environment.cpp:486,509-528).  Multi-GPU
+// runs shard the tree after the first rounds (minotaur_amd/bnb.py) and
+// exchange the incumbent with an RCCL all-reduce MIN between rounds.
+#include <cmath>
+#include <cstring>
+
+#include "bnb_internal.h"
+#include "ctx.h"
+
+struct BnbState {
+  int n = 0, cap = 0, count = 0, maxb = 0;
+  bool root_ok = false;
+  double inc = INFINITY;
+  std::vector<double> best_x;
+  mgpu_bnb_stats tot{};
+  DevBuf plb, pub, pnlb, pdepth;
+  DevBuf wlb, wub, inf, nm, st, obj, it, x, dec, cand, bvar, bval, bup, depth_in, pos, bsum,
+      bidx, boff, bmin, bcnt, out;
+  DevBuf ws_head, ws_st, ws_d, ws_binv, r_st, r_obj, r_it;
+  void release() {
+    for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
+                      &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
+                      &bmin, &bcnt, &out, &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj,
+                      &r_it})
+      b->release();
+  }
+};
+
+void bnb_state_free(mgpu_ctx *c) {
+  if (c && c->bnb) {
+    c->bnb->release();
+    delete c->bnb;
+    c->bnb = nullptr;
+  }
+}
+
+namespace {
+
+int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
+  if (B <= s.maxb) return MGPU_OK;
+  const size_t n = (size_t)s.n, m = (size_t)c->lp.m;
+  const size_t nblk = ((size_t)B + 255) / 256;
+  (void)m;
+  HIPCHK(c, s.wlb.ensure((size_t)B * n * 8));
+  HIPCHK(c, s.wub.ensure((size_t)B * n * 8));
+  HIPCHK(c, s.x.ensure((size_t)B * n * 8));
+  for (DevBuf *b : {&s.inf, &s.nm, &s.st, &s.it, &s.dec, &s.bvar, &s.depth_in, &s.pos})
+    HIPCHK(c, b->ensure((size_t)B * 4));
+  for (DevBuf *b : {&s.obj, &s.cand, &s.bval}) HIPCHK(c, b->ensure((size_t)B * 8));
+  HIPCHK(c, s.bup.ensure((size_t)B));
+  for (DevBuf *b : {&s.bsum, &s.bidx, &s.boff}) HIPCHK(c, b->ensure(nblk * 4));
+  HIPCHK(c, s.bmin.ensure(nblk * 8));
+  HIPCHK(c, s.bcnt.ensure(nblk * 5 * 4));
+  HIPCHK(c, s.out.ensure(sizeof(BnbOut)));
+  s.maxb = B;
+  return MGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double *root_ub,
+                  double incumbent) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_init: no problem loaded");
+  if (capacity < 2 || !root_lb || !root_ub)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: bad argument");
+  if (c->lp.m > kLpMaxM)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: m=%d rows > %d not supported yet", c->lp.m,
+                kLpMaxM);
+  HIPCHK(c, hipSetDevice(c->device));
+  bnb_state_free(c);
+  BnbState *s = new BnbState();
+  c->bnb = s;
+  const int n = c->lp.n, m = c->lp.m, N = n + m;
+  s->n = n;
+  s->cap = capacity;
+  s->inc = incumbent;
+  s->tot.incumbent = incumbent;
+  HIPCHK(c, s->plb.ensure((size_t)capacity * n * 8));
+  HIPCHK(c, s->pub.ensure((size_t)capacity * n * 8));
+  HIPCHK(c, s->pnlb.ensure((size_t)capacity * 8));
+  HIPCHK(c, s->pdepth.ensure((size_t)capacity * 4));
+  HIPCHK(c, s->ws_head.ensure((size_t)m * 4 + 4));
+  HIPCHK(c, s->ws_st.ensure((size_t)N + 4));
+  HIPCHK(c, s->ws_d.ensure((size_t)N * 8));
+  HIPCHK(c, s->ws_binv.ensure((size_t)m * m * 8 + 8));
+  HIPCHK(c, s->r_st.ensure(4));
+  HIPCHK(c, s->r_obj.ensure(8));
+  HIPCHK(c, s->r_it.ensure(4));
+  // root: its box is the first open node; its LP optimum is the shared warm
+  // start of every node LP (NodeIncRelaxer loads the parent's basis,
+  // NodeIncRelaxer.cpp:146-150; the root's is the one every node shares)
+  HIPCHK(c, hipMemcpyAsync(s->plb.p, root_lb, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(s->pub.p, root_ub, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+  const double ninf = -INFINITY;
+  const int32_t zero = 0;
+  HIPCHK(c, hipMemcpyAsync(s->pnlb.p, &ninf, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(s->pdepth.p, &zero, 4, hipMemcpyHostToDevice, c->stream));
+  int rc = mgpu_lp_solve_dev(c, 1, s->plb.as<double>(), s->pub.as<double>(), nullptr, nullptr,
+                             nullptr, nullptr, nullptr, 1, 0, s->r_st.as<int32_t>(),
+                             s->r_obj.as<double>(), s->r_it.as<int32_t>(), nullptr,
+                             s->ws_head.as<int32_t>(), s->ws_st.as<int8_t>(),
+                             s->ws_d.as<double>(), s->ws_binv.as<double>());
+  if (rc != MGPU_OK) return rc;
+  int32_t rst = 0;
+  HIPCHK(c, hipMemcpyAsync(&rst, s->r_st.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s->root_ok = rst == 0;
+  s->count = 1;
+  s->best_x.assign(n, NAN);
+  return MGPU_OK;
+}
+
+int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *stats) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_round: mgpu_bnb_init first");
+  if (batch <= 0) return fail(c, MGPU_ERR_ARG, "mgpu_bnb_round: batch must be > 0");
+  BnbState &s = *c->bnb;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (incumbent < s.inc) s.inc = incumbent;
+  int nb = batch < s.count ? batch : s.count;
+  if (s.count + nb > s.cap) nb = s.cap - s.count;  // children must fit: base + 2 nb <= cap
+  if (nb <= 0) {
+    if (s.count > 0) return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_round: node pool full");
+    if (stats) *stats = s.tot;
+    return MGPU_OK;
+  }
+  int rc = ensure_batch(c, s, nb);
+  if (rc != MGPU_OK) return rc;
+  const int n = s.n;
+  const int base = s.count - nb;
+  const double *lb = s.plb.as<double>() + (size_t)base * n;
+  const double *ub = s.pub.as<double>() + (size_t)base * n;
+  rc = mgpu_fbbt_dev(c, nb, lb, ub, s.inc, s.wlb.as<double>(), s.wub.as<double>(),
+                     s.inf.as<int32_t>(), s.nm.as<int32_t>(), 0, nullptr, nullptr, nullptr);
+  if (rc != MGPU_OK) return rc;
+  rc = mgpu_lp_solve_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(),
+                         s.root_ok ? s.ws_head.as<int32_t>() : nullptr,
+                         s.root_ok ? s.ws_st.as<int8_t>() : nullptr,
+                         s.root_ok ? s.ws_d.as<double>() : nullptr,
+                         s.root_ok ? s.ws_binv.as<double>() : nullptr, 1, 0,
+                         s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
+                         s.x.as<double>(), nullptr, nullptr, nullptr, nullptr);
+  if (rc != MGPU_OK) return rc;
+  DecideIO d{};
+  d.batch = nb;
+  d.fbbt_infeas = s.inf.as<int32_t>();
+  d.status = s.st.as<int32_t>();
+  d.obj = s.obj.as<double>();
+  d.x = s.x.as<double>();
+  d.incumbent = s.inc;
+  d.abs_tol = 1e-6;
+  d.rel_tol = 1e-6;
+  d.cutoff = INFINITY;
+  d.int_tol = 1e-6;
+  d.decision = s.dec.as<int32_t>();
+  d.cand_obj = s.cand.as<double>();
+  d.bvar = s.bvar.as<int32_t>();
+  d.bval = s.bval.as<double>();
+  d.bup = s.bup.as<int8_t>();
+  HIPCHK(c, launch_node_decide(c->lp, d, c->stream));
+  BnbIO io{};
+  io.nb = nb;
+  io.base = base;
+  io.decision = s.dec.as<int32_t>();
+  io.cand_obj = s.cand.as<double>();
+  io.obj = s.obj.as<double>();
+  io.bvar = s.bvar.as<int32_t>();
+  io.bval = s.bval.as<double>();
+  io.bup = s.bup.as<int8_t>();
+  io.wlb = s.wlb.as<double>();
+  io.wub = s.wub.as<double>();
+  io.depth_in = s.depth_in.as<int32_t>();
+  io.plb = s.plb.as<double>();
+  io.pub = s.pub.as<double>();
+  io.pnlb = s.pnlb.as<double>();
+  io.pdepth = s.pdepth.as<int32_t>();
+  io.pos = s.pos.as<int32_t>();
+  io.bsum = s.bsum.as<int32_t>();
+  io.bidx = s.bidx.as<int32_t>();
+  io.boff = s.boff.as<int32_t>();
+  io.bmin = s.bmin.as<double>();
+  io.bcnt = s.bcnt.as<int32_t>();
+  io.out = s.out.as<BnbOut>();
+  HIPCHK(c, hipMemsetAsync(s.out.p, 0, sizeof(BnbOut), c->stream));
+  HIPCHK(c, launch_bnb_tail(io, n, c->stream));
+  BnbOut o;
+  HIPCHK(c, hipMemcpyAsync(&o, s.out.p, sizeof o, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s.count = base + 2 * o.nbranched;
+  if (o.best_idx >= 0 && o.best < s.inc) {
+    s.inc = o.best;
+    HIPCHK(c, hipMemcpy(s.best_x.data(), s.x.as<double>() + (size_t)o.best_idx * n,
+                        (size_t)n * 8, hipMemcpyDeviceToHost));
+  }
+  s.tot.rounds += 1;
+  s.tot.nodes += nb;
+  for (int k = 0; k < 5; ++k) s.tot.ndec[k] += o.ndec[k];
+  s.tot.open = s.count;
+  s.tot.incumbent = s.inc;
+  s.tot.last_batch = nb;
+  if (stats) *stats = s.tot;
+  return MGPU_OK;
+}
+
+int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_shard: mgpu_bnb_init first");
+  if (world < 1 || rank < 0 || rank >= world)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_shard: bad rank/world");
+  BnbState &s = *c->bnb;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t cnt = (size_t)(s.count > 0 ? s.count : 1);
+  DevBuf tlb, tub, tnlb, tdep;  // scratch for this call only
+  HIPCHK(c, tlb.ensure(cnt * s.n * 8));
+  HIPCHK(c, tub.ensure(cnt * s.n * 8));
+  HIPCHK(c, tnlb.ensure(cnt * 8));
+  HIPCHK(c, tdep.ensure(cnt * 4));
+  int k = 0;
+  hipError_t e = launch_bnb_shard(s.plb.as<double>(), s.pub.as<double>(), s.pnlb.as<double>(),
+                                  s.pdepth.as<int32_t>(), tlb.as<double>(), tub.as<double>(),
+                                  tnlb.as<double>(), tdep.as<int32_t>(), s.count, s.n, rank,
+                                  world, &k, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  tlb.release();
+  tub.release();
+  tnlb.release();
+  tdep.release();
+  HIPCHK(c, e);
+  s.count = k;
+  s.tot.open = k;
+  if (kept) *kept = k;
+  return MGPU_OK;
+}
+
+int mgpu_bnb_best(mgpu_ctx *c, double *obj, double *x) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_best: mgpu_bnb_init first");
+  BnbState &s = *c->bnb;
+  if (obj) *obj = s.inc;
+  if (x) std::memcpy(x, s.best_x.data(), (size_t)s.n * 8);
+  return MGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,224 @@
+// Batched branch-and-bound tree step, gfx950.
+//
+// The node pool lives in HBM as a stack of boxes ([cap][n] lb / ub, the
+// parent's relaxation value as the node's lower bound).  One round pops the
+// top B boxes (a contiguous slice: no gather), runs K1 FBBT -> K3 LP ->
+// decide on them (mgpu_bnb_round, bnb.cpp) and then, here:
+//   bnb_scan_block  : per 256-node block, the exclusive prefix of "branched"
+//                     flags, the block's incumbent candidate (min cand_obj,
+//                     lowest index on ties) and decision counts;
+//   bnb_scan_top    : one workgroup scans the block totals;
+//   bnb_children    : one wave per branched node writes its two children
+//                     (IntVarHandler::getBranches, IntVarHandler.cpp:125-175:
+//                     down ub = floor(x_j), up lb = ceil(x_j)) at
+//                     base + 2 * prefix, the preferred direction on top of
+//                     the stack so it is popped first.
+// Children inherit the node's FBBT-tightened box, as the reference keeps a
+// node's presolve mods (PCBProcessor::presolveNode_, :134-175).
+#include "bnb_internal.h"
+#include "wave.h"
+
+#include <climits>
+
+namespace mgpu {
+namespace {
+
+constexpr int kScanBlock = 256;
+
+__global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
+  __shared__ int s_pos[kScanBlock];
+  __shared__ double s_min[kScanBlock];
+  __shared__ int s_idx[kScanBlock];
+  __shared__ int s_cnt[kScanBlock][5];
+  const int t = threadIdx.x;
+  const int i = blockIdx.x * kScanBlock + t;
+  const bool live = i < io.nb;
+  const int dec = live ? io.decision[i] : -1;
+  if (live) io.depth_in[i] = io.pdepth[io.base + i];  // before children overwrite the slots
+  const int f = dec == 0 ? 1 : 0;
+  s_pos[t] = f;
+  s_min[t] = live ? io.cand_obj[i] : INFINITY;
+  s_idx[t] = live ? i : INT_MAX;
+  for (int k = 0; k < 5; ++k) s_cnt[t][k] = dec == k ? 1 : 0;
+  __syncthreads();
+  // Hillis-Steele inclusive scan of the flags
+  for (int o = 1; o < kScanBlock; o <<= 1) {
+    const int v = t >= o ? s_pos[t - o] : 0;
+    __syncthreads();
+    s_pos[t] += v;
+    __syncthreads();
+  }
+  if (live) io.pos[i] = s_pos[t] - f;  // exclusive, within the block
+  // min / argmin of the incumbent candidates and decision counts
+  for (int o = kScanBlock / 2; o > 0; o >>= 1) {
+    if (t < o) {
+      const double a = s_min[t], b = s_min[t + o];
+      const int ia = s_idx[t], ib = s_idx[t + o];
+      if (b < a || (b == a && ib < ia)) {
+        s_min[t] = b;
+        s_idx[t] = ib;
+      }
+      for (int k = 0; k < 5; ++k) s_cnt[t][k] += s_cnt[t + o][k];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    io.bsum[blockIdx.x] = s_pos[kScanBlock - 1];
+    io.bmin[blockIdx.x] = s_min[0];
+    io.bidx[blockIdx.x] = s_idx[0];
+    for (int k = 0; k < 5; ++k) io.bcnt[blockIdx.x * 5 + k] = s_cnt[0][k];
+  }
+}
+
+// One workgroup: exclusive scan of the block sums (any number of blocks,
+// 1024 at a time), global min / argmin, decision totals -> io.out.
+__global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
+  __shared__ int s[1024];
+  __shared__ double s_min[1024];
+  __shared__ int s_idx[1024];
+  __shared__ int s_carry;
+  const int t = threadIdx.x;
+  if (t == 0) s_carry = 0;
+  double my_min = INFINITY;
+  int my_idx = INT_MAX;
+  long cnt[5] = {0, 0, 0, 0, 0};
+  for (int c0 = 0; c0 < nblk; c0 += 1024) {
+    const int b = c0 + t;
+    const int v = b < nblk ? io.bsum[b] : 0;
+    if (b < nblk) {
+      const double m = io.bmin[b];
+      const int ix = io.bidx[b];
+      if (m < my_min || (m == my_min && ix < my_idx)) {
+        my_min = m;
+        my_idx = ix;
+      }
+      for (int k = 0; k < 5; ++k) cnt[k] += io.bcnt[b * 5 + k];
+    }
+    s[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int u = t >= o ? s[t - o] : 0;
+      __syncthreads();
+      s[t] += u;
+      __syncthreads();
+    }
+    if (b < nblk) io.boff[b] = s_carry + s[t] - v;
+    __syncthreads();
+    if (t == 1023) s_carry += s[1023];
+    __syncthreads();
+  }
+  s_min[t] = my_min;
+  s_idx[t] = my_idx;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (t < o) {
+      const double a = s_min[t], b = s_min[t + o];
+      const int ia = s_idx[t], ib = s_idx[t + o];
+      if (b < a || (b == a && ib < ia)) {
+        s_min[t] = b;
+        s_idx[t] = ib;
+      }
+    }
+    __syncthreads();
+  }
+  // decision totals: lane-0 atomics into a zeroed slot
+  for (int k = 0; k < 5; ++k)
+    if (cnt[k]) atomicAdd(reinterpret_cast<unsigned long long *>(&io.out->ndec[k]),
+                          (unsigned long long)cnt[k]);
+  if (t == 0) {
+    io.out->nbranched = s_carry;
+    io.out->best = s_min[0];
+    io.out->best_idx = s_idx[0] == INT_MAX ? -1 : s_idx[0];
+  }
+}
+
+// One wave per node: copy the node's (FBBT-tightened) box into its two
+// children, apply the branching bound, set the children's lower bound.
+__global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= io.nb || io.decision[i] != 0) return;
+  const int p = io.boff[i / kScanBlock] + io.pos[i];
+  const int j = io.bvar[i];
+  const double v = io.bval[i];
+  const bool up_first = io.bup[i] != 0;
+  // stack order: slot base + 2p + 1 is popped first
+  const size_t c_first = (size_t)io.base + 2 * (size_t)p + 1;
+  const size_t c_second = c_first - 1;
+  const size_t c_down = up_first ? c_second : c_first;
+  const size_t c_up = up_first ? c_first : c_second;
+  const double *sl = io.wlb + (size_t)i * n, *su = io.wub + (size_t)i * n;
+  double *dl = io.plb + c_down * n, *du = io.pub + c_down * n;
+  double *ul = io.plb + c_up * n, *uu = io.pub + c_up * n;
+  for (int k = lane; k < n; k += 64) {
+    const double l = sl[k], u = su[k];
+    dl[k] = l;
+    du[k] = k == j ? floor(v) : u;
+    ul[k] = k == j ? ceil(v) : l;
+    uu[k] = u;
+  }
+  if (lane == 0) {
+    const double bound = io.obj[i];
+    io.pnlb[c_down] = bound;
+    io.pnlb[c_up] = bound;
+    io.pdepth[c_down] = io.depth_in[i] + 1;
+    io.pdepth[c_up] = io.depth_in[i] + 1;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_bnb_tail(const BnbIO &io, int n, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  const int nblk = (io.nb + kScanBlock - 1) / kScanBlock;
+  hipLaunchKernelGGL(bnb_scan_block, dim3(nblk), dim3(kScanBlock), 0, stream, io);
+  hipLaunchKernelGGL(bnb_scan_top, dim3(1), dim3(1024), 0, stream, io, nblk);
+  hipLaunchKernelGGL(bnb_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io, n);
+  return hipGetLastError();
+}
+
+}  // namespace mgpu
+
+namespace mgpu {
+namespace {
+
+// Keeps pool slots i = rank (mod world) of [0, count) and packs them to
+// slots i / world, through a scratch copy (src -> tmp -> pool).
+__global__ __launch_bounds__(256) void bnb_shard_copy(const double *slb, const double *sub,
+                                                      const double *snlb, const int32_t *sdep,
+                                                      double *dlb, double *dub, double *dnlb,
+                                                      int32_t *ddep, int count, int n, int rank,
+                                                      int world, int to_tmp) {
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);  // kept node
+  const int i = rank + k * world;                      // its pool slot
+  if (i >= count) return;
+  const size_t from = to_tmp ? (size_t)i : (size_t)k;
+  const size_t to = (size_t)k;
+  for (int j = lane; j < n; j += 64) {
+    dlb[to * n + j] = slb[from * n + j];
+    dub[to * n + j] = sub[from * n + j];
+  }
+  if (lane == 0) {
+    dnlb[to] = snlb[from];
+    ddep[to] = sdep[from];
+  }
+}
+
+}  // namespace
+
+hipError_t launch_bnb_shard(double *plb, double *pub, double *pnlb, int32_t *pdep, double *tlb,
+                            double *tub, double *tnlb, int32_t *tdep, int count, int n,
+                            int rank, int world, int *kept, hipStream_t stream) {
+  const int k = count > rank ? (count - rank + world - 1) / world : 0;
+  *kept = k;
+  if (k == 0) return hipSuccess;
+  const dim3 grid((k + 3) / 4), blk(256);
+  hipLaunchKernelGGL(bnb_shard_copy, grid, blk, 0, stream, plb, pub, pnlb, pdep, tlb, tub, tnlb,
+                     tdep, count, n, rank, world, 1);
+  hipLaunchKernelGGL(bnb_shard_copy, grid, blk, 0, stream, tlb, tub, tnlb, tdep, plb, pub, pnlb,
+                     pdep, count, n, rank, world, 0);
+  return hipGetLastError();
+}
+
+}  // namespace mgpu

@@ -14,6 +14,7 @@
 using namespace mgpu;
 
 struct QuadState;  // quad_runtime.cpp
+struct BnbState;   // bnb.cpp
 
 struct DevBuf {
   void *p = nullptr;
@@ -58,6 +59,7 @@ struct mgpu_ctx {
             ev5 = nullptr;
   double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0;
   QuadState *quad = nullptr;   // K2 problem (mgpu_load_quad)
+  BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
 };
 
 namespace {
@@ -93,3 +95,4 @@ hipError_t upload(DevBuf &b, const T *src, size_t count) {
 }  // namespace
 
 void quad_state_free(mgpu_ctx *c);  // quad_runtime.cpp
+void bnb_state_free(mgpu_ctx *c);   // bnb.cpp

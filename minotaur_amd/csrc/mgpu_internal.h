@@ -111,6 +111,9 @@ struct DecideIO {
   int32_t *decision;            // [B]
   double *inf_meas;             // [B] or null
   double *cand_obj;             // [B] or null: obj if integer feasible else +inf
+  int32_t *bvar;                // [B] or null: branching variable when decision 0
+  double *bval;                 // [B] its LP value
+  int8_t *bup;                  // [B] 1: up branch preferred (dd > ud)
 };
 
 hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t stream);

@@ -66,6 +66,7 @@ int mgpu_destroy(mgpu_ctx *c) {
   if (c->ev4) (void)hipEventDestroy(c->ev4);
   if (c->ev5) (void)hipEventDestroy(c->ev5);
   quad_state_free(c);
+  bnb_state_free(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return MGPU_OK;
@@ -113,6 +114,7 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  bnb_state_free(c);  // a tree belongs to the problem it was started on
   // CSR terms, packed
   c->h_terms.resize(nnz > 0 ? nnz : 1);
   for (int k = 0; k < nnz; ++k) c->h_terms[k] = Term{val[k], colidx[k], 0};

@@ -9,6 +9,8 @@
 #include "mgpu_internal.h"
 #include "wave.h"
 
+#include <climits>
+
 namespace mgpu {
 namespace {
 
@@ -50,6 +52,35 @@ __global__ __launch_bounds__(64 * kNodesPerBlock) void node_decide_kernel(DevLP 
       }
       inf_meas = wave_sum(meas);
       dec = __any(frac) ? 0 : 3;
+      if (dec == 0 && io.bvar != nullptr) {
+        // MaxVioBrancher::findBestCandidate_ (MaxVioBrancher.cpp) over the
+        // IntVarHandler candidates (IntVarHandler.cpp:86-108): score
+        // 0.1 * (0.8 min(dd, ud) + 0.2 max(dd, ud)) (VarOrig), largest
+        // wins, ties -> lowest index (candidate set ordered by index);
+        // up branch first when dd > ud.
+        double best = -INFINITY;
+        int bj = INT_MAX;
+        for (int j = lane; j < lp.n; j += 64) {
+          const uint8_t t = lp.vtype[j];
+          if (t != kBinary && t != kInteger) continue;
+          const double v = x[j];
+          if (!(fabs(floor(v + 0.5) - v) > io.int_tol)) continue;
+          const double dd = v - floor(v), ud = ceil(v) - v;
+          const double lo = (ud < dd) ? ud : dd, hi = (dd < ud) ? ud : dd;
+          const double sc = 0.1 * (0.8 * lo + 0.2 * hi);
+          if (sc > best) {
+            best = sc;
+            bj = j;
+          }
+        }
+        wave_argmax(best, bj);
+        if (lane == 0) {
+          const double v = x[bj];
+          io.bvar[b] = bj;
+          io.bval[b] = v;
+          io.bup[b] = (v - floor(v)) > (ceil(v) - v) ? 1 : 0;
+        }
+      }
     }
   } else {
     dec = 4;

@@ -295,3 +295,16 @@ def random_problem(seed: int, n: int = 40, m: int = 30, density: float = 0.15,
     obj[rng.random(n) < 0.3] = 0.0
     return from_rows(f"random-{seed}", n, rows, rlo, rhi, vlb, vub, vtype, obj,
                      obj_const=float(np.round(rng.uniform(-5, 5), 2)))
+
+
+def random_mkp(seed: int, n: int = 40, m: int = 5, tight: float = 0.5):
+    """Seeded multi-dimensional 0-1 knapsack (a classic weak-LP-bound MILP,
+    for tree-search throughput): max c'x s.t. A x <= tight * A 1, x binary,
+    written as min -c'x.  A, c integer in [1, 100] (c correlated with A)."""
+    rng = np.random.default_rng(seed)
+    A = rng.integers(1, 101, size=(m, n)).astype(np.float64)
+    c = np.floor(A.mean(axis=0) + rng.integers(0, 21, size=n)).astype(np.float64)
+    b = np.floor(tight * A.sum(axis=1))
+    rows = [[(j, A[i, j]) for j in range(n)] for i in range(m)]
+    return from_rows(f"mkp-{seed}-n{n}-m{m}", n, rows, np.full(m, -np.inf), b,
+                     np.zeros(n), np.ones(n), np.full(n, BINARY, dtype=np.int32), -c)

@@ -25,8 +25,16 @@ EXPORTS = [
     'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
     'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
-    'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev',
+    'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
+    'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard',
 ]
+
+
+class BnbStats(ctypes.Structure):
+    """mgpu_bnb_stats (include/mgpu.h)."""
+    _fields_ = [('rounds', ctypes.c_longlong), ('nodes', ctypes.c_longlong),
+                ('ndec', ctypes.c_longlong * 5), ('open', ctypes.c_int),
+                ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double)]
 
 _lib = None
 
@@ -74,6 +82,10 @@ def load_library():
                                        + [_P] * 4)
     lib.mgpu_lp_bound.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
     lib.mgpu_lp_bound_dev.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
+    lib.mgpu_bnb_init.argtypes = [_P, _I, _P, _P, _D]
+    lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
+    lib.mgpu_bnb_best.argtypes = [_P, _P, _P]
+    lib.mgpu_bnb_shard.argtypes = [_P, _I, _I, _P]
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -374,6 +386,32 @@ class Context:
             _dp(ws.head) if ws is not None else None, _dp(ws.st) if ws is not None else None,
             _dp(ws.binv) if ws is not None else None, int(iter_limit), _dp(status), _dp(obj),
             _dp(iters), _dp(x)), 'mgpu_lp_bound_dev')
+
+    # -- batched branch-and-bound ---------------------------------------------
+    def bnb_init(self, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
+        p = self.problem
+        lb = _np(p.vlb if root_lb is None else root_lb, np.float64)
+        ub = _np(p.vub if root_ub is None else root_ub, np.float64)
+        self._chk(self.lib.mgpu_bnb_init(self.h, int(capacity), _hp(lb), _hp(ub),
+                                         float(incumbent)), 'mgpu_bnb_init')
+
+    def bnb_round(self, batch, incumbent=math.inf) -> BnbStats:
+        st = BnbStats()
+        self._chk(self.lib.mgpu_bnb_round(self.h, int(batch), float(incumbent),
+                                          ctypes.byref(st)), 'mgpu_bnb_round')
+        return st
+
+    def bnb_shard(self, rank, world) -> int:
+        k = ctypes.c_int(0)
+        self._chk(self.lib.mgpu_bnb_shard(self.h, int(rank), int(world), ctypes.byref(k)),
+                  'mgpu_bnb_shard')
+        return k.value
+
+    def bnb_best(self):
+        x = np.empty(self.problem.n)
+        v = ctypes.c_double(0.0)
+        self._chk(self.lib.mgpu_bnb_best(self.h, ctypes.byref(v), _hp(x)), 'mgpu_bnb_best')
+        return v.value, x
 
     def root_solve(self, iter_limit=0):
         """Solve the root LP from the slack basis; returns (LpOut, WarmStart)."""

@@ -417,3 +417,22 @@ def highs_obj(p, c, lb=None, ub=None):
     import dataclasses
     q = dataclasses.replace(p, obj=np.asarray(c, dtype=np.float64), obj_const=0.0)
     return highs(q, lb, ub)
+
+
+def highs_milp(p, time_limit=60.0):
+    """scipy HiGHS MILP (Binary/Integer columns integral): (status, objective
+    incl. constant); status 0 optimal, 2 infeasible, 4 unbounded, 12 other."""
+    from scipy.optimize import Bounds, LinearConstraint, milp
+    from scipy.sparse import csr_matrix
+    A = csr_matrix((p.val, p.colidx, p.rowptr), shape=(p.m, p.n))
+    cons = [LinearConstraint(A, p.rlo, p.rhi)] if p.m > 0 else []
+    integ = np.isin(p.vtype, (0, 1)).astype(int)
+    r = milp(p.obj, constraints=cons, integrality=integ, bounds=Bounds(p.vlb, p.vub),
+             options={'time_limit': time_limit, 'mip_rel_gap': 1e-9})
+    if r.status == 0:
+        return 0, float(r.fun) + p.obj_const
+    if r.status == 2:
+        return 2, math.inf
+    if r.status == 3:
+        return 4, -math.inf
+    return 12, math.nan
