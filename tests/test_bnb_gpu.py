@@ -96,3 +96,18 @@ def test_bnb_two_shards_interleaved(ctx):
         assert abs(inc - hobj) <= 1e-6 * max(1.0, abs(hobj))
     finally:
         ctxs[1].close()
+
+
+@pytest.mark.parametrize('batch', [4, 64])
+def test_bnb_tree_matches_cpu_restatement(ctx, batch):
+    """Same rounds, same decisions: the GPU tree and the CPU restatement of
+    the tree step (oracle/bnb.py over the C oracles) evaluate the same number
+    of nodes with the same decision counts and find the same incumbent."""
+    from bnb import CpuBnbContext
+    for p in (knapsack_oa(), random_mkp(6, 16, 3)):
+        ctx.load(p)
+        og, xg, sg, _ = bnb.solve(ctx, batch=batch, capacity=1 << 15)
+        oc, xc, sc, _ = bnb.solve(CpuBnbContext(p), batch=batch, capacity=1 << 15)
+        assert sg.open == sc.open == 0
+        assert abs(og - oc) <= 1e-9 * max(1.0, abs(oc))
+        assert (sg.rounds, sg.nodes, list(sg.ndec)) == (sc.rounds, sc.nodes, list(sc.ndec))

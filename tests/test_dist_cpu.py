@@ -72,3 +72,57 @@ def test_round_robin_deal_covers_all():
     from minotaur_amd.dist import deal_round_robin
     items = sorted(sum((deal_round_robin(10, r, 4) for r in range(4)), []))
     assert items == list(range(10))
+
+
+def _bnb_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from bnb import CpuBnbContext
+    from minotaur_amd import bnb
+    from minotaur_amd import dist as mdist
+    from minotaur_amd.problem import random_mkp
+    p = random_mkp(2, 16, 3)
+    ctx = CpuBnbContext(p)
+
+    def amin(v):
+        return float(mdist.allreduce_incumbent(torch.tensor([v], dtype=torch.float64)).item())
+
+    def amax(v):
+        return float(mdist.allreduce_max(torch.tensor([v], dtype=torch.float64)).item())
+
+    inc, x, st, rounds, mine = bnb.solve_distributed(ctx, 8, rank, world, amin, amax,
+                                                     capacity=1 << 14)
+    out[rank] = (inc, rounds, mine, st.nodes)
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_tree_search():
+    """bnb.solve_distributed over gloo with the CPU restatement of the tree
+    step: both ranks prove the HiGHS optimum, stop in the same round, and
+    split the work."""
+    import oracle
+    from minotaur_amd.problem import random_mkp
+    hs, hobj = oracle.highs_milp(random_mkp(2, 16, 3))
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bnb_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    (i0, r0, m0, n0), (i1, r1, m1, n1) = out[0], out[1]
+    assert i0 == i1 and abs(i0 - hobj) <= 1e-6 * max(1.0, abs(hobj))
+    assert r0 == r1
+    assert m0 > 0 and m1 > 0
+
+
+def test_cpu_tree_step_matches_highs():
+    import oracle
+    from bnb import CpuBnbContext
+    from minotaur_amd import bnb
+    from minotaur_amd.problem import knapsack_oa, random_mkp
+    for p in (knapsack_oa(), random_mkp(3, 14, 2)):
+        hs, hobj = oracle.highs_milp(p)
+        obj, x, st, _ = bnb.solve(CpuBnbContext(p), batch=16, capacity=1 << 14)
+        assert st.open == 0 and abs(obj - hobj) <= 1e-6 * max(1.0, abs(hobj))
