@@ -199,6 +199,24 @@ int mgpu_bnb_init(mgpu_ctx *ctx, int capacity, const double *root_lb, const doub
                   double incumbent);
 int mgpu_bnb_round(mgpu_ctx *ctx, int batch, double incumbent, mgpu_bnb_stats *stats);
 int mgpu_bnb_best(mgpu_ctx *ctx, double *obj, double *x);
+/* Strong branching (ReliabilityBrancher::strongBranch_, ReliabilityBrancher.cpp:
+ * 469-506, with the iteration cap of :101): for ncand candidates (variable,
+ * LP value) of one node, 2*ncand child LPs in ONE batch — child 2c = down
+ * (ub = floor(val)), 2c+1 = up (lb = ceil(val)) of the node box lb/ub [n] —
+ * all warm-started from the node's optimal basis (shared; head/st/d/binv as
+ * mgpu_lp_solve, d may be the parent's reduced costs), iter_limit pivots
+ * each (status 6 when hit).  The _dev form also returns the child boxes. */
+int mgpu_strong_branch(mgpu_ctx *ctx, const double *lb, const double *ub, int ncand,
+                       const int32_t *cand_var, const double *cand_val, const int32_t *ws_head,
+                       const int8_t *ws_st, const double *ws_d, const double *ws_binv,
+                       int iter_limit, int32_t *status, double *obj, int32_t *iters);
+int mgpu_strong_branch_dev(mgpu_ctx *ctx, const double *d_lb, const double *d_ub, int ncand,
+                           const int32_t *d_cand_var, const double *d_cand_val,
+                           const int32_t *d_ws_head, const int8_t *d_ws_st,
+                           const double *d_ws_d, const double *d_ws_binv, int iter_limit,
+                           double *d_child_lb, double *d_child_ub, int32_t *d_status,
+                           double *d_obj, int32_t *d_iters);
+
 /* Node-sharded multi-GPU search (MpiBranchAndBound's round-robin deal,
  * src/base/MpiBranchAndBound.cpp:142-188): keeps open nodes i with
  * i = rank (mod world), packed in order; *kept = nodes left. */

@@ -248,6 +248,83 @@ int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
   return MGPU_OK;
 }
 
+int mgpu_strong_branch_dev(mgpu_ctx *c, const double *lb, const double *ub, int ncand,
+                           const int32_t *cand_var, const double *cand_val,
+                           const int32_t *ws_head, const int8_t *ws_st, const double *ws_d,
+                           const double *ws_binv, int iter_limit, double *child_lb,
+                           double *child_ub, int32_t *status, double *obj, int32_t *iters) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_strong_branch: no problem loaded");
+  if (ncand < 0 || (ncand > 0 && (!lb || !ub || !cand_var || !cand_val || !child_lb ||
+                                  !child_ub || !status || !obj || !iters)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_strong_branch: bad argument");
+  if (ncand == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, launch_sb_boxes(lb, ub, cand_var, cand_val, ncand, c->lp.n, child_lb, child_ub,
+                            c->stream));
+  return mgpu_lp_solve_dev(c, 2 * ncand, child_lb, child_ub, nullptr, ws_head, ws_st, ws_d,
+                           ws_binv, 1, iter_limit, status, obj, iters, nullptr, nullptr,
+                           nullptr, nullptr, nullptr);
+}
+
+int mgpu_strong_branch(mgpu_ctx *c, const double *lb, const double *ub, int ncand,
+                       const int32_t *cand_var, const double *cand_val, const int32_t *ws_head,
+                       const int8_t *ws_st, const double *ws_d, const double *ws_binv,
+                       int iter_limit, int32_t *status, double *obj, int32_t *iters) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_strong_branch: no problem loaded");
+  if (ncand < 0 || (ncand > 0 && (!lb || !ub || !cand_var || !cand_val || !status || !obj ||
+                                  !iters)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_strong_branch: bad argument");
+  if (ncand == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = c->lp.n, m = c->lp.m, N = n + m, nch = 2 * ncand;
+  DevBuf box, cb, io, wsb;  // per-call workspace
+  const size_t nb = (size_t)n * 8;
+  HIPCHK(c, box.ensure(2 * nb + (size_t)ncand * 12));
+  HIPCHK(c, cb.ensure(2 * (size_t)nch * nb));
+  HIPCHK(c, io.ensure((size_t)nch * 16));
+  double *d_lb = box.as<double>(), *d_ub = d_lb + n;
+  double *d_val = d_ub + n;
+  int32_t *d_var = reinterpret_cast<int32_t *>(d_val + ncand);
+  double *d_clb = cb.as<double>(), *d_cub = d_clb + (size_t)nch * n;
+  int32_t *d_st = io.as<int32_t>(), *d_it = d_st + nch;
+  double *d_obj = reinterpret_cast<double *>(d_it + nch);
+  const int32_t *w_head = nullptr;
+  const int8_t *w_st = nullptr;
+  const double *w_d = nullptr, *w_binv = nullptr;
+  if (ws_head) {
+    if (!ws_st || !ws_d || !ws_binv)
+      return fail(c, MGPU_ERR_ARG, "mgpu_strong_branch: warm start needs head, st, d and binv");
+    HIPCHK(c, wsb.ensure((size_t)m * 4 + (size_t)N * 9 + (size_t)m * m * 8 + 64));
+    char *w = wsb.as<char>();
+    double *pb = reinterpret_cast<double *>(w);
+    double *pd = pb + (size_t)m * m;
+    int32_t *ph = reinterpret_cast<int32_t *>(pd + N);
+    int8_t *ps = reinterpret_cast<int8_t *>(ph + m);
+    HIPCHK(c, hipMemcpyAsync(pb, ws_binv, (size_t)m * m * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(pd, ws_d, (size_t)N * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ph, ws_head, (size_t)m * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ps, ws_st, (size_t)N, hipMemcpyHostToDevice, c->stream));
+    w_head = ph;
+    w_st = ps;
+    w_d = pd;
+    w_binv = pb;
+  }
+  HIPCHK(c, hipMemcpyAsync(d_lb, lb, nb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_ub, ub, nb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_val, cand_val, (size_t)ncand * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_var, cand_var, (size_t)ncand * 4, hipMemcpyHostToDevice, c->stream));
+  int rc = mgpu_strong_branch_dev(c, d_lb, d_ub, ncand, d_var, d_val, w_head, w_st, w_d, w_binv,
+                                  iter_limit, d_clb, d_cub, d_st, d_obj, d_it);
+  if (rc != MGPU_OK) return rc;
+  HIPCHK(c, hipMemcpyAsync(status, d_st, (size_t)nch * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(obj, d_obj, (size_t)nch * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(iters, d_it, (size_t)nch * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MGPU_OK;
+}
+
 int mgpu_bnb_best(mgpu_ctx *c, double *obj, double *x) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_best: mgpu_bnb_init first");

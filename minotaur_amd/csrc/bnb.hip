@@ -222,3 +222,46 @@ hipError_t launch_bnb_shard(double *plb, double *pub, double *pnlb, int32_t *pde
 }
 
 }  // namespace mgpu
+
+namespace mgpu {
+namespace {
+
+// Child boxes of strong branching (ReliabilityBrancher::strongBranch_,
+// ReliabilityBrancher.cpp:469-506 via IntVarHandler::getBrMod,
+// IntVarHandler.cpp:111-126): child 2c = down (ub = floor(x)), child 2c+1 =
+// up (lb = ceil(x)) of candidate c; one wave per child.
+__global__ __launch_bounds__(256) void sb_boxes(const double *plb, const double *pub,
+                                                const int32_t *var, const double *val,
+                                                int nchild, int n, double *clb, double *cub) {
+  const int lane = threadIdx.x & 63;
+  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ch >= nchild) return;
+  const int c = ch >> 1;
+  const bool up = ch & 1;
+  const int j = var[c];
+  const double v = val[c];
+  double *dl = clb + (size_t)ch * n, *du = cub + (size_t)ch * n;
+  for (int k = lane; k < n; k += 64) {
+    double l = plb[k], u = pub[k];
+    if (k == j) {
+      if (up) l = ceil(v);
+      else u = floor(v);
+    }
+    dl[k] = l;
+    du[k] = u;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_sb_boxes(const double *plb, const double *pub, const int32_t *var,
+                           const double *val, int ncand, int n, double *clb, double *cub,
+                           hipStream_t stream) {
+  if (ncand <= 0) return hipSuccess;
+  const int nchild = 2 * ncand;
+  hipLaunchKernelGGL(sb_boxes, dim3((nchild + 3) / 4), dim3(256), 0, stream, plb, pub, var, val,
+                     nchild, n, clb, cub);
+  return hipGetLastError();
+}
+
+}  // namespace mgpu

@@ -34,6 +34,9 @@ struct BnbIO {
 };
 
 hipError_t launch_bnb_tail(const BnbIO &io, int n, hipStream_t stream);
+hipError_t launch_sb_boxes(const double *plb, const double *pub, const int32_t *var,
+                           const double *val, int ncand, int n, double *clb, double *cub,
+                           hipStream_t stream);
 hipError_t launch_bnb_shard(double *plb, double *pub, double *pnlb, int32_t *pdep, double *tlb,
                             double *tub, double *tnlb, int32_t *tdep, int count, int n,
                             int rank, int world, int *kept, hipStream_t stream);

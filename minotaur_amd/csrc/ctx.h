@@ -19,6 +19,10 @@ struct BnbState;   // bnb.cpp
 struct DevBuf {
   void *p = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  ~DevBuf() { release(); }
   hipError_t ensure(size_t want) {
     if (want <= bytes) return hipSuccess;
     if (p) (void)hipFree(p);

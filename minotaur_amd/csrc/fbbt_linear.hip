@@ -605,8 +605,8 @@ template <bool kLds, bool kBitFlags>
 __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x;
-  const int b0 = blockIdx.x * kLanes;
-  const int nb = min(kLanes, io.batch - b0);
+  const int b0 = blockIdx.x * io.npw;
+  const int nb = min(io.npw, io.batch - b0);
   const int n = lp.n, m = lp.m;
 
   NodeView<kBitFlags> v;
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
 
 template <bool kLds, bool kBits>
 hipError_t launch_variant(const DevLP &lp, const FbbtIO &io, size_t lds, hipStream_t stream) {
-  const int waves = (io.batch + kLanes - 1) / kLanes;
+  const int waves = (io.batch + io.npw - 1) / io.npw;
   if constexpr (kLds) {
     static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted in
     if (!attr_set) {

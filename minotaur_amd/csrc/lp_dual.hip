@@ -40,7 +40,7 @@ __device__ unsigned long long g_lp_stamps[16];
     st_t = t_;                                                \
   } while (0)
 #define STAMP_FLUSH                                            \
-  if (lane == 0)                                               \
+  if ((threadIdx.x & 63) == 0)                                \
     for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_lp_stamps[i_], st_acc[i_]);
 #else
 #define STAMP_DECL

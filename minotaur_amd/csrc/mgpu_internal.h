@@ -132,6 +132,7 @@ struct FbbtIO {
   int batch;
   int has_inc;
   double inc_ub;                // incumbent - objective constant
+  int npw;                      // nodes per wave (64, or fewer for more waves)
   double *scratch;              // global-bounds variant: [waves][2][n][kLanes]
   uint8_t *flag_scratch;        // global-bounds variant: [waves][m][kLanes]
 };

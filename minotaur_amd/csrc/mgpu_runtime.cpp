@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -276,7 +277,15 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   // (best value - objective constant).
   io.has_inc = std::isfinite(incumbent) ? 1 : 0;
   io.inc_ub = io.has_inc ? incumbent - c->lp.objoff : 0.0;
-  const int waves = (batch + kLanes - 1) / kLanes;
+  // nodes per wave: fewer than 64 puts more waves in flight (latency-bound
+  // kernel); MGPU_FBBT_NPW overrides for experiments
+  int npw = kLanes;
+  if (const char *e = getenv("MGPU_FBBT_NPW")) {
+    const int v = atoi(e);
+    if (v >= 1 && v <= kLanes) npw = v;
+  }
+  io.npw = npw;
+  const int waves = (batch + npw - 1) / npw;
   const bool fits = fbbt_lds_bytes(c->lp.n, c->lp.m) <= 160 * 1024;
   // Auto: the LDS variant holds one wave per CU when the node bounds take
   // most of the 160 KiB; once there are more waves than CUs the global-

@@ -26,7 +26,8 @@ EXPORTS = [
     'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
     'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
-    'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard',
+    'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_strong_branch',
+    'mgpu_strong_branch_dev',
 ]
 
 
@@ -86,6 +87,8 @@ def load_library():
     lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
     lib.mgpu_bnb_best.argtypes = [_P, _P, _P]
     lib.mgpu_bnb_shard.argtypes = [_P, _I, _I, _P]
+    lib.mgpu_strong_branch.argtypes = [_P, _P, _P, _I] + [_P] * 6 + [_I] + [_P] * 3
+    lib.mgpu_strong_branch_dev.argtypes = [_P, _P, _P, _I] + [_P] * 6 + [_I] + [_P] * 5
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -400,6 +403,26 @@ class Context:
         self._chk(self.lib.mgpu_bnb_round(self.h, int(batch), float(incumbent),
                                           ctypes.byref(st)), 'mgpu_bnb_round')
         return st
+
+    def strong_branch(self, lb, ub, cand_var, cand_val, ws=None, iter_limit=25):
+        """Down/up child LPs of each candidate (host arrays); returns
+        (status[2k], obj[2k], iters[2k]) with child 2c = down, 2c+1 = up."""
+        cv = _np(cand_var, np.int32)
+        cx = _np(cand_val, np.float64)
+        k = cv.size
+        st = np.zeros(2 * k, dtype=np.int32)
+        ob = np.zeros(2 * k)
+        it = np.zeros(2 * k, dtype=np.int32)
+        wh = wst = wd = wb = None
+        if ws is not None:
+            wh, wst = _np(ws.head, np.int32), _np(ws.st, np.int8)
+            wd, wb = _np(ws.d, np.float64), _np(ws.binv, np.float64)
+        self._chk(self.lib.mgpu_strong_branch(self.h, _hp(_np(lb, np.float64)),
+                                              _hp(_np(ub, np.float64)), k, _hp(cv), _hp(cx),
+                                              _hp(wh), _hp(wst), _hp(wd), _hp(wb),
+                                              int(iter_limit), _hp(st), _hp(ob), _hp(it)),
+                  'mgpu_strong_branch')
+        return st, ob, it
 
     def bnb_shard(self, rank, world) -> int:
         k = ctypes.c_int(0)

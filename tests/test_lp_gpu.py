@@ -141,3 +141,36 @@ def test_lp_device_path(ctx):
     assert np.array_equal(st.cpu().numpy(), host.status)
     assert np.array_equal(it.cpu().numpy(), host.iters)
     assert np.array_equal(obj.cpu().numpy(), host.obj)
+
+
+def test_strong_branching_children_match_oracle():
+    """mgpu_strong_branch: the 2k child LPs (down/up per candidate, parent
+    basis, iteration cap 25) equal the oracle's solves of the same boxes."""
+    import os
+    from minotaur_amd.problem import LinProblem
+    from minotaur_amd.runtime import Context
+    p = LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
+                                     'instances', 'tls4_lin.npz'))
+    ctx = Context(0)
+    try:
+        ctx.load(p)
+        r, ws = ctx.root_solve()
+        x = r.x[0]
+        ints = np.nonzero(np.isin(p.vtype, (0, 1)))[0]
+        frac = ints[np.abs(x[ints] - np.round(x[ints])) > 1e-6]
+        cand = frac if frac.size else ints[:8]
+        vals = np.where(np.abs(x[cand] - np.round(x[cand])) > 1e-6, x[cand], x[cand] + 0.5)
+        for lim in (25, 0):
+            st, ob, it = ctx.strong_branch(p.vlb, p.vub, cand, vals, ws, lim)
+            LB = np.repeat(p.vlb[None], 2 * cand.size, axis=0)
+            UB = np.repeat(p.vub[None], 2 * cand.size, axis=0)
+            for c, (j, v) in enumerate(zip(cand, vals)):
+                UB[2 * c, j] = np.floor(v)
+                LB[2 * c + 1, j] = np.ceil(v)
+            g = ctx.lp_solve(LB, UB, ws, iter_limit=lim)
+            assert np.array_equal(st, g.status) and np.array_equal(it, g.iters)
+            assert np.array_equal(ob, g.obj)
+            if lim:
+                assert it.max() <= 25
+    finally:
+        ctx.close()
