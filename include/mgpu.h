@@ -222,6 +222,25 @@ int mgpu_strong_branch_dev(mgpu_ctx *ctx, const double *d_lb, const double *d_ub
  * i = rank (mod world), packed in order; *kept = nodes left. */
 int mgpu_bnb_shard(mgpu_ctx *ctx, int rank, int world, int *kept);
 
+/* ---- QP relaxation with an MFMA KKT block (K5) ---------------
+ * Replaces BqpdEngine::solve (src/interfaces/BqpdEngine.cpp:449-534) on the
+ * QP relaxation QPDRelaxer builds (examples/QPDRelaxer.cpp:56-126):
+ *     min 1/2 x'Qx + c'x + k  s.t.  A x = b,  lb <= x <= ub   (node box)
+ * Q dense symmetric PSD [n][n] (row-major), A dense [m][n] (m <= 64).
+ * mgpu_qp_solve[_dev]: one primal-dual interior point solve per node box
+ * ([batch][n] lb/ub, finite), Mehrotra predictor-corrector, Newton systems
+ * through K = Q + D = L L' (MFMA blocked Cholesky) and M = A K^-1 A'.
+ *   status[b]: 0 optimal (residuals <= 1e-9 (1 + |b|, |c|), mu <= 1e-10),
+ *              6 iteration limit (maxit, default 80);
+ *   obj[b] = 1/2 x'Qx + c'x + k;  iters[b];  x [batch][n] optional. */
+int mgpu_load_qp(mgpu_ctx *ctx, int n, int m, const double *Q, const double *c, double k,
+                 const double *A, const double *b);
+int mgpu_qp_solve(mgpu_ctx *ctx, int batch, const double *lb, const double *ub, int maxit,
+                  int32_t *status, double *obj, int32_t *iters, double *x);
+int mgpu_qp_solve_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double *d_ub,
+                      int maxit, int32_t *d_status, double *d_obj, int32_t *d_iters,
+                      double *d_x);
+
 /* ---- quadratic node FBBT (K2) ------------------------------------------
  * Replaces QuadHandler::presolveNode (src/base/QuadHandler.cpp:1204-1269)
  * for a batch of node boxes over the transformed problem p_ of mglob.
@@ -277,7 +296,7 @@ int mgpu_quad_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in, const do
                        int32_t *d_mod_idx, double *d_mod_v1, double *d_mod_v2);
 
 /* Device-side timing of the last launch of the named kernel family
- * ("fbbt", "lp", "quad"), measured with hipEvents on the context stream. */
+ * ("fbbt", "lp", "quad", "qp"), measured with hipEvents on the context stream. */
 double mgpu_last_kernel_ms(mgpu_ctx *ctx, const char *which);
 
 #ifdef __cplusplus

@@ -15,6 +15,7 @@ using namespace mgpu;
 
 struct QuadState;  // quad_runtime.cpp
 struct BnbState;   // bnb.cpp
+struct QpState;    // qp_runtime.cpp
 
 struct DevBuf {
   void *p = nullptr;
@@ -60,10 +61,11 @@ struct mgpu_ctx {
   int fbbt_variant = 0;
   int num_cus = 256;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr,
-            ev5 = nullptr;
-  double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0;
+            ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;
+  double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0, last_qp_ms = 0.0;
   QuadState *quad = nullptr;   // K2 problem (mgpu_load_quad)
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
+  QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)
 };
 
 namespace {
@@ -100,3 +102,4 @@ hipError_t upload(DevBuf &b, const T *src, size_t count) {
 
 void quad_state_free(mgpu_ctx *c);  // quad_runtime.cpp
 void bnb_state_free(mgpu_ctx *c);   // bnb.cpp
+void qp_state_free(mgpu_ctx *c);    // qp_runtime.cpp

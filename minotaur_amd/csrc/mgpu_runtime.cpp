@@ -35,7 +35,8 @@ int mgpu_create(int device, mgpu_ctx **out) {
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess ||
-      hipEventCreate(&c->ev4) != hipSuccess || hipEventCreate(&c->ev5) != hipSuccess) {
+      hipEventCreate(&c->ev4) != hipSuccess || hipEventCreate(&c->ev5) != hipSuccess ||
+      hipEventCreate(&c->ev6) != hipSuccess || hipEventCreate(&c->ev7) != hipSuccess) {
     delete c;
     return MGPU_ERR_HIP;
   }
@@ -66,8 +67,11 @@ int mgpu_destroy(mgpu_ctx *c) {
   if (c->ev3) (void)hipEventDestroy(c->ev3);
   if (c->ev4) (void)hipEventDestroy(c->ev4);
   if (c->ev5) (void)hipEventDestroy(c->ev5);
+  if (c->ev6) (void)hipEventDestroy(c->ev6);
+  if (c->ev7) (void)hipEventDestroy(c->ev7);
   quad_state_free(c);
   bnb_state_free(c);
+  qp_state_free(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return MGPU_OK;
@@ -238,6 +242,13 @@ double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
         hipEventElapsedTime(&ms, c->ev2, c->ev3) == hipSuccess)
       c->last_lp_ms = ms;
     return c->last_lp_ms;
+  }
+  if (!strcmp(which, "qp")) {
+    float ms = 0.f;
+    if (hipEventSynchronize(c->ev7) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev6, c->ev7) == hipSuccess)
+      c->last_qp_ms = ms;
+    return c->last_qp_ms;
   }
   if (!strcmp(which, "quad")) {
     float ms = 0.f;

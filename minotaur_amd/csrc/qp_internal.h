@@ -1,0 +1,44 @@
+// Device-side structures of the batched QP relaxation solve (qp_kkt.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mgpu {
+
+constexpr double kQpTolMu = 1e-10;   // complementarity (oracle/qp_ipm.py TOL_MU)
+constexpr double kQpReg = 1e-12;     // relative regularisation of M
+constexpr double kQpStep = 0.995;    // fraction to the boundary
+
+struct DevQP {
+  int n, m, np, mp;          // sizes and their multiples of 16
+  const double *Q;           // [np][np] symmetric, zero padded
+  const double *c;           // [np]
+  const double *A;           // [mp][np]
+  const double *AT;          // [np][mp]
+  const double *b;           // [mp]
+  double k;                  // objective constant
+  double tp, td;             // primal / dual residual tolerances
+};
+
+struct QpWork {
+  int B;
+  double *l, *u;             // [B][np] node boxes (padding fixed at 0)
+  double *x, *zl, *zu;       // [B][np]
+  double *y;                 // [B][mp]
+  double *rd;                // [B][np]
+  double *rp;                // [B][mp]
+  double *K;                 // [B][np][np]
+  double *W;                 // [B][np][mp]
+  double *M;                 // [B][mp][mp]
+  int32_t *done, *iters, *status;
+  double *obj;
+};
+
+size_t qp_step_lds(int np, int mp);
+hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s);
+hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s);
+hipError_t launch_qp_iteration_check(const DevQP &q, const QpWork &w, hipStream_t s);
+hipError_t launch_qp_final(const DevQP &q, const QpWork &w, hipStream_t s);
+
+}  // namespace mgpu

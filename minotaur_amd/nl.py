@@ -342,3 +342,61 @@ def read_nl(path: str) -> NlModel:
         if model.var_type[j] == INTEGER and var_lb[j] > -1e-8 and var_ub[j] < 1 + 1e-8:
             model.var_type[j] = BINARY
     return model
+
+
+def quadratic_form(expr, n):
+    """Expand an expression tree of degree <= 2 (the ``o0`` plus, ``o1``
+    minus, ``o2`` mult, ``o5`` pow with exponent 2, ``o16`` negation,
+    ``o54`` sumlist, numbers and variables) into (Q, c, k) with
+    f(x) = 1/2 x'Qx + c'x + k, Q symmetric.  Raises ValueError for anything
+    else (the QP relaxation path takes quadratic objectives only)."""
+    def poly(e):
+        if e[0] == 'n':
+            return {(): float(e[1])}
+        if e[0] == 'v':
+            return {(int(e[1]),): 1.0}
+        op, args = e[1], e[2]
+        if op == 54 or op == 0:
+            out = {}
+            for a in args:
+                for k, v in poly(a).items():
+                    out[k] = out.get(k, 0.0) + v
+            return out
+        if op == 1:
+            a, b = poly(args[0]), poly(args[1])
+            for k, v in b.items():
+                a[k] = a.get(k, 0.0) - v
+            return a
+        if op == 16:
+            return {k: -v for k, v in poly(args[0]).items()}
+        if op == 2:
+            a, b = poly(args[0]), poly(args[1])
+            out = {}
+            for ka, va in a.items():
+                for kb, vb in b.items():
+                    k = tuple(sorted(ka + kb))
+                    if len(k) > 2:
+                        raise ValueError('degree > 2')
+                    out[k] = out.get(k, 0.0) + va * vb
+            return out
+        if op == 5 and args[1][0] == 'n' and float(args[1][1]) == 2.0:
+            a = poly(args[0])
+            return poly(('o', 2, [args[0], args[0]])) if a else {(): 0.0}
+        raise ValueError(f'opcode {op} is not quadratic')
+
+    Q = np.zeros((n, n))
+    c = np.zeros(n)
+    k0 = 0.0
+    for key, v in poly(expr).items():
+        if len(key) == 0:
+            k0 += v
+        elif len(key) == 1:
+            c[key[0]] += v
+        else:
+            i, j = key
+            if i == j:
+                Q[i, i] += 2.0 * v
+            else:
+                Q[i, j] += v
+                Q[j, i] += v
+    return Q, c, k0

@@ -1,0 +1,116 @@
+"""Host-side data of the QP relaxation path.
+
+``QpProblem``: min 1/2 x'Qx + c'x + k  s.t.  A x = b (equality rows),
+l <= x <= u, dense Q (shared by every node), the node data being the box.
+``from_nl`` builds it from an ``.nl`` model with a quadratic objective and
+linear equality rows (color_lab2_4x0: 300 binaries, 61 rows, dense Q),
+relaxing integrality (the QP relaxation QPDRelaxer hands to BQPD,
+examples/QPDRelaxer.cpp:56-126).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import nl as nlmod
+
+
+@dataclass
+class QpProblem:
+    name: str
+    Q: np.ndarray      # [n, n] symmetric PSD
+    c: np.ndarray      # [n]
+    k: float
+    A: np.ndarray      # [m, n] dense
+    b: np.ndarray      # [m]
+    l: np.ndarray      # [n] root box
+    u: np.ndarray
+    vtype: np.ndarray  # reference VariableType numerics
+
+    @property
+    def n(self):
+        return self.Q.shape[0]
+
+    @property
+    def m(self):
+        return self.A.shape[0]
+
+
+def from_nl(path, name=None) -> QpProblem:
+    m = nlmod.read_nl(path)
+    Q, c, k = nlmod.quadratic_form(m.obj_expr, m.n)
+    for j, a in m.obj_grad:
+        c[j] += a
+    k += m.obj_const
+    if m.obj_sense == 1:
+        Q, c, k = -Q, -c, -k
+    if not np.all(m.con_lb == m.con_ub):
+        raise ValueError('QP path takes equality rows only')
+    A = np.zeros((m.m, m.n))
+    for i, row in enumerate(m.rows):
+        for j, a in row:
+            A[i, j] += a
+    return QpProblem(name or m.name, Q, c, k, A, m.con_lb.astype(np.float64),
+                     m.var_lb.astype(np.float64), m.var_ub.astype(np.float64),
+                     np.asarray(m.var_type, dtype=np.int32))
+
+
+def feasible_binary_point(qp: QpProblem, seed: int):
+    """A 0/1 point with A x = b for assignment-type rows (every row a
+    sum of binaries = 1 with disjoint supports, plus coupling rows): greedy
+    with random order, returns None if the greedy pick fails."""
+    rng = np.random.default_rng(seed)
+    x = np.zeros(qp.n)
+    # rows  sum a_j x_j = 0  with all a_j > 0 force their binaries to 0
+    zero = np.zeros(qp.n, dtype=bool)
+    for i in range(qp.m):
+        nz = np.nonzero(qp.A[i])[0]
+        if qp.b[i] == 0.0 and np.all(qp.A[i, nz] > 0):
+            zero[nz] = True
+    for i in rng.permutation(qp.m):
+        r = qp.A[i]
+        need = qp.b[i] - r @ x
+        if abs(need) < 1e-12:
+            continue
+        cand = [j for j in np.nonzero(r)[0]
+                if x[j] == 0.0 and not zero[j] and abs(r[j] - need) < 1e-12]
+        if not cand:
+            return None
+        x[rng.choice(cand)] = 1.0
+    return x if np.allclose(qp.A @ x, qp.b) else None
+
+
+def random_node_boxes(qp: QpProblem, B: int, seed: int, max_fix: int = 40):
+    """Node boxes that fix a random subset of binaries to the values of a
+    feasible 0/1 point (so every node QP is feasible); the rest keep the
+    root box."""
+    rng = np.random.default_rng(seed)
+    LB = np.tile(qp.l, (B, 1))
+    UB = np.tile(qp.u, (B, 1))
+    for b in range(B):
+        x = None
+        s = int(rng.integers(0, 1 << 30))
+        for _ in range(1000):
+            x = feasible_binary_point(qp, s)
+            s += 1
+            if x is not None:
+                break
+        if x is None:
+            raise ValueError('no feasible 0/1 point found for the node boxes')
+        k = int(rng.integers(0, max_fix + 1))
+        js = rng.choice(qp.n, size=k, replace=False)
+        LB[b, js] = x[js]
+        UB[b, js] = x[js]
+    return LB, UB
+
+
+def save(qp: QpProblem, path):
+    np.savez_compressed(path, name=qp.name, Q=qp.Q, c=qp.c, k=qp.k, A=qp.A, b=qp.b, l=qp.l,
+                        u=qp.u, vtype=qp.vtype)
+
+
+def load(path) -> QpProblem:
+    z = np.load(path, allow_pickle=False)
+    return QpProblem(str(z['name']), z['Q'], z['c'], float(z['k']), z['A'], z['b'], z['l'],
+                     z['u'], z['vtype'])

@@ -27,7 +27,7 @@ EXPORTS = [
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
     'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
     'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_strong_branch',
-    'mgpu_strong_branch_dev',
+    'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
 ]
 
 
@@ -89,6 +89,9 @@ def load_library():
     lib.mgpu_bnb_shard.argtypes = [_P, _I, _I, _P]
     lib.mgpu_strong_branch.argtypes = [_P, _P, _P, _I] + [_P] * 6 + [_I] + [_P] * 3
     lib.mgpu_strong_branch_dev.argtypes = [_P, _P, _P, _I] + [_P] * 6 + [_I] + [_P] * 5
+    lib.mgpu_load_qp.argtypes = [_P, _I, _I, _P, _P, _D, _P, _P]
+    lib.mgpu_qp_solve.argtypes = [_P, _I, _P, _P, _I, _P, _P, _P, _P]
+    lib.mgpu_qp_solve_dev.argtypes = [_P, _I, _P, _P, _I, _P, _P, _P, _P]
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -423,6 +426,32 @@ class Context:
                                               int(iter_limit), _hp(st), _hp(ob), _hp(it)),
                   'mgpu_strong_branch')
         return st, ob, it
+
+    # -- QP relaxation (K5) ----------------------------------------------------
+    def load_qp(self, qp):
+        self._qpkeep = [_np(qp.Q, np.float64), _np(qp.c, np.float64), _np(qp.A, np.float64),
+                        _np(qp.b, np.float64)]
+        Q, c, A, b = self._qpkeep
+        self._chk(self.lib.mgpu_load_qp(self.h, qp.n, qp.m, _hp(Q), _hp(c), float(qp.k),
+                                        _hp(A), _hp(b)), 'mgpu_load_qp')
+        self.qp = qp
+
+    def qp_solve(self, lb, ub, maxit=0, want_x=True):
+        lb = _np(lb, np.float64)
+        ub = _np(ub, np.float64)
+        B = lb.shape[0]
+        st = np.zeros(B, dtype=np.int32)
+        ob = np.zeros(B)
+        it = np.zeros(B, dtype=np.int32)
+        x = np.zeros_like(lb) if want_x else None
+        self._chk(self.lib.mgpu_qp_solve(self.h, B, _hp(lb), _hp(ub), int(maxit), _hp(st),
+                                         _hp(ob), _hp(it), _hp(x)), 'mgpu_qp_solve')
+        return st, ob, it, x
+
+    def qp_solve_dev(self, lb, ub, status, obj, iters, x=None, maxit=0):
+        self._chk(self.lib.mgpu_qp_solve_dev(self.h, int(lb.shape[0]), _dp(lb), _dp(ub),
+                                             int(maxit), _dp(status), _dp(obj), _dp(iters),
+                                             _dp(x)), 'mgpu_qp_solve_dev')
 
     def bnb_shard(self, rank, world) -> int:
         k = ctypes.c_int(0)

@@ -1,0 +1,55 @@
+"""CPU: the interior-point restatement of the QP relaxation solve
+(oracle/qp_ipm.py) converges on color_lab2_4x0 node boxes with a KKT
+certificate (primal/dual residuals, duality gap) and agrees with an
+independent solver (scipy SLSQP) on small convex QPs.  BQPD itself is
+absent, so iterates are unpinned; the optimal objective of a convex QP is
+unique and is what the GPU tests compare."""
+import os
+
+import numpy as np
+import pytest
+
+import qp_ipm
+from minotaur_amd import qp as qpm
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
+
+
+def random_qp(seed, n=12, m=3):
+    rng = np.random.default_rng(seed)
+    G = rng.normal(size=(n, n))
+    Q = G @ G.T / n + 1e-3 * np.eye(n)
+    c = rng.normal(size=n)
+    A = rng.normal(size=(m, n))
+    x0 = rng.uniform(0.2, 0.8, size=n)
+    return qpm.QpProblem(f'rqp{seed}', Q, c, 0.0, A, A @ x0, np.zeros(n), np.ones(n),
+                         np.full(n, 4, dtype=np.int32))
+
+
+def test_color_lab2_nodes_certified():
+    P = qpm.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'color_lab2_qp.npz'))
+    assert (P.n, P.m) == (300, 61)
+    LB, UB = qpm.random_node_boxes(P, 3, 5)
+    for b in range(3):
+        r = qp_ipm.solve_node(P.Q, P.c, P.A, P.b, LB[b], UB[b])
+        assert r['status'] == 0
+        cert = qp_ipm.kkt_certificate(P.Q, P.c, P.A, P.b, LB[b], UB[b], r['x'], r['y'],
+                                      r['zl'], r['zu'])
+        assert cert['rp'] <= 1e-8 and cert['rd'] <= 1e-8 and cert['box'] == 0.0
+        assert abs(cert['gap']) <= 1e-6 and cert['zmin'] >= 0.0
+
+
+@pytest.mark.parametrize('seed', range(4))
+def test_small_qp_matches_slsqp(seed):
+    from scipy.optimize import minimize
+    P = random_qp(seed)
+    r = qp_ipm.solve_node(P.Q, P.c, P.A, P.b, P.l, P.u)
+    assert r['status'] == 0
+    f = lambda x: 0.5 * x @ P.Q @ x + P.c @ x
+    s = minimize(f, np.full(P.n, 0.5), jac=lambda x: P.Q @ x + P.c, method='SLSQP',
+                 bounds=list(zip(P.l, P.u)),
+                 constraints=[{'type': 'eq', 'fun': lambda x: P.A @ x - P.b,
+                               'jac': lambda x: P.A}],
+                 options={'ftol': 1e-14, 'maxiter': 500})
+    assert s.success
+    assert abs(r['obj'] - s.fun) <= 1e-6 * max(1.0, abs(s.fun))

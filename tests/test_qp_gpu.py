@@ -1,0 +1,56 @@
+"""GPU: the batched QP relaxation solve (K5, MFMA KKT block) reaches the
+same optimal objectives as the interior-point restatement (within 1e-6,
+the north-star bar for relaxation objectives) with primal-feasible
+solutions, on color_lab2_4x0 node boxes and on small random convex QPs."""
+import os
+
+import numpy as np
+import pytest
+
+import qp_ipm
+from minotaur_amd import qp as qpm
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from minotaur_amd.runtime import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _check(P, LB, UB, st, ob, x, nref=None):
+    B = LB.shape[0]
+    assert np.all(st == 0)
+    for b in range(B):
+        assert np.max(np.abs(P.A @ x[b] - P.b), initial=0.0) <= 1e-7
+        assert np.all(x[b] >= LB[b] - 1e-9) and np.all(x[b] <= UB[b] + 1e-9)
+    for b in range(B if nref is None else nref):
+        r = qp_ipm.solve_node(P.Q, P.c, P.A, P.b, LB[b], UB[b])
+        assert r['status'] == 0
+        assert abs(ob[b] - (r['obj'] + P.k)) <= 1e-6 * max(1.0, abs(r['obj']))
+
+
+def test_color_lab2_batch(ctx):
+    P = qpm.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'color_lab2_qp.npz'))
+    ctx.load_qp(P)
+    LB, UB = qpm.random_node_boxes(P, 24, 9)
+    st, ob, it, x = ctx.qp_solve(LB, UB)
+    _check(P, LB, UB, st, ob, x, nref=6)
+    assert it.max() < 80 and ctx.last_kernel_ms('qp') > 0
+
+
+@pytest.mark.parametrize('seed', range(3))
+def test_random_qps(ctx, seed):
+    from test_qp_cpu import random_qp
+    P = random_qp(seed, n=20 + 7 * seed, m=3 + seed)
+    ctx.load_qp(P)
+    rng = np.random.default_rng(seed)
+    B = 33
+    LB = np.tile(P.l, (B, 1))
+    UB = np.tile(P.u, (B, 1))
+    st, ob, it, x = ctx.qp_solve(LB, UB)
+    _check(P, LB, UB, st, ob, x, nref=3)

@@ -4,6 +4,8 @@ fixtures under minotaur_amd/instances/ (run in the container that has
 
   tls4_lin.npz     — linear rows of test_instances/tls4.nl
   knapsack9.npz    — OA-LP of examples/knapsack (config 3)
+  color_lab2_qp.npz — QP relaxation data of test_instances/color_lab2_4x0.nl
+                      (dense Q, equality rows; config 4)
 """
 import os
 import sys
@@ -25,6 +27,11 @@ def main():
     ks = knapsack_oa()
     ks.save(os.path.join(OUT, 'knapsack9.npz'))
     print('knapsack9', ks.n, ks.m, ks.nnz)
+    from minotaur_amd.qp import from_nl as qp_from_nl, save as qp_save
+    cl = qp_from_nl(os.path.join(REF, 'test_instances', 'color_lab2_4x0.nl'),
+                    name='color_lab2_4x0')
+    qp_save(cl, os.path.join(OUT, 'color_lab2_qp.npz'))
+    print('color_lab2 QP', cl.n, cl.m)
 
 
 if __name__ == '__main__':
