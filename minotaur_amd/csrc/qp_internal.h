@@ -30,6 +30,7 @@ struct QpWork {
   double *rp;                // [B][mp]
   double *K;                 // [B][np][np]
   double *W;                 // [B][np][mp]
+  double *WT;                // [B][mp][np] (W', for W dy)
   double *M;                 // [B][mp][mp]
   int32_t *done, *iters, *status;
   double *obj;

@@ -308,6 +308,12 @@ __global__ __launch_bounds__(kT) void qp_trsm_syrk(QpWork w, int np, int mp) {
     }
     __syncthreads();
   }
+  // W' copy for the step kernel's W dy (coalesced writes along j)
+  double *WT = w.WT + (size_t)b * np * mp;
+  for (size_t e = t; e < (size_t)np * mp; e += kT) {
+    const int i = (int)(e / np), j = (int)(e % np);
+    WT[e] = W[(size_t)j * mp + i];
+  }
   // M = W'W: CB x CB output tiles, summed over the T row tiles of W
   for (int tix = wave; tix < CB * CB; tix += 4) {
     const int ib = tix / CB, jb = tix % CB;
@@ -333,12 +339,16 @@ struct StepSm {
   double *y, *rp, *tt, *dy;
   double *Lm;     // [mp][mp+1]
   double *part;   // [16][17] partial sums
+  double *dt;     // [16][17] diagonal tile of L
   double *red;    // [kT]
 };
 
-// v = L^-1 r (blocked by 16 rows: GEMV against solved rows, then the
-// diagonal block by one thread)
-__device__ void fwd_L(const double *K, int np, const double *r, double *v, double *part) {
+// v = L^-1 r, blocked by 16 rows: a GEMV of the block's rows against the
+// solved part (256 threads, 16 partial sums per row), then the diagonal
+// tile (staged in LDS) by a 16-lane substitution with v_readlane
+// broadcasts.  dt: [16][17] LDS tile.
+__device__ void fwd_L(const double *K, int np, const double *r, double *v, double *part,
+                      double *dt) {
   const int t = threadIdx.x, rr = t & 15, pp = t >> 4;
   const int T = np / 16;
   for (int ib = 0; ib < T; ++ib) {
@@ -346,22 +356,30 @@ __device__ void fwd_L(const double *K, int np, const double *r, double *v, doubl
     double acc = 0.0;
     for (int c = pp; c < r0; c += 16) acc += K[(size_t)(r0 + rr) * np + c] * v[c];
     part[pp * 17 + rr] = acc;
+    dt[(t >> 4) * 17 + (t & 15)] = K[(size_t)(r0 + (t >> 4)) * np + r0 + (t & 15)];
     __syncthreads();
-    if (t == 0) {
-      for (int i = 0; i < 16; ++i) {
-        double s = 0.0;
-        for (int q2 = 0; q2 < 16; ++q2) s += part[q2 * 17 + i];
-        double val = r[r0 + i] - s;
-        for (int p = 0; p < i; ++p) val -= K[(size_t)(r0 + i) * np + r0 + p] * v[r0 + p];
-        v[r0 + i] = val / K[(size_t)(r0 + i) * np + r0 + i];
+    if (t < 64) {
+      double val = 0.0;
+      if (t < 16) {
+        double sum = 0.0;
+        for (int q2 = 0; q2 < 16; ++q2) sum += part[q2 * 17 + t];
+        val = r[r0 + t] - sum;
       }
+      double mine = 0.0;
+      for (int c = 0; c < 16; ++c) {
+        const double vc = __shfl(val, c, 64) / dt[c * 17 + c];
+        if (t == c) mine = vc;
+        if (t > c && t < 16) val -= dt[t * 17 + c] * vc;
+      }
+      if (t < 16) v[r0 + t] = mine;
     }
     __syncthreads();
   }
 }
 
-// x = L^-T s (blocked, from the last row block up)
-__device__ void bwd_LT(const double *K, int np, const double *s, double *xo, double *part) {
+// x = L^-T s (blocked, from the last row block up; same scheme)
+__device__ void bwd_LT(const double *K, int np, const double *s, double *xo, double *part,
+                       double *dt) {
   const int t = threadIdx.x, rr = t & 15, pp = t >> 4;
   const int T = np / 16;
   for (int ib = T - 1; ib >= 0; --ib) {
@@ -369,15 +387,22 @@ __device__ void bwd_LT(const double *K, int np, const double *s, double *xo, dou
     double acc = 0.0;
     for (int k = r0 + 16 + pp; k < np; k += 16) acc += K[(size_t)k * np + r0 + rr] * xo[k];
     part[pp * 17 + rr] = acc;
+    dt[(t >> 4) * 17 + (t & 15)] = K[(size_t)(r0 + (t >> 4)) * np + r0 + (t & 15)];
     __syncthreads();
-    if (t == 0) {
-      for (int i = 15; i >= 0; --i) {
+    if (t < 64) {
+      double val = 0.0;
+      if (t < 16) {
         double sum = 0.0;
-        for (int q2 = 0; q2 < 16; ++q2) sum += part[q2 * 17 + i];
-        double val = s[r0 + i] - sum;
-        for (int p = i + 1; p < 16; ++p) val -= K[(size_t)(r0 + p) * np + r0 + i] * xo[r0 + p];
-        xo[r0 + i] = val / K[(size_t)(r0 + i) * np + r0 + i];
+        for (int q2 = 0; q2 < 16; ++q2) sum += part[q2 * 17 + t];
+        val = s[r0 + t] - sum;
       }
+      double mine = 0.0;
+      for (int c = 15; c >= 0; --c) {
+        const double xc = __shfl(val, c, 64) / dt[c * 17 + c];
+        if (t == c) mine = xc;
+        if (t < c) val -= dt[c * 17 + t] * xc;
+      }
+      if (t < 16) xo[r0 + t] = mine;
     }
     __syncthreads();
   }
@@ -385,10 +410,10 @@ __device__ void bwd_LT(const double *K, int np, const double *s, double *xo, dou
 
 // (dx, dy) for right-hand side r1: v = L^-1 r1, Lm Lm' dy = rp - W'v,
 // dx = L^-T (v + W dy), dx = 0 on fixed variables
-__device__ void kkt_solve(const double *K, const double *W, int np, int mp, const StepSm &s,
-                          const double *r1) {
+__device__ void kkt_solve(const double *K, const double *W, const double *WT, int np, int mp,
+                          const StepSm &s, const double *r1) {
   const int t = threadIdx.x;
-  fwd_L(K, np, r1, s.v, s.part);
+  fwd_L(K, np, r1, s.v, s.part, s.dt);
   // tt = rp - W'v (4 partial sums per column, coalesced over the column)
   {
     const int i = t & 63, pp = t >> 6;
@@ -423,14 +448,14 @@ __device__ void kkt_solve(const double *K, const double *W, int np, int mp, cons
     }
   }
   __syncthreads();
-  // s2 = v + W dy
+  // s2 = v + W dy  (W' [mp][np] copy: coalesced across j)
   for (int j = t; j < np; j += kT) {
     double acc = 0.0;
-    for (int i = 0; i < mp; ++i) acc += W[(size_t)j * mp + i] * s.dy[i];
+    for (int i = 0; i < mp; ++i) acc += WT[(size_t)i * np + j] * s.dy[i];
     s.s2[j] = s.v[j] + acc;
   }
   __syncthreads();
-  bwd_LT(K, np, s.s2, s.dx, s.part);
+  bwd_LT(K, np, s.s2, s.dx, s.part, s.dt);
   for (int j = t; j < np; j += kT)
     if (!(s.l[j] < s.u[j])) s.dx[j] = 0.0;
   __syncthreads();
@@ -464,11 +489,13 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   s.rd = p; p += np; s.v = p; p += np; s.dx = p; p += np; s.s2 = p; p += np;
   s.dzl = p; p += np; s.dzu = p; p += np; s.rl = p; p += np; s.ru = p; p += np;
   s.y = p; p += mp; s.rp = p; p += mp; s.tt = p; p += mp; s.dy = p; p += mp;
-  s.Lm = p; p += mp * mpad; s.part = p; p += 16 * 17; s.red = p; p += kT;
+  s.Lm = p; p += mp * mpad; s.part = p; p += 16 * 17; s.dt = p; p += 16 * 17;
+  s.red = p; p += kT;
   double *r1 = s.s2;  // reuse: r1 is consumed by fwd_L before s2 is written
   const size_t o = (size_t)b * np, oy = (size_t)b * mp;
   const double *K = w.K + (size_t)b * np * np;
   const double *W = w.W + (size_t)b * np * mp;
+  const double *WT = w.WT + (size_t)b * np * mp;
   for (int j = t; j < np; j += kT) {
     s.x[j] = w.x[o + j];
     s.l[j] = w.l[o + j];
@@ -519,7 +546,7 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   for (int j = t; j < np; j += kT)
     r1[j] = s.l[j] < s.u[j] ? -s.rd[j] - s.zl[j] + s.zu[j] : 0.0;
   __syncthreads();
-  kkt_solve(K, W, np, mp, s, r1);
+  kkt_solve(K, W, WT, np, mp, s, r1);
   for (int j = t; j < np; j += kT) {
     const bool fr = s.l[j] < s.u[j];
     const double sl = s.x[j] - s.l[j], su = s.u[j] - s.x[j];
@@ -550,7 +577,7 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
     r1[j] = fr ? -s.rd[j] + rl / sl - ru / su : 0.0;
   }
   __syncthreads();
-  kkt_solve(K, W, np, mp, s, r1);
+  kkt_solve(K, W, WT, np, mp, s, r1);
   for (int j = t; j < np; j += kT) {
     const bool fr = s.l[j] < s.u[j];
     const double sl = s.x[j] - s.l[j], su = s.u[j] - s.x[j];
@@ -593,7 +620,7 @@ __global__ __launch_bounds__(kT) void qp_final(DevQP q, QpWork w) {
 }  // namespace
 
 size_t qp_step_lds(int np, int mp) {
-  return sizeof(double) * ((size_t)13 * np + 4 * mp + (size_t)mp * (mp + 1) + 16 * 17 + kT);
+  return sizeof(double) * ((size_t)13 * np + 4 * mp + (size_t)mp * (mp + 1) + 2 * 16 * 17 + kT);
 }
 
 hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s) {

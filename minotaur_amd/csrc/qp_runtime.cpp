@@ -14,11 +14,11 @@ struct QpState {
   DevQP dq{};
   int n = 0, m = 0;
   DevBuf Q, c, A, AT, b;
-  DevBuf l, u, x, zl, zu, y, rd, rp, K, W, M, done, iters, status, obj;
+  DevBuf l, u, x, zl, zu, y, rd, rp, K, W, WT, M, done, iters, status, obj;
   int maxB = 0;
   DevBuf h_l, h_u, h_st, h_obj, h_it, h_x;  // host-path device copies
   void release() {
-    for (DevBuf *p : {&Q, &c, &A, &AT, &b, &l, &u, &x, &zl, &zu, &y, &rd, &rp, &K, &W, &M,
+    for (DevBuf *p : {&Q, &c, &A, &AT, &b, &l, &u, &x, &zl, &zu, &y, &rd, &rp, &K, &W, &WT, &M,
                       &done, &iters, &status, &obj, &h_l, &h_u, &h_st, &h_obj, &h_it, &h_x})
       p->release();
   }
@@ -58,6 +58,7 @@ int ensure_qp_batch(mgpu_ctx *c, QpState &s, int B) {
   HIPCHK(c, s.rp.ensure((size_t)B * mp * 8));
   HIPCHK(c, s.K.ensure((size_t)B * np * np * 8));
   HIPCHK(c, s.W.ensure((size_t)B * np * mp * 8));
+  HIPCHK(c, s.WT.ensure((size_t)B * np * mp * 8));
   HIPCHK(c, s.M.ensure((size_t)B * mp * mp * 8));
   for (DevBuf *p : {&s.done, &s.iters, &s.status}) HIPCHK(c, p->ensure((size_t)B * 4));
   HIPCHK(c, s.obj.ensure((size_t)B * 8));
@@ -144,6 +145,7 @@ int mgpu_qp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   w.rp = s.rp.as<double>();
   w.K = s.K.as<double>();
   w.W = s.W.as<double>();
+  w.WT = s.WT.as<double>();
   w.M = s.M.as<double>();
   w.done = s.done.as<int32_t>();
   w.iters = s.iters.as<int32_t>();
