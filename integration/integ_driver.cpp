@@ -15,6 +15,13 @@
 #include "Function.h"
 #include "HipLPEngine.h"
 #include "HipLinearHandler.h"
+#include "HipQuadHandler.h"
+#include "LinConMod.h"
+#include "QuadHandler.h"
+#include "QuadraticFunction.h"
+#include "Relaxation.h"
+#include "SolutionPool.h"
+#include "VarBoundMod.h"
 #include "IntVarHandler.h"
 #include "LinearFunction.h"
 #include "LinearHandler.h"
@@ -170,6 +177,147 @@ int integ_bnb(int device, int hip_fbbt, int n, int m, const int *rowptr, const i
   delete nproc;
   delete nr;
   delete bab;
+  delete env;
+  return 0;
+}
+
+// ---- quadratic handler: reference QuadHandler vs HipQuadHandler ----------
+// Same layout as oracle/ref/ref_quad.cpp's QSpec (oracle.qspec builds it).
+struct QSpecI {
+  int nv0, nv;
+  const int *vtype;
+  const double *vlb, *vub;
+  int nsq;
+  const int *sq_x, *sq_y;
+  int nbil;
+  const int *bil_x0, *bil_x1, *bil_y;
+  int ncon;
+  const int *lptr, *lvar;
+  const double *lval;
+  const int *qptr, *qv1, *qv2;
+  const double *qval;
+  const double *clb, *cub;
+  int has_obj;
+  double obj_const;
+};
+
+static FunctionPtr qfun(const QSpecI &s, ProblemPtr prob, int c) {
+  LinearFunctionPtr lf = LinearFunctionPtr();
+  QuadraticFunctionPtr qf = QuadraticFunctionPtr();
+  if (s.lptr[c + 1] > s.lptr[c]) {
+    lf = (LinearFunctionPtr) new LinearFunction();
+    for (int k = s.lptr[c]; k < s.lptr[c + 1]; ++k) lf->addTerm(prob->getVariable(s.lvar[k]), s.lval[k]);
+  }
+  if (s.qptr[c + 1] > s.qptr[c]) {
+    qf = (QuadraticFunctionPtr) new QuadraticFunction();
+    for (int k = s.qptr[c]; k < s.qptr[c + 1]; ++k)
+      qf->addTerm(prob->getVariable(s.qv1[k]), prob->getVariable(s.qv2[k]), s.qval[k]);
+  }
+  return qf ? (FunctionPtr) new Function(lf, qf) : (FunctionPtr) new Function(lf);
+}
+
+// Runs presolveNode of a QuadHandler (hip = 0 reference, 1 HipQuadHandler)
+// on the root box, then on every node box with the relaxation rows reset to
+// their root state; outputs the bounds, verdicts, r_mods counts, the row
+// state after each call, and (hip) the GPU / CPU call counts.
+int integ_quad(int device, int hip, const QSpecI *sp, int has_inc, double inc, int B,
+               const double *node_lb, const double *node_ub, double *out_lb, double *out_ub,
+               int *infeas, int *nmods, double *rows_out, int *calls) {
+  const QSpecI &s = *sp;
+  EnvPtr env = (EnvPtr) new Environment();
+  int err = 0;
+  env->startTimer(err);
+  ProblemPtr orig = (ProblemPtr) new Problem(env);
+  for (int j = 0; j < s.nv0; ++j) orig->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
+  for (int c = 0; c < s.ncon; ++c) orig->newConstraint(qfun(s, orig, c), s.clb[c], s.cub[c]);
+  if (s.has_obj) orig->newObjective(qfun(s, orig, s.ncon), s.obj_const, Minimize);
+  else orig->newObjective((FunctionPtr) new Function((LinearFunctionPtr) new LinearFunction()),
+                          s.obj_const, Minimize);
+  orig->calculateSize();
+  ProblemPtr p = (ProblemPtr) new Problem(env);
+  for (int j = 0; j < s.nv; ++j) p->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
+  QuadHandler *qh = hip ? (QuadHandler *) new HipQuadHandler(env, p, orig, device)
+                        : new QuadHandler(env, p, orig);
+  auto add_aux = [&](int x0, int x1, int y) {
+    LinearFunctionPtr lf = (LinearFunctionPtr) new LinearFunction();
+    lf->addTerm(p->getVariable(y), -1.0);
+    QuadraticFunctionPtr qf = (QuadraticFunctionPtr) new QuadraticFunction();
+    qf->addTerm(p->getVariable(x0), p->getVariable(x1), 1.0);
+    qh->addConstraint(p->newConstraint((FunctionPtr) new Function(lf, qf), 0.0, 0.0));
+  };
+  for (int k = 0; k < s.nsq; ++k) add_aux(s.sq_x[k], s.sq_x[k], s.sq_y[k]);
+  for (int k = 0; k < s.nbil; ++k) add_aux(s.bil_x0[k], s.bil_x1[k], s.bil_y[k]);
+  p->calculateSize();
+  RelaxationPtr rel = (RelaxationPtr) new Relaxation(env);
+  for (int j = 0; j < s.nv; ++j) {
+    VariablePtr v = p->getVariable(j);
+    rel->newVariable(v->getLb(), v->getUb(), v->getType());
+  }
+  bool inf = false;
+  qh->relaxInitInc(rel, &inf);
+  rel->calculateSize();
+  SolutionPoolPtr spool = (SolutionPoolPtr) new SolutionPool(env, p, 1);
+  if (has_inc) {
+    std::vector<double> x(s.nv, 0.0);
+    spool->addSolution(x.data(), inc);
+  }
+  const int nrows = s.nsq + 4 * s.nbil;
+  std::vector<LinearFunctionPtr> lf0(nrows);
+  std::vector<double> ub0(nrows);
+  for (int i = 0; i < nrows; ++i) {
+    lf0[i] = rel->getConstraint(i)->getLinearFunction()->clone();
+    ub0[i] = rel->getConstraint(i)->getUb();
+  }
+  auto set_box = [&](const double *lb, const double *ub) {
+    for (int j = 0; j < s.nv; ++j) {
+      p->changeBound(p->getVariable(j), lb[j], ub[j]);
+      rel->changeBound(rel->getVariable(j), lb[j], ub[j]);
+    }
+    for (int i = 0; i < nrows; ++i)
+      rel->changeConstraint(rel->getConstraint(i), lf0[i]->clone(), -INFINITY, ub0[i]);
+  };
+  const int R = 2 * s.nsq + 12 * s.nbil;
+  for (int b = -1; b < B; ++b) {   // b = -1: the root call
+    if (b < 0) set_box(s.vlb, s.vub);
+    else set_box(node_lb + (size_t)b * s.nv, node_ub + (size_t)b * s.nv);
+    ModVector pm, rm;
+    const bool r = qh->presolveNode(rel, NodePtr(), spool, pm, rm);
+    if (b < 0) {
+      for (ModificationPtr m : pm) delete m;
+      for (ModificationPtr m : rm) delete m;
+      continue;
+    }
+    infeas[b] = r ? 1 : 0;
+    nmods[b] = (int)rm.size();
+    for (int j = 0; j < s.nv; ++j) {
+      out_lb[(size_t)b * s.nv + j] = rel->getVariable(j)->getLb();
+      out_ub[(size_t)b * s.nv + j] = rel->getVariable(j)->getUb();
+    }
+    double *ro = rows_out + (size_t)b * R;
+    int o = 0;
+    for (int k = 0; k < s.nsq; ++k) {
+      ConstraintPtr c = rel->getConstraint(k);
+      ro[o++] = c->getLinearFunction()->getWeight(rel->getVariable(s.sq_x[k]));
+      ro[o++] = c->getUb();
+    }
+    for (int k = 0; k < s.nbil; ++k)
+      for (int t = 0; t < 4; ++t) {
+        ConstraintPtr c = rel->getConstraint(s.nsq + 4 * k + t);
+        ro[o++] = c->getLinearFunction()->getWeight(rel->getVariable(s.bil_x0[k]));
+        ro[o++] = c->getLinearFunction()->getWeight(rel->getVariable(s.bil_x1[k]));
+        ro[o++] = c->getUb();
+      }
+    for (ModificationPtr m : pm) delete m;
+    for (ModificationPtr m : rm) delete m;
+  }
+  calls[0] = hip ? (int)((HipQuadHandler *)qh)->gpuCalls() : 0;
+  calls[1] = hip ? (int)((HipQuadHandler *)qh)->cpuCalls() : 0;
+  for (LinearFunctionPtr f : lf0) delete f;
+  delete qh;
+  delete spool;
+  delete rel;
+  delete p;
+  delete orig;
   delete env;
   return 0;
 }

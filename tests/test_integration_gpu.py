@@ -100,3 +100,37 @@ def test_bnb_gpu_fbbt_matches_reference_fbbt(integ, name):
         assert math.isinf(r1[0])
     else:
         assert abs(r1[0] - opt) <= 1e-6 * max(1.0, abs(opt))
+
+
+@pytest.mark.parametrize('seed,inc', [(0, None), (2, 'mid'), (4, None)])
+def test_hip_quad_handler_matches_reference(integ, seed, inc):
+    """HipQuadHandler (QuadHandler subclass, node FBBT via mgpu_quad_fbbt)
+    inside the reference's own Problem / Relaxation / SolutionPool objects
+    gives the reference QuadHandler's bounds, verdicts, r_mods counts and
+    secant / McCormick rows bit for bit; the root call stays on the CPU and
+    every node call runs on the GPU."""
+    import oracle
+    from golden_io import bits_equal
+    from minotaur_amd.quad import objective_at, random_qcqp, random_quad_boxes
+    integ.integ_quad.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_double,
+                                 ctypes.c_int] + [P] * 7
+    qp = random_qcqp(seed, nv0=10, ncon=6)
+    LB, UB = random_quad_boxes(qp, 40, 900 + seed, edge=True)
+    incv = objective_at(qp, 0.5 * (qp.vlb[:qp.nv0] + qp.vub[:qp.nv0])) if inc else 0.0
+    spec = oracle.qspec(qp)
+    out = {}
+    for hip in (0, 1):
+        B = LB.shape[0]
+        olb, oub = np.zeros_like(LB), np.zeros_like(UB)
+        inf = np.zeros(B, dtype=np.int32)
+        nm = np.zeros(B, dtype=np.int32)
+        rows = np.zeros((B, qp.nrow_state))
+        calls = np.zeros(2, dtype=np.int32)
+        integ.integ_quad(0, hip, ctypes.byref(spec), 1 if inc else 0, incv, B, _p(LB), _p(UB),
+                         _p(olb), _p(oub), _p(inf), _p(nm), _p(rows), _p(calls))
+        out[hip] = (olb, oub, inf, nm, rows, calls)
+    (a_lb, a_ub, a_inf, a_nm, a_rows, _), (b_lb, b_ub, b_inf, b_nm, b_rows, calls) = out[0], out[1]
+    assert bits_equal(a_lb, b_lb) and bits_equal(a_ub, b_ub)
+    assert np.array_equal(a_inf, b_inf) and np.array_equal(a_nm, b_nm)
+    assert bits_equal(a_rows, b_rows)
+    assert calls[0] == LB.shape[0] and calls[1] == 1   # only the root call on the CPU
