@@ -76,7 +76,7 @@ __host__ __device__ inline size_t shared_ws_bytes(int n, int m) {
          al16((size_t)m * 4);
 }
 __host__ __device__ inline size_t wave_bytes(int N) {
-  return 5 * al16((size_t)N * 8) + 2 * al16((size_t)N) + 2 * 64 * 8;
+  return 6 * al16((size_t)N * 8) + 2 * al16((size_t)N) + 2 * 64 * 8;
 }
 
 __device__ __forceinline__ double art_lo(double thi, double ab) {
@@ -91,7 +91,7 @@ struct Ctx {
   const int *colptr, *rowidx, *rowptr, *ccol;
   const double *cval, *rval;
   // per-wave column state
-  double *d, *z, *blo, *bhi, *al, *rho, *aq;
+  double *d, *z, *blo, *bhi, *al, *t2, *rho, *aq;
   int8_t *st, *art;
   // problem
   int n, m, N;
@@ -245,6 +245,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     C.blo = (double *)wp; wp += al16((size_t)N * 8);
     C.bhi = (double *)wp; wp += al16((size_t)N * 8);
     C.al = (double *)wp;  wp += al16((size_t)N * 8);
+    C.t2 = (double *)wp;  wp += al16((size_t)N * 8);
     C.st = (int8_t *)wp;  wp += al16((size_t)N);
     C.art = (int8_t *)wp; wp += al16((size_t)N);
     C.rho = (double *)wp; wp += 64 * 8;
@@ -384,8 +385,10 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       }
       double best = fabs(inf);
       int r = best > 0.0 ? lane : INT_MAX;
-      wave_argmax(best, r);
-      r = __builtin_amdgcn_readfirstlane(r);
+      wave_argmax_dpp(best, r);
+      // keep the (wave-uniform) result in a VGPR: as an SGPR value it lets
+      // LLVM re-schedule the pivot around it at +100 VGPRs
+      asm volatile("" : "+v"(best));
       if (best == 0.0) {
         if (!fresh) {
           zB = compute_primals(C, binv);
@@ -433,11 +436,12 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       const double sigma = delta > 0 ? 1.0 : -1.0;
 
       STAMP(2);
-      // ---- pivot row and Harris pass 1 ----
+      // ---- pivot row and Harris pass 1 (pass 2's ratio is cached in t2:
+      // +inf for columns that cannot enter) ----
       double tmax = INFINITY;
       for (int j = lane; j < N; j += 64) {
         const int8_t s = C.st[j];
-        double a = 0.0;
+        double a = 0.0, t2 = INFINITY;
         if (s != ST_BASIC && C.blo[j] != C.bhi[j]) {
           if (j >= n) {
             a = -C.rho[j - n];
@@ -447,18 +451,23 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
           const double at = sigma * a, dj = C.d[j];
           if (s == ST_LB && at > kPivTol) {
             const double t = (fmax(dj, 0.0) + kDTol) / at;
+            t2 = fmax(dj, 0.0) / at;
             if (t < tmax) tmax = t;
           } else if (s == ST_UB && at < -kPivTol) {
             const double t = (fmin(dj, 0.0) - kDTol) / at;
+            t2 = fmin(dj, 0.0) / at;
             if (t < tmax) tmax = t;
           } else if (s == ST_FREE && fabs(at) > kPivTol) {
             const double t = kDTol / fabs(at);
+            t2 = 0.0;
             if (t < tmax) tmax = t;
           }
         }
         C.al[j] = a;
+        C.t2[j] = t2;
       }
-      tmax = wave_min(tmax);
+      tmax = wave_min_dpp(tmax);
+      asm volatile("" : "+v"(tmax));
       if (tmax == INFINITY) {  // dual unbounded
         bool boxed = false;
         for (int j = lane; j < N; j += 64) boxed |= C.st[j] != ST_BASIC && C.art[j] != 0;
@@ -477,17 +486,12 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       double qa = 0.0;
       int q = INT_MAX;
       for (int j = lane; j < N; j += 64) {
-        const int8_t s = C.st[j];
-        if (s == ST_BASIC || C.blo[j] == C.bhi[j]) continue;
-        const double at = sigma * C.al[j], dj = C.d[j];
-        double t;
-        if (s == ST_LB && at > kPivTol) t = fmax(dj, 0.0) / at;
-        else if (s == ST_UB && at < -kPivTol) t = fmin(dj, 0.0) / at;
-        else if (s == ST_FREE && fabs(at) > kPivTol) t = 0.0;
-        else continue;
-        if (t <= tmax && fabs(at) > qa) {
-          qa = fabs(at);
-          q = j;
+        if (C.t2[j] <= tmax) {
+          const double fa = fabs(C.al[j]);
+          if (fa > qa) {
+            qa = fa;
+            q = j;
+          }
         }
       }
       wave_argmax_dpp(qa, q);
