@@ -112,6 +112,25 @@ struct Ctx {
   }
 };
 
+// rho' a_j over CSC column j in CSC order; four entries' loads are issued
+// before their products are summed (the adds keep the sequential order)
+__device__ __forceinline__ double col_dot(const Ctx &C, int j) {
+  double a = 0.0;
+  int t = C.colptr[j];
+  const int e = C.colptr[j + 1];
+  for (; t + 4 <= e; t += 4) {
+    const int i0 = C.rowidx[t], i1 = C.rowidx[t + 1], i2 = C.rowidx[t + 2], i3 = C.rowidx[t + 3];
+    const double v0 = C.cval[t], v1 = C.cval[t + 1], v2 = C.cval[t + 2], v3 = C.cval[t + 3];
+    const double r0 = C.rho[i0], r1 = C.rho[i1], r2 = C.rho[i2], r3 = C.rho[i3];
+    a += v0 * r0;
+    a += v1 * r1;
+    a += v2 * r2;
+    a += v3 * r3;
+  }
+  for (; t < e; ++t) a += C.cval[t] * C.rho[C.rowidx[t]];
+  return a;
+}
+
 // oracle place_nonbasic
 __device__ __forceinline__ void place_nonbasic(const Ctx &C, int j, double ab) {
   const double lo = C.blo[j], hi = C.bhi[j], dj = C.d[j];
@@ -446,20 +465,20 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
           if (j >= n) {
             a = -C.rho[j - n];
           } else {
-            for (int t = C.colptr[j]; t < C.colptr[j + 1]; ++t) a += C.cval[t] * C.rho[C.rowidx[t]];
+            a = col_dot(C, j);
           }
-          const double at = sigma * a, dj = C.d[j];
-          if (s == ST_LB && at > kPivTol) {
-            const double t = (fmax(dj, 0.0) + kDTol) / at;
-            t2 = fmax(dj, 0.0) / at;
-            if (t < tmax) tmax = t;
-          } else if (s == ST_UB && at < -kPivTol) {
-            const double t = (fmin(dj, 0.0) - kDTol) / at;
-            t2 = fmin(dj, 0.0) / at;
-            if (t < tmax) tmax = t;
-          } else if (s == ST_FREE && fabs(at) > kPivTol) {
-            const double t = kDTol / fabs(at);
-            t2 = 0.0;
+          // Harris ratios without divergent branches: one numerator pair and
+          // denominator per case, two divisions for every lane (the same
+          // operands as the per-case formulas, so the same values)
+          const double at = sigma * a, dj = C.d[j], fat = fabs(at);
+          const bool lb = s == ST_LB && at > kPivTol, ub = s == ST_UB && at < -kPivTol,
+                     fr = s == ST_FREE && fat > kPivTol;
+          const double n2 = lb ? fmax(dj, 0.0) : ub ? fmin(dj, 0.0) : 0.0;
+          const double n1 = lb ? n2 + kDTol : ub ? n2 - kDTol : kDTol;
+          const double den = fr ? fat : at;
+          if (lb || ub || fr) {
+            const double t = n1 / den;
+            t2 = fr ? 0.0 : n2 / den;
             if (t < tmax) tmax = t;
           }
         }
