@@ -241,10 +241,18 @@ def main():
     from minotaur_amd.runtime import Context, WarmStart
 
     rank, world, local = mdist.env_ranks()
+    # MGPU_BENCH_REHEARSAL=1 (test hook): every rank on device 0 over gloo, to
+    # rehearse the N>1 path on a one-GPU box (RCCL refuses a shared device)
+    rehearse = os.environ.get('MGPU_BENCH_REHEARSAL') == '1'
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if rehearse:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=dev)
 
     p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_lin.npz'))
     B = args.batch
@@ -385,6 +393,8 @@ def main():
             "tree_search": tree,
             "qp_relaxation": qprel,
         }
+        if rehearse:
+            line["rehearsal"] = "all ranks on device 0 over gloo (not a scaling number)"
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:

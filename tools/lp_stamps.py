@@ -10,8 +10,9 @@ import sys
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
 sys.path.insert(0, ROOT)
 OUT = os.environ.get('STAMP_LIB', os.path.join(ROOT, 'gpurun_out', 'libmgpu_stamps.so'))
-NAMES = ['setup', 'pricing', 'rho_write', 'pass1+min', 'pass2+argmax', 'column_q',
-         'steps/updates', 'binv_update', 'tail', 'outputs']
+NAMES = ['setup:primals', 'pricing', 'rho_write', 'pass1+min', 'pass2+argmax', 'column_q',
+         'steps/updates', 'binv_update', 'tail', 'outputs', 'setup:skip',
+         'setup:bounds', 'setup:basis', 'setup:place']
 
 
 def build():
@@ -42,7 +43,7 @@ def main():
     lib.mgpu_debug_lp_stamps(buf, 1)
     r = ctx.lp_solve(f.lb, f.ub, wsh, skip=f.infeasible)
     lib.mgpu_debug_lp_stamps(buf, 1)
-    tot = sum(buf[i] for i in range(10))
+    tot = sum(buf[i] for i in range(len(NAMES)))
     piv = int(r.iters.sum())
     print(f"pivots {piv}  total wave-cycles {tot:.3e}  per pivot {tot / max(piv, 1):.0f}")
     for i, nme in enumerate(NAMES):
