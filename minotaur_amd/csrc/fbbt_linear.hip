@@ -601,7 +601,7 @@ __device__ __forceinline__ bool check_bounds(const DevLP &lp, const V &v) {
   return bad || lp.cons_bad != 0;
 }
 
-template <bool kLds, bool kBitFlags>
+template <bool kLds, bool kBitFlags, bool kRC>
 __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x;
@@ -688,9 +688,9 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
           bool tch;
           v.clear(r);
           bool inf;
-          if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
+          if (kRC && nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (kRC && nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (kRC && nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
           else inf = lin_bnd_tighten(lp.trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
           if (inf) {
             cons_on = false;
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
       }
     }
     if (go && io.has_inc && lp.nobj > 0) {
-      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
+      if (kRC && lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
       else bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
     }
     tighten_ints(lp, v, s, log, go, changed);
@@ -722,20 +722,20 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   }
 }
 
-template <bool kLds, bool kBits>
+template <bool kLds, bool kBits, bool kRC = true>
 hipError_t launch_variant(const DevLP &lp, const FbbtIO &io, size_t lds, hipStream_t stream) {
   const int waves = (io.batch + io.npw - 1) / io.npw;
   if constexpr (kLds) {
     static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted in
     if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute((const void *)fbbt_linear_kernel<kLds, kBits>,
+      hipError_t e = hipFuncSetAttribute((const void *)fbbt_linear_kernel<kLds, kBits, kRC>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024);
       if (e != hipSuccess) return e;
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL((fbbt_linear_kernel<kLds, kBits>), dim3(waves), dim3(kLanes),
+  hipLaunchKernelGGL((fbbt_linear_kernel<kLds, kBits, kRC>), dim3(waves), dim3(kLanes),
                      kLds ? lds : 0, stream, lp, io);
   return hipGetLastError();
 }
@@ -752,6 +752,17 @@ hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
   const size_t lds = fbbt_lds_bytes(lp.n, lp.m);
   const bool use_lds = variant == 1 || (variant == 0 && lds <= 160 * 1024);
   const bool bits = lp.m <= 64;
+  // experiment switch: the generic (rolled) row path only, no register-
+  // cached row templates (code size vs instruction cache)
+  static const bool norc = getenv("MGPU_FBBT_NORC") != nullptr;
+  if (norc && bits) {
+    if (use_lds) {
+      if (lds > 160 * 1024) return hipErrorInvalidValue;
+      return launch_variant<true, true, false>(lp, io, lds, stream);
+    }
+    if (io.scratch == nullptr) return hipErrorInvalidValue;
+    return launch_variant<false, true, false>(lp, io, 0, stream);
+  }
   if (use_lds) {
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     return bits ? launch_variant<true, true>(lp, io, lds, stream)
