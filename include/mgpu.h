@@ -120,7 +120,8 @@ int mgpu_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in,
  *                 +INF for infeasible nodes.
  *   x           : [batch][n] primal solution, or NULL.
  *   wo_*        : [batch] warm starts out (children's warm start), or NULL.
- * Current limit: m <= 64 rows (basis inverse rows held one per lane). */
+ * Kernels: K3 (basis-inverse rows one per lane, m <= 64) or, for more rows,
+ * K3L (one node per workgroup, B^-1 in HBM; n + m up to ~3000). */
 int mgpu_lp_solve(mgpu_ctx *ctx, int batch, const double *lb, const double *ub,
                   const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,
                   const double *ws_d, const double *ws_binv, int ws_shared,
@@ -153,6 +154,11 @@ int mgpu_node_decide_dev(mgpu_ctx *ctx, int batch, const int32_t *d_fbbt_infeas,
  * K2): 0 auto, 1 node state in LDS, 2 node state in a global scratch
  * (large n). For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
+
+/* Which LP kernel the next LP calls use: 0 auto (K3 when m <= 64 and the
+ * matrix fits LDS, else K3L), 1 K3, 2 K3L.  Both restate oracle/lp_dual.c
+ * pivot for pivot.  For tests/benchmarks. */
+int mgpu_set_lp_variant(mgpu_ctx *ctx, int variant);
 
 /* Batched bound LPs: LP b minimises obj_sign[b] * x[obj_col[b]] over the
  * loaded relaxation on ONE box lb/ub [n] (the relaxation's), warm-started

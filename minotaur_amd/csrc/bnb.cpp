@@ -79,9 +79,6 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_init: no problem loaded");
   if (capacity < 2 || !root_lb || !root_ub)
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: bad argument");
-  if (c->lp.m > kLpMaxM)
-    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: m=%d rows > %d not supported yet", c->lp.m,
-                kLpMaxM);
   HIPCHK(c, hipSetDevice(c->device));
   bnb_state_free(c);
   BnbState *s = new BnbState();

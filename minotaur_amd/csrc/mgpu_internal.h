@@ -120,6 +120,12 @@ hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t s
 
 size_t lp_lds_bytes(int n, int m, int nnz);
 hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, int num_cus, hipStream_t stream);
+// K3L (lp_large.hip): one node per 256-thread workgroup, B^-1 in HBM slots
+size_t lp_large_lds_bytes(int n, int m);
+int lp_large_grid(int batch, int n, int m, int num_cus);
+hipError_t lp_large_prepare();
+hipError_t launch_lp_large(const DevLP &lp, const LpIO &io, double *binv_slots, int grid,
+                           hipStream_t stream);
 
 // Output/optional mod-log arguments of one FBBT launch.
 struct FbbtIO {

@@ -57,7 +57,7 @@ int mgpu_destroy(mgpu_ctx *c) {
                     &c->trec, &c->orec, &c->irec, &c->cval, &c->ccol, &c->rval,
                     &c->lp_lb, &c->lp_ub, &c->lp_skip, &c->lp_wh, &c->lp_wst, &c->lp_wd,
                     &c->lp_wb, &c->lp_st, &c->lp_obj, &c->lp_it, &c->lp_x, &c->lp_oh,
-                    &c->lp_ost, &c->lp_od, &c->lp_ob, &c->io_lb_in,
+                    &c->lp_ost, &c->lp_od, &c->lp_ob, &c->lp_slots, &c->io_lb_in,
                     &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
                     &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch})
     b->release();
@@ -221,6 +221,12 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   return MGPU_OK;
 }
 
+int mgpu_set_lp_variant(mgpu_ctx *c, int variant) {
+  if (!c || variant < 0 || variant > 2) return MGPU_ERR_ARG;
+  c->lp_variant = variant;
+  return MGPU_OK;
+}
+
 int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
   if (!c || variant < 0 || variant > 2) return MGPU_ERR_ARG;
   c->fbbt_variant = variant;
@@ -369,6 +375,35 @@ int mgpu_fbbt(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
   return MGPU_OK;
 }
 
+namespace {
+// K3 (B^-1 rows in VGPRs, m <= 64, LDS-staged matrix) unless the problem
+// needs K3L (more rows, or a matrix that does not fit LDS) or a test forces
+// one of them (mgpu_set_lp_variant).
+bool use_large_lp(const mgpu_ctx *c) {
+  if (c->lp_variant == 2) return true;
+  if (c->lp_variant == 1) return false;
+  return c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024;
+}
+
+int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
+  if (!use_large_lp(c)) {
+    if (c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
+      return fail(c, MGPU_ERR_ARG, "%s: problem too large for K3 (m=%d)", who, c->lp.m);
+    HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
+    return MGPU_OK;
+  }
+  if (lp_large_lds_bytes(c->lp.n, c->lp.m) > 160 * 1024)
+    return fail(c, MGPU_ERR_ARG, "%s: n+m=%d too large for K3L's LDS state", who,
+                c->lp.n + c->lp.m);
+  const int grid = lp_large_grid(io.batch, c->lp.n, c->lp.m, c->num_cus);
+  HIPCHK(c, c->lp_slots.ensure((size_t)grid * c->lp.m * c->lp.m * sizeof(double) + 8));
+  HIPCHK(c, lp_large_prepare());
+  (void)hipGetLastError();  // clear a stale error so the launch check is its own
+  HIPCHK(c, launch_lp_large(c->lp, io, c->lp_slots.as<double>(), grid, c->stream));
+  return MGPU_OK;
+}
+}  // namespace
+
 int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub,
                       const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,
                       const double *ws_d, const double *ws_binv, int ws_shared, int iter_limit,
@@ -382,11 +417,6 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: warm start needs head, st, d and binv");
   if (wo_head && (!wo_st || !wo_d || !wo_binv))
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: warm-start output needs all four arrays");
-  if (c->lp.m > kLpMaxM)
-    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: m=%d rows > %d not supported yet", c->lp.m,
-                kLpMaxM);
-  if (lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
-    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: problem too large for the LDS kernel");
   if (batch == 0) return MGPU_OK;
   HIPCHK(c, hipSetDevice(c->device));
   const int n = c->lp.n, m = c->lp.m, N = n + m;
@@ -414,7 +444,8 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   io.wo_d = wo_d;
   io.wo_binv = wo_binv;
   HIPCHK(c, hipEventRecord(c->ev2, c->stream));
-  HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
+  const int rc = launch_lp(c, io, "mgpu_lp_solve");
+  if (rc != MGPU_OK) return rc;
   HIPCHK(c, hipEventRecord(c->ev3, c->stream));
   return MGPU_OK;
 }
@@ -430,11 +461,6 @@ int mgpu_lp_bound_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: bad argument");
   if (ws_head && (!ws_st || !ws_binv))
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: warm start needs head, st and binv");
-  if (c->lp.m > kLpMaxM)
-    return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: m=%d rows > %d not supported yet", c->lp.m,
-                kLpMaxM);
-  if (lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
-    return fail(c, MGPU_ERR_ARG, "mgpu_lp_bound: problem too large for the LDS kernel");
   if (batch == 0) return MGPU_OK;
   HIPCHK(c, hipSetDevice(c->device));
   LpIO io{};
@@ -454,7 +480,8 @@ int mgpu_lp_bound_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   io.iters = iters;
   io.x = x;
   HIPCHK(c, hipEventRecord(c->ev2, c->stream));
-  HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
+  const int rc = launch_lp(c, io, "mgpu_lp_bound");
+  if (rc != MGPU_OK) return rc;
   HIPCHK(c, hipEventRecord(c->ev3, c->stream));
   return MGPU_OK;
 }

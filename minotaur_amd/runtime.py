@@ -23,7 +23,7 @@ _D = ctypes.c_double
 EXPORTS = [
     'mgpu_create', 'mgpu_destroy', 'mgpu_last_error', 'mgpu_set_stream',
     'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
-    'mgpu_set_fbbt_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
+    'mgpu_set_fbbt_variant', 'mgpu_set_lp_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
     'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
     'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_strong_branch',
@@ -72,6 +72,7 @@ def load_library():
     lib.mgpu_fbbt.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
     lib.mgpu_fbbt_dev.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
     lib.mgpu_set_fbbt_variant.argtypes = [_P, _I]
+    lib.mgpu_set_lp_variant.argtypes = [_P, _I]
     lib.mgpu_lp_solve.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_lp_solve_dev.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_node_decide_dev.argtypes = [_P, _I] + [_P] * 4 + [_D] * 5 + [_P] * 3
@@ -193,6 +194,10 @@ class Context:
 
     def sync(self):
         self._chk(self.lib.mgpu_sync(self.h), 'mgpu_sync')
+
+    def set_lp_variant(self, v: int):
+        """0 auto, 1 K3 (m <= 64), 2 K3L (any m; one node per workgroup)."""
+        self._chk(self.lib.mgpu_set_lp_variant(self.h, int(v)), 'mgpu_set_lp_variant')
 
     def set_fbbt_variant(self, v: int):
         self._chk(self.lib.mgpu_set_fbbt_variant(self.h, int(v)), 'mgpu_set_fbbt_variant')

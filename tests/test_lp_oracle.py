@@ -49,3 +49,24 @@ def test_oracle_iteration_limit():
     p, g = load_lp('tls4')
     st, obj, it, _ = oracle.dual_simplex(p, g['lb'][:1], g['ub'][:1], None, iter_limit=3)
     assert st[0] == 6 and it[0] == 3
+
+
+def test_oracle_large_m_knapsack_oa_matches_highs():
+    """The restatement beyond one wave of rows (the K3L regime): the knapsack
+    outer-approximation LP with f = 64 terms (m = 257), root and seeded node
+    boxes warm-started from the root, against scipy HiGHS (1e-6)."""
+    import math
+    from minotaur_amd.problem import knapsack_oa, random_boxes
+    p = knapsack_oa(f=64, N=256)
+    rs, robj, x, y, it, ws = oracle.dual_simplex_root(p)
+    hs, hobj = oracle.highs(p)
+    assert rs == hs == 0 and abs(robj - hobj) <= 1e-6 * max(1.0, abs(hobj))
+    LB, UB = random_boxes(p, 24, 4306)
+    st, obj, its, _ = oracle.dual_simplex(p, LB, UB, ws)
+    for b in range(24):
+        hs, hobj = oracle.highs(p, LB[b], UB[b])
+        assert st[b] == hs
+        if hs == 0:
+            assert abs(obj[b] - hobj) <= 1e-6 * max(1.0, abs(hobj))
+        else:
+            assert math.isinf(obj[b])
