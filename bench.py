@@ -100,12 +100,21 @@ def cpu_baseline(p, LB, UB, budget_s):
     probe = min(256, LB.shape[0])
     a, b, _ = run(LB[:probe], UB[:probe])
     per = (a + b) / probe
-    S = int(min(LB.shape[0], max(probe, budget_s / max(per, 1e-9))))
+    # about budget_s of one-core work: the rank-0 boxes, extended (when the
+    # budget asks for more) by further boxes of the same generator
+    S = int(min(16 * LB.shape[0], max(probe, budget_s / max(per, 1e-9))))
+    what = f"first {S} of the rank-0 node boxes"
+    if S > LB.shape[0]:
+        from minotaur_amd.problem import random_boxes
+        XL, XU = random_boxes(p, S - LB.shape[0], 99991)
+        what = (f"the {LB.shape[0]} rank-0 node boxes + {XL.shape[0]} more of the same "
+                "generator")
+        LB, UB = np.concatenate([LB, XL]), np.concatenate([UB, XU])
     tf, tl, solved = run(LB[:S], UB[:S])
     return {
         "value": S / (tf + tl), "unit": "nodes/s", "cores": 1,
         "kind": "reference" if use_ref else "port",
-        "sample": (f"first {S} of the rank-0 node boxes (tls4-lin), one core: FBBT by "
+        "sample": (f"{what} (tls4-lin), one core: FBBT by "
                    f"{'the reference LinearHandler::presolveNode (oracle/_ref)' if use_ref else 'the C restatement'}"
                    f" {tf:.2f}s, then {solved} warm-started LPs by the dual-simplex "
                    f"restatement (Clp absent) {tl:.2f}s"),
@@ -160,6 +169,68 @@ def tree_search(ctx, dev, rank, world, B, args):
         c["sample"] = c["sample"].replace("tls4-lin", "mkp random-branching boxes")
         out["cpu_baseline"] = c
     return out
+
+
+# Config 5 ("64 synthetic convex separable MINLPs (knapsack
+# family) until MINLPLib .nl files are provided", node-sharded): outer-
+# approximation LPs of examples/knapsack (knapsack_oa: min sum a_i x_i^b_i,
+# sum x <= N, x integer in [1, N], 4 tangents per term) with f terms,
+# N = 3 f; m = 1 + 4 f rows, so f >= 16 crosses the K3 / K3L boundary
+# (m > 64 -> K3L).  Optima: scipy HiGHS MILP on the same LPs (this
+# container; tools/convex_batch_optima.py prints them).
+CONVEX_BATCH = [(16, 48, 6.931342750371372), (20, 60, 7.812507818465321),
+                (24, 72, 9.458626537799338), (28, 84, 13.920825697253907)]
+
+
+def convex_batch(ctx, dev, rank, world, B, args):
+    """Supplementary (config 5): complete trees over the convex batch, each
+    node-sharded across ranks (mgpu_bnb_shard) with an incumbent all-reduce
+    MIN per round; nodes/s and LP relaxations/s over the whole batch."""
+    import torch
+    from minotaur_amd import bnb
+    from minotaur_amd import dist as mdist
+    from minotaur_amd.problem import knapsack_oa
+
+    def amin(v):
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        return float(mdist.allreduce_incumbent(t).item())
+
+    def amax(v):
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        return float(mdist.allreduce_max(t).item())
+
+    per, tot_nodes, tot_s, ok = [], 0.0, 0.0, True
+    for f, N, opt in CONVEX_BATCH:
+        p = knapsack_oa(f=f, N=N)
+        ctx.load(p)
+        bnb.solve_distributed(ctx, 64, rank, world, amin, amax, capacity=1 << 14,
+                              max_rounds=2)                  # warm-up (kernel loads)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, amin, amax,
+                                                         capacity=1 << 21)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        nd = torch.tensor([float(mine)], dtype=torch.float64, device=dev)
+        mdist.allreduce_max(el)
+        mdist.allreduce_sum(nd)
+        el, nodes = float(el.item()), float(nd.item())
+        good = abs(inc - opt) <= 1e-6 * max(1.0, abs(opt))
+        ok &= good
+        tot_nodes += nodes
+        tot_s += el
+        per.append({"f": f, "rows": p.m, "lp_kernel": "K3L" if p.m > 64 else "K3",
+                    "nodes": nodes, "seconds": el, "rounds": rounds, "optimum": inc,
+                    "optimum_highs": opt})
+    return {"instances": per, "nodes": tot_nodes, "seconds": tot_s,
+            "nodes_per_s": tot_nodes / tot_s, "all_optima_match_highs": bool(ok),
+            "batch_per_gpu": B,
+            "search": "depth-first over batches, MaxVio branching, root-basis warm start, "
+                      "node-sharded after the shared first rounds"}
 
 
 def qp_relaxation(ctx, dev, rank, world, args, B=1024, reps=3):
@@ -230,6 +301,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-bnb', action='store_true',
                     help='skip the supplementary full tree search (mkp MILP)')
+    ap.add_argument('--no-convex', action='store_true',
+                    help='skip the supplementary convex batch (config 5, knapsack OA trees)')
     ap.add_argument('--no-qp', action='store_true',
                     help='skip the supplementary QP relaxation batch (color_lab2, MFMA KKT)')
     args = ap.parse_args()
@@ -326,6 +399,7 @@ def main():
     elapsed = float(tot.item())
     solved, pivots = (float(v) for v in cnt.tolist())
     tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, B, args)
+    cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, B, args)
     qprel = None if args.no_qp else qp_relaxation(ctx, dev, rank, world, args)
     ctx.load(p)
     nodes = float(B) * world * args.steps
@@ -391,6 +465,7 @@ def main():
             "cpu_baseline": cpu,
             "incumbent": state["incumbent"],
             "tree_search": tree,
+            "convex_batch": cvx,
             "qp_relaxation": qprel,
         }
         if rehearse:

@@ -111,3 +111,23 @@ def test_bnb_tree_matches_cpu_restatement(ctx, batch):
         assert sg.open == sc.open == 0
         assert abs(og - oc) <= 1e-9 * max(1.0, abs(oc))
         assert (sg.rounds, sg.nodes, list(sg.ndec)) == (sc.rounds, sc.nodes, list(sc.ndec))
+
+
+def test_bnb_k3l_tree_matches_cpu_and_highs(ctx):
+    """More rows than a wave has lanes: the batched tree on the knapsack OA
+    LP with f = 17 terms, N = 64 (m = 69 -> K3L node LPs) evaluates the same
+    tree as the CPU restatement (rounds, nodes, decisions), ends on the same
+    incumbent bit for bit (K3L sums like the oracle) and proves the HiGHS
+    MILP optimum."""
+    from bnb import CpuBnbContext
+    p = knapsack_oa(f=17, N=64)
+    assert p.m > 64
+    hs, hobj = oracle.highs_milp(p)
+    ctx.load(p)
+    og, xg, sg, _ = bnb.solve(ctx, batch=512, capacity=1 << 17)
+    oc, xc, sc, _ = bnb.solve(CpuBnbContext(p), batch=512, capacity=1 << 17)
+    assert sg.open == sc.open == 0
+    assert (sg.rounds, sg.nodes, list(sg.ndec)) == (sc.rounds, sc.nodes, list(sc.ndec))
+    assert og == oc
+    assert hs == 0 and abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
+    _check_solution(p, xg, og)
