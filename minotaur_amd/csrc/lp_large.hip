@@ -11,8 +11,9 @@
 // a sequential sum, so a node follows the oracle's pivot sequence and ends
 // on the oracle's objective bit for bit.
 //
-// Mapping (MI355X-first): ONE NODE PER WORKGROUP of 256 threads (4 waves),
-// persistent over nodes.
+// Mapping (MI355X-first): ONE NODE PER WORKGROUP, persistent over nodes: one
+// wave for m <= 256 (wave-level reductions, up to 16 nodes in flight per
+// CU), four waves beyond.
 //  * B^{-1} (m x m f64) is too large for registers or LDS at these sizes
 //    (m = 1025: 8.4 MB): it lives in HBM, COLUMN-major, one slot per
 //    workgroup.  Thread i owns basis row i, so every per-row sweep over a
@@ -36,7 +37,6 @@
 namespace mgpu {
 namespace {
 
-constexpr int kT = 256;           // threads per workgroup = one node
 constexpr double kPTol = 1e-7;    // primal feasibility (Clp default)
 constexpr double kDTol = 1e-7;    // dual feasibility (Clp default)
 constexpr double kPivTol = 1e-9;  // smallest |alpha_rq| allowed to pivot
@@ -51,9 +51,10 @@ __host__ __device__ constexpr size_t al16(size_t b) { return (b + 15) & ~(size_t
 __host__ __device__ inline size_t large_lds_bytes(int n, int m) {
   const size_t N = (size_t)n + m;
   return 6 * al16(N * 8) + 2 * al16(N) + 3 * al16((size_t)m * 8) + al16((size_t)m * 4) +
-         al16(4 * 8) + al16(4 * 4);
+         al16(4 * 8) + al16(4 * 4);  // reduction slots: up to 4 waves
 }
 
+template <int kT>  // threads per workgroup = one node
 struct S {
   double *d, *z, *blo, *bhi, *al, *t2, *rho, *aq, *w, *redv;
   int8_t *st, *art;
@@ -80,24 +81,34 @@ struct S {
 // ---- workgroup reductions (every thread calls them) ------------------------
 // (not __syncthreads_or: its reduction scratch is static LDS, which would not
 // leave the full 160 KiB for the dynamic state)
-__device__ __forceinline__ bool blk_any(bool p, const S &s) {
+template <int kT>
+__device__ __forceinline__ bool blk_any(bool p, const S<kT> &s) {
   const bool w = __builtin_amdgcn_ballot_w64(p) != 0;
+  if constexpr (kT == 64) return w;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) s.redi[threadIdx.x >> 6] = w ? 1 : 0;
   __syncthreads();
-  return (s.redi[0] | s.redi[1] | s.redi[2] | s.redi[3]) != 0;
+  int any = 0;
+  for (int w = 0; w < kT / 64; ++w) any |= s.redi[w];
+  return any != 0;
 }
 
-__device__ __forceinline__ double blk_min(double v, const S &s) {
+template <int kT>
+__device__ __forceinline__ double blk_min(double v, const S<kT> &s) {
   v = wave_min_dpp(v);
+  if constexpr (kT == 64) return v;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) s.redv[threadIdx.x >> 6] = v;
   __syncthreads();
-  return fmin(fmin(s.redv[0], s.redv[1]), fmin(s.redv[2], s.redv[3]));
+  double r = s.redv[0];
+  for (int w = 1; w < kT / 64; ++w) r = fmin(r, s.redv[w]);
+  return r;
 }
 
-__device__ __forceinline__ void blk_argmax(double &v, int &i, const S &s) {
+template <int kT>
+__device__ __forceinline__ void blk_argmax(double &v, int &i, const S<kT> &s) {
   wave_argmax_dpp(v, i);
+  if constexpr (kT == 64) return;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) {
     s.redv[threadIdx.x >> 6] = v;
@@ -110,7 +121,8 @@ __device__ __forceinline__ void blk_argmax(double &v, int &i, const S &s) {
 }
 
 // oracle col_dot: v' a_j over CSC column j in CSC order (v in LDS)
-__device__ __forceinline__ double col_dot(const S &s, const double *v, int j) {
+template <int kT>
+__device__ __forceinline__ double col_dot(const S<kT> &s, const double *v, int j) {
   if (j >= s.n) return -v[j - s.n];
   double a = 0.0;
   for (int t = s.colptr[j]; t < s.colptr[j + 1]; ++t) a += s.cval[t] * v[s.rowidx[t]];
@@ -118,7 +130,8 @@ __device__ __forceinline__ double col_dot(const S &s, const double *v, int j) {
 }
 
 // oracle place_nonbasic
-__device__ __forceinline__ void place_nonbasic(const S &s, int j, double ab) {
+template <int kT>
+__device__ __forceinline__ void place_nonbasic(const S<kT> &s, int j, double ab) {
   const double lo = s.blo[j], hi = s.bhi[j], dj = s.d[j];
   const bool lo_f = lo > -kInfB, hi_f = hi < kInfB;
   if (lo_f && hi_f && lo == hi) {
@@ -153,7 +166,8 @@ __device__ __forceinline__ void place_nonbasic(const S &s, int j, double ab) {
 }
 
 // oracle grow_art
-__device__ __forceinline__ void grow_art(const S &s, double ab) {
+template <int kT>
+__device__ __forceinline__ void grow_art(const S<kT> &s, double ab) {
   for (int j = threadIdx.x; j < s.N; j += kT) {
     const int8_t a = s.art[j];
     if (!a || s.st[j] == ST_BASIC) continue;
@@ -167,7 +181,8 @@ __device__ __forceinline__ void grow_art(const S &s, double ab) {
 
 // oracle compute_primals: w = N z_N per row (CSR row k in column order, the
 // logical last), then z_B = -B^{-1} w with k ascending.
-__device__ __forceinline__ void compute_primals(const S &s) {
+template <int kT>
+__device__ __forceinline__ void compute_primals(const S<kT> &s) {
   __syncthreads();
   for (int k = threadIdx.x; k < s.m; k += kT) {
     double w = 0.0;
@@ -189,17 +204,26 @@ __device__ __forceinline__ void compute_primals(const S &s) {
   for (int i = threadIdx.x; i < s.m; i += kT) {
     double acc = 0.0;
     const double *col = s.Bi + i;
-    for (int k = 0; k < s.m; ++k) acc += col[(size_t)k * s.m] * s.w[k];
+    int k0 = 0;
+    for (; k0 + 8 <= s.m; k0 += 8) {  // loads first, adds in k order
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = col[(size_t)(k0 + u) * s.m];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u] * s.w[k0 + u];
+    }
+    for (; k0 < s.m; ++k0) acc += col[(size_t)k0 * s.m] * s.w[k0];
     s.z[s.head[i]] = -acc;
   }
   __syncthreads();
 }
 
+template <int kT>
 __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double *binv_slots) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = lp.n, m = lp.m, N = n + m;
   const int tid = threadIdx.x;
-  S s;
+  S<kT> s;
   {
     unsigned char *p = smem;
     s.d = (double *)p;    p += al16((size_t)N * 8);
@@ -481,13 +505,23 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
         }
       }
       // ---- rank-1 update of B^{-1} (HBM): rows with alpha_iq = 0 untouched
+      // (8 independent loads in flight per thread, then the 8 stores: the
+      // column walk is a chain of HBM round trips otherwise)
       for (int i = tid; i < m; i += kT) {
         const double f = s.aq[i];
         double *col = s.Bi + i;
         if (i == r) {
           for (int k = 0; k < m; ++k) col[(size_t)k * m] = s.rho[k];
         } else if (f != 0.0) {
-          for (int k = 0; k < m; ++k) col[(size_t)k * m] -= f * s.rho[k];
+          int k0 = 0;
+          for (; k0 + 8 <= m; k0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = col[(size_t)(k0 + u) * m];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) col[(size_t)(k0 + u) * m] = v[u] - f * s.rho[k0 + u];
+          }
+          for (; k0 < m; ++k0) col[(size_t)k0 * m] -= f * s.rho[k0];
         }
       }
       __syncthreads();
@@ -532,10 +566,17 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
 
 size_t lp_large_lds_bytes(int n, int m) { return large_lds_bytes(n, m); }
 
+// Workgroup size: one wave per node up to m = 256 rows (wave-level
+// reductions, no cross-wave barriers, many nodes in flight per CU); four
+// waves per node beyond, where the per-pivot sweeps over m rows dominate.
+int lp_large_threads(int m) { return m <= 256 ? 64 : 256; }
+
 int lp_large_grid(int batch, int n, int m, int num_cus) {
   const size_t lds = large_lds_bytes(n, m);
+  const int waves = lp_large_threads(m) / 64;
   int per_cu = (int)((160 * 1024) / (lds > 0 ? lds : 1));
-  if (per_cu > 4) per_cu = 4;  // 4 x 256-thread workgroups: 4 waves per SIMD
+  const int cap = 16 / waves;  // 16 waves per CU
+  if (per_cu > cap) per_cu = cap;
   if (per_cu < 1) per_cu = 1;
   const int g = per_cu * num_cus;
   return batch < g ? batch : g;
@@ -544,8 +585,11 @@ int lp_large_grid(int batch, int n, int m, int num_cus) {
 hipError_t lp_large_prepare() {
   static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted in
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)lp_large_kernel,
+    hipError_t e = hipFuncSetAttribute((const void *)lp_large_kernel<64>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void *)lp_large_kernel<256>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -557,7 +601,12 @@ hipError_t launch_lp_large(const DevLP &lp, const LpIO &io, double *binv_slots, 
   if (io.batch <= 0) return hipSuccess;
   const size_t lds = large_lds_bytes(lp.n, lp.m);
   if (lds > 160 * 1024 || grid <= 0 || binv_slots == nullptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lp_large_kernel, dim3(grid), dim3(kT), lds, stream, lp, io, binv_slots);
+  if (lp_large_threads(lp.m) == 64)
+    hipLaunchKernelGGL(lp_large_kernel<64>, dim3(grid), dim3(64), lds, stream, lp, io,
+                       binv_slots);
+  else
+    hipLaunchKernelGGL(lp_large_kernel<256>, dim3(grid), dim3(256), lds, stream, lp, io,
+                       binv_slots);
   return hipGetLastError();
 }
 
