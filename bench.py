@@ -63,7 +63,7 @@ def pmc_traffic(kernel, batch):
         except (OSError, ValueError):
             continue
         args = d.get("bench_args", "").split()
-        b = int(args[args.index('--batch') + 1]) if '--batch' in args else 65536
+        b = int(args[args.index('--batch') + 1]) if '--batch' in args else 131072
         k = d.get("kernels", {}).get(key)
         if b == batch and k and k.get("hbm_bytes_per_launch"):
             return k["hbm_bytes_per_launch"], os.path.basename(f)
@@ -296,7 +296,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=65536, help='open nodes per GPU per step')
+    ap.add_argument('--batch', type=int, default=131072,
+                    help='open nodes per GPU per step (131072: two K1 waves per SIMD)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-bnb', action='store_true',

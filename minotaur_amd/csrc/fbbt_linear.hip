@@ -601,7 +601,7 @@ __device__ __forceinline__ bool check_bounds(const DevLP &lp, const V &v) {
   return bad || lp.cons_bad != 0;
 }
 
-template <bool kLds, bool kBitFlags, bool kRC>
+template <bool kLds, bool kBitFlags, bool kTL>
 __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x;
@@ -625,6 +625,26 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
     v.flag = io.flag_scratch + (size_t)blockIdx.x * m * kLanes;
   }
 
+  // kTL: the row and term records are staged once into LDS (after the
+  // bounds, if any): a row visit then reads its records with ds_read
+  // (lgkmcnt) instead of global loads that would also wait (vmcnt, in
+  // order) for the previous row's bound stores in the global variant.
+  const TermRec *trec = lp.trec;
+  const RowRec *rows = lp.rows;
+  if constexpr (kTL) {
+    char *tp = reinterpret_cast<char *>(lds) +
+               (kLds ? (size_t)2 * n * kLdsStride * sizeof(double) : 0);
+    RowRec *s_rows = reinterpret_cast<RowRec *>(tp);
+    TermRec *s_trec = reinterpret_cast<TermRec *>(tp + (size_t)m * sizeof(RowRec));
+    const uint4 *src = reinterpret_cast<const uint4 *>(lp.rows);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_rows);
+    for (int i = lane; i < 2 * m; i += kLanes) dst[i] = src[i];
+    src = reinterpret_cast<const uint4 *>(lp.trec);
+    dst = reinterpret_cast<uint4 *>(s_trec);
+    for (int i = lane; i < 2 * lp.nnz; i += kLanes) dst[i] = src[i];
+    trec = s_trec;
+    rows = s_rows;
+  }
   // Stage the wave's node boxes (row-major [node][var] in HBM, coalesced
   // reads) into the [var][lane] layout.
   for (int nd = 0; nd < nb; ++nd) {
@@ -675,23 +695,23 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
     for (int r0 = 0; r0 < m; r0 += kLanes) {
       const int rcnt = m - r0 < kLanes ? m - r0 : kLanes;
       RowRec rr{0.0, 0.0, 0, 0, 0, 0};
-      if (lane < rcnt) rr = lp.rows[r0 + lane];
+      if (lane < rcnt) rr = rows[r0 + lane];
       for (int q = 0; q < rcnt; ++q) {
         const int r = r0 + q;
         const bool mine = cons_on && v.flagged(r);
         if (!__any(mine)) continue;
         // full wave active here: load the row's first 64 terms for broadcast
         const int k0 = rl(rr.k0, q), nt = rl(rr.nt, q);
-        const TermChunk pre = load_terms(lp.trec + k0, nt < kLanes ? nt : kLanes, lane);
+        const TermChunk pre = load_terms(trec + k0, nt < kLanes ? nt : kLanes, lane);
         if (mine) {
           const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
           bool tch;
           v.clear(r);
           bool inf;
-          if (kRC && nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (kRC && nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (kRC && nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
-          else inf = lin_bnd_tighten(lp.trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
+          if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
+          else inf = lin_bnd_tighten(trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
           if (inf) {
             cons_on = false;
           } else if (tch) {
@@ -701,7 +721,7 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
       }
     }
     if (go && io.has_inc && lp.nobj > 0) {
-      if (kRC && lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
+      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
       else bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
     }
     tighten_ints(lp, v, s, log, go, changed);
@@ -722,21 +742,21 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   }
 }
 
-template <bool kLds, bool kBits, bool kRC = true>
+template <bool kLds, bool kBits, bool kTL>
 hipError_t launch_variant(const DevLP &lp, const FbbtIO &io, size_t lds, hipStream_t stream) {
   const int waves = (io.batch + io.npw - 1) / io.npw;
-  if constexpr (kLds) {
+  {
     static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted in
     if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute((const void *)fbbt_linear_kernel<kLds, kBits, kRC>,
+      hipError_t e = hipFuncSetAttribute((const void *)fbbt_linear_kernel<kLds, kBits, kTL>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024);
       if (e != hipSuccess) return e;
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL((fbbt_linear_kernel<kLds, kBits, kRC>), dim3(waves), dim3(kLanes),
-                     kLds ? lds : 0, stream, lp, io);
+  hipLaunchKernelGGL((fbbt_linear_kernel<kLds, kBits, kTL>), dim3(waves), dim3(kLanes),
+                     lds, stream, lp, io);
   return hipGetLastError();
 }
 
@@ -752,25 +772,21 @@ hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
   const size_t lds = fbbt_lds_bytes(lp.n, lp.m);
   const bool use_lds = variant == 1 || (variant == 0 && lds <= 160 * 1024);
   const bool bits = lp.m <= 64;
-  // experiment switch: the generic (rolled) row path only, no register-
-  // cached row templates (code size vs instruction cache)
-  static const bool norc = getenv("MGPU_FBBT_NORC") != nullptr;
-  if (norc && bits) {
-    if (use_lds) {
-      if (lds > 160 * 1024) return hipErrorInvalidValue;
-      return launch_variant<true, true, false>(lp, io, lds, stream);
-    }
-    if (io.scratch == nullptr) return hipErrorInvalidValue;
-    return launch_variant<false, true, false>(lp, io, 0, stream);
-  }
+  // records table next to the bounds (LDS variant) or alone (global variant)
+  const size_t tab = (size_t)lp.m * sizeof(RowRec) + (size_t)lp.nnz * sizeof(TermRec);
+  static const bool no_tl = getenv("MGPU_FBBT_NOTL") != nullptr;  // A/B switch
   if (use_lds) {
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    return bits ? launch_variant<true, true>(lp, io, lds, stream)
-                : launch_variant<true, false>(lp, io, lds, stream);
+    const bool tl = !no_tl && bits && lds + tab <= 160 * 1024;
+    if (tl) return launch_variant<true, true, true>(lp, io, lds + tab, stream);
+    return bits ? launch_variant<true, true, false>(lp, io, lds, stream)
+                : launch_variant<true, false, false>(lp, io, lds, stream);
   }
   if (io.scratch == nullptr || (!bits && io.flag_scratch == nullptr)) return hipErrorInvalidValue;
-  return bits ? launch_variant<false, true>(lp, io, 0, stream)
-              : launch_variant<false, false>(lp, io, 0, stream);
+  const bool tl = !no_tl && bits && tab <= 64 * 1024;
+  if (tl) return launch_variant<false, true, true>(lp, io, tab, stream);
+  return bits ? launch_variant<false, true, false>(lp, io, 0, stream)
+              : launch_variant<false, false, false>(lp, io, 0, stream);
 }
 
 }  // namespace mgpu

@@ -1,5 +1,5 @@
-"""K1 timing over (row path: register-cached templates vs rolled generic,
-MGPU_FBBT_NORC) x (nodes per wave, MGPU_FBBT_NPW) x (LDS / global scratch),
+"""K1 timing over (row/term records staged in LDS or read from HBM,
+MGPU_FBBT_NOTL) x (nodes per wave, MGPU_FBBT_NPW) x (LDS / global scratch),
 tls4-lin, with a bit-exact check against the first configuration.
 Usage: python tools/fbbt_variant_probe.py            (spawns both row paths)"""
 import math
@@ -30,7 +30,7 @@ def run_one(tag):
         inf = torch.zeros(B, dtype=torch.int32, device=dev)
         nm = torch.zeros(B, dtype=torch.int32, device=dev)
         ref = os.path.join('/tmp', f'fbbt_probe_ref_{B}.npy')
-        for npw in (64, 32, 16):
+        for npw in (64, 32):
             os.environ['MGPU_FBBT_NPW'] = str(npw)
             for variant in (2, 1):
                 ctx.set_fbbt_variant(variant)
@@ -54,7 +54,7 @@ if __name__ == '__main__':
     if len(sys.argv) > 1:
         run_one(sys.argv[1])
     else:
-        for tag, extra in (('rc', {}), ('norc', {'MGPU_FBBT_NORC': '1'})):
+        for tag, extra in (('tl', {}), ('notl', {'MGPU_FBBT_NOTL': '1'})):
             env = dict(os.environ, **extra)
             r = subprocess.run([sys.executable, '-u', __file__, tag], env=env)
             if r.returncode != 0:
