@@ -63,7 +63,7 @@ def pmc_traffic(kernel, batch):
         except (OSError, ValueError):
             continue
         args = d.get("bench_args", "").split()
-        b = int(args[args.index('--batch') + 1]) if '--batch' in args else 131072
+        b = int(args[args.index('--batch') + 1]) if '--batch' in args else 65536
         k = d.get("kernels", {}).get(key)
         if b == batch and k and k.get("hbm_bytes_per_launch"):
             return k["hbm_bytes_per_launch"], os.path.basename(f)
