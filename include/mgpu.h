@@ -155,10 +155,19 @@ int mgpu_node_decide_dev(mgpu_ctx *ctx, int batch, const int32_t *d_fbbt_infeas,
  * (large n). For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
 
-/* Which LP kernel the next LP calls use: 0 auto (K3 when m <= 64 and the
- * matrix fits LDS, else K3L), 1 K3, 2 K3L.  Both restate oracle/lp_dual.c
- * pivot for pivot.  For tests/benchmarks. */
+/* Which LP kernel the next LP calls use: 0 auto, 1 K3, 2 K3L, 3 K3P.
+ * Auto: K3P (product form against the shared inverse) for a batch that
+ * shares one warm start and wants no warm start back, when m <= 64 and
+ * n + m <= 256; else K3 when m <= 64 and the matrix fits LDS; else K3L.
+ * K3 and K3L restate oracle/lp_dual.c pivot for pivot, K3P its product-form
+ * mode (oracle dual_simplex(..., pfi=k)).  For tests/benchmarks. */
 int mgpu_set_lp_variant(mgpu_ctx *ctx, int variant);
+
+/* K3P eta-file cap: a node that needs more pivots is re-solved by K3 from
+ * the same warm start.  0 keeps auto mode off K3P; 1..MGPU_LP_PFI_MAX
+ * (default MGPU_LP_PFI_MAX). */
+#define MGPU_LP_PFI_MAX 24
+int mgpu_set_lp_pfi(mgpu_ctx *ctx, int kmax);
 
 /* Batched bound LPs: LP b minimises obj_sign[b] * x[obj_col[b]] over the
  * loaded relaxation on ONE box lb/ub [n] (the relaxation's), warm-started

@@ -59,8 +59,10 @@ struct mgpu_ctx {
   DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_inf, io_nmods, io_mv, io_ml, io_mval;
   DevBuf scratch, flag_scratch;
   int fbbt_variant = 0;
-  int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L
+  int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L, 3 K3P
+  int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)
   DevBuf lp_slots;             // K3L: one B^-1 [m][m] per resident workgroup
+  DevBuf pfi_ovf;              // K3P: overflow counter + node list
   int num_cus = 256;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr,
             ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;

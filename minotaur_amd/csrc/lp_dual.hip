@@ -211,6 +211,10 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz;
   const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // node list (K3P overflow re-solve): a workgroup with no node of it
+  // leaves before staging anything (uniform over the workgroup)
+  const int nsolve = io.node_list != nullptr ? *io.node_count : io.batch;
+  if (blockIdx.x * W >= nsolve) return;
 
   // ---- stage the constraint matrix (CSC + CSR) once per workgroup ----
   unsigned char *p = smem;
@@ -249,7 +253,8 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   // for the workgroup; each wave then solves nodes b, b + grid*W, ...
   // (no workgroup barrier below this point).
   STAMP_DECL
-  for (int b = blockIdx.x * W + wave; b < io.batch; b += gridDim.x * W) {
+  for (int bi = blockIdx.x * W + wave; bi < nsolve; bi += gridDim.x * W) {
+    const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
 
     // lane index made opaque per node: otherwise LICM hoists the 64
     // loop-invariant B^-1 init values / LDS addresses out of the node loop

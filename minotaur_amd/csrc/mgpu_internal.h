@@ -93,10 +93,28 @@ struct LpIO {
   int8_t *wo_st;                // [B][n+m]
   double *wo_d;                 // [B][n+m]
   double *wo_binv;              // [B][m][m]
+  // K3 only: solve just the nodes node_list[0 .. *node_count) (device
+  // memory; the overflow list of K3P), null = every node of the batch
+  const int32_t *node_list;
+  const int32_t *node_count;
 };
 
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
+
+// K3P (lp_pfi.hip): product-form dual simplex for a batch that shares its
+// warm start.  At most kPfiMax eta columns per node, n + m <= 64*kPfiSlots.
+constexpr int kPfiMax = 24;
+constexpr int kPfiSlots = 4;
+struct PfiIO {
+  int kmax;                     // eta-file cap for this launch (1..kPfiMax)
+  int32_t *ovf_list;            // [B] nodes that needed more than kmax pivots
+  int32_t *ovf_count;           // device counter, zeroed before the launch
+};
+size_t lp_pfi_lds_bytes(int n, int m, int nnz);
+bool lp_pfi_fits(int n, int m, int nnz);
+hipError_t launch_lp_pfi(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
+                         hipStream_t stream);
 
 struct DecideIO {
   int batch;

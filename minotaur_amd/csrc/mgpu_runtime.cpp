@@ -222,10 +222,18 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
 }
 
 int mgpu_set_lp_variant(mgpu_ctx *c, int variant) {
-  if (!c || variant < 0 || variant > 2) return MGPU_ERR_ARG;
+  if (!c || variant < 0 || variant > 3) return MGPU_ERR_ARG;
   c->lp_variant = variant;
   return MGPU_OK;
 }
+
+int mgpu_set_lp_pfi(mgpu_ctx *c, int kmax) {
+  if (!c || kmax < 0 || kmax > MGPU_LP_PFI_MAX) return MGPU_ERR_ARG;
+  c->lp_pfi = kmax;
+  return MGPU_OK;
+}
+
+static_assert(MGPU_LP_PFI_MAX == kPfiMax, "ABI eta-file cap = kernel's");
 
 int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
   if (!c || variant < 0 || variant > 2) return MGPU_ERR_ARG;
@@ -385,7 +393,38 @@ bool use_large_lp(const mgpu_ctx *c) {
   return c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024;
 }
 
+// K3P serves a batch that shares one warm start and asks for no warm start
+// back; in auto mode whenever the problem fits it, variant 3 insists.
+bool use_pfi(const mgpu_ctx *c, const LpIO &io) {
+  if (c->lp_variant != 0 && c->lp_variant != 3) return false;
+  const bool shared = io.ws.head != nullptr && io.ws.s_head == 0 && io.ws.s_st == 0 &&
+                      io.ws.s_d == 0 && io.ws.s_binv == 0;
+  const int kmax = c->lp_variant == 3 && c->lp_pfi == 0 ? kPfiMax : c->lp_pfi;
+  return shared && io.wo_head == nullptr && kmax > 0 &&
+         lp_pfi_fits(c->lp.n, c->lp.m, c->lp.nnz) &&
+         lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) <= 160 * 1024;
+}
+
 int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
+  if (use_pfi(c, io)) {
+    // K3P, then the dense K3 on exactly the nodes that filled the eta file
+    HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 1) * sizeof(int32_t)));
+    int32_t *cnt = c->pfi_ovf.as<int32_t>();
+    HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(int32_t), c->stream));
+    PfiIO px{};
+    px.kmax = c->lp_pfi > 0 ? c->lp_pfi : kPfiMax;
+    px.ovf_count = cnt;
+    px.ovf_list = cnt + 1;
+    HIPCHK(c, launch_lp_pfi(c->lp, io, px, c->num_cus, c->stream));
+    LpIO io2 = io;
+    io2.node_list = px.ovf_list;
+    io2.node_count = px.ovf_count;
+    HIPCHK(c, launch_lp_dual(c->lp, io2, c->num_cus, c->stream));
+    return MGPU_OK;
+  }
+  if (c->lp_variant == 3)
+    return fail(c, MGPU_ERR_ARG, "%s: K3P needs a shared warm start, no warm-start output, "
+                "m <= 64 and n + m <= %d", who, 64 * kPfiSlots);
   if (!use_large_lp(c)) {
     if (c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
       return fail(c, MGPU_ERR_ARG, "%s: problem too large for K3 (m=%d)", who, c->lp.m);

@@ -19,11 +19,14 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _D = ctypes.c_double
 
+LP_PFI_MAX = 24  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
+
 # Every entry point declared in include/mgpu.h (checked by the CPU tests).
 EXPORTS = [
     'mgpu_create', 'mgpu_destroy', 'mgpu_last_error', 'mgpu_set_stream',
     'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
-    'mgpu_set_fbbt_variant', 'mgpu_set_lp_variant', 'mgpu_last_kernel_ms', 'mgpu_lp_solve', 'mgpu_lp_solve_dev',
+    'mgpu_set_fbbt_variant', 'mgpu_set_lp_variant', 'mgpu_set_lp_pfi', 'mgpu_last_kernel_ms',
+    'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
     'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
     'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_strong_branch',
@@ -73,6 +76,7 @@ def load_library():
     lib.mgpu_fbbt_dev.argtypes = [_P, _I, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P]
     lib.mgpu_set_fbbt_variant.argtypes = [_P, _I]
     lib.mgpu_set_lp_variant.argtypes = [_P, _I]
+    lib.mgpu_set_lp_pfi.argtypes = [_P, _I]
     lib.mgpu_lp_solve.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_lp_solve_dev.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_node_decide_dev.argtypes = [_P, _I] + [_P] * 4 + [_D] * 5 + [_P] * 3
@@ -196,8 +200,27 @@ class Context:
         self._chk(self.lib.mgpu_sync(self.h), 'mgpu_sync')
 
     def set_lp_variant(self, v: int):
-        """0 auto, 1 K3 (m <= 64), 2 K3L (any m; one node per workgroup)."""
+        """0 auto, 1 K3 (m <= 64), 2 K3L (any m; one node per workgroup),
+        3 K3P (product form; shared warm start only)."""
         self._chk(self.lib.mgpu_set_lp_variant(self.h, int(v)), 'mgpu_set_lp_variant')
+        self.lp_variant = int(v)
+
+    def set_lp_pfi(self, kmax: int):
+        """K3P eta-file cap (0: auto mode never picks K3P)."""
+        self._chk(self.lib.mgpu_set_lp_pfi(self.h, int(kmax)), 'mgpu_set_lp_pfi')
+        self.lp_pfi = int(kmax)
+
+    def oracle_pfi(self, shared_ws=True, want_ws=False):
+        """The ``pfi`` argument under which oracle.dual_simplex / lp_bound
+        restate what this context runs for such a batch (0 = dense K3/K3L)."""
+        p = self.problem
+        v, k = getattr(self, 'lp_variant', 0), getattr(self, 'lp_pfi', LP_PFI_MAX)
+        if v == 3:
+            k = k or LP_PFI_MAX
+        elif v != 0:
+            return 0
+        fits = p is not None and p.m <= 64 and p.n + p.m <= 256
+        return k if (shared_ws and not want_ws and fits) else 0
 
     def set_fbbt_variant(self, v: int):
         self._chk(self.lib.mgpu_set_fbbt_variant(self.h, int(v)), 'mgpu_set_fbbt_variant')

@@ -31,8 +31,9 @@ class _Stats:
 
 
 class CpuBnbContext:
-    def __init__(self, p):
+    def __init__(self, p, pfi=0):
         self.problem = p
+        self.pfi = pfi   # node LPs in K3P's product form (Context.oracle_pfi())
 
     # -- mgpu_bnb_init ------------------------------------------------------
     def bnb_init(self, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
@@ -69,7 +70,8 @@ class CpuBnbContext:
         x = np.zeros((nb, p.n))
         keep = np.nonzero(f.infeas == 0)[0]
         if keep.size:
-            s2, o2, _, x2 = oracle.dual_simplex(p, f.lb[keep], f.ub[keep], self.ws, want_x=True)
+            s2, o2, _, x2 = oracle.dual_simplex(p, f.lb[keep], f.ub[keep], self.ws, want_x=True,
+                                                 pfi=self.pfi if self.ws is not None else 0)
             status[keep], obj[keep], x[keep] = s2, o2, x2
         ints = np.isin(p.vtype, (0, 1))
         children = []

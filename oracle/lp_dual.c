@@ -42,6 +42,14 @@ typedef struct {
   int *head;           /* basic column of each row */
   signed char *st;
   double *rho, *alpha_r, *alpha_q, *w;
+  /* product-form mode (K3P, repo:minotaur_amd/csrc/lp_pfi.hip): B^{-1} =
+   * E_{k-1} ... E_0 B0^{-1} with B0^{-1} the shared warm-start inverse
+   * (row-major, never modified) and at most pfi eta columns */
+  int pfi, neta;
+  const double *binv0;
+  double *eta;         /* pfi x m: eta column t */
+  int *prow;           /* pivot row of eta t */
+  double *u;           /* m: BTRAN work vector */
 } lpw;
 
 static double bnd_lo(const orc_lp *P, const double *lb, int j) {
@@ -59,10 +67,62 @@ static double col_dot(const orc_lp *P, const double *v, int j) {
   return s;
 }
 
+/* ---- product form (K3P): every loop below is the kernel's, in its order */
+
+/* out <- E_{k-1} ... E_0 out.  E_t is the identity except column p = prow[t]
+ * (= eta t): out_p' = eta_p out_p, out_i' = out_i + eta_i out_p. */
+static void pfi_apply_etas(const lpw *W, double *out) {
+  int m = W->P->m;
+  for (int t = 0; t < W->neta; ++t) {
+    const double *e = W->eta + (size_t) t * m;
+    int p = W->prow[t];
+    double vp = out[p];
+    if (vp == 0.0) continue;
+    for (int i = 0; i < m; ++i) out[i] = i == p ? e[i] * vp : out[i] + e[i] * vp;
+  }
+}
+
+/* rho = e_r' B^{-1}: u = e_r' E_{k-1} ... E_0 (each E_t' only rewrites
+ * component prow[t], a dot product over the nonzeros of u in ascending row
+ * order), then rho = u' B0^{-1} over the same nonzeros. */
+static void pfi_btran(const lpw *W, int r, double *rho) {
+  int m = W->P->m;
+  double *u = W->u;
+  for (int i = 0; i < m; ++i) u[i] = 0.0;
+  u[r] = 1.0;
+  for (int t = W->neta - 1; t >= 0; --t) {
+    const double *e = W->eta + (size_t) t * m;
+    double acc = 0.0;
+    for (int i = 0; i < m; ++i)
+      if (u[i] != 0.0) acc += u[i] * e[i];
+    u[W->prow[t]] = acc;
+  }
+  for (int k = 0; k < m; ++k) rho[k] = 0.0;
+  for (int i = 0; i < m; ++i) {
+    if (u[i] == 0.0) continue;
+    for (int k = 0; k < m; ++k) rho[k] += u[i] * W->binv0[(size_t) i * m + k];
+  }
+}
+
 /* out = B^{-1} a_j */
 static void ftran_col(const lpw *W, int j, double *out) {
   const orc_lp *P = W->P;
   int m = P->m;
+  if (W->pfi) {
+    if (j >= P->n) {
+      int i0 = j - P->n;
+      for (int i = 0; i < m; ++i) out[i] = -W->binv0[(size_t) i * m + i0];
+    } else {
+      for (int i = 0; i < m; ++i) out[i] = 0.0;
+      for (int k = P->colptr[j]; k < P->colptr[j + 1]; ++k) {
+        int r = P->rowidx[k];
+        double a = P->cval[k];
+        for (int i = 0; i < m; ++i) out[i] += W->binv0[(size_t) i * m + r] * a;
+      }
+    }
+    pfi_apply_etas(W, out);
+    return;
+  }
   if (j >= P->n) {
     int i0 = j - P->n;
     for (int i = 0; i < m; ++i) out[i] = -W->binv[i * m + i0];
@@ -125,12 +185,14 @@ static void compute_duals(lpw *W) {
   int m = P->m, N = W->N;
   /* y = c_B' B^{-1}; reuse rho as y */
   double *y = W->rho;
+  /* product form: only called before the first pivot, where B^{-1} = B0^{-1} */
+  const double *bi = W->pfi ? W->binv0 : W->binv;
   for (int k = 0; k < m; ++k) y[k] = 0.0;
   for (int i = 0; i < m; ++i) {
     int h = W->head[i];
     double cb = h < P->n ? P->c[h] : 0.0;
     if (cb != 0.0)
-      for (int k = 0; k < m; ++k) y[k] += cb * W->binv[i * m + k];
+      for (int k = 0; k < m; ++k) y[k] += cb * bi[i * m + k];
   }
   for (int j = 0; j < N; ++j) {
     if (W->st[j] == ST_BASIC) { W->d[j] = 0.0; continue; }
@@ -153,6 +215,16 @@ static void compute_primals(lpw *W) {
     } else {
       for (int k = P->colptr[j]; k < P->colptr[j + 1]; ++k) w[P->rowidx[k]] += P->cval[k] * zj;
     }
+  }
+  if (W->pfi) {
+    double *s = W->alpha_q;   /* free outside a pivot */
+    for (int i = 0; i < m; ++i) {
+      s[i] = 0.0;
+      for (int k = 0; k < m; ++k) s[i] += W->binv0[(size_t) i * m + k] * w[k];
+    }
+    pfi_apply_etas(W, s);
+    for (int i = 0; i < m; ++i) W->z[W->head[i]] = -s[i];
+    return;
   }
   for (int i = 0; i < m; ++i) {
     double s = 0.0;
@@ -210,10 +282,17 @@ static int invert_basis(lpw *W) {
  * Solve one LP.  ws_head/ws_st/ws_binv: warm start in/out (NULL = slack
  * basis).  Returns an EngineStatus numeric (Types.h:152-166).
  */
-int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
-                     int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
-                     int have_ws, int have_binv, int iter_limit, double *obj_out,
-                     double *x_out, double *y_out, int *iters_out)
+/*
+ * pfi > 0: product-form mode of K3P (only with a supplied warm-start inverse,
+ * which becomes B0^{-1}): pivots append eta columns instead of updating a
+ * dense inverse, and a solve that needs more than pfi pivots stops with
+ * status -1 (the caller re-solves it densely, as the GPU does).  No
+ * warm-start or dual output in this mode.
+ */
+static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub,
+                             int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
+                             int have_ws, int have_binv, int iter_limit, double *obj_out,
+                             double *x_out, double *y_out, int *iters_out, int pfi)
 {
   int n = P->n, m = P->m, N = n + m;
   lpw W;
@@ -221,6 +300,13 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
   double art_bound = ART_BOUND;
   memset(&W, 0, sizeof W);
   W.P = P; W.N = N; W.lb = lb; W.ub = ub;
+  if (pfi > 0 && have_ws && have_binv) {
+    W.pfi = pfi;
+    W.binv0 = ws_binv;
+    W.eta = (double *) malloc(sizeof(double) * (size_t) pfi * m + 8);
+    W.prow = (int *) malloc(sizeof(int) * (size_t) pfi + 4);
+    W.u = (double *) malloc(sizeof(double) * (size_t) m + 8);
+  }
   W.blo = (double *) malloc(sizeof(double) * N);
   W.bhi = (double *) malloc(sizeof(double) * N);
   W.art = (unsigned char *) calloc((size_t) N, 1);
@@ -315,8 +401,10 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
       continue;
     }
     if (iters >= iter_limit) { status = 6; break; }   /* EngineIterationLimit */
+    if (W.pfi && iters >= W.pfi) { status = -1; break; }   /* eta file full */
     /* ---- row r of B^{-1}, pivot row ---- */
-    for (int k = 0; k < m; ++k) W.rho[k] = W.binv[r * m + k];
+    if (W.pfi) pfi_btran(&W, r, W.rho);
+    else for (int k = 0; k < m; ++k) W.rho[k] = W.binv[r * m + k];
     double sigma = delta > 0 ? 1.0 : -1.0;
     /* ---- Harris two-pass ratio test ---- */
     double tmax = INFINITY;
@@ -391,7 +479,13 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
       W.bhi[q] = bnd_hi(P, ub, q) > INF_B ? INFINITY : bnd_hi(P, ub, q);
       W.art[q] = 0;
     }
-    {
+    if (W.pfi) {
+      /* eta column of this pivot: -alpha_q / alpha_rq, 1 / alpha_rq at r */
+      double inv = 1.0 / arq;
+      double *e = W.eta + (size_t) W.neta * m;
+      for (int i = 0; i < m; ++i) e[i] = i == r ? inv : -W.alpha_q[i] * inv;
+      W.prow[W.neta++] = r;
+    } else {
       double inv = 1.0 / arq;
       double *br = W.binv + (size_t) r * m;
       for (int k = 0; k < m; ++k) br[k] *= inv;
@@ -411,7 +505,7 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
 done:
   /* warm start out: the maintained reduced costs (reduced costs of fixed
    * nonbasic columns are not maintained: they can never enter) */
-  if (ws_head && (status == 0 || status == 6)) {
+  if (ws_head && !W.pfi && (status == 0 || status == 6)) {
     memcpy(ws_head, W.head, sizeof(int) * (size_t) m);
     if (ws_st) for (int j = 0; j < N; ++j) ws_st[j] = W.st[j];
     if (ws_binv) memcpy(ws_binv, W.binv, sizeof(double) * (size_t) m * m);
@@ -422,7 +516,7 @@ done:
     for (int j = 0; j < n; ++j) obj += P->c[j] * W.z[j];
     if (obj_out) *obj_out = obj;
     if (x_out) for (int j = 0; j < n; ++j) x_out[j] = W.z[j];
-    if (y_out) {
+    if (y_out && !W.pfi) {
       compute_duals(&W);
       for (int i = 0; i < m; ++i) y_out[i] = W.rho[i];
     }
@@ -432,7 +526,39 @@ done:
   if (iters_out) *iters_out = iters;
   free(W.blo); free(W.bhi); free(W.art); free(W.z); free(W.d); free(W.binv);
   free(W.head); free(W.st); free(W.rho); free(W.w); free(W.alpha_r); free(W.alpha_q);
+  free(W.eta); free(W.prow); free(W.u);
   return status;
+}
+
+int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
+                     int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
+                     int have_ws, int have_binv, int iter_limit, double *obj_out,
+                     double *x_out, double *y_out, int *iters_out)
+{
+  return dual_simplex_impl(P, lb, ub, ws_head, ws_st, ws_binv, ws_d, have_ws, have_binv,
+                           iter_limit, obj_out, x_out, y_out, iters_out, 0);
+}
+
+/* What the GPU runs for one LP of a batch that shares its warm start: K3P
+ * (product form, at most pfi pivots), and the dense K3 from the same warm
+ * start for an LP that fills the eta file.  ws_* are read-only here. */
+static int solve_shared(const orc_lp *P, const double *lb, const double *ub, const int *ws_head,
+                        const signed char *ws_st, const double *ws_binv, const double *ws_d,
+                        int have_ws, int have_binv, int iter_limit, double *obj, double *x,
+                        int *iters, int pfi, int *h, signed char *s, double *bi, double *dd)
+{
+  int n = P->n, m = P->m, st = -1;
+  for (int pass = pfi > 0 && have_ws && have_binv ? 0 : 1; pass < 2 && st < 0; ++pass) {
+    if (have_ws) {
+      memcpy(h, ws_head, sizeof(int) * (size_t) m);
+      memcpy(s, ws_st, (size_t) (n + m));
+      if (ws_binv) memcpy(bi, ws_binv, sizeof(double) * (size_t) m * m);
+      if (ws_d) memcpy(dd, ws_d, sizeof(double) * (size_t) (n + m));
+    }
+    st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, have_ws, have_binv, iter_limit,
+                           obj, x, 0, iters, pass == 0 ? pfi : 0);
+  }
+  return st;
 }
 
 /* Batch entry for ctypes: one LP per node box, optional shared warm start
@@ -445,7 +571,7 @@ int orc_dual_simplex_batch(int n, int m, const int *colptr, const int *rowidx,
                            const double *rhi, int B, const double *lb, const double *ub,
                            const int *ws_head, const signed char *ws_st,
                            const double *ws_binv, const double *ws_d, int iter_limit, int *status,
-                           double *obj, double *x, int *iters, int nthreads)
+                           double *obj, double *x, int *iters, int nthreads, int pfi)
 {
   orc_lp P;
   P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cval; P.c = c;
@@ -460,16 +586,10 @@ int orc_dual_simplex_batch(int n, int m, const int *colptr, const int *rowidx,
 #pragma omp for schedule(dynamic, 16)
     for (int b = 0; b < B; ++b) {
       int have = ws_head != 0;
-      if (have) {
-        memcpy(h, ws_head, sizeof(int) * (size_t) m);
-        memcpy(s, ws_st, (size_t) (n + m));
-        if (ws_binv) memcpy(bi, ws_binv, sizeof(double) * (size_t) m * m);
-        if (ws_d) memcpy(dd, ws_d, sizeof(double) * (size_t) (n + m));
-      }
-      status[b] = orc_dual_simplex(&P, lb + (size_t) b * n, ub + (size_t) b * n, h, s, bi,
-                                   ws_d ? dd : 0, have, have && ws_binv != 0 && ws_d != 0,
-                                   iter_limit, obj + b, x ? x + (size_t) b * n : 0, 0,
-                                   iters + b);
+      status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n, ws_head, ws_st,
+                               ws_binv, ws_d, have, have && ws_binv != 0 && ws_d != 0,
+                               iter_limit, obj + b, x ? x + (size_t) b * n : 0, iters + b, pfi,
+                               h, s, bi, dd);
     }
     free(h); free(s); free(bi); free(dd);
   }
@@ -498,7 +618,7 @@ int orc_lp_bound_batch(int n, int m, const int *colptr, const int *rowidx, const
                        const double *rlo, const double *rhi, const double *lb, const double *ub,
                        int B, const int *col, const double *sign, const int *ws_head,
                        const signed char *ws_st, const double *ws_binv, int iter_limit,
-                       int *status, double *obj, double *x, int *iters, int nthreads)
+                       int *status, double *obj, double *x, int *iters, int nthreads, int pfi)
 {
   if (nthreads < 1) nthreads = 1;
 #pragma omp parallel num_threads(nthreads)
@@ -507,23 +627,20 @@ int orc_lp_bound_batch(int n, int m, const int *colptr, const int *rowidx, const
     signed char *s = (signed char *) malloc((size_t) (n + m + 1));
     double *bi = (double *) malloc(sizeof(double) * (size_t) m * m + 8);
     double *c = (double *) calloc((size_t) n + 1, sizeof(double));
+    double *dd = (double *) malloc(sizeof(double) * (size_t) (n + m) + 8);
     orc_lp P;
     P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cval; P.c = c;
     P.rlo = rlo; P.rhi = rhi;
 #pragma omp for schedule(dynamic, 4)
     for (int b = 0; b < B; ++b) {
       const int have = ws_head != 0;
-      if (have) {
-        memcpy(h, ws_head, sizeof(int) * (size_t) m);
-        memcpy(s, ws_st, (size_t) (n + m));
-        memcpy(bi, ws_binv, sizeof(double) * (size_t) m * m);
-      }
       c[col[b]] = sign[b];
-      status[b] = orc_dual_simplex(&P, lb, ub, h, s, bi, 0, have, have, iter_limit, obj + b,
-                                   x ? x + (size_t) b * n : 0, 0, iters + b);
+      status[b] = solve_shared(&P, lb, ub, ws_head, ws_st, ws_binv, 0, have, have, iter_limit,
+                               obj + b, x ? x + (size_t) b * n : 0, iters + b, pfi, h, s, bi,
+                               dd);
       c[col[b]] = 0.0;
     }
-    free(h); free(s); free(bi); free(c);
+    free(h); free(s); free(bi); free(c); free(dd);
   }
   return 0;
 }

@@ -173,13 +173,16 @@ class WarmStart:
 def _lp_sig(l):
     l.orc_dual_simplex_batch.restype = _I
     l.orc_dual_simplex_batch.argtypes = [_I, _I] + [_P] * 6 + [_I, _P, _P, _P, _P, _P, _P,
-                                         _I, _P, _P, _P, _P, _I]
+                                         _I, _P, _P, _P, _P, _I, _I]
     l.orc_dual_simplex_root.restype = _I
     l.orc_dual_simplex_root.argtypes = [_I, _I] + [_P] * 8 + [_I] + [_P] * 8
 
 
-def dual_simplex(p, LB, UB, ws=None, iter_limit=10000, nthreads=1, want_x=False):
-    """Per-node LP solves; returns (status[B], obj[B] incl. constant, iters[B], x)."""
+def dual_simplex(p, LB, UB, ws=None, iter_limit=10000, nthreads=1, want_x=False, pfi=0):
+    """Per-node LP solves; returns (status[B], obj[B] incl. constant, iters[B], x).
+    pfi > 0 (with a shared ``ws``): the product-form arithmetic of K3P with an
+    eta file of ``pfi`` columns, and the dense solve for an LP that fills it
+    (what the GPU runs for a shared warm start)."""
     l = lib()
     _lp_sig(l)
     LB = np.ascontiguousarray(LB, dtype=np.float64)
@@ -199,7 +202,7 @@ def dual_simplex(p, LB, UB, ws=None, iter_limit=10000, nthreads=1, want_x=False)
     l.orc_dual_simplex_batch(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj),
                              _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(h),
                              _ptr(s), _ptr(bi), _ptr(dd), iter_limit, _ptr(st), _ptr(obj), _ptr(x),
-                             _ptr(it), nthreads)
+                             _ptr(it), nthreads, int(pfi))
     obj = obj + p.obj_const
     return st, obj, it, x
 
@@ -384,12 +387,14 @@ def ref_quad_fbbt(qp, lb, ub, incumbent=None, qt=1, rows=None, mod_cap=0):
     return QuadFbbtResult(olb, oub, infeas, nmods, orows, kind, idx, v1, v2, float(secs[0]))
 
 
-def lp_bound(p, cols, signs, lb=None, ub=None, ws=None, iter_limit=100000, nthreads=1):
+def lp_bound(p, cols, signs, lb=None, ub=None, ws=None, iter_limit=100000, nthreads=1, pfi=0):
     """C restatement of the bound LPs (min sign_b * x[col_b] on one box,
-    warm-started from ws = oracle WarmStart, binv row-major)."""
+    warm-started from ws = oracle WarmStart, binv row-major); pfi as in
+    dual_simplex."""
     L = lib()
     L.orc_lp_bound_batch.restype = _I
-    L.orc_lp_bound_batch.argtypes = [_I, _I] + [_P] * 7 + [_I] + [_P] * 5 + [_I] + [_P] * 4 + [_I]
+    L.orc_lp_bound_batch.argtypes = ([_I, _I] + [_P] * 7 + [_I] + [_P] * 5 + [_I] + [_P] * 4
+                                     + [_I, _I])
     colptr, rowidx, cval = lp_csc(p)
     lb = np.ascontiguousarray(p.vlb if lb is None else lb, dtype=np.float64)
     ub = np.ascontiguousarray(p.vub if ub is None else ub, dtype=np.float64)
@@ -408,7 +413,7 @@ def lp_bound(p, cols, signs, lb=None, ub=None, ws=None, iter_limit=100000, nthre
     L.orc_lp_bound_batch(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.rlo),
                          _ptr(p.rhi), _ptr(lb), _ptr(ub), B, _ptr(cols), _ptr(signs), _ptr(wh),
                          _ptr(wst), _ptr(wb), iter_limit, _ptr(st), _ptr(obj), _ptr(x), _ptr(it),
-                         nthreads)
+                         nthreads, int(pfi))
     return st, obj, it, x
 
 

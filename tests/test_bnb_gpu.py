@@ -107,7 +107,7 @@ def test_bnb_tree_matches_cpu_restatement(ctx, batch):
     for p in (knapsack_oa(), random_mkp(6, 16, 3)):
         ctx.load(p)
         og, xg, sg, _ = bnb.solve(ctx, batch=batch, capacity=1 << 15)
-        oc, xc, sc, _ = bnb.solve(CpuBnbContext(p), batch=batch, capacity=1 << 15)
+        oc, xc, sc, _ = bnb.solve(CpuBnbContext(p, ctx.oracle_pfi()), batch=batch, capacity=1 << 15)
         assert sg.open == sc.open == 0
         assert abs(og - oc) <= 1e-9 * max(1.0, abs(oc))
         assert (sg.rounds, sg.nodes, list(sg.ndec)) == (sc.rounds, sc.nodes, list(sc.ndec))
@@ -125,7 +125,7 @@ def test_bnb_k3l_tree_matches_cpu_and_highs(ctx):
     hs, hobj = oracle.highs_milp(p)
     ctx.load(p)
     og, xg, sg, _ = bnb.solve(ctx, batch=512, capacity=1 << 17)
-    oc, xc, sc, _ = bnb.solve(CpuBnbContext(p), batch=512, capacity=1 << 17)
+    oc, xc, sc, _ = bnb.solve(CpuBnbContext(p, ctx.oracle_pfi()), batch=512, capacity=1 << 17)
     assert sg.open == sc.open == 0
     assert (sg.rounds, sg.nodes, list(sg.ndec)) == (sc.rounds, sc.nodes, list(sc.ndec))
     assert og == oc

@@ -57,9 +57,18 @@ def test_lp_warm_from_root(ctx, name):
     assert np.allclose(ws.d, ows.d, rtol=1e-9, atol=1e-12)
     r = ctx.lp_solve(g['lb'], g['ub'], ws)
     assert_lp_matches(r.status, r.obj, g)
-    st, obj, its, _ = oracle.dual_simplex(p, g['lb'], g['ub'], ows)
+    st, obj, its, _ = oracle.dual_simplex(p, g['lb'], g['ub'], ows, pfi=ctx.oracle_pfi())
     assert np.array_equal(r.status, st)
     assert np.array_equal(r.iters, its)
+    assert _close(r.obj, obj)
+    # the dense K3 on the same shared warm start: the oracle's dense mode
+    ctx.set_lp_variant(1)
+    try:
+        r = ctx.lp_solve(g['lb'], g['ub'], ws)
+    finally:
+        ctx.set_lp_variant(0)
+    st, obj, its, _ = oracle.dual_simplex(p, g['lb'], g['ub'], ows)
+    assert np.array_equal(r.status, st) and np.array_equal(r.iters, its)
     assert _close(r.obj, obj)
 
 
@@ -117,7 +126,7 @@ def test_lp_large_batch_vs_oracle(ctx):
     LB, UB = random_boxes(p, 5003, 31337)
     r = ctx.lp_solve(LB, UB, ws)
     _, _, _, _, _, ows = oracle.dual_simplex_root(p)
-    st, obj, its, _ = oracle.dual_simplex(p, LB, UB, ows, nthreads=8)
+    st, obj, its, _ = oracle.dual_simplex(p, LB, UB, ows, nthreads=8, pfi=ctx.oracle_pfi())
     assert np.array_equal(r.status, st)
     assert np.array_equal(r.iters, its)
     assert _close(r.obj, obj)

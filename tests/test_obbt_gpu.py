@@ -50,7 +50,7 @@ def test_bound_lps_gpu_vs_oracle(ctx, seed, cutoff):
         cols = np.arange(p.n, dtype=np.int32)
         signs = np.where(np.arange(p.n) % 2 == 0, 1.0, -1.0)
     g = ctx.lp_bound(cols, signs, ws=ws, want_x=True)
-    st, ob, it, xs = oracle.lp_bound(p, cols, signs, ws=ows)
+    st, ob, it, xs = oracle.lp_bound(p, cols, signs, ws=ows, pfi=ctx.oracle_pfi())
     assert np.array_equal(g.status, st)
     assert np.array_equal(g.iters, it)
     ok = st == 0
@@ -69,7 +69,7 @@ def test_obbt_gpu_matches_oracle_replay(ctx, seed):
     inf, lb, ub, mods, nlp, used = obbt.obbt(ctx, qp, rows, x, ws)
     itmp = obbt.select_vars(qp, x, qp.vlb, qp.vub)
     cols, signs = obbt.bound_lp_batch(itmp)
-    st, ob, it, xs = oracle.lp_bound(p, cols, signs, ws=ows)
+    st, ob, it, xs = oracle.lp_bound(p, cols, signs, ws=ows, pfi=ctx.oracle_pfi())
     res = {(int(c), float(s)): (int(st[i]), float(ob[i]), xs[i])
            for i, (c, s) in enumerate(zip(cols, signs))}
     inf2, lb2, ub2, mods2, used2 = obbt.replay(qp, itmp, qp.vlb, qp.vub, res)

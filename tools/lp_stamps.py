@@ -1,4 +1,4 @@
-"""Diagnostic: where K3 spends its cycles.  Builds a stamped variant of
+"""Diagnostic: where K3 (or K3P with --pfi) spends its cycles.  Builds a stamped variant of
 libmgpu (-DMGPU_STAMPS) into /tmp, runs the LP probe workload and prints the
 s_memtime share of each section (see cdna_hip_programming.md §7: read the
 SHARES, not the run time, of a stamped build)."""
@@ -13,6 +13,8 @@ OUT = os.environ.get('STAMP_LIB', os.path.join(ROOT, 'gpurun_out', 'libmgpu_stam
 NAMES = ['setup:primals', 'pricing', 'rho_write', 'pass1+min', 'pass2+argmax', 'column_q',
          'steps/updates', 'binv_update', 'tail', 'outputs', 'setup:skip',
          'setup:bounds', 'setup:basis', 'setup:place']
+PFI_NAMES = ['setup', 'primals', 'pricing', 'btran+rho', 'pass1+min', 'pass2+argmax', 'ftran',
+             'steps+eta', 'outputs', 'skip/empty']
 
 
 def build():
@@ -24,6 +26,7 @@ def build():
 
 
 def main():
+    pfi = '--pfi' in sys.argv
     if not os.path.exists(OUT):
         build()
     os.environ['MGPU_LIB'] = OUT
@@ -40,13 +43,19 @@ def main():
     LB, UB = random_boxes(p, B, 20261015)
     f = ctx.fbbt(LB, UB)
     buf = (ctypes.c_ulonglong * 16)()
-    lib.mgpu_debug_lp_stamps(buf, 1)
+    if pfi:
+        ctx.set_lp_variant(3)
+        fn, names = lib.mgpu_debug_pfi_stamps, PFI_NAMES
+    else:
+        ctx.set_lp_variant(1)
+        fn, names = lib.mgpu_debug_lp_stamps, NAMES
+    fn(buf, 1)
     r = ctx.lp_solve(f.lb, f.ub, wsh, skip=f.infeasible)
-    lib.mgpu_debug_lp_stamps(buf, 1)
-    tot = sum(buf[i] for i in range(len(NAMES)))
+    fn(buf, 1)
+    tot = sum(buf[i] for i in range(len(names)))
     piv = int(r.iters.sum())
     print(f"pivots {piv}  total wave-cycles {tot:.3e}  per pivot {tot / max(piv, 1):.0f}")
-    for i, nme in enumerate(NAMES):
+    for i, nme in enumerate(names):
         print(f"  {nme:14s} {100.0 * buf[i] / tot:6.2f} %   {buf[i] / max(piv, 1):9.0f} cyc/pivot")
 
 
