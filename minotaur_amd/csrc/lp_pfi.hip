@@ -7,17 +7,22 @@
 // starting inverse B0^{-1} is the same for all of them and only the few
 // pivots each node makes (5.9 on average for tls4-lin, 99.9 % <= 24) differ.
 //
-// MI355X-first mapping:
-//  * B0^{-1} is staged ONCE per workgroup in LDS, in both layouts (column
-//    major for B^{-1} a_q, row major for rho' = u' B0^{-1}); a node's own
-//    inverse is B^{-1} = E_{k-1} ... E_0 B0^{-1}: k eta columns in VGPRs
-//    (lane i holds eta_t[i]; at most kPfiMax of them).  The dense inverse of
-//    K3 (128 VGPRs per node, 60 FMAs per lane per pivot to update) is gone,
-//    which takes the kernel from 2 to 4 waves per SIMD.
-//  * Column state (reduced costs, values, working bounds, status, pivot row,
-//    Harris ratios) lives in VGPRs too: column j = s*64 + lane is slot s of
-//    that lane (S slots, N = n + m <= 64*S).  Only the broadcast vectors (rho,
-//    the nonbasic values for the primal recompute) go through LDS.
+// MI355X-first mapping (the kernel is latency-bound, so the design goal is
+// waves per SIMD: few VGPRs per node, LDS sized for 16 waves per CU):
+//  * B0^{-1} is staged ONCE per workgroup in LDS, column-major with an odd
+//    leading dimension m+1, so lanes reading a column (B0^{-1} a_q, the
+//    primal recompute) and lanes reading a row (rho' = u' B0^{-1}) both hit
+//    distinct banks.  A node's inverse is B^{-1} = E_{k-1} ... E_0 B0^{-1}:
+//    k eta columns in VGPRs (lane i holds eta_t[i]; at most kPfiMax).  The
+//    dense inverse of K3 (128 VGPRs per node, m FMAs per lane per pivot to
+//    update) is gone.
+//  * Per column j = s*64 + lane (slot s of that lane, N = n + m <= 64*S):
+//    reduced cost, pivot-row entry, Harris ratio and packed status bits stay
+//    in VGPRs; value and working bounds live in a per-wave LDS slice (they
+//    are read by wave-uniform index or rarely).  The entering column's data
+//    is captured by its owner lane during pass 2 and broadcast with
+//    v_readlane: no dynamically indexed register arrays (those were demoted
+//    to scratch).
 //  * BTRAN visits only the nonzeros of u (a ballot mask, ascending rows) with
 //    v_readlane broadcasts; FTRAN reads the CSC column of a_q from LDS and
 //    applies the etas lane-parallel.
@@ -65,22 +70,25 @@ constexpr double kInfB = 1e30;
 constexpr int kUnknownStatus = 12;
 constexpr int kWaves = 12;  // one 768-thread workgroup per CU: 3 waves per SIMD (<= 168 VGPRs)
 
+// packed column status: bits 0-1 status, 2-3 artificial-bound flags, 4 fixed
 enum : int { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
+constexpr int kArtLo = 4, kArtHi = 8, kFixed = 16;
 
 static_assert(kPfiMax < 64, "K3P never reaches K3's 64-pivot primal refresh");
 
 __host__ __device__ constexpr size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
 
-// matrix (CSC + CSR), B0^{-1} both ways, warm-start d / status / head
+// matrix (CSC + CSR), B0^{-1} (column-major, leading dimension m + 1),
+// warm-start d / status / head
 __host__ __device__ inline size_t pfi_shared_bytes(int n, int m, int nnz) {
   const int N = n + m;
   return al16((size_t)(n + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
          al16((size_t)(m + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
-         2 * al16((size_t)m * m * 8) + al16((size_t)N * 8) + al16((size_t)N * 4) +
+         al16((size_t)m * (m + 1) * 8) + al16((size_t)N * 8) + al16((size_t)N * 4) +
          al16((size_t)m * 4);
 }
-// per wave: rho [64] + two column vectors [N] (values; basic-row bounds)
-__host__ __device__ inline size_t pfi_wave_bytes(int N) { return 64 * 8 + 2 * al16((size_t)N * 8); }
+// per wave: rho [64] + column values, lower and upper working bounds [N]
+__host__ __device__ inline size_t pfi_wave_bytes(int N) { return 64 * 8 + 3 * al16((size_t)N * 8); }
 
 __device__ __forceinline__ double art_lo(double thi, double ab) {
   return (thi < kInfB ? thi : 0.0) - ab;
@@ -89,37 +97,11 @@ __device__ __forceinline__ double art_hi(double tlo, double ab) {
   return (tlo > -kInfB ? tlo : 0.0) + ab;
 }
 
-// value of column j (wave-uniform j) held in slot j>>6 of lane j&63
-template <int S>
-__device__ __forceinline__ double colget(const double (&a)[S], int j) {
-  const int s = j >> 6;
-  double v = a[0];
-#pragma unroll
-  for (int t = 1; t < S; ++t)
-    if (s == t) v = a[t];
-  return rld(v, j & 63);
-}
-template <int S>
-__device__ __forceinline__ int colget(const int (&a)[S], int j) {
-  const int s = j >> 6;
-  int v = a[0];
-#pragma unroll
-  for (int t = 1; t < S; ++t)
-    if (s == t) v = a[t];
-  return rl(v, j & 63);
-}
-template <int S, class T>
-__device__ __forceinline__ void colset(T (&a)[S], int j, T v, int lane) {
-#pragma unroll
-  for (int t = 0; t < S; ++t)
-    if (t == (j >> 6) && lane == (j & 63)) a[t] = v;
-}
-
 struct Prob {
   const int *colptr, *rowidx, *rowptr, *ccol;
   const double *cval, *rval;
-  const double *b0c, *b0r;  // B0^{-1}: b0c[k*m + i] = b0r[i*m + k] = (B0^{-1})_{ik}
-  int n, m, N;
+  const double *b0;  // (B0^{-1})_{ik} = b0[k*ld + i]
+  int n, m, N, ld;
   const double *nlb, *nub, *rlo, *rhi, *c;
   int ocol;
   double osign;
@@ -154,8 +136,8 @@ struct Prob {
   }
 };
 
-// v <- E_{k-1} ... E_0 v (oracle pfi_apply_etas); lanes >= m hold eta 0
-// (pivot row of eta t = lane t of prow)
+// v <- E_{k-1} ... E_0 v (oracle pfi_apply_etas); lanes >= m hold eta 0;
+// the pivot row of eta t is lane t of prow
 __device__ __forceinline__ double apply_etas(double v, const double (&eta)[kPfiMax], int prow,
                                              int k, int lane) {
 #pragma unroll
@@ -172,11 +154,11 @@ __device__ __forceinline__ double apply_etas(double v, const double (&eta)[kPfiM
 template <int S>
 __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, PfiIO px) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz;
+  const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz, ld = m + 1;
   const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kmax = px.kmax;
 
-  // ---- stage the matrix, B0^{-1} (both layouts) and the warm start once ----
+  // ---- stage the matrix, B0^{-1} and the warm start once per workgroup ----
   unsigned char *p = smem;
   int *s_colptr = (int *)p;      p += al16((size_t)(n + 1) * 4);
   int *s_rowidx = (int *)p;      p += al16((size_t)nnz * 4);
@@ -184,8 +166,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
   int *s_rowptr = (int *)p;      p += al16((size_t)(m + 1) * 4);
   int *s_ccol = (int *)p;        p += al16((size_t)nnz * 4);
   double *s_rval = (double *)p;  p += al16((size_t)nnz * 8);
-  double *s_b0c = (double *)p;   p += al16((size_t)m * m * 8);
-  double *s_b0r = (double *)p;   p += al16((size_t)m * m * 8);
+  double *s_b0 = (double *)p;    p += al16((size_t)m * ld * 8);
   double *s_wd = (double *)p;    p += al16((size_t)N * 8);
   int *s_wst = (int *)p;         p += al16((size_t)N * 4);
   int *s_whead = (int *)p;       p += al16((size_t)m * 4);
@@ -198,11 +179,8 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
     s_ccol[t] = lp.ccol[t];
     s_rval[t] = lp.rval[t];
   }
-  for (int t = threadIdx.x; t < m * m; t += T) {
-    const double v = io.ws.binv[t];  // column-major: t = k*m + i
-    s_b0c[t] = v;
-    s_b0r[(t % m) * m + t / m] = v;
-  }
+  for (int t = threadIdx.x; t < m * m; t += T)  // ABI: column-major, t = k*m + i
+    s_b0[(t / m) * ld + t % m] = io.ws.binv[t];
   for (int t = threadIdx.x; t < N; t += T) {
     s_wd[t] = io.ws.d != nullptr ? io.ws.d[t] : 0.0;  // bound LPs rebuild d
     const int8_t s = io.ws.st[t];
@@ -216,12 +194,14 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
   Prob P;
   P.colptr = s_colptr; P.rowidx = s_rowidx; P.cval = s_cval;
   P.rowptr = s_rowptr; P.ccol = s_ccol; P.rval = s_rval;
-  P.b0c = s_b0c; P.b0r = s_b0r;
-  P.n = n; P.m = m; P.N = N;
+  P.b0 = s_b0;
+  P.n = n; P.m = m; P.N = N; P.ld = ld;
   P.rlo = lp.rlo; P.rhi = lp.rhi; P.c = lp.objd;
   double *rho = (double *)(p + (size_t)wave * pfi_wave_bytes(N));
-  double *zbuf = rho + 64;
-  double *ybuf = zbuf + al16((size_t)N * 8) / 8;
+  const size_t Np = al16((size_t)N * 8) / 8;
+  double *zc = rho + 64;   // value of each nonbasic column, 0 for basic ones
+  double *lo = zc + Np;    // working bounds (artificial where marked)
+  double *hi = lo + Np;
 
   // persistent waves over nodes (no workgroup barrier below this point)
   PSTAMP_DECL
@@ -243,22 +223,22 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       continue;
     }
 
-    // ---- column slots: working bounds; an empty box is infeasible ----
-    double d[S], z[S], blo[S], bhi[S], al[S], t2[S];
-    int st[S], art[S];
+    // ---- working bounds; an empty box is infeasible before any pivot ----
+    double tl[S], th[S];
+    int sa[S];
     bool bad = false;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int j = s * 64 + lane;
       const bool valid = j < N;
-      blo[s] = valid ? P.tlo(j) : 0.0;
-      bhi[s] = valid ? P.thi(j) : 0.0;
-      art[s] = 0;
-      z[s] = 0.0;
-      al[s] = 0.0;
-      t2[s] = INFINITY;
-      st[s] = valid ? s_wst[j] : ST_BASIC;  // slots past N act as basic: never touched
-      bad |= valid && blo[s] > bhi[s] + kPTol;
+      tl[s] = valid ? P.tlo(j) : 0.0;
+      th[s] = valid ? P.thi(j) : 0.0;
+      sa[s] = valid ? s_wst[j] : ST_BASIC;  // slots past N act as basic: never touched
+      bad |= valid && tl[s] > th[s] + kPTol;
+      if (valid) {
+        lo[j] = tl[s];
+        hi[j] = th[s];
+      }
     }
     if (__any(bad)) {
       if (lane == 0) {
@@ -269,44 +249,36 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       PSTAMP(9);
       continue;
     }
-
-    // ---- basis rows: head, bounds (basic columns carry no artificial box;
-    // read back through LDS, not a second HBM gather) ----
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const int j = s * 64 + lane;
-      if (j < N) {
-        zbuf[j] = blo[s];
-        ybuf[j] = bhi[s];
-      }
-    }
     wave_sync();
+
+    // ---- basis rows: head and bounds (basic columns carry no artificial box)
     int h = lane < m ? s_whead[lane] : -1;
     double lbB = 0.0, ubB = 0.0;
     if (lane < m) {
-      lbB = zbuf[h];
-      ubB = ybuf[h];
+      lbB = lo[h];
+      ubB = hi[h];
     }
-    wave_sync();
+    double d[S];
     if (P.ocol < 0) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int j = s * 64 + lane;
-        d[s] = (j < N && st[s] != ST_BASIC) ? s_wd[j] : 0.0;
+        d[s] = (j < N && sa[s] != ST_BASIC) ? s_wd[j] : 0.0;
       }
     } else {
       // bound LP (oracle compute_duals at B = B0): y = osign * row r of B0^{-1}
       // when ocol is basic in row r, else 0; d_j = c_j - y' a_j
       const uint64_t on = __ballot(lane < m && h == P.ocol);
       double y = 0.0;
-      if (on != 0ull && lane < m) y = 0.0 + P.osign * s_b0r[(size_t)__builtin_ctzll(on) * m + lane];
+      if (on != 0ull && lane < m)
+        y = 0.0 + P.osign * P.b0[(size_t)lane * ld + __builtin_ctzll(on)];
       rho[lane] = y;
       wave_sync();
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int j = s * 64 + lane;
         d[s] = 0.0;
-        if (j < N && st[s] != ST_BASIC)
+        if (j < N && sa[s] != ST_BASIC)
           d[s] = P.cj(j) - (j >= n ? -rho[j - n] : P.col_dot(rho, j));
       }
       wave_sync();
@@ -316,40 +288,52 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
     double art_bound = kArt0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      if (st[s] == ST_BASIC) continue;
-      const double lo = blo[s], hi = bhi[s], dj = d[s];
-      const bool lo_f = lo > -kInfB, hi_f = hi < kInfB;
-      if (st[s] == ST_LB && lo_f && dj >= -kDTol) {
-        z[s] = lo;
-      } else if (st[s] == ST_UB && hi_f && dj <= kDTol) {
-        z[s] = hi;
-      } else if (lo == hi && lo_f) {
-        st[s] = ST_LB;
-        z[s] = lo;
+      const int j = s * 64 + lane;
+      if (j >= N) continue;
+      if (sa[s] == ST_BASIC) {  // the fixed bit matters once it leaves the basis
+        zc[j] = 0.0;
+        sa[s] = ST_BASIC | (tl[s] == th[s] ? kFixed : 0);
+        continue;
+      }
+      double lo_j = tl[s], hi_j = th[s], z;
+      const double dj = d[s];
+      const bool lo_f = lo_j > -kInfB, hi_f = hi_j < kInfB;
+      int st = sa[s], art = 0;
+      if (st == ST_LB && lo_f && dj >= -kDTol) {
+        z = lo_j;
+      } else if (st == ST_UB && hi_f && dj <= kDTol) {
+        z = hi_j;
+      } else if (lo_j == hi_j && lo_f) {
+        st = ST_LB;
+        z = lo_j;
       } else if (dj > kDTol) {  // oracle place_nonbasic
         if (!lo_f) {
-          blo[s] = art_lo(hi, art_bound);
-          art[s] |= 1;
+          lo_j = art_lo(hi_j, art_bound);
+          lo[j] = lo_j;
+          art = kArtLo;
         }
-        st[s] = ST_LB;
-        z[s] = blo[s];
+        st = ST_LB;
+        z = lo_j;
       } else if (dj < -kDTol) {
         if (!hi_f) {
-          bhi[s] = art_hi(lo, art_bound);
-          art[s] |= 2;
+          hi_j = art_hi(lo_j, art_bound);
+          hi[j] = hi_j;
+          art = kArtHi;
         }
-        st[s] = ST_UB;
-        z[s] = bhi[s];
+        st = ST_UB;
+        z = hi_j;
       } else if (lo_f) {
-        st[s] = ST_LB;
-        z[s] = lo;
+        st = ST_LB;
+        z = lo_j;
       } else if (hi_f) {
-        st[s] = ST_UB;
-        z[s] = hi;
+        st = ST_UB;
+        z = hi_j;
       } else {
-        st[s] = ST_FREE;
-        z[s] = 0.0;
+        st = ST_FREE;
+        z = 0.0;
       }
+      zc[j] = z;
+      sa[s] = st | art | (lo_j == hi_j ? kFixed : 0);
     }
 
     double eta[kPfiMax];
@@ -360,48 +344,46 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
 
     // oracle compute_primals (product form): z_B = -E...E B0^{-1} (N z_N)
     auto primals = [&]() -> double {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int j = s * 64 + lane;
-        if (j < N) zbuf[j] = st[s] == ST_BASIC ? 0.0 : z[s];
-      }
       wave_sync();
       double w = 0.0;
       if (lane < m) {
         for (int t = P.rowptr[lane]; t < P.rowptr[lane + 1]; ++t) {
-          const double zj = zbuf[P.ccol[t]];
+          const double zj = zc[P.ccol[t]];
           if (zj == 0.0) continue;
           w += P.rval[t] * zj;
         }
-        const double zl = zbuf[n + lane];
+        const double zl = zc[n + lane];
         if (zl != 0.0) w -= zl;
       }
-      wave_sync();
       double sacc = 0.0;
       const int li = lane < m ? lane : 0;
       int k = 0;
       for (; k + 4 <= m; k += 4) {  // four LDS loads in flight, adds in order
-        const double b0 = P.b0c[(size_t)k * m + li], b1 = P.b0c[(size_t)(k + 1) * m + li];
-        const double b2 = P.b0c[(size_t)(k + 2) * m + li], b3 = P.b0c[(size_t)(k + 3) * m + li];
+        const double b0 = P.b0[(size_t)k * ld + li], b1 = P.b0[(size_t)(k + 1) * ld + li];
+        const double b2 = P.b0[(size_t)(k + 2) * ld + li], b3 = P.b0[(size_t)(k + 3) * ld + li];
         sacc += b0 * rld(w, k);
         sacc += b1 * rld(w, k + 1);
         sacc += b2 * rld(w, k + 2);
         sacc += b3 * rld(w, k + 3);
       }
-      for (; k < m; ++k) sacc += P.b0c[(size_t)k * m + li] * rld(w, k);
+      for (; k < m; ++k) sacc += P.b0[(size_t)k * ld + li] * rld(w, k);
       if (lane >= m) sacc = 0.0;
       sacc = apply_etas(sacc, eta, prow, iters, lane);
       return -sacc;
     };
+    // oracle grow_art
     auto grow = [&](double ab) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int j = s * 64 + lane;
-        if (!art[s] || st[s] == ST_BASIC) continue;
-        if (art[s] & 1) blo[s] = art_lo(P.thi(j), ab);
-        if (art[s] & 2) bhi[s] = art_hi(P.tlo(j), ab);
-        if (st[s] == ST_LB) z[s] = blo[s];
-        if (st[s] == ST_UB) z[s] = bhi[s];
+        const int st = sa[s] & 3;
+        if (!(sa[s] & (kArtLo | kArtHi)) || st == ST_BASIC) continue;
+        double lo_j = lo[j], hi_j = hi[j];
+        if (sa[s] & kArtLo) lo_j = lo[j] = art_lo(P.thi(j), ab);
+        if (sa[s] & kArtHi) hi_j = hi[j] = art_hi(P.tlo(j), ab);
+        if (st == ST_LB) zc[j] = lo_j;
+        if (st == ST_UB) zc[j] = hi_j;
+        sa[s] = (sa[s] & ~kFixed) | (lo_j == hi_j ? kFixed : 0);
       }
     };
 
@@ -431,10 +413,12 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
         }
         bool g = false;
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          if (st[s] != ST_BASIC && art[s] &&
-              ((st[s] == ST_LB && (art[s] & 1)) || (st[s] == ST_UB && (art[s] & 2))))
+        for (int s = 0; s < S; ++s) {
+          const int st = sa[s] & 3;
+          if (st != ST_BASIC && (((st == ST_LB) && (sa[s] & kArtLo)) ||
+                                 ((st == ST_UB) && (sa[s] & kArtHi))))
             g = true;
+        }
         if (!__any(g)) {
           status = 0;
           break;
@@ -479,7 +463,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       {  // rho' = u' B0^{-1} (ascending nonzero rows), published to LDS
         uint64_t mask = __ballot(u != 0.0);
         double rk = 0.0;
-        const int lk = lane < m ? lane : 0;
+        const size_t lk = (size_t)(lane < m ? lane : 0) * ld;
         while (mask) {  // up to four rows per round: loads first, adds in order
           int ii[4];
           int c = 0;
@@ -491,7 +475,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
           }
           double bv[4];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) bv[t] = P.b0r[(size_t)ii[t] * m + lk];
+          for (int t = 0; t < 4; ++t) bv[t] = P.b0[lk + ii[t]];
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             if (t < c) rk += rld(u, ii[t]) * bv[t];
@@ -501,17 +485,19 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       wave_sync();
       PSTAMP(3);
 
-      // ---- pivot row and Harris pass 1 (pass-2 ratio cached in t2) ----
+      // ---- pivot row and Harris pass 1 (pass-2 ratio kept per slot) ----
+      double al[S], t2[S];
       double tmax = INFINITY;
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int j = s * 64 + lane;
         double a = 0.0, tt = INFINITY;
-        if (st[s] != ST_BASIC && blo[s] != bhi[s]) {
+        const int st = sa[s] & 3;
+        if (st != ST_BASIC && !(sa[s] & kFixed)) {
           a = j >= n ? -rho[j - n] : P.col_dot(rho, j);
           const double at = sigma * a, dj = d[s], fat = fabs(at);
-          const bool lb = st[s] == ST_LB && at > kPivTol, ub = st[s] == ST_UB && at < -kPivTol,
-                     fr = st[s] == ST_FREE && fat > kPivTol;
+          const bool lb = st == ST_LB && at > kPivTol, ub = st == ST_UB && at < -kPivTol,
+                     fr = st == ST_FREE && fat > kPivTol;
           const double n2 = lb ? fmax(dj, 0.0) : ub ? fmin(dj, 0.0) : 0.0;
           const double n1 = lb ? n2 + kDTol : ub ? n2 - kDTol : kDTol;
           const double den = fr ? fat : at;
@@ -530,7 +516,8 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       if (tmax == INFINITY) {  // dual unbounded
         bool boxed = false;
 #pragma unroll
-        for (int s = 0; s < S; ++s) boxed |= st[s] != ST_BASIC && art[s] != 0;
+        for (int s = 0; s < S; ++s)
+          boxed |= (sa[s] & 3) != ST_BASIC && (sa[s] & (kArtLo | kArtHi)) != 0;
         if (!__any(boxed) || art_bound >= 1e13) {
           status = 2;
           break;
@@ -538,12 +525,14 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
         art_bound *= 1e3;
         grow(art_bound);
         zB = primals();
+        PSTAMP(1);
         fresh = true;
         continue;
       }
-      // ---- Harris pass 2: largest |alpha| among ratios <= tmax ----
-      double qa = 0.0;
-      int q = INT_MAX;
+      // ---- Harris pass 2: largest |alpha| among ratios <= tmax; the owner
+      // lane keeps its candidate's reduced cost, alpha and status bits ----
+      double qa = 0.0, cd = 0.0, cal = 0.0;
+      int q = INT_MAX, csa = 0;
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if (t2[s] <= tmax) {
@@ -551,6 +540,9 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
           if (fa > qa) {
             qa = fa;
             q = s * 64 + lane;
+            cd = d[s];
+            cal = al[s];
+            csa = sa[s];
           }
         }
       }
@@ -560,6 +552,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
         status = 2;
         break;
       }
+      const int ql = q & 63, qs = q >> 6;
 
       // ---- FTRAN: alpha_q = E...E B0^{-1} a_q ----
       double alq = 0.0;
@@ -567,9 +560,9 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
         const int li = lane < m ? lane : 0;
         if (q < n) {
           for (int t = P.colptr[q]; t < P.colptr[q + 1]; ++t)
-            alq += P.b0c[(size_t)P.rowidx[t] * m + li] * P.cval[t];
+            alq += P.b0[(size_t)P.rowidx[t] * ld + li] * P.cval[t];
         } else {
-          alq = -P.b0c[(size_t)(q - n) * m + li];
+          alq = -P.b0[(size_t)(q - n) * ld + li];
         }
         if (lane >= m) alq = 0.0;
       }
@@ -578,29 +571,39 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       PSTAMP(6);
 
       // ---- steps ----
-      double theta_d = colget(d, q) / colget(al, q);
+      double theta_d = rld(cd, ql) / rld(cal, ql);
       if (sigma * theta_d < 0) theta_d = 0.0;
       const double theta_p = delta / arq;
       const int pl = rl(h, r);
+      const int pls = pl >> 6, pll = pl & 63;
 #pragma unroll
       for (int s = 0; s < S; ++s)
-        if (st[s] != ST_BASIC) d[s] -= theta_d * al[s];
-      const double zq = colget(z, q) + theta_p;
-      const int art_q = colget(art, q);
-      double bloq = colget(blo, q), bhiq = colget(bhi, q);
-      const double bound_p = delta < 0 ? colget(blo, pl) : colget(bhi, pl);
-      colset(d, q, 0.0, lane);
-      colset(d, pl, -theta_d, lane);
-      colset(st, pl, delta < 0 ? (int)ST_LB : (int)ST_UB, lane);
-      colset(z, pl, bound_p, lane);
-      colset(st, q, (int)ST_BASIC, lane);
-      colset(z, q, zq, lane);
+        if ((sa[s] & 3) != ST_BASIC) d[s] -= theta_d * al[s];
+      const double zq = zc[q] + theta_p;
+      const bool art_q = (rl(csa, ql) & (kArtLo | kArtHi)) != 0;
+      double bloq = lo[q], bhiq = hi[q];
+      const double bound_p = delta < 0 ? lo[pl] : hi[pl];
+      wave_sync();
       if (art_q) {  // basic columns keep their true (infinite) bounds
         bloq = P.tlo(q);
         bhiq = P.thi(q);
-        colset(blo, q, bloq, lane);
-        colset(bhi, q, bhiq, lane);
-        colset(art, q, 0, lane);
+      }
+      if (lane == 0) {
+        zc[q] = 0.0;        // basic now (its value is zB of row r)
+        zc[pl] = bound_p;   // leaving column to its violated bound
+        lo[q] = bloq;
+        hi[q] = bhiq;
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s == qs && lane == ql) {
+          d[s] = 0.0;
+          sa[s] = ST_BASIC | (bloq == bhiq ? kFixed : 0);
+        }
+        if (s == pls && lane == pll) {
+          d[s] = -theta_d;
+          sa[s] = (delta < 0 ? ST_LB : ST_UB) | (sa[s] & kFixed);
+        }
       }
       if (lane < m) zB -= theta_p * alq;
       if (lane == r) {
@@ -627,21 +630,15 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       continue;
     }
     if (status == 0 || status == 6) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int j = s * 64 + lane;
-        if (j < N) zbuf[j] = z[s];
-      }
       wave_sync();
-      if (lane < m) zbuf[h] = zB;
+      if (lane < m) zc[h] = zB;
       wave_sync();
       double sum = 0.0;
-      for (int j = lane; j < n; j += 64) sum += P.cj(j) * zbuf[j];
+      for (int j = lane; j < n; j += 64) sum += P.cj(j) * zc[j];
       sum = wave_sum(sum);
       if (lane == 0) io.obj[b] = P.ocol < 0 ? sum + lp.objoff : sum;
       if (io.x != nullptr)
-        for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = zbuf[j];
-      wave_sync();
+        for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = zc[j];
     } else if (lane == 0) {
       io.obj[b] = status == 2 ? INFINITY : -INFINITY;
     }
@@ -649,6 +646,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       io.status[b] = status;
       io.iters[b] = iters;
     }
+    wave_sync();
     PSTAMP(8);
   }
   PSTAMP_FLUSH
