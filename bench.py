@@ -31,6 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+PFI_CAP = 24                # MGPU_LP_PFI_MAX: K3P's eta-file cap (default)
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 dense (vector = matrix rate), spec
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec
 
@@ -56,7 +57,8 @@ def pmc_traffic(kernel, batch):
     (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3
     FETCH_SIZE/WRITE_SIZE passes of this same bench at the same batch)."""
     import glob
-    key = {'fbbt': 'fbbt_linear_kernel', 'lp_dual': 'lp_dual_kernel'}[kernel]
+    key = {'fbbt': 'fbbt_linear_kernel', 'lp_dual': 'lp_dual_kernel',
+           'lp_pfi': 'lp_pfi_kernel'}[kernel]
     for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')), reverse=True):
         try:
             d = json.load(open(f))
@@ -368,15 +370,23 @@ def main():
         best = mdist.allreduce_incumbent(cand.min().reshape(1))
         acc["solved"] += (status != 12).sum()
         acc["pivots"] += iters.sum()
+        # LPs finished by K3P itself (the rest went to its dense overflow re-solve)
+        mine = (status != 12) & (iters <= PFI_CAP)
+        acc["pfi_solved"] += mine.sum()
+        acc["pfi_pivots"] += torch.where(mine, iters, 0).sum()
         b = float(best.item())          # one host sync per step
         state["incumbent"] = min(inc, b)
         acc["fbbt_ms"].append(ctx.last_kernel_ms('fbbt'))
         acc["lp_ms"].append(ctx.last_kernel_ms('lp'))
+        acc["lp_main_ms"].append(ctx.last_kernel_ms('lp_main'))
+        acc["lp_tail_ms"].append(ctx.last_kernel_ms('lp_tail'))
 
     def new_acc():
         return {"solved": torch.zeros((), dtype=torch.int64, device=dev),
                 "pivots": torch.zeros((), dtype=torch.int64, device=dev),
-                "fbbt_ms": [], "lp_ms": []}
+                "pfi_solved": torch.zeros((), dtype=torch.int64, device=dev),
+                "pfi_pivots": torch.zeros((), dtype=torch.int64, device=dev),
+                "fbbt_ms": [], "lp_ms": [], "lp_main_ms": [], "lp_tail_ms": []}
 
     # warm-up runs the exact timed step (also loads torch's lazily-loaded
     # reduction kernels, which otherwise land in the first timed step)
@@ -394,11 +404,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tot = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    cnt = torch.stack([acc["solved"].double(), acc["pivots"].double()])
+    cnt = torch.stack([acc["solved"].double(), acc["pivots"].double(),
+                       acc["pfi_solved"].double(), acc["pfi_pivots"].double()])
     mdist.allreduce_max(tot)
     mdist.allreduce_sum(cnt)
     elapsed = float(tot.item())
-    solved, pivots = (float(v) for v in cnt.tolist())
+    solved, pivots, pfi_solved, pfi_pivots = (float(v) for v in cnt.tolist())
     tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, B, args)
     cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, B, args)
     qprel = None if args.no_qp else qp_relaxation(ctx, dev, rank, world, args)
@@ -406,24 +417,34 @@ def main():
     nodes = float(B) * world * args.steps
     fbbt_ms = float(np.mean(acc["fbbt_ms"]))
     lp_ms = float(np.mean(acc["lp_ms"]))
+    lp_main_ms = float(np.mean(acc["lp_main_ms"]))
+    lp_tail_ms = float(np.mean(acc["lp_tail_ms"]))
+    lp_kernel = "lp_pfi" if lp_tail_ms > 0.0 else "lp_dual"
 
     if rank == 0:
         # per-launch algorithmic work of rank 0's kernels
         solved_r0 = solved / world / args.steps
         pivots_r0 = pivots / world / args.steps
         fb = fbbt_bytes(p, B)
-        lpf = lp_flops(p, pivots_r0, solved_r0)
+        if lp_kernel == "lp_pfi":   # K3P's own LPs; its overflow list goes to K3 (tail)
+            lp_solves, lp_pivots = pfi_solved / world / args.steps, pfi_pivots / world / args.steps
+        else:
+            lp_solves, lp_pivots = solved_r0, pivots_r0
+        lpf = lp_flops(p, lp_pivots, lp_solves)
         kernels = {
             "fbbt": {"ms": fbbt_ms, "bound": "hbm", "achieved": fb / (fbbt_ms * 1e-3) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "bytes_per_launch": fb},
-            "lp_dual": {"ms": lp_ms, "bound": "fp64", "unit": "TFLOP/s",
-                        "achieved": lpf / (lp_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
-                        "flops_per_launch": lpf, "pivots_per_solve": pivots_r0 / max(solved_r0, 1)},
+            lp_kernel: {"ms": lp_main_ms, "bound": "fp64", "unit": "TFLOP/s",
+                        "achieved": lpf / (lp_main_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                        "flops_per_launch": lpf, "solves_per_launch": lp_solves,
+                        "pivots_per_solve": lp_pivots / max(lp_solves, 1),
+                        "lp_call_ms": lp_ms, "overflow_resolve_ms": lp_tail_ms,
+                        "overflow_lps_per_launch": solved_r0 - lp_solves},
         }
         for k in kernels.values():
             k["frac"] = k["achieved"] / k["peak"]
-        dom = "lp_dual" if lp_ms >= fbbt_ms else "fbbt"
+        dom = lp_kernel if lp_main_ms >= fbbt_ms else "fbbt"
         kd = kernels[dom]
         traffic, tsrc = pmc_traffic(dom, B)
         roofline = {"kernel": dom, "bound": "hbm" if dom == "fbbt" else "mfma",
@@ -431,9 +452,10 @@ def main():
                     "frac": kd["frac"], "traffic": traffic}
         if tsrc:
             roofline["traffic_source"] = f"profiles/{tsrc} (PMC, bytes per launch)"
-        if dom == "lp_dual":
-            roofline["note"] = ("FP64 VALU kernel (no MFMA: per-node rank-1 updates); peak = "
-                                "MI355X FP64 dense rate 78.6 TF/s")
+        if dom != "fbbt":
+            roofline["note"] = ("FP64 VALU kernel (no MFMA: per-node pivots); achieved = the "
+                                "dual simplex's algorithmic flops (DESIGN.md §5) / kernel time; "
+                                "peak = MI355X FP64 dense rate 78.6 TF/s")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(p, LB, UB, args.cpu_seconds)

@@ -120,8 +120,11 @@ int mgpu_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in,
  *                 +INF for infeasible nodes.
  *   x           : [batch][n] primal solution, or NULL.
  *   wo_*        : [batch] warm starts out (children's warm start), or NULL.
- * Kernels: K3 (basis-inverse rows one per lane, m <= 64) or, for more rows,
- * K3L (one node per workgroup, B^-1 in HBM; n + m up to ~3000). */
+ * Kernels: K3P when the batch shares one warm start and wants none back
+ * (product form against the shared inverse, m <= 64, n + m <= 256; an LP
+ * needing more than the eta-file cap is re-solved by K3), else K3
+ * (basis-inverse rows one per lane, m <= 64) or, for more rows, K3L (one
+ * node per workgroup, B^-1 in HBM; n + m up to ~3000). */
 int mgpu_lp_solve(mgpu_ctx *ctx, int batch, const double *lb, const double *ub,
                   const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,
                   const double *ws_d, const double *ws_binv, int ws_shared,
@@ -311,7 +314,10 @@ int mgpu_quad_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in, const do
                        int32_t *d_mod_idx, double *d_mod_v1, double *d_mod_v2);
 
 /* Device-side timing of the last launch of the named kernel family
- * ("fbbt", "lp", "quad", "qp"), measured with hipEvents on the context stream. */
+ * ("fbbt", "lp", "quad", "qp"), measured with hipEvents on the context stream.
+ * "lp" is the whole LP call; "lp_main" its first kernel (K3P, or the only
+ * one) and "lp_tail" the dense K3 re-solve of K3P's overflow list (0 when
+ * K3P did not run). */
 double mgpu_last_kernel_ms(mgpu_ctx *ctx, const char *which);
 
 #ifdef __cplusplus

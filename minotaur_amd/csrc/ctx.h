@@ -66,6 +66,8 @@ struct mgpu_ctx {
   int num_cus = 256;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr,
             ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;
+  hipEvent_t ev8 = nullptr;    // between K3P and its dense overflow re-solve
+  bool last_lp_pfi = false;    // the last LP call ran K3P
   double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0, last_qp_ms = 0.0;
   QuadState *quad = nullptr;   // K2 problem (mgpu_load_quad)
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)

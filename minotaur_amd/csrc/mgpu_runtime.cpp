@@ -36,7 +36,8 @@ int mgpu_create(int device, mgpu_ctx **out) {
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess ||
       hipEventCreate(&c->ev4) != hipSuccess || hipEventCreate(&c->ev5) != hipSuccess ||
-      hipEventCreate(&c->ev6) != hipSuccess || hipEventCreate(&c->ev7) != hipSuccess) {
+      hipEventCreate(&c->ev6) != hipSuccess || hipEventCreate(&c->ev7) != hipSuccess ||
+      hipEventCreate(&c->ev8) != hipSuccess) {
     delete c;
     return MGPU_ERR_HIP;
   }
@@ -69,6 +70,7 @@ int mgpu_destroy(mgpu_ctx *c) {
   if (c->ev5) (void)hipEventDestroy(c->ev5);
   if (c->ev6) (void)hipEventDestroy(c->ev6);
   if (c->ev7) (void)hipEventDestroy(c->ev7);
+  if (c->ev8) (void)hipEventDestroy(c->ev8);
   quad_state_free(c);
   bnb_state_free(c);
   qp_state_free(c);
@@ -257,6 +259,19 @@ double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
       c->last_lp_ms = ms;
     return c->last_lp_ms;
   }
+  // K3P alone / its dense overflow re-solve (lp = both); without K3P,
+  // lp_main = lp and lp_tail = 0
+  if (!strcmp(which, "lp_main") || !strcmp(which, "lp_tail")) {
+    float a = 0.f, t = 0.f;
+    if (hipEventSynchronize(c->ev3) != hipSuccess) return -1.0;
+    if (!c->last_lp_pfi) {
+      if (hipEventElapsedTime(&a, c->ev2, c->ev3) != hipSuccess) return -1.0;
+    } else if (hipEventElapsedTime(&a, c->ev2, c->ev8) != hipSuccess ||
+               hipEventElapsedTime(&t, c->ev8, c->ev3) != hipSuccess) {
+      return -1.0;
+    }
+    return which[3] == 'm' ? a : t;
+  }
   if (!strcmp(which, "qp")) {
     float ms = 0.f;
     if (hipEventSynchronize(c->ev7) == hipSuccess &&
@@ -416,12 +431,15 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     px.ovf_count = cnt;
     px.ovf_list = cnt + 1;
     HIPCHK(c, launch_lp_pfi(c->lp, io, px, c->num_cus, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev8, c->stream));
+    c->last_lp_pfi = true;
     LpIO io2 = io;
     io2.node_list = px.ovf_list;
     io2.node_count = px.ovf_count;
     HIPCHK(c, launch_lp_dual(c->lp, io2, c->num_cus, c->stream));
     return MGPU_OK;
   }
+  c->last_lp_pfi = false;
   if (c->lp_variant == 3)
     return fail(c, MGPU_ERR_ARG, "%s: K3P needs a shared warm start, no warm-start output, "
                 "m <= 64 and n + m <= %d", who, 64 * kPfiSlots);
