@@ -63,6 +63,7 @@ struct mgpu_ctx {
   int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)
   DevBuf lp_slots;             // K3L: one B^-1 [m][m] per resident workgroup
   DevBuf pfi_ovf;              // K3P: overflow counter + node list
+  DevBuf pfi_cont;             // K3P: continuation state of overflowing LPs
   int num_cus = 256;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr,
             ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;
@@ -96,6 +97,8 @@ int fail(mgpu_ctx *c, int code, const char *fmt, ...) {
                   "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,      \
                   __LINE__);                                                     \
   } while (0)
+
+inline size_t al16h(size_t b) { return (b + 15) & ~(size_t)15; }
 
 template <class T>
 hipError_t upload(DevBuf &b, const T *src, size_t count) {

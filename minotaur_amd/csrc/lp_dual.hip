@@ -213,8 +213,13 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // node list (K3P overflow re-solve): a workgroup with no node of it
   // leaves before staging anything (uniform over the workgroup)
-  const int nsolve = io.node_list != nullptr ? *io.node_count : io.batch;
-  if (blockIdx.x * W >= nsolve) return;
+  const int lo = io.node_list != nullptr ? io.list_lo : 0;
+  int nsolve = io.batch;
+  if (io.node_list != nullptr) {
+    nsolve = *io.node_count;
+    if (nsolve > io.list_hi) nsolve = io.list_hi;
+  }
+  if (lo + (int)blockIdx.x * W >= nsolve) return;
 
   // ---- stage the constraint matrix (CSC + CSR) once per workgroup ----
   unsigned char *p = smem;
@@ -253,8 +258,9 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   // for the workgroup; each wave then solves nodes b, b + grid*W, ...
   // (no workgroup barrier below this point).
   STAMP_DECL
-  for (int bi = blockIdx.x * W + wave; bi < nsolve; bi += gridDim.x * W) {
+  for (int bi = lo + blockIdx.x * W + wave; bi < nsolve; bi += gridDim.x * W) {
     const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
+    const int bw = io.list_ws ? bi : b;  // warm-start index
 
     // lane index made opaque per node: otherwise LICM hoists the 64
     // loop-invariant B^-1 init values / LDS addresses out of the node loop
@@ -313,10 +319,10 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     double binv[kLpMaxM];
     int h = -1;
     if (warm) {
-      const int32_t *wh = kSharedWs ? s_whead : io.ws.head + (size_t)b * io.ws.s_head;
-      const int8_t *wst = kSharedWs ? s_wst : io.ws.st + (size_t)b * io.ws.s_st;
-      const double *wd = kSharedWs ? s_wd : io.ws.d + (size_t)b * io.ws.s_d;
-      const double *wb = kSharedWs ? s_wbinv : io.ws.binv + (size_t)b * io.ws.s_binv;
+      const int32_t *wh = kSharedWs ? s_whead : io.ws.head + (size_t)bw * io.ws.s_head;
+      const int8_t *wst = kSharedWs ? s_wst : io.ws.st + (size_t)bw * io.ws.s_st;
+      const double *wd = kSharedWs ? s_wd : io.ws.d + (size_t)bw * io.ws.s_d;
+      const double *wb = kSharedWs ? s_wbinv : io.ws.binv + (size_t)bw * io.ws.s_binv;
       for (int j = lane; j < N; j += 64) {
         const int8_t s = wst[j];
         C.st[j] = s == ST_BASIC ? ST_LB : s;
@@ -624,7 +630,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     }
     if (lane == 0) {
       io.status[b] = status;
-      io.iters[b] = iters;
+      io.iters[b] = iters + io.iter_base;
     }
     STAMP(9);
   }

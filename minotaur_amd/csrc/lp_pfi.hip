@@ -626,7 +626,33 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
 
     // ---- outputs ----
     if (status == -1) {
-      if (lane == 0) px.ovf_list[atomicAdd(px.ovf_count, 1)] = b;
+      // overflow: take a list slot; within the slot capacity, hand K3 this
+      // basis with its explicit inverse (oracle: the same loops) so it
+      // continues instead of restarting
+      int slot = 0;
+      if (lane == 0) slot = atomicAdd(px.ovf_count, 1);
+      slot = rl(slot, 0);
+      if (lane == 0) px.ovf_list[slot] = b;
+      if (slot < px.ovf_cap) {
+        if (lane < m) px.c_head[(size_t)slot * m + lane] = h;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int j = s * 64 + lane;
+          if (j < N) {
+            px.c_st[(size_t)slot * N + j] = (int8_t)(sa[s] & 3);
+            px.c_d[(size_t)slot * N + j] = d[s];
+          }
+        }
+        double *cb = px.c_binv + (size_t)slot * m * m;
+        const int li = lane < m ? lane : 0;
+        for (int c = 0; c < m; ++c) {
+          double v = lane < m ? P.b0[(size_t)c * ld + li] : 0.0;
+          v = apply_etas(v, eta, prow, iters, lane);
+          if (lane < m) cb[(size_t)c * m + lane] = v;  // column-major (ABI layout)
+        }
+      }
+      wave_sync();
+      PSTAMP(8);
       continue;
     }
     if (status == 0 || status == 6) {

@@ -93,10 +93,14 @@ struct LpIO {
   int8_t *wo_st;                // [B][n+m]
   double *wo_d;                 // [B][n+m]
   double *wo_binv;              // [B][m][m]
-  // K3 only: solve just the nodes node_list[0 .. *node_count) (device
-  // memory; the overflow list of K3P), null = every node of the batch
+  // K3 only: solve just the nodes node_list[list_lo .. min(*node_count,
+  // list_hi)) (device memory; the overflow list of K3P), null = every node
+  // of the batch.  list_ws: the per-node warm start is indexed by list
+  // position (K3P's continuation slots), not by node.  iter_base is added to
+  // the reported iteration counts (the pivots K3P already made).
   const int32_t *node_list;
   const int32_t *node_count;
+  int list_lo, list_hi, list_ws, iter_base;
 };
 
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
@@ -110,7 +114,16 @@ struct PfiIO {
   int kmax;                     // eta-file cap for this launch (1..kPfiMax)
   int32_t *ovf_list;            // [B] nodes that needed more than kmax pivots
   int32_t *ovf_count;           // device counter, zeroed before the launch
+  // continuation state of overflow slot i < ovf_cap (K3 goes on from it):
+  // basis head [m], column status [n+m], reduced costs [n+m], explicit
+  // B^-1 = E...E B0^-1 [m][m] column-major
+  int ovf_cap;
+  int32_t *c_head;
+  int8_t *c_st;
+  double *c_d, *c_binv;
 };
+// continuation slots per LP call (K3P overflow beyond this restarts in K3)
+constexpr int kPfiOvfSlots = 16384;
 size_t lp_pfi_lds_bytes(int n, int m, int nnz);
 bool lp_pfi_fits(int n, int m, int nnz);
 hipError_t launch_lp_pfi(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,

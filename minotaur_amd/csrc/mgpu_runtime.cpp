@@ -422,21 +422,48 @@ bool use_pfi(const mgpu_ctx *c, const LpIO &io) {
 
 int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
   if (use_pfi(c, io)) {
-    // K3P, then the dense K3 on exactly the nodes that filled the eta file
+    // K3P, then the dense K3 on exactly the nodes that filled the eta file:
+    // it continues from K3P's basis and explicit inverse (continuation
+    // slots), or restarts from the shared warm start past the slot capacity
+    const int m = c->lp.m, N = c->lp.n + c->lp.m;
+    const int cap = io.batch < kPfiOvfSlots ? io.batch : kPfiOvfSlots;
     HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 1) * sizeof(int32_t)));
+    const size_t sb_head = al16h((size_t)cap * m * 4), sb_st = al16h((size_t)cap * N),
+                 sb_d = al16h((size_t)cap * N * 8), sb_binv = (size_t)cap * m * m * 8;
+    HIPCHK(c, c->pfi_cont.ensure(sb_head + sb_st + sb_d + sb_binv));
     int32_t *cnt = c->pfi_ovf.as<int32_t>();
     HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(int32_t), c->stream));
     PfiIO px{};
     px.kmax = c->lp_pfi > 0 ? c->lp_pfi : kPfiMax;
     px.ovf_count = cnt;
     px.ovf_list = cnt + 1;
+    px.ovf_cap = cap;
+    char *cp = c->pfi_cont.as<char>();
+    px.c_head = (int32_t *)cp;
+    px.c_st = (int8_t *)(cp + sb_head);
+    px.c_d = (double *)(cp + sb_head + sb_st);
+    px.c_binv = (double *)(cp + sb_head + sb_st + sb_d);
     HIPCHK(c, launch_lp_pfi(c->lp, io, px, c->num_cus, c->stream));
     HIPCHK(c, hipEventRecord(c->ev8, c->stream));
     c->last_lp_pfi = true;
     LpIO io2 = io;
     io2.node_list = px.ovf_list;
     io2.node_count = px.ovf_count;
+    io2.list_lo = 0;
+    io2.list_hi = cap;
+    io2.list_ws = 1;
+    io2.iter_base = px.kmax;
+    io2.iter_limit = io.iter_limit - px.kmax;  // K3P only overflows below the limit
+    io2.ws = LpWarm{px.c_head, px.c_st, px.c_d, px.c_binv, m, N, N, (long)m * m};
     HIPCHK(c, launch_lp_dual(c->lp, io2, c->num_cus, c->stream));
+    if (io.batch > cap) {  // overflow beyond the slots: restart from the shared warm start
+      LpIO io3 = io;
+      io3.node_list = px.ovf_list;
+      io3.node_count = px.ovf_count;
+      io3.list_lo = cap;
+      io3.list_hi = 0x7fffffff;
+      HIPCHK(c, launch_lp_dual(c->lp, io3, c->num_cus, c->stream));
+    }
     return MGPU_OK;
   }
   c->last_lp_pfi = false;

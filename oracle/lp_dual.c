@@ -401,7 +401,17 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       continue;
     }
     if (iters >= iter_limit) { status = 6; break; }   /* EngineIterationLimit */
-    if (W.pfi && iters >= W.pfi) { status = -1; break; }   /* eta file full */
+    if (W.pfi && iters >= W.pfi) {
+      /* eta file full: the dense solve continues from this basis with its
+       * explicit inverse E_{k-1}...E_0 B0^{-1}, column by column */
+      for (int c = 0; c < m; ++c) {
+        for (int i = 0; i < m; ++i) W.alpha_q[i] = W.binv0[(size_t) i * m + c];
+        pfi_apply_etas(&W, W.alpha_q);
+        for (int i = 0; i < m; ++i) W.binv[(size_t) i * m + c] = W.alpha_q[i];
+      }
+      status = -1;
+      break;
+    }
     /* ---- row r of B^{-1}, pivot row ---- */
     if (W.pfi) pfi_btran(&W, r, W.rho);
     else for (int k = 0; k < m; ++k) W.rho[k] = W.binv[r * m + k];
@@ -503,6 +513,12 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
     if (iters % 64 == 0) { compute_primals(&W); fresh = 1; }
   }
 done:
+  if (status == -1 && ws_head) {   /* product form: continuation state */
+    memcpy(ws_head, W.head, sizeof(int) * (size_t) m);
+    for (int j = 0; j < N; ++j) ws_st[j] = W.st[j];
+    memcpy(ws_binv, W.binv, sizeof(double) * (size_t) m * m);
+    if (ws_d) memcpy(ws_d, W.d, sizeof(double) * (size_t) N);
+  }
   /* warm start out: the maintained reduced costs (reduced costs of fixed
    * nonbasic columns are not maintained: they can never enter) */
   if (ws_head && !W.pfi && (status == 0 || status == 6)) {
@@ -540,23 +556,31 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
 }
 
 /* What the GPU runs for one LP of a batch that shares its warm start: K3P
- * (product form, at most pfi pivots), and the dense K3 from the same warm
- * start for an LP that fills the eta file.  ws_* are read-only here. */
+ * (product form, at most pfi pivots); an LP that fills the eta file is
+ * continued by the dense K3 from K3P's basis, status and reduced costs with
+ * the explicit inverse (iteration counts add up).  ws_* are read-only here. */
 static int solve_shared(const orc_lp *P, const double *lb, const double *ub, const int *ws_head,
                         const signed char *ws_st, const double *ws_binv, const double *ws_d,
                         int have_ws, int have_binv, int iter_limit, double *obj, double *x,
                         int *iters, int pfi, int *h, signed char *s, double *bi, double *dd)
 {
-  int n = P->n, m = P->m, st = -1;
-  for (int pass = pfi > 0 && have_ws && have_binv ? 0 : 1; pass < 2 && st < 0; ++pass) {
-    if (have_ws) {
-      memcpy(h, ws_head, sizeof(int) * (size_t) m);
-      memcpy(s, ws_st, (size_t) (n + m));
-      if (ws_binv) memcpy(bi, ws_binv, sizeof(double) * (size_t) m * m);
-      if (ws_d) memcpy(dd, ws_d, sizeof(double) * (size_t) (n + m));
-    }
-    st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, have_ws, have_binv, iter_limit,
-                           obj, x, 0, iters, pass == 0 ? pfi : 0);
+  int n = P->n, m = P->m, st;
+  if (have_ws) {
+    memcpy(h, ws_head, sizeof(int) * (size_t) m);
+    memcpy(s, ws_st, (size_t) (n + m));
+    if (ws_binv) memcpy(bi, ws_binv, sizeof(double) * (size_t) m * m);
+    if (ws_d) memcpy(dd, ws_d, sizeof(double) * (size_t) (n + m));
+  }
+  if (!(pfi > 0 && have_ws && have_binv))
+    return dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, have_ws, have_binv, iter_limit,
+                             obj, x, 0, iters, 0);
+  st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, 1, 1, iter_limit, obj, x, 0, iters,
+                         pfi);
+  if (st == -1) {
+    int it2 = 0;
+    st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, 1, 1, iter_limit - pfi, obj, x, 0,
+                           &it2, 0);
+    *iters = pfi + it2;
   }
   return st;
 }
