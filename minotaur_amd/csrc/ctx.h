@@ -50,7 +50,7 @@ struct mgpu_ctx {
   DevLP lp{};
   // problem storage
   DevBuf rowptr, terms, rlo, rhi, colptr, rowidx, vtype, obj, collb, colub, objd;
-  DevBuf rows, trec, orec, irec, cval, ccol, rval;
+  DevBuf rows, trec, orec, irec, ccont, cval, ccol, rval;
   // LP workspaces (host-pointer path)
   DevBuf lp_lb, lp_ub, lp_skip, lp_wh, lp_wst, lp_wd, lp_wb, lp_st, lp_obj, lp_it, lp_x,
       lp_oh, lp_ost, lp_od, lp_ob;

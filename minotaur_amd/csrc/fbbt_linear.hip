@@ -565,8 +565,9 @@ __device__ __forceinline__ void bnds_from_obj(const DevLP &lp, const TermChunk &
 // tightenInts_ in node mode (LinearHandler.cpp:415-490), over the list of
 // Binary/Integer columns in ascending order.
 template <class V>
-__device__ __forceinline__ void tighten_ints(const DevLP &lp, V &v, NodeState &s, const ModLog &log,
+__device__ __forceinline__ bool tighten_ints(const DevLP &lp, V &v, NodeState &s, const ModLog &log,
                              bool act, bool &changed) {
+  bool bad = false;  // checkBounds_ over the integer columns, after tightening
   // called with the full wave active: `act` predicates this lane's updates
   for (int c0 = 0; c0 < lp.nint; c0 += kLanes) {
     const int cnt = lp.nint - c0 < kLanes ? lp.nint - c0 : kLanes;
@@ -582,22 +583,37 @@ __device__ __forceinline__ void tighten_ints(const DevLP &lp, V &v, NodeState &s
         log.push(s, j, 0, nv);
         changed = true;
       }
+      double l2 = l, u2 = u;
+      if (act && l > -kInfty && fabs(l - floor(l + 0.5)) > kIntTol) l2 = ceil(l);
       if (act && u < kInfty && fabs(u - floor(u + 0.5)) > kIntTol) {
         const double nv = floor(u);
         v.U(j) = nv;
         v.change_bflag(t);
         log.push(s, j, 1, nv);
         changed = true;
+        u2 = nv;
       }
+      bad |= l2 > u2 + kETol;
     }
   }
+  return bad;
 }
 
-// checkBounds_ (LinearHandler.cpp:328-359); branch-free over the columns.
+// checkBounds_ (LinearHandler.cpp:328-359) after tightenInts_, fused: the
+// integer columns are checked inside tighten_ints on the bounds it just
+// wrote (no second load), the other columns here.  An OR over columns, so
+// the order does not matter.  Call with the full wave active: the column
+// list is broadcast with v_readlane.
 template <class V>
-__device__ __forceinline__ bool check_bounds(const DevLP &lp, const V &v) {
-  bool bad = false;
-  for (int j = 0; j < lp.n; ++j) bad |= v.L(j) > v.U(j) + kETol;
+__device__ __forceinline__ bool check_bounds_rest(const DevLP &lp, const V &v, bool bad) {
+  for (int c0 = 0; c0 < lp.ncont; c0 += kLanes) {
+    const int cnt = lp.ncont - c0 < kLanes ? lp.ncont - c0 : kLanes;
+    const int jl = v.lane < cnt ? lp.ccont[c0 + v.lane] : 0;
+    for (int k = 0; k < cnt; ++k) {
+      const int j = rl(jl, k);
+      bad |= v.L(j) > v.U(j) + kETol;
+    }
+  }
   return bad || lp.cons_bad != 0;
 }
 
@@ -724,8 +740,9 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
       if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
       else bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
     }
-    tighten_ints(lp, v, s, log, go, changed);
-    if (go) infeas = check_bounds(lp, v);
+    // both called with the full wave active (v_readlane broadcasts inside)
+    const bool bad = check_bounds_rest(lp, v, tighten_ints(lp, v, s, log, go, changed));
+    if (go) infeas = bad;
   }
   if (live) {
     io.infeas[b0 + lane] = infeas ? 1 : 0;

@@ -60,6 +60,8 @@ struct DevLP {
   const TermRec *orec;          // [nobj] objective terms
   const TermRec *irec;          // [nint] integer columns (tightenInts_)
   int nint;
+  const int32_t *ccont;         // [ncont] the other columns, ascending
+  int ncont;
   const double *cval;           // [nnz] CSC values (column order of colptr/rowidx)
   const int32_t *ccol;          // [nnz] CSR column indices
   const double *rval;           // [nnz] CSR values

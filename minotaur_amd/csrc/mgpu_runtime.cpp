@@ -55,7 +55,7 @@ int mgpu_destroy(mgpu_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->rowptr, &c->terms, &c->rlo, &c->rhi, &c->colptr, &c->rowidx,
                     &c->vtype, &c->obj, &c->collb, &c->colub, &c->objd, &c->rows,
-                    &c->trec, &c->orec, &c->irec, &c->cval, &c->ccol, &c->rval,
+                    &c->trec, &c->orec, &c->irec, &c->ccont, &c->cval, &c->ccol, &c->rval,
                     &c->lp_lb, &c->lp_ub, &c->lp_skip, &c->lp_wh, &c->lp_wst, &c->lp_wd,
                     &c->lp_wb, &c->lp_st, &c->lp_obj, &c->lp_it, &c->lp_x, &c->lp_oh,
                     &c->lp_ost, &c->lp_od, &c->lp_ob, &c->lp_slots, &c->io_lb_in,
@@ -169,8 +169,13 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   for (const Term &t : objt) orec.push_back(mkrec(t.a, t.j));
   for (int j = 0; j < n; ++j)
     if (vt[j] == kBinary || vt[j] == kInteger) irec.push_back(mkrec(0.0, j));
+  std::vector<int32_t> ccont;  // the other columns (checkBounds_ only)
+  for (int j = 0; j < n; ++j)
+    if (!(vt[j] == kBinary || vt[j] == kInteger)) ccont.push_back(j);
+  const int ncont = (int)ccont.size();
   if (orec.empty()) orec.push_back(TermRec{});
   if (irec.empty()) irec.push_back(TermRec{});
+  if (ccont.empty()) ccont.push_back(0);
 
   HIPCHK(c, upload(c->rowptr, rowptr, (size_t)m + 1));
   HIPCHK(c, upload(c->terms, c->h_terms.data(), (size_t)(nnz > 0 ? nnz : 1)));
@@ -188,6 +193,7 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   HIPCHK(c, upload(c->trec, trec.data(), trec.size()));
   HIPCHK(c, upload(c->orec, orec.data(), orec.size()));
   HIPCHK(c, upload(c->irec, irec.data(), irec.size()));
+  HIPCHK(c, upload(c->ccont, ccont.data(), ccont.size()));
   HIPCHK(c, upload(c->cval, cvalv.data(), cvalv.size()));
   HIPCHK(c, upload(c->ccol, nnz > 0 ? colidx : rowptr, (size_t)(nnz > 0 ? nnz : 1)));
   HIPCHK(c, upload(c->rval, nnz > 0 ? val : cvalv.data(), (size_t)(nnz > 0 ? nnz : 1)));
@@ -214,6 +220,8 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   lp.trec = c->trec.as<TermRec>();
   lp.orec = c->orec.as<TermRec>();
   lp.irec = c->irec.as<TermRec>();
+  lp.ccont = c->ccont.as<int32_t>();
+  lp.ncont = ncont;
   lp.cval = c->cval.as<double>();
   lp.ccol = c->ccol.as<int32_t>();
   lp.rval = c->rval.as<double>();

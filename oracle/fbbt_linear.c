@@ -229,6 +229,18 @@ static int lin_bnd_tighten(node_state *s, int i, int *changed)
   return 0;
 }
 
+/* Diagnostics (tools/fbbt_sweep_stats.py; single-threaded use): per sweep
+ * index, how many nodes ran it and how many rows they tightened. */
+static int g_stats_on;
+static long g_stats[2][16];
+static unsigned g_sweep;
+long *orc_fbbt_stats(int enable)
+{
+  g_stats_on = enable;
+  if (enable) memset(g_stats, 0, sizeof g_stats);
+  return &g_stats[0][0];
+}
+
 /* LinearHandler::varBndsFromCons_, LinearHandler.cpp:493-541 (node mode:
  * each flagged row is tightened once per sweep, :520-524). */
 static int bnds_from_cons(node_state *s, int *changed)
@@ -237,6 +249,7 @@ static int bnds_from_cons(node_state *s, int *changed)
     if (s->flag[i]) {
       int tch;
       s->flag[i] = 0;
+      if (g_stats_on && g_sweep < 16) g_stats[1][g_sweep]++;
       if (lin_bnd_tighten(s, i, &tch)) return 1;
       if (tch) *changed = 1;
     }
@@ -326,6 +339,8 @@ int orc_linear_fbbt_node(const orc_lin_problem *P, double *lb, double *ub,
          (iters <= min_iters || s.nintmods > 0) && !infeas) {
     s.nintmods = 0;
     changed = 0;
+    g_sweep = iters - 1;
+    if (g_stats_on && g_sweep < 16) g_stats[0][g_sweep]++;
     ++iters;
     (void) bnds_from_cons(&s, &changed);
     if (has_inc) (void) bnds_from_obj(&s, inc_ub, &changed);
