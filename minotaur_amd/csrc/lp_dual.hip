@@ -414,8 +414,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         else if (zB > ubB + kPTol) inf = zB - ubB;
       }
       double best = fabs(inf);
-      int r = best > 0.0 ? lane : INT_MAX;
-      wave_argmax_dpp(best, r);
+      const int r = wave_argmax_lane(best);  // used only when best > 0
       // keep the (wave-uniform) result in a VGPR: as an SGPR value it lets
       // LLVM re-schedule the pivot around it at +100 VGPRs
       asm volatile("" : "+v"(best));

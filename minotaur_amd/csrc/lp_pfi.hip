@@ -26,9 +26,10 @@
 //  * BTRAN visits only the nonzeros of u (a ballot mask, ascending rows) with
 //    v_readlane broadcasts; FTRAN reads the CSC column of a_q from LDS and
 //    applies the etas lane-parallel.
-//  * A node that would need more than kmax pivots stops and is appended to an
-//    overflow list; the dense K3 then re-solves exactly those nodes from the
-//    same warm start (launch_lp_dual with a node list, same stream).
+//  * A node that would need more than kmax pivots stops, is appended to an
+//    overflow list and writes its basis with the explicit inverse to a
+//    continuation slot; the dense K3 then continues exactly those nodes
+//    (launch_lp_dual with a node list, same stream, no host sync).
 //
 // Arithmetic: oracle/lp_dual.c in product-form mode (dual_simplex_impl with
 // pfi > 0: pfi_btran, ftran_col, pfi_apply_etas, compute_primals), loop for
@@ -400,8 +401,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
         else if (zB > ubB + kPTol) inf = zB - ubB;
       }
       double best = fabs(inf);
-      int r = best > 0.0 ? lane : INT_MAX;
-      wave_argmax_dpp(best, r);
+      const int r = wave_argmax_lane(best);  // used only when best > 0
       asm volatile("" : "+v"(best));
       PSTAMP(2);
       if (best == 0.0) {

@@ -100,6 +100,25 @@ __device__ __forceinline__ void wave_argmax_dpp(double &v, int &idx) {
   idx = ri;
 }
 
+__device__ __forceinline__ double wave_max_dpp(double v) {
+  v = fmax(v, dpp_f64<kDppXor1>(v));
+  v = fmax(v, dpp_f64<kDppXor2>(v));
+  v = fmax(v, dpp_f64<kDppRor4>(v));
+  v = fmax(v, dpp_f64<kDppRor8>(v));
+  return fmax(fmax(rld(v, 0), rld(v, 16)), fmax(rld(v, 32), rld(v, 48)));
+}
+
+// Arg-max where the index is the lane itself: larger value wins, equal
+// values -> lowest lane (wave_argmax_dpp(v, lane) for non-NaN v, with a
+// plain DPP max and one ballot instead of carrying the index through every
+// step).  v becomes the wave maximum.
+__device__ __forceinline__ int wave_argmax_lane(double &v) {
+  const double mx = wave_max_dpp(v);
+  const uint64_t hit = __ballot(v == mx);
+  v = mx;
+  return (int)__builtin_ctzll(hit);
+}
+
 __device__ __forceinline__ double wave_min_dpp(double v) {
   v = fmin(v, dpp_f64<kDppXor1>(v));
   v = fmin(v, dpp_f64<kDppXor2>(v));
