@@ -523,7 +523,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
           }
         }
       }
-      wave_argmax_dpp(qa, q);
+      wave_argmax_idx(qa, q);
       if (qa == 0.0) {
         status = 2;
         break;

@@ -546,7 +546,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
           }
         }
       }
-      wave_argmax_dpp(qa, q);
+      wave_argmax_idx(qa, q);
       PSTAMP(5);
       if (qa == 0.0) {
         status = 2;

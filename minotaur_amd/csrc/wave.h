@@ -119,6 +119,24 @@ __device__ __forceinline__ int wave_argmax_lane(double &v) {
   return (int)__builtin_ctzll(hit);
 }
 
+__device__ __forceinline__ int wave_min_i32_dpp(int v) {
+  v = min(v, dpp_i32<kDppXor1>(v));
+  v = min(v, dpp_i32<kDppXor2>(v));
+  v = min(v, dpp_i32<kDppRor4>(v));
+  v = min(v, dpp_i32<kDppRor8>(v));
+  return min(min(rl(v, 0), rl(v, 16)), min(rl(v, 32), rl(v, 48)));
+}
+
+// wave_argmax_dpp for a general index (e.g. a column slot*64 + lane): a DPP
+// max, then the holder's index (one ballot; an int min only on ties).
+__device__ __forceinline__ void wave_argmax_idx(double &v, int &idx) {
+  const double mx = wave_max_dpp(v);
+  const uint64_t hit = __ballot(v == mx);
+  idx = __popcll(hit) == 1 ? rl(idx, __builtin_ctzll(hit))
+                           : wave_min_i32_dpp(v == mx ? idx : INT_MAX);
+  v = mx;
+}
+
 __device__ __forceinline__ double wave_min_dpp(double v) {
   v = fmin(v, dpp_f64<kDppXor1>(v));
   v = fmin(v, dpp_f64<kDppXor2>(v));
