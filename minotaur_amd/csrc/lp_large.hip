@@ -107,7 +107,7 @@ __device__ __forceinline__ double blk_min(double v, const S<kT> &s) {
 
 template <int kT>
 __device__ __forceinline__ void blk_argmax(double &v, int &i, const S<kT> &s) {
-  wave_argmax_dpp(v, i);
+  wave_argmax_idx(v, i);
   if constexpr (kT == 64) return;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) {
