@@ -724,8 +724,13 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
           bool tch;
           v.clear(r);
           bool inf;
-          if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
+          // row-length classes: fewer masked slots (each costs a division)
+          if (nt <= 3) inf = rc_lin_bnd_tighten<3>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 5) inf = rc_lin_bnd_tighten<5>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 6) inf = rc_lin_bnd_tighten<6>(nt, pre, rlo, rhi, v, s, log, tch);
           else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 11) inf = rc_lin_bnd_tighten<11>(nt, pre, rlo, rhi, v, s, log, tch);
           else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
           else inf = lin_bnd_tighten(trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
           if (inf) {
