@@ -30,6 +30,14 @@
 namespace mgpu {
 namespace {
 
+// write-out order of the global variant (A/B switch for tools: build with
+// -DMGPU_FBBT_OUT_NODE_OUTER for the node-outer order)
+#ifdef MGPU_FBBT_OUT_NODE_OUTER
+constexpr bool kFbbtOutVarOuter = false;
+#else
+constexpr bool kFbbtOutVarOuter = true;
+#endif
+
 // ---- wave-uniform broadcast ------------------------------------------------
 __device__ __forceinline__ int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 __device__ __forceinline__ double rld(double v, int k) {
@@ -661,9 +669,21 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
     trec = s_trec;
     rows = s_rows;
   }
-  // Stage the wave's node boxes (row-major [node][var] in HBM, coalesced
-  // reads) into the [var][lane] layout.
-  for (int nd = 0; nd < nb; ++nd) {
+  // Stage the wave's node boxes (row-major [node][var] in HBM) into the
+  // [var][lane] layout.  Global variant: var-outer, each lane walks its own
+  // node's row (consecutive vars share cache lines) and every store is one
+  // coalesced 512-B scratch row.  LDS variant: node-outer, coalesced reads.
+  if constexpr (!kLds) {
+    if (lane < nb) {
+      const double *src_l = io.lb_in + (size_t)(b0 + lane) * n;
+      const double *src_u = io.ub_in + (size_t)(b0 + lane) * n;
+      for (int j = 0; j < n; ++j) {
+        v.lb[j * v.stride + lane] = src_l[j];
+        v.ub[j * v.stride + lane] = src_u[j];
+      }
+    }
+  }
+  for (int nd = 0; nd < (kLds ? nb : 0); ++nd) {
     const double *src_l = io.lb_in + (size_t)(b0 + nd) * n;
     const double *src_u = io.ub_in + (size_t)(b0 + nd) * n;
     for (int j = lane; j < n; j += kLanes) {
@@ -754,7 +774,17 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
     io.nmods[b0 + lane] = s.nmods;
   }
   __syncthreads();
-  for (int nd = 0; nd < nb; ++nd) {
+  if constexpr (!kLds) {  // var-outer: coalesced scratch reads (as the staging)
+    if (kFbbtOutVarOuter && lane < nb) {
+      double *dst_l = io.lb_out + (size_t)(b0 + lane) * n;
+      double *dst_u = io.ub_out + (size_t)(b0 + lane) * n;
+      for (int j = 0; j < n; ++j) {
+        dst_l[j] = v.lb[j * v.stride + lane];
+        dst_u[j] = v.ub[j * v.stride + lane];
+      }
+    }
+  }
+  for (int nd = 0; nd < (kLds || !kFbbtOutVarOuter ? nb : 0); ++nd) {
     double *dst_l = io.lb_out + (size_t)(b0 + nd) * n;
     double *dst_u = io.ub_out + (size_t)(b0 + nd) * n;
     for (int j = lane; j < n; j += kLanes) {
