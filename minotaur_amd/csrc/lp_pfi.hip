@@ -451,11 +451,12 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       for (int t = kPfiMax - 1; t >= 0; --t) {
         if (t < iters) {
           uint64_t mask = __ballot(u != 0.0);
+          const double pr = u * eta[t];  // the oracle's products, lane-parallel
           double acc = 0.0;
           while (mask) {
             const int i = __builtin_ctzll(mask);
             mask &= mask - 1;
-            acc += rld(u, i) * rld(eta[t], i);
+            acc += rld(pr, i);
           }
           if (lane == rl(prow, t)) u = acc;
         }
@@ -558,9 +559,22 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
       double alq = 0.0;
       {
         const int li = lane < m ? lane : 0;
-        if (q < n) {
-          for (int t = P.colptr[q]; t < P.colptr[q + 1]; ++t)
-            alq += P.b0[(size_t)P.rowidx[t] * ld + li] * P.cval[t];
+        if (q < n) {  // four entries' loads in flight, adds in CSC order
+          int t = P.colptr[q];
+          const int e = P.colptr[q + 1];
+          for (; t + 4 <= e; t += 4) {
+            const int r0 = P.rowidx[t], r1 = P.rowidx[t + 1], r2 = P.rowidx[t + 2],
+                      r3 = P.rowidx[t + 3];
+            const double c0 = P.cval[t], c1 = P.cval[t + 1], c2 = P.cval[t + 2],
+                         c3 = P.cval[t + 3];
+            const double b0 = P.b0[(size_t)r0 * ld + li], b1 = P.b0[(size_t)r1 * ld + li];
+            const double b2 = P.b0[(size_t)r2 * ld + li], b3 = P.b0[(size_t)r3 * ld + li];
+            alq += b0 * c0;
+            alq += b1 * c1;
+            alq += b2 * c2;
+            alq += b3 * c3;
+          }
+          for (; t < e; ++t) alq += P.b0[(size_t)P.rowidx[t] * ld + li] * P.cval[t];
         } else {
           alq = -P.b0[(size_t)(q - n) * ld + li];
         }
