@@ -99,7 +99,9 @@ __device__ __forceinline__ void for_terms(const TermRec *base, int nt, const Ter
 }
 
 // ---- per-lane node view ----------------------------------------------------
-template <bool kBitFlags>
+// kIL (global variant): lb and ub interleaved, [var][lane][2], so a term's
+// two bounds are one 16-B load per lane (one 1-KB wave access)
+template <bool kBitFlags, bool kIL>
 struct NodeView {
   double *lb;
   double *ub;
@@ -108,8 +110,14 @@ struct NodeView {
   int stride;        // elements between consecutive variables (same lane)
   int lane;
   const int32_t *rowidx;
-  __device__ __forceinline__ double &L(int j) const { return lb[j * stride + lane]; }
-  __device__ __forceinline__ double &U(int j) const { return ub[j * stride + lane]; }
+  __device__ __forceinline__ double &L(int j) const {
+    if constexpr (kIL) return lb[((size_t)j * kLanes + lane) * 2];
+    else return lb[j * stride + lane];
+  }
+  __device__ __forceinline__ double &U(int j) const {
+    if constexpr (kIL) return lb[((size_t)j * kLanes + lane) * 2 + 1];
+    else return ub[j * stride + lane];
+  }
   __device__ __forceinline__ bool flagged(int r) const {
     if constexpr (kBitFlags) return (bits >> r) & 1ull;
     else return flag[r * kLanes + lane] != 0;
@@ -633,7 +641,7 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   const int nb = min(io.npw, io.batch - b0);
   const int n = lp.n, m = lp.m;
 
-  NodeView<kBitFlags> v;
+  NodeView<kBitFlags, !kLds> v;
   v.lane = lane;
   v.rowidx = lp.rowidx;
   v.bits = 0ull;
@@ -678,8 +686,8 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
       const double *src_l = io.lb_in + (size_t)(b0 + lane) * n;
       const double *src_u = io.ub_in + (size_t)(b0 + lane) * n;
       for (int j = 0; j < n; ++j) {
-        v.lb[j * v.stride + lane] = src_l[j];
-        v.ub[j * v.stride + lane] = src_u[j];
+        v.L(j) = src_l[j];
+        v.U(j) = src_u[j];
       }
     }
   }
@@ -779,8 +787,8 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
       double *dst_l = io.lb_out + (size_t)(b0 + lane) * n;
       double *dst_u = io.ub_out + (size_t)(b0 + lane) * n;
       for (int j = 0; j < n; ++j) {
-        dst_l[j] = v.lb[j * v.stride + lane];
-        dst_u[j] = v.ub[j * v.stride + lane];
+        dst_l[j] = v.L(j);
+        dst_u[j] = v.U(j);
       }
     }
   }
