@@ -206,7 +206,14 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, 
 
   // persistent waves over nodes (no workgroup barrier below this point)
   PSTAMP_DECL
-  for (int b = blockIdx.x * kWaves + wave; b < io.batch; b += gridDim.x * kWaves) {
+  // Nodes are taken from a device counter: a wave that finishes early takes
+  // the next node, so the kernel ends with the last node, not with the wave
+  // that drew the longest static share (pivot counts range 0..24+).
+  for (;;) {
+    int b = 0;
+    if (lane0 == 0) b = atomicAdd(px.next, 1);
+    b = __builtin_amdgcn_readfirstlane(b);
+    if (b >= io.batch) break;
     int lane = lane0;
     asm volatile("" : "+v"(lane));
     P.nlb = io.lb + (size_t)b * io.box_stride;

@@ -116,6 +116,7 @@ struct PfiIO {
   int kmax;                     // eta-file cap for this launch (1..kPfiMax)
   int32_t *ovf_list;            // [B] nodes that needed more than kmax pivots
   int32_t *ovf_count;           // device counter, zeroed before the launch
+  int32_t *next;                // device node counter (dynamic schedule), zeroed
   // continuation state of overflow slot i < ovf_cap (K3 goes on from it):
   // basis head [m], column status [n+m], reduced costs [n+m], explicit
   // B^-1 = E...E B0^-1 [m][m] column-major

@@ -435,16 +435,17 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     // slots), or restarts from the shared warm start past the slot capacity
     const int m = c->lp.m, N = c->lp.n + c->lp.m;
     const int cap = io.batch < kPfiOvfSlots ? io.batch : kPfiOvfSlots;
-    HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 1) * sizeof(int32_t)));
+    HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 2) * sizeof(int32_t)));
     const size_t sb_head = al16h((size_t)cap * m * 4), sb_st = al16h((size_t)cap * N),
                  sb_d = al16h((size_t)cap * N * 8), sb_binv = (size_t)cap * m * m * 8;
     HIPCHK(c, c->pfi_cont.ensure(sb_head + sb_st + sb_d + sb_binv));
-    int32_t *cnt = c->pfi_ovf.as<int32_t>();
-    HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(int32_t), c->stream));
+    int32_t *cnt = c->pfi_ovf.as<int32_t>();  // [0] overflow count, [1] next node
+    HIPCHK(c, hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), c->stream));
     PfiIO px{};
     px.kmax = c->lp_pfi > 0 ? c->lp_pfi : kPfiMax;
     px.ovf_count = cnt;
-    px.ovf_list = cnt + 1;
+    px.next = cnt + 1;
+    px.ovf_list = cnt + 2;
     px.ovf_cap = cap;
     char *cp = c->pfi_cont.as<char>();
     px.c_head = (int32_t *)cp;
