@@ -62,6 +62,7 @@ struct mgpu_ctx {
   int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L, 3 K3P
   int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)
   DevBuf lp_slots;             // K3L: one B^-1 [m][m] per resident workgroup
+  DevBuf lp_next;              // K3L: node counter of the dynamic schedule
   DevBuf pfi_ovf;              // K3P: overflow counter + node list
   DevBuf pfi_cont;             // K3P: continuation state of overflowing LPs
   int num_cus = 256;

@@ -248,8 +248,17 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
   s.n = n; s.m = m; s.N = N;
   const size_t mm = (size_t)m * m;
 
-  for (int b = blockIdx.x; b < io.batch; b += gridDim.x) {
+  // nodes from a device counter when the host gives one (dynamic schedule:
+  // a workgroup that finishes early takes the next node), else a static stride
+  __shared__ int s_next;
+  for (int b = blockIdx.x;; b += gridDim.x) {
     __syncthreads();  // the previous node's LDS state is dead
+    if (io.next != nullptr) {
+      if (tid == 0) s_next = atomicAdd(io.next, 1);
+      __syncthreads();
+      b = s_next;
+    }
+    if (b >= io.batch) break;
     s.nlb = io.lb + (size_t)b * io.box_stride;
     s.nub = io.ub + (size_t)b * io.box_stride;
     s.ocol = io.obj_col != nullptr ? io.obj_col[b] : -1;
@@ -586,10 +595,10 @@ hipError_t lp_large_prepare() {
   static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted in
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void *)lp_large_kernel<64>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLargeLdsMax);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void *)lp_large_kernel<256>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLargeLdsMax);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -600,7 +609,7 @@ hipError_t launch_lp_large(const DevLP &lp, const LpIO &io, double *binv_slots, 
                            hipStream_t stream) {
   if (io.batch <= 0) return hipSuccess;
   const size_t lds = large_lds_bytes(lp.n, lp.m);
-  if (lds > 160 * 1024 || grid <= 0 || binv_slots == nullptr) return hipErrorInvalidValue;
+  if (lds > (size_t)kLargeLdsMax || grid <= 0 || binv_slots == nullptr) return hipErrorInvalidValue;
   if (lp_large_threads(lp.m) == 64)
     hipLaunchKernelGGL(lp_large_kernel<64>, dim3(grid), dim3(64), lds, stream, lp, io,
                        binv_slots);

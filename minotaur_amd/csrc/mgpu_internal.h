@@ -103,6 +103,7 @@ struct LpIO {
   const int32_t *node_list;
   const int32_t *node_count;
   int list_lo, list_hi, list_ws, iter_base;
+  int32_t *next;                // K3L: zeroed device node counter (dynamic schedule) or null
 };
 
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
@@ -156,6 +157,7 @@ size_t lp_lds_bytes(int n, int m, int nnz);
 hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, int num_cus, hipStream_t stream);
 // K3L (lp_large.hip): one node per 256-thread workgroup, B^-1 in HBM slots
 size_t lp_large_lds_bytes(int n, int m);
+constexpr int kLargeLdsMax = 160 * 1024 - 64;  // dynamic LDS cap (K3L has a static word too)
 int lp_large_grid(int batch, int n, int m, int num_cus);
 hipError_t lp_large_prepare();
 hipError_t launch_lp_large(const DevLP &lp, const LpIO &io, double *binv_slots, int grid,

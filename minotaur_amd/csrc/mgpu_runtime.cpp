@@ -485,14 +485,18 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
     return MGPU_OK;
   }
-  if (lp_large_lds_bytes(c->lp.n, c->lp.m) > 160 * 1024)
+  if (lp_large_lds_bytes(c->lp.n, c->lp.m) > (size_t)kLargeLdsMax)
     return fail(c, MGPU_ERR_ARG, "%s: n+m=%d too large for K3L's LDS state", who,
                 c->lp.n + c->lp.m);
   const int grid = lp_large_grid(io.batch, c->lp.n, c->lp.m, c->num_cus);
   HIPCHK(c, c->lp_slots.ensure((size_t)grid * c->lp.m * c->lp.m * sizeof(double) + 8));
+  HIPCHK(c, c->lp_next.ensure(sizeof(int32_t)));
+  HIPCHK(c, hipMemsetAsync(c->lp_next.p, 0, sizeof(int32_t), c->stream));
+  LpIO iod = io;
+  iod.next = c->lp_next.as<int32_t>();
   HIPCHK(c, lp_large_prepare());
   (void)hipGetLastError();  // clear a stale error so the launch check is its own
-  HIPCHK(c, launch_lp_large(c->lp, io, c->lp_slots.as<double>(), grid, c->stream));
+  HIPCHK(c, launch_lp_large(c->lp, iod, c->lp_slots.as<double>(), grid, c->stream));
   return MGPU_OK;
 }
 }  // namespace
