@@ -31,7 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PFI_CAP = 24                # MGPU_LP_PFI_MAX: K3P's eta-file cap (default)
+PFI_CAP = 16                # MGPU_LP_PFI_MAX: K3P's eta-file cap (default)
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 dense (vector = matrix rate), spec
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec
 

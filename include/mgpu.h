@@ -169,7 +169,7 @@ int mgpu_set_lp_variant(mgpu_ctx *ctx, int variant);
 /* K3P eta-file cap: a node that needs more pivots is re-solved by K3 from
  * the same warm start.  0 keeps auto mode off K3P; 1..MGPU_LP_PFI_MAX
  * (default MGPU_LP_PFI_MAX). */
-#define MGPU_LP_PFI_MAX 24
+#define MGPU_LP_PFI_MAX 16
 int mgpu_set_lp_pfi(mgpu_ctx *ctx, int kmax);
 
 /* Batched bound LPs: LP b minimises obj_sign[b] * x[obj_col[b]] over the

@@ -69,7 +69,13 @@ constexpr double kPivTol = 1e-9;
 constexpr double kArt0 = 1e7;
 constexpr double kInfB = 1e30;
 constexpr int kUnknownStatus = 12;
-constexpr int kWaves = 12;  // one 768-thread workgroup per CU: 3 waves per SIMD (<= 168 VGPRs)
+// waves per workgroup (one workgroup per CU): 16 = 4 per SIMD (<= 128 VGPRs)
+// up to 3 column slots; the 4-slot build keeps 12 (3 per SIMD) rather than
+// spilling.  A/B on tls4-lin (S = 3): 12 waves with a 24-eta file 2.12 ms,
+// 16 waves with a 16-eta file 1.75 ms + a longer overflow tail (0.16 ms).
+template <int S>
+constexpr int waves_for() { return S <= 3 ? 16 : 12; }
+__host__ __device__ inline int slots_for(int N) { return (N + 63) / 64; }
 
 // packed column status: bits 0-1 status, 2-3 artificial-bound flags, 4 fixed
 enum : int { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
@@ -153,7 +159,8 @@ __device__ __forceinline__ double apply_etas(double v, const double (&eta)[kPfiM
 }
 
 template <int S>
-__global__ __launch_bounds__(64 * kWaves) void lp_pfi_kernel(DevLP lp, LpIO io, PfiIO px) {
+__global__ __launch_bounds__(64 * waves_for<S>()) void lp_pfi_kernel(DevLP lp, LpIO io, PfiIO px) {
+  constexpr int kWaves = waves_for<S>();
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz, ld = m + 1;
   const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -709,6 +716,7 @@ hipError_t launch_s(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cu
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  constexpr int kWaves = waves_for<S>();
   const size_t lds = lp_pfi_lds_bytes(lp.n, lp.m, lp.nnz);
   const int want = (io.batch + kWaves - 1) / kWaves;
   const int blocks = want < num_cus ? want : num_cus;
@@ -733,7 +741,8 @@ extern "C" int mgpu_debug_pfi_stamps(unsigned long long *out, int reset) {
 #endif
 
 size_t lp_pfi_lds_bytes(int n, int m, int nnz) {
-  return pfi_shared_bytes(n, m, nnz) + (size_t)kWaves * pfi_wave_bytes(n + m);
+  const int waves = slots_for(n + m) <= 3 ? waves_for<3>() : waves_for<4>();
+  return pfi_shared_bytes(n, m, nnz) + (size_t)waves * pfi_wave_bytes(n + m);
 }
 
 bool lp_pfi_fits(int n, int m, int nnz) {

@@ -111,7 +111,7 @@ constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
 
 // K3P (lp_pfi.hip): product-form dual simplex for a batch that shares its
 // warm start.  At most kPfiMax eta columns per node, n + m <= 64*kPfiSlots.
-constexpr int kPfiMax = 24;
+constexpr int kPfiMax = 16;
 constexpr int kPfiSlots = 4;
 struct PfiIO {
   int kmax;                     // eta-file cap for this launch (1..kPfiMax)

@@ -19,7 +19,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _D = ctypes.c_double
 
-LP_PFI_MAX = 24  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
+LP_PFI_MAX = 16  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
 
 # Every entry point declared in include/mgpu.h (checked by the CPU tests).
 EXPORTS = [

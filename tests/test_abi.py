@@ -58,3 +58,10 @@ def test_ctypes_signatures_match_header():
     lib = runtime.load_library()
     for name, nargs in _header_arity().items():
         assert len(getattr(lib, name).argtypes) == nargs, name
+
+
+def test_pfi_cap_matches_header():
+    """runtime.LP_PFI_MAX (used by tests and bench.py) is the header's cap."""
+    hdr = open(os.path.join(ROOT, 'include', 'mgpu.h')).read()
+    m = re.search(r'#define MGPU_LP_PFI_MAX (\d+)', hdr)
+    assert m and int(m.group(1)) == runtime.LP_PFI_MAX

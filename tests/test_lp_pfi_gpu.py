@@ -20,6 +20,7 @@ import pytest
 import oracle
 from golden_io import assert_lp_matches, load_lp
 from minotaur_amd.problem import LinProblem, random_boxes, random_mkp, random_problem
+from minotaur_amd.runtime import LP_PFI_MAX as KCAP
 
 pytestmark = pytest.mark.gpu
 
@@ -38,7 +39,7 @@ class k3p:
     """LP calls inside run on K3P (variant 3: K3P or a loud error) with an
     eta-file cap of kmax; auto mode and the default cap afterwards."""
 
-    def __init__(self, ctx, kmax=24):
+    def __init__(self, ctx, kmax=KCAP):
         self.ctx, self.kmax = ctx, kmax
 
     def __enter__(self):
@@ -47,7 +48,7 @@ class k3p:
 
     def __exit__(self, *a):
         self.ctx.set_lp_variant(0)
-        self.ctx.set_lp_pfi(24)
+        self.ctx.set_lp_pfi(KCAP)
 
 
 def _tls4():
@@ -87,9 +88,9 @@ def _check(ctx, p, LB, UB, kmax, iter_limit=0, want_x=False):
     return r, its
 
 
-@pytest.mark.parametrize('kmax', [24, 8, 3])
+@pytest.mark.parametrize('kmax', [KCAP, 8, 3])
 def test_k3p_bench_boxes_vs_oracle(ctx, kmax):
-    """The bench's node boxes; kmax < 24 sends many LPs through the overflow
+    """The bench's node boxes; a small kmax sends many LPs through the overflow
     list to the dense K3 (the oracle runs the same two-stage solve)."""
     p = _tls4()
     ctx.load(p)
@@ -97,7 +98,7 @@ def test_k3p_bench_boxes_vs_oracle(ctx, kmax):
     f = oracle.linear_fbbt(p, LB, UB, None)
     keep = f.infeas == 0
     r, its = _check(ctx, p, f.lb[keep], f.ub[keep], kmax)
-    if kmax < 24:
+    if kmax <= 8:
         assert (its > kmax).any()   # the overflow path ran
     # north-star bar against HiGHS on a sample
     for b in np.nonzero(r.status == 0)[0][:40]:
@@ -115,7 +116,7 @@ def test_k3p_golden_warm_from_root(ctx, name):
     with k3p(ctx):
         r = ctx.lp_solve(g['lb'], g['ub'], ws)
     assert_lp_matches(r.status, r.obj, g)
-    st, obj, its, _ = oracle.dual_simplex(p, g['lb'], g['ub'], ows, pfi=24)
+    st, obj, its, _ = oracle.dual_simplex(p, g['lb'], g['ub'], ows, pfi=KCAP)
     assert np.array_equal(r.status, st) and np.array_equal(r.iters, its)
     assert _close(r.obj, obj)
 
@@ -124,8 +125,8 @@ def test_k3p_primal_vectors_and_iteration_limit(ctx):
     p = _tls4()
     ctx.load(p)
     LB, UB = random_boxes(p, 1024, 7)
-    _check(ctx, p, LB, UB, 24, want_x=True)
-    _check(ctx, p, LB, UB, 24, iter_limit=3)
+    _check(ctx, p, LB, UB, KCAP, want_x=True)
+    _check(ctx, p, LB, UB, KCAP, iter_limit=3)
     _check(ctx, p, LB, UB, 4, iter_limit=6)
 
 
@@ -154,7 +155,7 @@ def test_k3p_column_slot_counts(ctx, kind, n, m, seed):
     assert p.n + p.m <= 256 and p.m <= 64
     ctx.load(p)
     LB, UB = random_boxes(p, 777, seed)
-    _check(ctx, p, LB, UB, 24, want_x=True)
+    _check(ctx, p, LB, UB, KCAP, want_x=True)
     _check(ctx, p, LB, UB, 5)
 
 
@@ -167,7 +168,7 @@ def test_k3p_bound_lps_vs_oracle(ctx):
     signs = np.tile([1.0, -1.0], p.n)
     with k3p(ctx):
         g = ctx.lp_bound(cols, signs, ws=ws, want_x=True)
-    st, ob, it, xs = oracle.lp_bound(p, cols, signs, ws=ows, pfi=24)
+    st, ob, it, xs = oracle.lp_bound(p, cols, signs, ws=ows, pfi=KCAP)
     assert np.array_equal(g.status, st) and np.array_equal(g.iters, it)
     assert _close(g.obj, ob)
     for k in np.nonzero(st == 0)[0][::17]:
