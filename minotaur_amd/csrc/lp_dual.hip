@@ -258,7 +258,13 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   // for the workgroup; each wave then solves nodes b, b + grid*W, ...
   // (no workgroup barrier below this point).
   STAMP_DECL
-  for (int bi = lo + blockIdx.x * W + wave; bi < nsolve; bi += gridDim.x * W) {
+  for (int bi = lo + blockIdx.x * W + wave;; bi += gridDim.x * W) {
+    if (io.next != nullptr) {  // dynamic schedule: the next unsolved list position
+      int t = 0;
+      if (lane0 == 0) t = atomicAdd(io.next, 1);
+      bi = lo + __builtin_amdgcn_readfirstlane(t);
+    }
+    if (bi >= nsolve) break;
     const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
     const int bw = io.list_ws ? bi : b;  // warm-start index
 

@@ -435,17 +435,18 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     // slots), or restarts from the shared warm start past the slot capacity
     const int m = c->lp.m, N = c->lp.n + c->lp.m;
     const int cap = io.batch < kPfiOvfSlots ? io.batch : kPfiOvfSlots;
-    HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 2) * sizeof(int32_t)));
+    HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 4) * sizeof(int32_t)));
     const size_t sb_head = al16h((size_t)cap * m * 4), sb_st = al16h((size_t)cap * N),
                  sb_d = al16h((size_t)cap * N * 8), sb_binv = (size_t)cap * m * m * 8;
     HIPCHK(c, c->pfi_cont.ensure(sb_head + sb_st + sb_d + sb_binv));
-    int32_t *cnt = c->pfi_ovf.as<int32_t>();  // [0] overflow count, [1] next node
-    HIPCHK(c, hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), c->stream));
+    // [0] overflow count, [1] K3P's next node, [2]/[3] the K3 follow-ups'
+    int32_t *cnt = c->pfi_ovf.as<int32_t>();
+    HIPCHK(c, hipMemsetAsync(cnt, 0, 4 * sizeof(int32_t), c->stream));
     PfiIO px{};
     px.kmax = c->lp_pfi > 0 ? c->lp_pfi : kPfiMax;
     px.ovf_count = cnt;
     px.next = cnt + 1;
-    px.ovf_list = cnt + 2;
+    px.ovf_list = cnt + 4;
     px.ovf_cap = cap;
     char *cp = c->pfi_cont.as<char>();
     px.c_head = (int32_t *)cp;
@@ -464,6 +465,7 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     io2.iter_base = px.kmax;
     io2.iter_limit = io.iter_limit - px.kmax;  // K3P only overflows below the limit
     io2.ws = LpWarm{px.c_head, px.c_st, px.c_d, px.c_binv, m, N, N, (long)m * m};
+    io2.next = cnt + 2;
     HIPCHK(c, launch_lp_dual(c->lp, io2, c->num_cus, c->stream));
     if (io.batch > cap) {  // overflow beyond the slots: restart from the shared warm start
       LpIO io3 = io;
@@ -471,6 +473,7 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
       io3.node_count = px.ovf_count;
       io3.list_lo = cap;
       io3.list_hi = 0x7fffffff;
+      io3.next = cnt + 3;
       HIPCHK(c, launch_lp_dual(c->lp, io3, c->num_cus, c->stream));
     }
     return MGPU_OK;
@@ -482,7 +485,11 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
   if (!use_large_lp(c)) {
     if (c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
       return fail(c, MGPU_ERR_ARG, "%s: problem too large for K3 (m=%d)", who, c->lp.m);
-    HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
+    HIPCHK(c, c->lp_next.ensure(sizeof(int32_t)));  // dynamic node schedule
+    HIPCHK(c, hipMemsetAsync(c->lp_next.p, 0, sizeof(int32_t), c->stream));
+    LpIO iod = io;
+    iod.next = c->lp_next.as<int32_t>();
+    HIPCHK(c, launch_lp_dual(c->lp, iod, c->num_cus, c->stream));
     return MGPU_OK;
   }
   if (lp_large_lds_bytes(c->lp.n, c->lp.m) > (size_t)kLargeLdsMax)

@@ -10,7 +10,7 @@ import torch
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
 sys.path.insert(0, ROOT)
 from minotaur_amd.problem import LinProblem, random_boxes  # noqa: E402
-from minotaur_amd.runtime import Context, WarmStart  # noqa: E402
+from minotaur_amd.runtime import LP_PFI_MAX, Context, WarmStart  # noqa: E402
 
 
 def main():
@@ -36,7 +36,7 @@ def main():
     obj = torch.zeros(B, dtype=torch.float64, device=dev)
     it = torch.zeros(B, dtype=torch.int32, device=dev)
     ctx.fbbt_dev(lb0, ub0, lb, ub, inf, nm)
-    modes = [(1, 24)] + [(0, k) for k in (24, 20, 16, 12, 8)]
+    modes = [(1, LP_PFI_MAX)] + [(0, k) for k in (LP_PFI_MAX, 12, 8)]
     if os.environ.get('PROBE_MODES'):   # e.g. "0:24" (variant:kmax, comma separated)
         modes = [tuple(int(v) for v in mkv.split(':')) for mkv in
                  os.environ['PROBE_MODES'].split(',')]
@@ -60,7 +60,7 @@ def main():
         print(f"{name}: {k:7.3f} ms  {B / k / 1e3:7.2f} M LP/s  overflow {over:6d}  "
               f"max|dobj| vs dense {dev_obj:.2e}", flush=True)
     ctx.set_lp_variant(0)
-    ctx.set_lp_pfi(24)
+    ctx.set_lp_pfi(LP_PFI_MAX)
 
 
 if __name__ == '__main__':
