@@ -43,6 +43,7 @@ extern "C" {
 #define MGPU_ERR_HIP (-2)     /* HIP runtime error (maps to EngineError) */
 #define MGPU_ERR_STATE (-3)   /* call out of order (e.g. no problem loaded) */
 #define MGPU_ERR_NOMEM (-4)   /* device allocation failed */
+#define MGPU_ERR_ENGINE (-5)  /* a relaxation ended unbounded / unknown (tree search) */
 
 /* EngineStatus numerics (src/base/Types.h:152-166). */
 #define MGPU_PROVEN_OPTIMAL 0
@@ -72,6 +73,8 @@ int mgpu_sync(mgpu_ctx *ctx);
  * Terms inside a row must be given in the order the reference iterates them
  * (the LinearFunction's VariableGroup, ascending variable id: Types.cpp:30-34)
  * — FBBT sums in that order; each column at most once per row.
+ * A failed (re)load leaves the context without a problem: every call that
+ * needs one returns MGPU_ERR_STATE until a load succeeds.
  * Replaces OsiLPEngine::load (OsiLPEngine.cpp:390-498). */
 int mgpu_load_lp(mgpu_ctx *ctx, int n, int m, const int32_t *rowptr,
                  const int32_t *colidx, const double *val,
@@ -114,8 +117,10 @@ int mgpu_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in,
  *                 all nodes (e.g. the root optimum), else [batch] of each.
  *                 ws_head == NULL: slack basis.  Replaces
  *                 getWarmStartCopy/loadFromWarmStart (:375-384, :500-505).
- *   iter_limit  : <= 0 means none; hitting it gives status 6
- *                 (EngineIterationLimit, :561-569).
+ *   iter_limit  : pivots per LP; 0 = the reference default 10000
+ *                 (OsiLPEngine maxIterLimit_, OsiLPEngine.cpp:99), < 0 = no
+ *                 limit; hitting it gives status 6 (EngineIterationLimit,
+ *                 :561-569).
  *   status/obj/iters : [batch]; obj includes the objective constant and is
  *                 +INF for infeasible nodes.
  *   x           : [batch][n] primal solution, or NULL.
@@ -203,6 +208,9 @@ int mgpu_lp_bound_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double
  *   mgpu_bnb_round : one round; `incumbent` may lower the incumbent (e.g.
  *                    the all-reduced value of other ranks).  stats are
  *                    cumulative; open == 0 after a round = tree finished.
+ *                    MGPU_ERR_ENGINE (stats still filled) when a node LP
+ *                    ended unbounded or unknown (decision 4): the reference
+ *                    asserts there (PCBProcessor.cpp:437-442).
  *   mgpu_bnb_best  : incumbent value and solution (x NaN when none found).
  * decision codes in ndec[] are those of mgpu_node_decide_dev. */
 typedef struct {

@@ -25,10 +25,11 @@ HipLinearHandler::HipLinearHandler(EnvPtr env, ProblemPtr problem, int device)
     : LinearHandler(env, problem),
       ctx_(0),
       device_(device),
-      loadedRel_(0),
-      loadedCons_(0),
-      loadedVars_(0),
-      gpuCalls_(0) {
+      loaded_(false),
+      gpuCalls_(0),
+      gpuLoads_(0),
+      gpuErrors_(0),
+      objoff_(0.0) {
   if (mgpu_create(device_, &ctx_) != MGPU_OK) ctx_ = 0;
 }
 
@@ -42,7 +43,12 @@ std::string HipLinearHandler::getName() const {
 
 // Rows the reference's varBndsFromCons_ can tighten (LinearHandler.cpp:
 // 510-513, 966-968): linear, no quadratic / nonlinear part, not deleted.
-void HipLinearHandler::loadRel_(RelaxationPtr rel) {
+// The rows, column types and objective are rebuilt on the host every node
+// (cuts and McCormick rewrites change them through the Problem) but uploaded
+// (mgpu_load_lp: device CSR, CSC and FBBT records) only when they differ
+// from what is loaded.  Column bounds travel with each mgpu_fbbt call.
+// Returns false when the engine refused the load.
+bool HipLinearHandler::loadRel_(RelaxationPtr rel) {
   const int n = (int)rel->getNumVars();
   std::vector<int32_t> rowptr(1, 0), colidx, ctype(n);
   std::vector<double> val, rlo, rhi, clo(n), chi(n), obj(n, 0.0);
@@ -79,26 +85,41 @@ void HipLinearHandler::loadRel_(RelaxationPtr rel) {
       for (VariableGroupConstIterator t = lf->termsBegin(); t != lf->termsEnd(); ++t)
         obj[t->first->getIndex()] = t->second;
   }
+  if (loaded_ && rowptr == rowptr_ && colidx == colidx_ && val == val_ && rlo == rlo_ &&
+      rhi == rhi_ && ctype == ctype_ && obj == obj_ && objoff == objoff_)
+    return true;
   const int m = (int)rowmap_.size();
-  mgpu_load_lp(ctx_, n, m, rowptr.data(), colidx.empty() ? 0 : colidx.data(),
-               val.empty() ? 0 : val.data(), rlo.data(), rhi.data(), clo.data(), chi.data(),
-               ctype.data(), obj.data(), objoff);
-  loadedRel_ = rel;
-  loadedCons_ = rel->getNumCons();
-  loadedVars_ = rel->getNumVars();
+  loaded_ = false;
+  if (mgpu_load_lp(ctx_, n, m, rowptr.data(), colidx.empty() ? 0 : colidx.data(),
+                   val.empty() ? 0 : val.data(), rlo.data(), rhi.data(), clo.data(),
+                   chi.data(), ctype.data(), obj.data(), objoff) != MGPU_OK)
+    return false;
+  ++gpuLoads_;
+  loaded_ = true;
+  rowptr_.swap(rowptr);
+  colidx_.swap(colidx);
+  val_.swap(val);
+  rlo_.swap(rlo);
+  rhi_.swap(rhi);
+  ctype_.swap(ctype);
+  obj_.swap(obj);
+  objoff_ = objoff;
+  return true;
 }
 
-bool HipLinearHandler::presolveNode(RelaxationPtr rel, NodePtr, SolutionPoolPtr spool,
+bool HipLinearHandler::presolveNode(RelaxationPtr rel, NodePtr node, SolutionPoolPtr spool,
                                     ModVector &p_mods, ModVector &r_mods) {
   Timer *timer = env_->getNewTimer();
   timer->start();
-  if (!ctx_) {
-    logger_->errStream() << "HipLinearHandler: no HIP device" << std::endl;
-    delete timer;
-    return false;
-  }
   // rows, objective or constants may have changed (cuts, McCormick rows)
-  loadRel_(rel);
+  if (!ctx_ || !loadRel_(rel)) {
+    ++gpuErrors_;
+    logger_->errStream() << "HipLinearHandler: engine "
+                         << (ctx_ ? mgpu_last_error(ctx_) : "not created (no HIP device)")
+                         << "; node FBBT by the reference LinearHandler" << std::endl;
+    delete timer;
+    return LinearHandler::presolveNode(rel, node, spool, p_mods, r_mods);
+  }
   const int n = (int)rel->getNumVars();
   lb_.resize(n);
   ub_.resize(n);
@@ -118,8 +139,16 @@ bool HipLinearHandler::presolveNode(RelaxationPtr rel, NodePtr, SolutionPoolPtr 
     mvar_.resize(cap);
     mlu_.resize(cap);
     mval_.resize(cap);
-    mgpu_fbbt(ctx_, 1, lb_.data(), ub_.data(), inc, olb_.data(), oub_.data(), &infeas,
-              &nmods, cap, mvar_.data(), mlu_.data(), mval_.data());
+    if (mgpu_fbbt(ctx_, 1, lb_.data(), ub_.data(), inc, olb_.data(), oub_.data(), &infeas,
+                  &nmods, cap, mvar_.data(), mlu_.data(), mval_.data()) != MGPU_OK) {
+      // no mod of a failed call is replayed: the node runs on the host
+      ++gpuErrors_;
+      loaded_ = false;
+      logger_->errStream() << "HipLinearHandler: mgpu_fbbt failed: " << mgpu_last_error(ctx_)
+                           << "; node FBBT by the reference LinearHandler" << std::endl;
+      delete timer;
+      return LinearHandler::presolveNode(rel, node, spool, p_mods, r_mods);
+    }
     if (nmods <= cap) break;
     cap = nmods + 16;  // log was truncated: run again with room for all
   }

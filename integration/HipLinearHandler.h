@@ -36,16 +36,24 @@ class HipLinearHandler : public LinearHandler {
 
   /// Node FBBT calls served by the GPU engine.
   UInt gpuCalls() const { return gpuCalls_; }
+  /// Relaxation uploads (mgpu_load_lp): only when rows / objective changed.
+  UInt gpuLoads() const { return gpuLoads_; }
+  /// Engine failures (load or FBBT); each such node ran the reference's CPU
+  /// LinearHandler::presolveNode instead, after an error message.
+  UInt gpuErrors() const { return gpuErrors_; }
 
  private:
-  void loadRel_(RelaxationPtr rel);
+  bool loadRel_(RelaxationPtr rel);
 
   mgpu_ctx *ctx_;
   int device_;
-  RelaxationPtr loadedRel_;
-  UInt loadedCons_, loadedVars_;
+  bool loaded_;
   std::vector<int32_t> rowmap_;  // kernel row -> relaxation constraint
-  UInt gpuCalls_;
+  UInt gpuCalls_, gpuLoads_, gpuErrors_;
+  // what is loaded on the device (compared before every node)
+  std::vector<int32_t> rowptr_, colidx_, ctype_;
+  std::vector<double> val_, rlo_, rhi_, obj_;
+  double objoff_;
   std::vector<double> lb_, ub_, olb_, oub_;
   std::vector<int32_t> mvar_, mlu_;
   std::vector<double> mval_;

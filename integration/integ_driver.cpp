@@ -6,6 +6,7 @@
 // Mirrors the reference's own tests src/testing/AMPLOsiUT.cpp:46-170
 // (testOsiLP, testOsiLP2, testOsiWarmStart, testOsiBnB), with the instances
 // built programmatically from src/testing/instances/*.mod (ASL is absent).
+#include <chrono>
 #include <cmath>
 #include <vector>
 
@@ -130,8 +131,9 @@ int integ_lp_eg0(int device) {
 // AMPLOsiUT::testOsiBnB generalised: the reference BranchAndBound with
 // IntVarHandler + (reference LinearHandler | HipLinearHandler), PCBProcessor,
 // ReliabilityBrancher and NodeIncRelaxer, all on a HipLPEngine.
-// res[0] = UB, res[1] = LB; cnt[0] = nodes processed, cnt[1] = LP solves,
-// cnt[2] = GPU FBBT calls.
+// res[0] = UB, res[1] = LB, res[2] = wall seconds in BranchAndBound::solve;
+// cnt[0] = nodes processed, cnt[1] = LP solves, cnt[2] = GPU FBBT calls,
+// cnt[3] = relaxation uploads by HipLinearHandler, cnt[4] = its engine errors.
 int integ_bnb(int device, int hip_fbbt, int n, int m, const int *rowptr, const int *colidx,
               const double *val, const double *rlo, const double *rhi, const int *vtype,
               const double *vlb, const double *vub, const double *obj, double objc,
@@ -162,7 +164,9 @@ int integ_bnb(int device, int hip_fbbt, int n, int m, const int *rowptr, const i
   p->setNativeDer();
   bab->shouldCreateRoot(true);
   bab->setLogLevel(LogNone);
+  const auto t0 = std::chrono::steady_clock::now();
   bab->solve();
+  res[2] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   res[0] = bab->getUb();
   res[1] = bab->getLb();
   cnt[0] = (int)bab->getTreeManager()->getSize();
@@ -170,6 +174,8 @@ int integ_bnb(int device, int hip_fbbt, int n, int m, const int *rowptr, const i
   e->fillStats(lps);
   cnt[1] = (int)lps[0];
   cnt[2] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuCalls() : 0;
+  cnt[3] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuLoads() : 0;
+  cnt[4] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuErrors() : 0;
   delete v_hand;
   delete l_hand;
   delete e;

@@ -212,6 +212,12 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   s.tot.incumbent = s.inc;
   s.tot.last_batch = nb;
   if (stats) *stats = s.tot;
+  // decision 4 (ProvenUnbounded / EngineUnknownStatus): the reference asserts
+  // on an unbounded relaxation (PCBProcessor.cpp:437-442); such a node is not
+  // branched, so the tree would end on a wrong optimum: report it
+  if (o.ndec[4] > 0)
+    return fail(c, MGPU_ERR_ENGINE, "mgpu_bnb_round: %lld node LPs ended unbounded or with an "
+                "unknown status; their subtrees were not searched", (long long)o.ndec[4]);
   return MGPU_OK;
 }
 

@@ -108,6 +108,7 @@ struct LpIO {
 
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
+constexpr int kLpDefaultIterLimit = 10000;  // OsiLPEngine maxIterLimit_ (OsiLPEngine.cpp:99)
 
 // K3P (lp_pfi.hip): product-form dual simplex for a batch that shares its
 // warm start.  At most kPfiMax eta columns per node, n + m <= 64*kPfiSlots.

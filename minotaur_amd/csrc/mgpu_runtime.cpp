@@ -100,6 +100,10 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
                  const double *collb, const double *colub, const int32_t *coltype,
                  const double *obj, double objoff) {
   if (!c) return MGPU_ERR_ARG;
+  // A (re)load replaces the problem: until it has completed, nothing may run
+  // on the old one (its buffers are freed as the new ones are allocated), so
+  // a failed load leaves the context with no problem (MGPU_ERR_STATE).
+  c->loaded = false;
   if (n <= 0 || m < 0 || !rowptr || (m > 0 && (!rowlb || !rowub)) || !collb || !colub ||
       !coltype || !obj)
     return fail(c, MGPU_ERR_ARG, "mgpu_load_lp: bad argument");
@@ -122,6 +126,7 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   bnb_state_free(c);  // a tree belongs to the problem it was started on
+  c->lp = DevLP{};
   // CSR terms, packed
   c->h_terms.resize(nnz > 0 ? nnz : 1);
   for (int k = 0; k < nnz; ++k) c->h_terms[k] = Term{val[k], colidx[k], 0};
@@ -407,6 +412,14 @@ int mgpu_fbbt(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
 }
 
 namespace {
+// OsiLPEngine caps Clp at maxIterLimit_ = 10000 pivots (OsiLPEngine.cpp:99):
+// 0 selects that default, a negative value none (explicit opt-in), as
+// include/mgpu.h documents.  The LP kernels have no anti-cycling rule, so the
+// cap is what ends a cycling degenerate LP (status 6).
+int lp_iter_limit(int iter_limit) {
+  return iter_limit > 0 ? iter_limit : iter_limit == 0 ? kLpDefaultIterLimit : 0x7fffffff;
+}
+
 // K3 (B^-1 rows in VGPRs, m <= 64, LDS-staged matrix) unless the problem
 // needs K3L (more rows, or a matrix that does not fit LDS) or a test forces
 // one of them (mgpu_set_lp_variant).
@@ -538,7 +551,7 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   io.ws.s_st = ws_shared ? 0 : N;
   io.ws.s_d = ws_shared ? 0 : N;
   io.ws.s_binv = ws_shared ? 0 : (long)m * m;
-  io.iter_limit = iter_limit > 0 ? iter_limit : 0x7fffffff;
+  io.iter_limit = lp_iter_limit(iter_limit);
   io.status = status;
   io.obj = obj;
   io.iters = iters;
@@ -578,7 +591,7 @@ int mgpu_lp_bound_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   io.ws.st = ws_st;
   io.ws.d = nullptr;  // reduced costs are rebuilt for each objective
   io.ws.binv = ws_binv;
-  io.iter_limit = iter_limit > 0 ? iter_limit : 0x7fffffff;
+  io.iter_limit = lp_iter_limit(iter_limit);
   io.status = status;
   io.obj = obj;
   io.iters = iters;

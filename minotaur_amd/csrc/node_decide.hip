@@ -3,9 +3,11 @@
 // and the integrality test of IntVarHandler::isFeasible
 // (src/base/IntVarHandler.cpp:54-84), one wave per node.
 //
-// decision codes (mgpu.h): 0 continue/branch, 1 infeasible (FBBT or LP),
-// 2 pruned by bound (NodeHitUb), 3 integer feasible (new incumbent
-// candidate), 4 engine problem (unbounded / unknown).
+// decision codes (mgpu.h): 0 continue/branch, 1 infeasible (FBBT, LP or
+// engine error), 2 pruned by bound (NodeHitUb), 3 integer feasible (new
+// incumbent candidate), 4 engine problem (unbounded / unknown status).
+// Pinned against the reference's own shouldPrune_ + isFeasible
+// (tests/golden/decide_*.npz, oracle/ref/ref_decide.cpp).
 #include "mgpu_internal.h"
 #include "wave.h"
 
@@ -25,33 +27,50 @@ __global__ __launch_bounds__(64 * kNodesPerBlock) void node_decide_kernel(DevLP 
   const double solval = io.obj[b];
   int dec;
   double inf_meas = 0.0;
+  // EngineStatus numerics (Types.h:152-166)
+  const bool optimal = st == 0 || st == 1 || st == 6;   // Proven(Local)Optimal, IterationLimit
+  const bool cont = st == 7 || st == 9;                 // ProvenFailedCQFeas, FailedFeas
   if (io.fbbt_infeas != nullptr && io.fbbt_infeas[b] != 0) {
     dec = 1;  // presolveNode reported infeasible: pruned before the solve
-  } else if (st == 2 || st == 3) {
-    dec = 1;  // ProvenInfeasible / ProvenLocalInfeasible
-  } else if (st == 0 || st == 1 || st == 6) {
-    // ProvenOptimal / ProvenLocalOptimal / EngineIterationLimit
+  } else if (st == 2 || st == 3 || st == 8 || st == 10 || st == 11) {
+    // Proven(Local)Infeasible, ProvenFailedCQInfeas, FailedInfeas, and
+    // EngineError (contOnErr_ is false in PCBProcessor, :39, :497-515)
+    dec = 1;
+  } else if (st == 5) {
+    dec = 2;  // ProvenObjectiveCutOff -> NodeHitUb (:431-435)
+  } else {
+    // ProvenUnbounded (the reference asserts, :437-442) and
+    // EngineUnknownStatus (no case) keep the node (shouldPrune_ false) and
+    // still reach isFeasible (its inf_meas is reported), decision 4
+    const bool engine = !(optimal || cont);
     const double cut = io.incumbent;
-    if (solval >= cut - io.abs_tol || solval >= cut - fabs(cut) * io.rel_tol ||
-        solval >= io.cutoff) {
-      dec = 2;
+    if (optimal && (solval >= cut - io.abs_tol || solval >= cut - fabs(cut) * io.rel_tol ||
+                    solval >= io.cutoff)) {
+      dec = 2;  // :486-491
     } else {
-      // IntVarHandler::isFeasible over Binary/Integer columns
+      // IntVarHandler::isFeasible over Binary/Integer columns.  inf_meas is
+      // accumulated in column order as the reference's loop does (:64-79):
+      // each lane holds one column's violation (0 when integral), the wave
+      // adds them lane by lane through v_readlane, so the sum is the
+      // reference's sequential sum bit for bit (adding +0.0 is exact).
       const double *x = io.x + (size_t)b * lp.n;
       bool frac = false;
-      double meas = 0.0;
-      for (int j = lane; j < lp.n; j += 64) {
-        const uint8_t t = lp.vtype[j];
-        if (t != kBinary && t != kInteger) continue;
-        const double v = x[j];
-        const double f = fabs(v - floor(v + 0.5));
-        if (f > io.int_tol) {
-          frac = true;
-          meas += f;
+      for (int j0 = 0; j0 < lp.n; j0 += 64) {
+        const int j = j0 + lane;
+        double f = 0.0;
+        if (j < lp.n) {
+          const uint8_t t = lp.vtype[j];
+          if (t == kBinary || t == kInteger) {
+            const double v = x[j];
+            const double g = fabs(v - floor(v + 0.5));
+            if (g > io.int_tol) f = g;
+          }
         }
+        frac |= f > 0.0;
+        const int cnt = lp.n - j0 < 64 ? lp.n - j0 : 64;
+        for (int k = 0; k < cnt; ++k) inf_meas += rld(f, k);
       }
-      inf_meas = wave_sum(meas);
-      dec = __any(frac) ? 0 : 3;
+      dec = engine ? 4 : __any(frac) ? 0 : 3;
       if (dec == 0 && io.bvar != nullptr) {
         // MaxVioBrancher::findBestCandidate_ (MaxVioBrancher.cpp) over the
         // IntVarHandler candidates (IntVarHandler.cpp:86-108): score
@@ -82,8 +101,6 @@ __global__ __launch_bounds__(64 * kNodesPerBlock) void node_decide_kernel(DevLP 
         }
       }
     }
-  } else {
-    dec = 4;
   }
   if (lane == 0) {
     io.decision[b] = dec;

@@ -400,3 +400,77 @@ def quadratic_form(expr, n):
                 Q[i, j] += v
                 Q[j, i] += v
     return Q, c, k0
+
+
+def evaluate(expr, x):
+    """Value and gradient (dense, len(x)) of an ``.nl`` expression tree at x
+    (forward mode).  Opcodes: o0 plus, o1 minus, o2 mult, o3 div, o5 pow,
+    o16 negation, o39 sqrt, o54 sumlist, numbers and variables — the set
+    tls4.nl, nvs08.nl and color_lab2_4x0.nl use.  The outer-approximation
+    builders (minotaur_amd/problem.py) linearise rows with it."""
+    x = np.asarray(x, dtype=np.float64)
+    n = x.size
+
+    def ev(e):
+        if e[0] == 'n':
+            return float(e[1]), np.zeros(n)
+        if e[0] == 'v':
+            g = np.zeros(n)
+            g[int(e[1])] = 1.0
+            return float(x[int(e[1])]), g
+        if e[0] != 'o':
+            raise ValueError(f'unsupported expression node {e[0]!r}')
+        op, args = e[1], e[2]
+        if op in (0, 54):
+            v, g = 0.0, np.zeros(n)
+            for a in args:
+                va, ga = ev(a)
+                v += va
+                g = g + ga
+            return v, g
+        if op == 1:
+            (va, ga), (vb, gb) = ev(args[0]), ev(args[1])
+            return va - vb, ga - gb
+        if op == 2:
+            (va, ga), (vb, gb) = ev(args[0]), ev(args[1])
+            return va * vb, vb * ga + va * gb
+        if op == 3:
+            (va, ga), (vb, gb) = ev(args[0]), ev(args[1])
+            return va / vb, (ga * vb - va * gb) / (vb * vb)
+        if op == 5:
+            (va, ga), (vb, gb) = ev(args[0]), ev(args[1])
+            if not gb.any():                        # constant exponent
+                return va ** vb, vb * va ** (vb - 1.0) * ga
+            v = va ** vb
+            return v, v * (gb * math.log(va) + vb * ga / va)
+        if op == 16:
+            va, ga = ev(args[0])
+            return -va, -ga
+        if op == 39:
+            va, ga = ev(args[0])
+            s = math.sqrt(va)
+            return s, ga / (2.0 * s)
+        raise ValueError(f'opcode o{op} not supported by evaluate()')
+
+    return ev(expr)
+
+
+def row_value(model, i, x):
+    """Value and gradient of row i's body: nonlinear part + linear (J) part."""
+    x = np.asarray(x, dtype=np.float64)
+    v, g = (evaluate(model.con_expr[i], x) if model.con_nonlinear[i]
+            else (0.0, np.zeros(model.n)))
+    for j, a in model.rows[i]:
+        v += a * x[j]
+        g[j] += a
+    return v, g
+
+
+def objective_value(model, x):
+    """Value and gradient of the objective (nonlinear part + G gradient + constant)."""
+    x = np.asarray(x, dtype=np.float64)
+    v, g = (evaluate(model.obj_expr, x) if model.obj_nonlinear else (0.0, np.zeros(model.n)))
+    for j, a in model.obj_grad:
+        v += a * x[j]
+        g[j] += a
+    return v + model.obj_const, g

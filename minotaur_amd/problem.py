@@ -308,3 +308,69 @@ def random_mkp(seed: int, n: int = 40, m: int = 5, tight: float = 0.5):
     rows = [[(j, A[i, j]) for j in range(n)] for i in range(m)]
     return from_rows(f"mkp-{seed}-n{n}-m{m}", n, rows, np.full(m, -np.inf), b,
                      np.zeros(n), np.ones(n), np.full(n, BINARY, dtype=np.int32), -c)
+
+
+def nvs08_oa(model, npts=4, nobj=8, seed=20261016):
+    """Outer-approximation LP of test_instances/nvs08.nl (BASELINE config 1,
+    SURVEY §0.1 / §8d: "OA-LP with tangent rows at seeded points").
+
+    nvs08 is nonlinear in every row (nvs08.nl:2-44), so OsiLPEngine cannot
+    load it (OsiLPEngine.cpp:420); the LP this engine solves for it is built
+    from the model the .nl reader returns (nl.row_value / objective_value
+    evaluate the file's own expression trees):
+
+      columns  x0 (continuous, [1e-3, 200]), x1, x2 (integer, [0, 200]), eta;
+      C0  sqrt(x0) + x1 + 2 x2 >= 10        concave: tangent rows at x0 = t_k
+      C1  q x1^2 + a x0 - x2 >= -3          x1^2 convex: its secant over the
+                                            root box [l1, u1] (over-estimates)
+      C2  x2^2 - x0^-3.5 - 4 x1 >= -12      x2^2 by its secant, -x0^-3.5
+                                            concave: tangent rows at x0 = t_k
+      obj (x1-3)^2 + (x2-2)^2 + (x0+4)^2    convex: min eta, eta >= tangent
+                                            planes at seeded points p_k
+
+    Every row over-estimates its (>=) row body on the root box, so the LP is
+    a relaxation of nvs08 and the OA-MILP optimum is a lower bound on the
+    MINLP optimum (23.4497, MINLPLib; x = (0.63, 4, 3)).  The linearisation
+    points sit around that region as an OA solver's NLP iterates would
+    (seeded): t_k log-uniform in [0.3, 5]; p_k with x0 uniform in [0.3, 2],
+    x1 integer in [2, 5], x2 integer in [1, 4]; eta >= 0 (the objective is a
+    sum of squares)."""
+    from .nl import objective_value, row_value
+    assert model.n == 3 and model.m == 3, 'nvs08 has 3 variables and 3 rows'
+    rng = np.random.default_rng(seed)
+    n = 4                                          # x0, x1, x2, eta
+    l1, u1 = float(model.var_lb[1]), float(model.var_ub[1])
+    l2, u2 = float(model.var_lb[2]), float(model.var_ub[2])
+    ts = np.exp(rng.uniform(math.log(0.3), math.log(5.0), npts))
+    rows, rlo, rhi = [], [], []
+
+    def tangent(i, p, extra=(), shift=0.0):
+        v, g = row_value(model, i, p)
+        terms = [(j, g[j]) for j in range(3) if g[j] != 0.0] + list(extra)
+        rows.append(terms)
+        rlo.append(model.con_lb[i] - v + float(np.dot(g, p)) + shift)
+        rhi.append(math.inf)
+
+    for t in ts:                                   # C0 tangents
+        tangent(0, np.array([t, 0.0, 0.0]))
+    # C1: the quadratic coefficient from the file's expression (value at x1 = 1)
+    q = row_value(model, 1, np.array([0.0, 1.0, 0.0]))[0] - \
+        row_value(model, 1, np.zeros(3))[0] - dict(model.rows[1]).get(1, 0.0)
+    _, g1 = row_value(model, 1, np.zeros(3))      # the linear terms (x1^2' = 0 at 0)
+    rows.append([(0, g1[0]), (1, q * (l1 + u1) + g1[1]), (2, g1[2])])
+    rlo.append(model.con_lb[1] + q * l1 * u1)
+    rhi.append(math.inf)
+    for t in ts:                                   # C2: -x0^-3.5 tangent + x2^2 secant
+        tangent(2, np.array([t, 0.0, 0.0]), extra=[(2, l2 + u2)], shift=l2 * u2)
+    for _ in range(nobj):                          # objective tangent planes
+        p = np.array([rng.uniform(0.3, 2.0), float(rng.integers(2, 6)),
+                      float(rng.integers(1, 5))])
+        f, g = objective_value(model, p)
+        rows.append([(j, -g[j]) for j in range(3)] + [(3, 1.0)])
+        rlo.append(f - float(np.dot(g, p)))
+        rhi.append(math.inf)
+    vlb = list(model.var_lb) + [0.0]            # the objective is a sum of squares
+    vub = list(model.var_ub) + [math.inf]
+    vtype = list(model.var_type) + [CONTINUOUS]
+    obj = [0.0, 0.0, 0.0, 1.0]
+    return from_rows('nvs08-oa', n, rows, rlo, rhi, vlb, vub, vtype, obj)

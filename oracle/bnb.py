@@ -101,17 +101,9 @@ class CpuBnbContext:
         return self.tot
 
     def _decide(self, finf, st, solval, x, ints):
-        if finf:
-            return 1
-        if st in (2, 3):
-            return 1
-        if st in (0, 1, 6):
-            cut = self.inc
-            if solval >= cut - ABS_TOL or solval >= cut - abs(cut) * REL_TOL:
-                return 2
-            fr = np.abs(x[ints] - np.floor(x[ints] + 0.5)) > INT_TOL
-            return 0 if fr.any() else 3
-        return 4
+        dec, _ = oracle.node_decide(self.problem.vtype, [st], [solval], x[None], self.inc,
+                                    [finf], ABS_TOL, REL_TOL, math.inf, INT_TOL)
+        return int(dec[0])
 
     @staticmethod
     def _branch(x, ints):

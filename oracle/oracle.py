@@ -441,3 +441,84 @@ def highs_milp(p, time_limit=60.0):
     if r.status == 3:
         return 4, -math.inf
     return 12, math.nan
+
+
+# ---------------------------------------------------------------------------
+# Node decision: PCBProcessor::shouldPrune_ + IntVarHandler::isFeasible
+# ---------------------------------------------------------------------------
+DEC_BRANCH, DEC_INFEAS, DEC_PRUNED, DEC_FEASIBLE, DEC_ENGINE = 0, 1, 2, 3, 4
+NODE_INFEASIBLE, NODE_HIT_UB, NODE_CONTINUE = 1, 2, 5   # NodeStatus (Types.h:184-194)
+
+
+def ref_node_decide(vtype, status, obj, x, incumbent=None):
+    """The reference's own PCBProcessor::shouldPrune_ (PCBProcessor.cpp:400-523)
+    then, for kept nodes, IntVarHandler::isFeasible (IntVarHandler.cpp:54-84)
+    (_ref/libref_fbbt.so, oracle/ref/ref_decide.cpp).  Returns (prune,
+    node_status, feas (-1 = not evaluated), inf_meas) per node."""
+    R = ref_lib()
+    R.ref_node_decide.restype = _I
+    R.ref_node_decide.argtypes = [_I, _P, _I, _P, _P, _P, _I, _D, _P, _P, _P, _P]
+    vtype = np.ascontiguousarray(vtype, dtype=np.int32)
+    status = np.ascontiguousarray(status, dtype=np.int32)
+    obj = np.ascontiguousarray(obj, dtype=np.float64)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    B = status.size
+    prune = np.zeros(B, np.int32)
+    nstat = np.zeros(B, np.int32)
+    feas = np.zeros(B, np.int32)
+    meas = np.zeros(B)
+    has = 0 if incumbent is None or not math.isfinite(incumbent) else 1
+    R.ref_node_decide(vtype.size, _ptr(vtype), B, _ptr(status), _ptr(obj), _ptr(x), has,
+                      float(incumbent) if has else 0.0, _ptr(prune), _ptr(nstat), _ptr(feas),
+                      _ptr(meas))
+    return prune, nstat, feas, meas
+
+
+def decision_from_ref(prune, nstat, feas):
+    """The engine's decision code (include/mgpu.h mgpu_node_decide_dev) for a
+    reference (shouldPrune_, NodeStatus, isFeasible) outcome."""
+    dec = np.full(prune.size, DEC_ENGINE, np.int32)
+    dec[(prune == 1) & (nstat == NODE_INFEASIBLE)] = DEC_INFEAS
+    dec[(prune == 1) & (nstat == NODE_HIT_UB)] = DEC_PRUNED
+    dec[(prune == 0) & (nstat == NODE_CONTINUE) & (feas == 1)] = DEC_FEASIBLE
+    dec[(prune == 0) & (nstat == NODE_CONTINUE) & (feas == 0)] = DEC_BRANCH
+    return dec
+
+
+def node_decide(vtype, status, obj, x, incumbent=math.inf, fbbt_infeas=None, abs_tol=1e-6,
+                rel_tol=1e-6, cutoff=math.inf, int_tol=1e-6):
+    """CPU restatement of node_decide_kernel: shouldPrune_'s status switch
+    (PCBProcessor.cpp:409-520, contOnErr_ false) and IntVarHandler::isFeasible
+    with its sequential inf_meas (IntVarHandler.cpp:64-79).  Returns
+    (decision, inf_meas)."""
+    ints = np.isin(np.asarray(vtype), (0, 1))
+    B = len(status)
+    dec = np.full(B, DEC_ENGINE, np.int32)
+    meas = np.zeros(B)
+    for b in range(B):
+        st, sv = int(status[b]), float(obj[b])
+        if fbbt_infeas is not None and fbbt_infeas[b]:
+            dec[b] = DEC_INFEAS
+        elif st in (2, 3, 8, 10, 11):
+            dec[b] = DEC_INFEAS
+        elif st == 5:
+            dec[b] = DEC_PRUNED
+        else:
+            cut = incumbent
+            if st in (0, 1, 6) and (sv >= cut - abs_tol or sv >= cut - abs(cut) * rel_tol
+                                    or sv >= cutoff):
+                dec[b] = DEC_PRUNED
+            else:   # 7 / 9: NodeContinue with the parent's bound (:444-467)
+                s, frac = 0.0, False
+                for j in np.nonzero(ints)[0]:
+                    v = float(x[b, j])
+                    f = abs(v - math.floor(v + 0.5))
+                    if f > int_tol:
+                        frac = True
+                        s += f
+                meas[b] = s
+                # 4 / 12 / others: shouldPrune_ keeps the node, isFeasible
+                # runs, the engine reports a problem
+                dec[b] = (DEC_ENGINE if st not in (0, 1, 6, 7, 9) else
+                          DEC_BRANCH if frac else DEC_FEASIBLE)
+    return dec, meas

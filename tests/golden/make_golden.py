@@ -25,10 +25,14 @@ from minotaur_amd.problem import (LinProblem, knapsack_oa, random_boxes,  # noqa
                                   random_problem)
 
 OUT = os.path.dirname(os.path.abspath(__file__))
+# optional: regenerate only the named cases (argv), e.g. nvs08_oa
+ONLY = set(sys.argv[1:])
 CAP = 256
 
 
 def dump(name, p, LB, UB, incumbent):
+    if ONLY and name not in ONLY:
+        return
     r = oracle.ref_linear_fbbt(p, LB, UB, incumbent, CAP)
     np.savez_compressed(
         os.path.join(OUT, f'fbbt_{name}.npz'),
@@ -54,6 +58,12 @@ def main():
     # root box (the node every tree starts from) and a tight incumbent
     dump('tls4_root', tls4, tls4.vlb[None, :].copy(), tls4.vub[None, :].copy(), None)
     dump('tls4_inc8', tls4, LB[:64], UB[:64], 8.0)
+    # config 1: the nvs08 outer-approximation LP (root + seeded boxes)
+    nv = LinProblem.load(os.path.join(inst, 'nvs08_oa.npz'))
+    LB, UB = random_boxes(nv, 255, 808)
+    LB, UB = np.vstack([nv.vlb[None], LB]), np.vstack([nv.vub[None], UB])
+    dump('nvs08_oa', nv, LB, UB, None)
+    dump('nvs08_oa_inc20', nv, LB, UB, 20.0)
     ks = knapsack_oa()
     LB, UB = random_boxes(ks, 1000, 7)
     dump('knapsack_noinc', ks, LB, UB, None)

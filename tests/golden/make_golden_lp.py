@@ -20,6 +20,8 @@ from minotaur_amd.problem import (LinProblem, from_rows, knapsack_oa,  # noqa: E
                                   random_boxes, random_problem)
 
 OUT = os.path.dirname(os.path.abspath(__file__))
+# optional: regenerate only the named cases (argv), e.g. nvs08_oa
+ONLY = set(sys.argv[1:])
 INF = math.inf
 
 
@@ -37,6 +39,8 @@ def known_problems():
 
 
 def dump(name, p, LB, UB):
+    if ONLY and name not in ONLY:
+        return
     st = np.zeros(LB.shape[0], dtype=np.int32)
     obj = np.zeros(LB.shape[0])
     for b in range(LB.shape[0]):
@@ -55,6 +59,9 @@ def main():
     tls4 = LinProblem.load(os.path.join(inst, 'tls4_lin.npz'))
     LB, UB = random_boxes(tls4, 200, 20261015)
     dump('tls4', tls4, np.vstack([tls4.vlb[None], LB]), np.vstack([tls4.vub[None], UB]))
+    nv = LinProblem.load(os.path.join(inst, 'nvs08_oa.npz'))
+    LB, UB = random_boxes(nv, 200, 808)
+    dump('nvs08_oa', nv, np.vstack([nv.vlb[None], LB]), np.vstack([nv.vub[None], UB]))
     ks = knapsack_oa()
     LB, UB = random_boxes(ks, 300, 7)
     dump('knapsack', ks, np.vstack([ks.vlb[None], LB]), np.vstack([ks.vub[None], UB]))

@@ -54,8 +54,8 @@ def test_amplosiut_lp(integ):
 
 
 def _bnb(integ, p, hip_fbbt):
-    res = np.zeros(2)
-    cnt = np.zeros(3, dtype=np.int32)
+    res = np.zeros(3)
+    cnt = np.zeros(5, dtype=np.int32)
     maximize = 0
     integ.integ_bnb(0, hip_fbbt, p.n, p.m, _p(p.rowptr), _p(p.colidx), _p(p.val), _p(p.rlo),
                     _p(p.rhi), _p(p.vtype), _p(p.vlb), _p(p.vub), _p(p.obj), float(p.obj_const),
@@ -95,6 +95,8 @@ def test_bnb_gpu_fbbt_matches_reference_fbbt(integ, name):
     assert r0[0] == r1[0]
     assert c0[1] == c1[1]            # identical number of LP solves
     assert c1[2] > 0                 # node FBBT really ran on the GPU
+    assert c1[4] == 0                # no engine error (no host fallback node)
+    assert c1[3] == 1                # rows never change: uploaded once
     opt = _milp_opt(p)
     if math.isinf(opt):
         assert math.isinf(r1[0])

@@ -6,6 +6,7 @@ dual simplex step for step, so statuses and iteration counts must equal the
 oracle's exactly and objectives agree to ~1e-9.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -152,34 +153,110 @@ def test_lp_device_path(ctx):
     assert np.array_equal(obj.cpu().numpy(), host.obj)
 
 
-def test_strong_branching_children_match_oracle():
-    """mgpu_strong_branch: the 2k child LPs (down/up per candidate, parent
-    basis, iteration cap 25) equal the oracle's solves of the same boxes."""
+@pytest.mark.parametrize('name', ['tls4', 'mkp'])
+def test_strong_branching_children_match_oracle(name):
+    """mgpu_strong_branch (ReliabilityBrancher::strongBranch_, :469-506): the
+    2k child LPs (down ub = floor(v) / up lb = ceil(v) per candidate, all from
+    the node's optimal basis, iteration cap 25 as ReliabilityBrancher.cpp:101
+    or none) equal the ORACLE's solves of the same child boxes from the same
+    basis (oracle.dual_simplex in the arithmetic the context runs: statuses,
+    pivot counts, objectives within 1e-9), and the uncapped optima equal
+    HiGHS within 1e-6."""
     import os
-    from minotaur_amd.problem import LinProblem
-    from minotaur_amd.runtime import Context
+    from minotaur_amd.problem import LinProblem, random_mkp
+    from minotaur_amd.runtime import Context, WarmStart
+    if name == 'tls4':
+        p = LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
+                                         'instances', 'tls4_lin.npz'))
+    else:
+        p = random_mkp(7, 40, 6)
+    st0, _, x, _, _, ows = oracle.dual_simplex_root(p)
+    assert st0 == 0
+    ws = WarmStart(ows.head, ows.st, ows.d, np.ascontiguousarray(ows.binv.T))
+    ints = np.nonzero(np.isin(p.vtype, (0, 1)))[0]
+    frac = ints[np.abs(x[ints] - np.round(x[ints])) > 1e-6]
+    cand = frac[:20] if frac.size else ints[:8]     # maxStrongCands_ = 20 (:43-67)
+    vals = np.where(np.abs(x[cand] - np.round(x[cand])) > 1e-6, x[cand], x[cand] + 0.5)
+    LB = np.repeat(p.vlb[None], 2 * cand.size, axis=0)
+    UB = np.repeat(p.vub[None], 2 * cand.size, axis=0)
+    for c, (j, v) in enumerate(zip(cand, vals)):
+        UB[2 * c, j] = np.floor(v)
+        LB[2 * c + 1, j] = np.ceil(v)
+    ctx = Context(0)
+    try:
+        ctx.load(p)
+        for lim in (25, 0):
+            st, ob, it = ctx.strong_branch(p.vlb, p.vub, cand, vals, ws, lim)
+            so, oo, io, _ = oracle.dual_simplex(p, LB, UB, ows, iter_limit=lim or 10000,
+                                                pfi=ctx.oracle_pfi())
+            assert np.array_equal(st, so) and np.array_equal(it, io)
+            ok = np.isfinite(oo)
+            assert np.array_equal(np.isfinite(ob), ok)
+            assert np.all(np.abs(ob[ok] - oo[ok]) <= 1e-9 * np.maximum(1.0, np.abs(oo[ok])))
+            if lim:
+                assert it.max() <= 25
+            else:
+                for c in range(2 * cand.size):
+                    hs, ho = oracle.highs(p, LB[c], UB[c])
+                    assert hs == st[c]
+                    if hs == 0:
+                        assert abs(ob[c] - ho) <= 1e-6 * max(1.0, abs(ho))
+    finally:
+        ctx.close()
+
+
+def test_failed_reload_leaves_no_problem():
+    """A failed mgpu_load_lp invalidates the context's problem (no kernel may
+    run on freed or stale buffers): the next mgpu_fbbt / mgpu_lp_solve
+    returns MGPU_ERR_STATE (-3) until a load succeeds."""
+    import ctypes
+    from minotaur_amd.runtime import Context, MgpuError
     p = LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
                                      'instances', 'tls4_lin.npz'))
     ctx = Context(0)
     try:
         ctx.load(p)
-        r, ws = ctx.root_solve()
-        x = r.x[0]
-        ints = np.nonzero(np.isin(p.vtype, (0, 1)))[0]
-        frac = ints[np.abs(x[ints] - np.round(x[ints])) > 1e-6]
-        cand = frac if frac.size else ints[:8]
-        vals = np.where(np.abs(x[cand] - np.round(x[cand])) > 1e-6, x[cand], x[cand] + 0.5)
-        for lim in (25, 0):
-            st, ob, it = ctx.strong_branch(p.vlb, p.vub, cand, vals, ws, lim)
-            LB = np.repeat(p.vlb[None], 2 * cand.size, axis=0)
-            UB = np.repeat(p.vub[None], 2 * cand.size, axis=0)
-            for c, (j, v) in enumerate(zip(cand, vals)):
-                UB[2 * c, j] = np.floor(v)
-                LB[2 * c + 1, j] = np.ceil(v)
-            g = ctx.lp_solve(LB, UB, ws, iter_limit=lim)
-            assert np.array_equal(st, g.status) and np.array_equal(it, g.iters)
-            assert np.array_equal(ob, g.obj)
-            if lim:
-                assert it.max() <= 25
+        ctx.fbbt(p.vlb[None], p.vub[None])
+        bad = np.array(p.colidx, dtype=np.int32)
+        bad[3] = p.n + 7                                   # column out of range
+        k = [np.ascontiguousarray(a) for a in (p.rowptr, bad, p.val, p.rlo, p.rhi, p.vlb, p.vub,
+                                               p.vtype.astype(np.int32), p.obj)]
+        rc = ctx.lib.mgpu_load_lp(ctx.h, p.n, p.m, *[a.ctypes.data_as(ctypes.c_void_p)
+                                                      for a in k], 0.0)
+        assert rc == -1
+        with pytest.raises(MgpuError, match='rc=-3'):
+            ctx.fbbt(p.vlb[None], p.vub[None])
+        with pytest.raises(MgpuError, match='rc=-3'):
+            ctx.lp_solve(p.vlb[None], p.vub[None])
+        ctx.load(p)                                        # a good load restores it
+        g = ctx.fbbt(p.vlb[None], p.vub[None])
+        o = oracle.linear_fbbt(p, p.vlb[None], p.vub[None])
+        assert np.array_equal(g.lb, o.lb) and np.array_equal(g.ub, o.ub)
+    finally:
+        ctx.close()
+
+
+def test_default_iteration_limit_is_osilp_default():
+    """iter_limit 0 = OsiLPEngine's maxIterLimit_ 10000 (OsiLPEngine.cpp:99),
+    < 0 = none: on LPs far below the cap all three agree with the oracle at
+    its default 10000, and a small explicit cap gives status 6 at exactly
+    that pivot count."""
+    from minotaur_amd.problem import knapsack_oa
+    from minotaur_amd.runtime import Context
+    p = knapsack_oa(f=40, N=64)       # m = 161: K3L from the slack basis
+    LB, UB = random_boxes(p, 32, 3)
+    ctx = Context(0)
+    try:
+        ctx.load(p)
+        so, oo, io, _ = oracle.dual_simplex(p, LB, UB)
+        for lim in (0, 10000, -1):
+            g = ctx.lp_solve(LB, UB, iter_limit=lim)
+            assert np.array_equal(g.status, so) and np.array_equal(g.iters, io)
+            assert np.array_equal(g.obj, oo)
+        cap = int(max(2, io.max() // 2))
+        g = ctx.lp_solve(LB, UB, iter_limit=cap)
+        s2, o2, i2, _ = oracle.dual_simplex(p, LB, UB, iter_limit=cap)
+        assert np.array_equal(g.status, s2) and np.array_equal(g.iters, i2)
+        assert np.any(g.status == 6) and np.all(g.iters[g.status == 6] == cap)
     finally:
         ctx.close()

@@ -6,13 +6,15 @@ fixtures under minotaur_amd/instances/ (run in the container that has
   knapsack9.npz    — OA-LP of examples/knapsack (config 3)
   color_lab2_qp.npz — QP relaxation data of test_instances/color_lab2_4x0.nl
                       (dense Q, equality rows; config 4)
+  nvs08_oa.npz     — outer-approximation LP of test_instances/nvs08.nl
+                      (config 1; minotaur_amd.problem.nvs08_oa)
 """
 import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
 from minotaur_amd.nl import read_nl            # noqa: E402
-from minotaur_amd.problem import from_nl_linear, knapsack_oa  # noqa: E402
+from minotaur_amd.problem import from_nl_linear, knapsack_oa, nvs08_oa  # noqa: E402
 
 REF = os.environ.get('MINOTAUR_REF', '/root/reference')
 OUT = os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd', 'instances')
@@ -24,6 +26,9 @@ def main():
                           name='tls4-lin')
     tls4.save(os.path.join(OUT, 'tls4_lin.npz'))
     print('tls4-lin', tls4.n, tls4.m, tls4.nnz)
+    nv = nvs08_oa(read_nl(os.path.join(REF, 'test_instances', 'nvs08.nl')))
+    nv.save(os.path.join(OUT, 'nvs08_oa.npz'))
+    print('nvs08-oa', nv.n, nv.m, nv.nnz)
     ks = knapsack_oa()
     ks.save(os.path.join(OUT, 'knapsack9.npz'))
     print('knapsack9', ks.n, ks.m, ks.nnz)
