@@ -72,11 +72,34 @@ def pmc_traffic(kernel, batch):
     return None, None
 
 
-def cpu_baseline(p, LB, UB, budget_s):
-    """Rank 0, N=1: the same node boxes on ONE host core — FBBT with the
-    reference's own LinearHandler (oracle/_ref, prebuilt) when present else
-    the C restatement, then the dual-simplex restatement warm-started from the
-    root basis (Clp is unavailable: SURVEY §8c)."""
+def host_cpu():
+    """(model name, threads the all-cores leg uses): the OpenMP thread count
+    the box allows (OMP_NUM_THREADS; 16 per GPU on the GPU pool) capped by the
+    CPUs this process may run on."""
+    model = "unknown"
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for ln in fh:
+                if ln.startswith('model name'):
+                    model = ln.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    avail = len(os.sched_getaffinity(0))
+    want = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or avail
+    return model, max(1, min(want, avail))
+
+
+def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
+    """Rank 0, N=1, the same node boxes on the host:
+
+    * all-cores leg (the reported value): the C restatement of the FBBT
+      (bit-identical to the reference's LinearHandler::presolveNode, pinned
+      by tests/golden/fbbt_*.npz) and of the dual simplex warm-started from
+      the root basis, OpenMP over nodes on every core the box grants;
+    * one-core leg: FBBT by the reference's own LinearHandler::presolveNode
+      (oracle/_ref, prebuilt) when present, then the same dual simplex.
+    Clp is unavailable, so the LP is the restatement in both."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle
     use_ref = oracle.have_ref()
@@ -86,41 +109,56 @@ def cpu_baseline(p, LB, UB, budget_s):
     except OSError:
         use_ref = False
     _, _, _, _, _, ws = oracle.dual_simplex_root(p)
+    model, T = host_cpu()
 
-    def run(lb, ub):
+    def run(lb, ub, threads, ref):
         t0 = time.perf_counter()
-        if use_ref:
+        if ref:
             f = oracle.ref_linear_fbbt(p, lb, ub, None)
         else:
-            f = oracle.linear_fbbt(p, lb, ub, None)
+            f = oracle.linear_fbbt(p, lb, ub, None, nthreads=threads)
         t1 = time.perf_counter()
         keep = f.infeas == 0
-        st, obj, it, _ = oracle.dual_simplex(p, f.lb[keep], f.ub[keep], ws, nthreads=1)
+        oracle.dual_simplex(p, f.lb[keep], f.ub[keep], ws, nthreads=threads)
         t2 = time.perf_counter()
         return t1 - t0, t2 - t1, int(keep.sum())
 
-    probe = min(256, LB.shape[0])
-    a, b, _ = run(LB[:probe], UB[:probe])
-    per = (a + b) / probe
-    # about budget_s of one-core work: the rank-0 boxes, extended (when the
-    # budget asks for more) by further boxes of the same generator
-    S = int(min(16 * LB.shape[0], max(probe, budget_s / max(per, 1e-9))))
-    what = f"first {S} of the rank-0 node boxes"
-    if S > LB.shape[0]:
+    def sample(S):
+        if S <= LB.shape[0]:
+            return LB[:S], UB[:S], f"first {S} of the rank-0 node boxes"
         from minotaur_amd.problem import random_boxes
         XL, XU = random_boxes(p, S - LB.shape[0], 99991)
-        what = (f"the {LB.shape[0]} rank-0 node boxes + {XL.shape[0]} more of the same "
-                "generator")
-        LB, UB = np.concatenate([LB, XL]), np.concatenate([UB, XU])
-    tf, tl, solved = run(LB[:S], UB[:S])
+        return (np.concatenate([LB, XL]), np.concatenate([UB, XU]),
+                f"the {LB.shape[0]} rank-0 node boxes + {XL.shape[0]} more of the same generator")
+
+    def leg(threads, ref, budget):
+        probe = min(256 * threads, LB.shape[0])
+        a, b, _ = run(LB[:probe], UB[:probe], threads, ref)
+        per = (a + b) / probe
+        S = int(min(64 * LB.shape[0], max(probe, budget / max(per, 1e-9))))
+        lb, ub, what = sample(S)
+        tf, tl, solved = run(lb, ub, threads, ref)
+        return S, tf, tl, solved, what
+
+    S, tf, tl, solved, what = leg(T, False, 0.5 * budget_s)
+    S1, tf1, tl1, solved1, what1 = leg(1, use_ref, 0.5 * budget_s)
+    fb1 = ('the reference LinearHandler::presolveNode (oracle/_ref)' if use_ref
+           else 'the C restatement')
     return {
-        "value": S / (tf + tl), "unit": "nodes/s", "cores": 1,
-        "kind": "reference" if use_ref else "port",
-        "sample": (f"{what} (tls4-lin), one core: FBBT by "
-                   f"{'the reference LinearHandler::presolveNode (oracle/_ref)' if use_ref else 'the C restatement'}"
-                   f" {tf:.2f}s, then {solved} warm-started LPs by the dual-simplex "
-                   f"restatement (Clp absent) {tl:.2f}s"),
+        "value": S / (tf + tl), "unit": "nodes/s", "cores": T, "kind": "port",
+        "cpu_model": model,
+        "sample": (f"{what} ({what_inst}), {T} threads (OpenMP over nodes): FBBT by the C "
+                   f"restatement (bit-identical to the reference) {tf:.2f}s, then {solved} "
+                   f"root-warm-started LPs by the dual-simplex restatement (Clp absent) "
+                   f"{tl:.2f}s"),
         "relaxations_per_s": solved / (tf + tl),
+        "one_core": {
+            "value": S1 / (tf1 + tl1), "unit": "nodes/s", "cores": 1,
+            "kind": "reference" if use_ref else "port",
+            "sample": (f"{what1} ({what_inst}), one core: FBBT by {fb1} {tf1:.2f}s, then "
+                       f"{solved1} LPs by the dual-simplex restatement {tl1:.2f}s"),
+            "relaxations_per_s": solved1 / (tf1 + tl1),
+        },
     }
 
 
@@ -167,9 +205,7 @@ def tree_search(ctx, dev, rank, world, B, args):
            "search": "depth-first over batches, MaxVio branching, root-basis warm start"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         LB, UB = random_boxes(p, 4096, 7)
-        c = cpu_baseline(p, LB, UB, 5.0)
-        c["sample"] = c["sample"].replace("tls4-lin", "mkp random-branching boxes")
-        out["cpu_baseline"] = c
+        out["cpu_baseline"] = cpu_baseline(p, LB, UB, 5.0, "mkp random-branching boxes")
     return out
 
 
@@ -300,7 +336,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=131072,
                     help='open nodes per GPU per step (131072: two K1 waves per SIMD)')
-    ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--cpu-seconds', type=float, default=16.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-bnb', action='store_true',
                     help='skip the supplementary full tree search (mkp MILP)')
