@@ -202,7 +202,8 @@ int mgpu_lp_bound_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double
  * nodes, each FBBT (LinearHandler::presolveNode) -> LP (warm-started from
  * the root optimum) -> PCBProcessor::shouldPrune_ / IntVarHandler::
  * isFeasible -> MaxVioBrancher choice -> IntVarHandler::getBranches, with an
- * HBM-resident stack of open nodes (depth-first over batches).
+ * HBM-resident pool of open nodes (depth-first stack or best-first, see
+ * mgpu_bnb_config).
  *   mgpu_bnb_init  : starts a tree at the root box (pool of `capacity`
  *                    nodes) with a known incumbent value (+INF if none).
  *   mgpu_bnb_round : one round; `incumbent` may lower the incumbent (e.g.
@@ -219,7 +220,26 @@ typedef struct {
   int open;                     /* open nodes after the last round        */
   int last_batch;               /* nodes evaluated in the last round      */
   double incumbent;             /* best objective value (+INF if none)    */
+  long long pruned;             /* best-first: open nodes pruned by the
+                                   incumbent before evaluation
+                                   (TreeManager::getCandidate)            */
 } mgpu_bnb_stats;
+
+/* Search options of the next mgpu_bnb_init (default 0, 0):
+ *   order 0: depth-first over batches (the pool is a stack; the preferred
+ *            child is popped first, TreeManager's dive);
+ *   order 1: best-first (TreeManager tree_search "bfs", NodeHeap.cpp:24-47):
+ *            each round takes the `batch` open nodes with the lowest
+ *            (bound, pool slot), after pruning the open nodes whose bound
+ *            cannot beat the incumbent (TreeManager::getCandidate /
+ *            shouldPrune_, TreeManager.cpp:162-186, :403-413);
+ *   warm 0:  every node LP starts from the root optimum (one shared basis:
+ *            K3P for m <= 64);
+ *   warm 1:  every node LP starts from its parent's optimal basis
+ *            (NodeIncRelaxer::createNodeRelaxation, NodeIncRelaxer.cpp:
+ *            146-150); the basis lives with the node in HBM, m*4 + (n+m)*9 +
+ *            m*m*8 bytes per pool slot (K3 / K3L per-node warm starts). */
+int mgpu_bnb_config(mgpu_ctx *ctx, int order, int warm);
 
 int mgpu_bnb_init(mgpu_ctx *ctx, int capacity, const double *root_lb, const double *root_ub,
                   double incumbent);

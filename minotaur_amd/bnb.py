@@ -16,10 +16,13 @@ import time
 
 
 def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
-          root_lb=None, root_ub=None):
-    """Tree search on the loaded LinProblem: returns (obj, x, stats, seconds)."""
+          root_lb=None, root_ub=None, order=0, warm=0):
+    """Tree search on the loaded LinProblem: returns (obj, x, stats, seconds).
+    order 0 depth-first / 1 best-first; warm 0 root basis / 1 parent basis
+    (mgpu_bnb_config)."""
     cap = capacity or 64 * batch
     t0 = time.perf_counter()
+    ctx.bnb_config(order, warm)
     ctx.bnb_init(cap, root_lb, root_ub, incumbent)
     st = None
     for _ in range(max_rounds):
@@ -31,7 +34,7 @@ def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
 
 
 def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
-                      capacity=None, max_rounds=10**9, shard_at=None):
+                      capacity=None, max_rounds=10**9, shard_at=None, order=0, warm=0):
     """Node-sharded tree search.  Every rank runs the same deterministic
     rounds until the pool holds at least ``shard_at`` (default 4 * world)
     open nodes, then keeps nodes i = rank (mod world) (mgpu_bnb_shard) and
@@ -40,6 +43,7 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
     tests).  Returns (incumbent, x or None, stats, rounds, nodes_this_rank)."""
     cap = capacity or 64 * batch
     shard_at = shard_at or 4 * world
+    ctx.bnb_config(order, warm)
     ctx.bnb_init(cap, None, None, math.inf)
     inc = math.inf
     sharded = world == 1

@@ -16,6 +16,7 @@
 // exchange the incumbent with an RCCL all-reduce MIN between rounds.
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "bnb_internal.h"
 #include "ctx.h"
@@ -26,15 +27,25 @@ struct BnbState {
   double inc = INFINITY;
   std::vector<double> best_x;
   mgpu_bnb_stats tot{};
+  int order = 0, warm = 0;     // mgpu_bnb_config at init
+  int hw = 0;                  // best-first: pool high-water mark
+  size_t sort_bytes = 0;
   DevBuf plb, pub, pnlb, pdepth;
   DevBuf wlb, wub, inf, nm, st, obj, it, x, dec, cand, bvar, bval, bup, depth_in, pos, bsum,
       bidx, boff, bmin, bcnt, out;
   DevBuf ws_head, ws_st, ws_d, ws_binv, r_st, r_obj, r_it;
+  // best-first selection
+  DevBuf plive, keys, keys2, vals, vals2, sort_tmp, counts;
+  // parent warm starts: per pool slot, per batch (gathered in) and out
+  DevBuf pws_head, pws_st, pws_d, pws_binv, bws_head, bws_st, bws_d, bws_binv, wo_head, wo_st,
+      wo_d, wo_binv;
   void release() {
     for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
                       &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
                       &bmin, &bcnt, &out, &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj,
-                      &r_it})
+                      &r_it, &plive, &keys, &keys2, &vals, &vals2, &sort_tmp, &counts,
+                      &pws_head, &pws_st, &pws_d, &pws_binv, &bws_head, &bws_st, &bws_d,
+                      &bws_binv, &wo_head, &wo_st, &wo_d, &wo_binv})
       b->release();
   }
 };
@@ -53,7 +64,6 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
   if (B <= s.maxb) return MGPU_OK;
   const size_t n = (size_t)s.n, m = (size_t)c->lp.m;
   const size_t nblk = ((size_t)B + 255) / 256;
-  (void)m;
   HIPCHK(c, s.wlb.ensure((size_t)B * n * 8));
   HIPCHK(c, s.wub.ensure((size_t)B * n * 8));
   HIPCHK(c, s.x.ensure((size_t)B * n * 8));
@@ -65,6 +75,17 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
   HIPCHK(c, s.bmin.ensure(nblk * 8));
   HIPCHK(c, s.bcnt.ensure(nblk * 5 * 4));
   HIPCHK(c, s.out.ensure(sizeof(BnbOut)));
+  if (s.warm) {
+    const size_t N = n + m;
+    HIPCHK(c, s.bws_head.ensure((size_t)B * m * 4 + 4));
+    HIPCHK(c, s.bws_st.ensure((size_t)B * N + 4));
+    HIPCHK(c, s.bws_d.ensure((size_t)B * N * 8));
+    HIPCHK(c, s.bws_binv.ensure((size_t)B * m * m * 8 + 8));
+    HIPCHK(c, s.wo_head.ensure((size_t)B * m * 4 + 4));
+    HIPCHK(c, s.wo_st.ensure((size_t)B * N + 4));
+    HIPCHK(c, s.wo_d.ensure((size_t)B * N * 8));
+    HIPCHK(c, s.wo_binv.ensure((size_t)B * m * m * 8 + 8));
+  }
   s.maxb = B;
   return MGPU_OK;
 }
@@ -72,6 +93,15 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
 }  // namespace
 
 extern "C" {
+
+int mgpu_bnb_config(mgpu_ctx *c, int order, int warm) {
+  if (!c) return MGPU_ERR_ARG;
+  if (order < 0 || order > 1 || warm < 0 || warm > 1)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_config: order and warm are 0 or 1");
+  c->bnb_order = order;
+  c->bnb_warm = warm;
+  return MGPU_OK;
+}
 
 int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double *root_ub,
                   double incumbent) {
@@ -87,6 +117,8 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   s->n = n;
   s->cap = capacity;
   s->inc = incumbent;
+  s->order = c->bnb_order;
+  s->warm = c->bnb_warm;
   s->tot.incumbent = incumbent;
   HIPCHK(c, s->plb.ensure((size_t)capacity * n * 8));
   HIPCHK(c, s->pub.ensure((size_t)capacity * n * 8));
@@ -120,6 +152,41 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   s->root_ok = rst == 0;
   s->count = 1;
   s->best_x.assign(n, NAN);
+  if (s->order == 1) {
+    // best-first pool: slot array with live flags, sort keys and scratch
+    HIPCHK(c, s->plive.ensure((size_t)capacity));
+    HIPCHK(c, hipMemsetAsync(s->plive.p, 0, (size_t)capacity, c->stream));
+    const uint8_t one = 1;
+    HIPCHK(c, hipMemcpyAsync(s->plive.p, &one, 1, hipMemcpyHostToDevice, c->stream));
+    for (DevBuf *b : {&s->keys, &s->keys2}) HIPCHK(c, b->ensure((size_t)capacity * 8));
+    for (DevBuf *b : {&s->vals, &s->vals2}) HIPCHK(c, b->ensure((size_t)capacity * 4));
+    HIPCHK(c, s->counts.ensure(16));
+    size_t tb = 0;
+    HIPCHK(c, bnb_sort_pairs(nullptr, tb, s->keys.as<uint64_t>(), s->keys2.as<uint64_t>(),
+                             s->vals.as<uint32_t>(), s->vals2.as<uint32_t>(), capacity,
+                             c->stream));
+    HIPCHK(c, s->sort_tmp.ensure(tb + 16));
+    s->sort_bytes = tb;
+    s->hw = 1;
+  }
+  if (s->warm) {
+    if (!s->root_ok)
+      return fail(c, MGPU_ERR_STATE, "mgpu_bnb_init: parent warm starts need an optimal root");
+    // every pool slot keeps its node's warm start (the parent's optimal basis)
+    HIPCHK(c, s->pws_head.ensure((size_t)capacity * m * 4 + 4));
+    HIPCHK(c, s->pws_st.ensure((size_t)capacity * N + 4));
+    HIPCHK(c, s->pws_d.ensure((size_t)capacity * N * 8));
+    HIPCHK(c, s->pws_binv.ensure((size_t)capacity * m * m * 8 + 8));
+    HIPCHK(c, hipMemcpyAsync(s->pws_head.p, s->ws_head.p, (size_t)m * 4, hipMemcpyDeviceToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(s->pws_st.p, s->ws_st.p, (size_t)N, hipMemcpyDeviceToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(s->pws_d.p, s->ws_d.p, (size_t)N * 8, hipMemcpyDeviceToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(s->pws_binv.p, s->ws_binv.p, (size_t)m * m * 8,
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   return MGPU_OK;
 }
 
@@ -130,29 +197,112 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   BnbState &s = *c->bnb;
   HIPCHK(c, hipSetDevice(c->device));
   if (incumbent < s.inc) s.inc = incumbent;
-  int nb = batch < s.count ? batch : s.count;
-  if (s.count + nb > s.cap) nb = s.cap - s.count;  // children must fit: base + 2 nb <= cap
-  if (nb <= 0) {
-    if (s.count > 0) return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_round: node pool full");
-    if (stats) *stats = s.tot;
-    return MGPU_OK;
+  const int n = s.n, m = c->lp.m, N = n + m;
+  const bool bfs = s.order == 1;
+  int nb, base = 0, live = 0, holes = 0;
+  if (!bfs) {
+    nb = batch < s.count ? batch : s.count;
+    if (s.count + nb > s.cap) nb = s.cap - s.count;  // children must fit: base + 2 nb <= cap
+    if (nb <= 0) {
+      if (s.count > 0) return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_round: node pool full");
+      if (stats) *stats = s.tot;
+      return MGPU_OK;
+    }
+    base = s.count - nb;
+  } else {
+    // TreeManager::getCandidate's pruning by the incumbent, then the keys of
+    // the live nodes; one small read-back gives the live count
+    HIPCHK(c, hipMemsetAsync(s.counts.p, 0, 8, c->stream));
+    HIPCHK(c, launch_bnb_keys(s.pnlb.as<double>(), s.plive.as<uint8_t>(), s.hw, s.inc, s.inc,
+                              s.keys.as<uint64_t>(), s.vals.as<uint32_t>(),
+                              s.counts.as<int32_t>(), c->stream));
+    int32_t cnt[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(cnt, s.counts.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    live = cnt[0];
+    s.tot.pruned += cnt[1];
+    s.count = live;
+    holes = s.hw - live;
+    nb = batch < live ? batch : live;
+    if (nb <= 0) {
+      s.tot.open = 0;
+      if (stats) *stats = s.tot;
+      return MGPU_OK;
+    }
+    const long grow = 2L * nb - nb - holes;  // new slots the children may need
+    if (s.hw + (grow > 0 ? grow : 0) > s.cap)
+      return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_round: node pool full (%d slots)", s.cap);
   }
   int rc = ensure_batch(c, s, nb);
   if (rc != MGPU_OK) return rc;
-  const int n = s.n;
-  const int base = s.count - nb;
-  const double *lb = s.plb.as<double>() + (size_t)base * n;
-  const double *ub = s.pub.as<double>() + (size_t)base * n;
+  const double *lb, *ub;
+  const int32_t *w_head = nullptr;
+  const int8_t *w_st = nullptr;
+  const double *w_d = nullptr, *w_binv = nullptr;
+  if (!bfs) {
+    lb = s.plb.as<double>() + (size_t)base * n;
+    ub = s.pub.as<double>() + (size_t)base * n;
+    if (s.warm) {  // the popped nodes are contiguous: their bases are read in place
+      w_head = s.pws_head.as<int32_t>() + (size_t)base * m;
+      w_st = s.pws_st.as<int8_t>() + (size_t)base * N;
+      w_d = s.pws_d.as<double>() + (size_t)base * N;
+      w_binv = s.pws_binv.as<double>() + (size_t)base * m * m;
+    }
+  } else {
+    size_t tb = s.sort_bytes;
+    HIPCHK(c, bnb_sort_pairs(s.sort_tmp.p, tb, s.keys.as<uint64_t>(), s.keys2.as<uint64_t>(),
+                             s.vals.as<uint32_t>(), s.vals2.as<uint32_t>(), s.hw, c->stream));
+    BnbSelIO g{};
+    g.nb = nb;
+    g.n = n;
+    g.m = m;
+    g.N = N;
+    g.slots = s.vals2.as<uint32_t>();
+    g.plb = s.plb.as<double>();
+    g.pub = s.pub.as<double>();
+    g.pdepth = s.pdepth.as<int32_t>();
+    g.plive = s.plive.as<uint8_t>();
+    g.wlb = s.wlb.as<double>();
+    g.wub = s.wub.as<double>();
+    g.depth_in = s.depth_in.as<int32_t>();
+    if (s.warm) {
+      g.ws_head = s.pws_head.as<int32_t>();
+      g.ws_st = s.pws_st.as<int8_t>();
+      g.ws_d = s.pws_d.as<double>();
+      g.ws_binv = s.pws_binv.as<double>();
+      g.bws_head = s.bws_head.as<int32_t>();
+      g.bws_st = s.bws_st.as<int8_t>();
+      g.bws_d = s.bws_d.as<double>();
+      g.bws_binv = s.bws_binv.as<double>();
+      w_head = g.bws_head;
+      w_st = g.bws_st;
+      w_d = g.bws_d;
+      w_binv = g.bws_binv;
+    }
+    HIPCHK(c, launch_bnb_gather(g, c->stream));
+    lb = s.wlb.as<double>();
+    ub = s.wub.as<double>();
+  }
   rc = mgpu_fbbt_dev(c, nb, lb, ub, s.inc, s.wlb.as<double>(), s.wub.as<double>(),
                      s.inf.as<int32_t>(), s.nm.as<int32_t>(), 0, nullptr, nullptr, nullptr);
   if (rc != MGPU_OK) return rc;
-  rc = mgpu_lp_solve_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(),
-                         s.root_ok ? s.ws_head.as<int32_t>() : nullptr,
-                         s.root_ok ? s.ws_st.as<int8_t>() : nullptr,
-                         s.root_ok ? s.ws_d.as<double>() : nullptr,
-                         s.root_ok ? s.ws_binv.as<double>() : nullptr, 1, 0,
-                         s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
-                         s.x.as<double>(), nullptr, nullptr, nullptr, nullptr);
+  if (s.warm) {
+    // each node from its parent's optimal basis (NodeIncRelaxer.cpp:146-150);
+    // its own optimal basis comes back for its children
+    rc = mgpu_lp_solve_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(),
+                           w_head, w_st, w_d, w_binv, 0, 0, s.st.as<int32_t>(),
+                           s.obj.as<double>(), s.it.as<int32_t>(), s.x.as<double>(),
+                           s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), s.wo_d.as<double>(),
+                           s.wo_binv.as<double>());
+  } else {
+    rc = mgpu_lp_solve_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(),
+                           s.root_ok ? s.ws_head.as<int32_t>() : nullptr,
+                           s.root_ok ? s.ws_st.as<int8_t>() : nullptr,
+                           s.root_ok ? s.ws_d.as<double>() : nullptr,
+                           s.root_ok ? s.ws_binv.as<double>() : nullptr, 1, 0,
+                           s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
+                           s.x.as<double>(), nullptr, nullptr, nullptr, nullptr);
+  }
   if (rc != MGPU_OK) return rc;
   DecideIO d{};
   d.batch = nb;
@@ -194,12 +344,36 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   io.bmin = s.bmin.as<double>();
   io.bcnt = s.bcnt.as<int32_t>();
   io.out = s.out.as<BnbOut>();
+  if (bfs) {
+    io.slots = s.vals2.as<uint32_t>();
+    io.live = live;
+    io.hw = s.hw;
+    io.plive = s.plive.as<uint8_t>();
+  }
+  if (s.warm) {
+    io.m = m;
+    io.N = N;
+    io.wo_head = s.wo_head.as<int32_t>();
+    io.wo_st = s.wo_st.as<int8_t>();
+    io.wo_d = s.wo_d.as<double>();
+    io.wo_binv = s.wo_binv.as<double>();
+    io.ws_head = s.pws_head.as<int32_t>();
+    io.ws_st = s.pws_st.as<int8_t>();
+    io.ws_d = s.pws_d.as<double>();
+    io.ws_binv = s.pws_binv.as<double>();
+  }
   HIPCHK(c, hipMemsetAsync(s.out.p, 0, sizeof(BnbOut), c->stream));
   HIPCHK(c, launch_bnb_tail(io, n, c->stream));
   BnbOut o;
   HIPCHK(c, hipMemcpyAsync(&o, s.out.p, sizeof o, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  s.count = base + 2 * o.nbranched;
+  if (!bfs) {
+    s.count = base + 2 * o.nbranched;
+  } else {
+    s.count = live - nb + 2 * o.nbranched;
+    const long grow = 2L * o.nbranched - nb - holes;
+    if (grow > 0) s.hw += (int)grow;
+  }
   if (o.best_idx >= 0 && o.best < s.inc) {
     s.inc = o.best;
     HIPCHK(c, hipMemcpy(s.best_x.data(), s.x.as<double>() + (size_t)o.best_idx * n,
@@ -228,6 +402,25 @@ int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_shard: bad rank/world");
   BnbState &s = *c->bnb;
   HIPCHK(c, hipSetDevice(c->device));
+  if (s.order == 1) {
+    // best-first pool: keep the live nodes whose index among the live nodes
+    // in slot order is rank (mod world); the others become free slots
+    std::vector<uint8_t> live((size_t)(s.hw > 0 ? s.hw : 1));
+    HIPCHK(c, hipMemcpyAsync(live.data(), s.plive.p, (size_t)s.hw, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int k = 0, idx = 0;
+    for (int i = 0; i < s.hw; ++i) {
+      if (!live[i]) continue;
+      if (idx++ % world == rank) ++k;
+      else live[i] = 0;
+    }
+    HIPCHK(c, hipMemcpy(s.plive.p, live.data(), (size_t)s.hw, hipMemcpyHostToDevice));
+    s.count = k;
+    s.tot.open = k;
+    if (kept) *kept = k;
+    return MGPU_OK;
+  }
   const size_t cnt = (size_t)(s.count > 0 ? s.count : 1);
   DevBuf tlb, tub, tnlb, tdep;  // scratch for this call only
   HIPCHK(c, tlb.ensure(cnt * s.n * 8));

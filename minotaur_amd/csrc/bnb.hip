@@ -34,7 +34,8 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
   const int i = blockIdx.x * kScanBlock + t;
   const bool live = i < io.nb;
   const int dec = live ? io.decision[i] : -1;
-  if (live) io.depth_in[i] = io.pdepth[io.base + i];  // before children overwrite the slots
+  // stack mode: depth before children overwrite the slots (best-first: gathered)
+  if (live && io.slots == nullptr) io.depth_in[i] = io.pdepth[io.base + i];
   const int f = dec == 0 ? 1 : 0;
   s_pos[t] = f;
   s_min[t] = live ? io.cand_obj[i] : INFINITY;
@@ -133,7 +134,8 @@ __global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
 }
 
 // One wave per node: copy the node's (FBBT-tightened) box into its two
-// children, apply the branching bound, set the children's lower bound.
+// children, apply the branching bound, set the children's lower bound (and,
+// with parent warm starts, give both children the node's optimal basis).
 __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -142,11 +144,25 @@ __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
   const int j = io.bvar[i];
   const double v = io.bval[i];
   const bool up_first = io.bup[i] != 0;
-  // stack order: slot base + 2p + 1 is popped first
-  const size_t c_first = (size_t)io.base + 2 * (size_t)p + 1;
-  const size_t c_second = c_first - 1;
-  const size_t c_down = up_first ? c_second : c_first;
-  const size_t c_up = up_first ? c_first : c_second;
+  size_t c_down, c_up;
+  if (io.slots == nullptr) {
+    // stack order: slot base + 2p + 1 is popped first
+    const size_t c_first = (size_t)io.base + 2 * (size_t)p + 1;
+    const size_t c_second = c_first - 1;
+    c_down = up_first ? c_second : c_first;
+    c_up = up_first ? c_first : c_second;
+  } else {
+    // free list F: the preferred child takes the lower child index 2p
+    auto slot_of = [&](long c) -> size_t {
+      if (c < io.nb) return io.slots[c];
+      const long h = c - io.nb, holes = io.hw - io.live;
+      if (h < holes) return io.slots[io.live + h];
+      return (size_t)(io.hw + (h - holes));
+    };
+    const size_t c_first = slot_of(2L * p), c_second = slot_of(2L * p + 1);
+    c_down = up_first ? c_second : c_first;
+    c_up = up_first ? c_first : c_second;
+  }
   const double *sl = io.wlb + (size_t)i * n, *su = io.wub + (size_t)i * n;
   double *dl = io.plb + c_down * n, *du = io.pub + c_down * n;
   double *ul = io.plb + c_up * n, *uu = io.pub + c_up * n;
@@ -157,12 +173,38 @@ __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
     ul[k] = k == j ? ceil(v) : l;
     uu[k] = u;
   }
+  if (io.ws_head != nullptr) {
+    const int m = io.m, N = io.N;
+    const size_t mm = (size_t)m * m;
+    for (int k = lane; k < m; k += 64) {
+      const int32_t h = io.wo_head[(size_t)i * m + k];
+      io.ws_head[c_down * m + k] = h;
+      io.ws_head[c_up * m + k] = h;
+    }
+    for (int k = lane; k < N; k += 64) {
+      const int8_t st = io.wo_st[(size_t)i * N + k];
+      const double d = io.wo_d[(size_t)i * N + k];
+      io.ws_st[c_down * N + k] = st;
+      io.ws_st[c_up * N + k] = st;
+      io.ws_d[c_down * N + k] = d;
+      io.ws_d[c_up * N + k] = d;
+    }
+    for (size_t k = lane; k < mm; k += 64) {
+      const double b = io.wo_binv[(size_t)i * mm + k];
+      io.ws_binv[c_down * mm + k] = b;
+      io.ws_binv[c_up * mm + k] = b;
+    }
+  }
   if (lane == 0) {
     const double bound = io.obj[i];
     io.pnlb[c_down] = bound;
     io.pnlb[c_up] = bound;
     io.pdepth[c_down] = io.depth_in[i] + 1;
     io.pdepth[c_up] = io.depth_in[i] + 1;
+    if (io.plive != nullptr) {
+      io.plive[c_down] = 1;
+      io.plive[c_up] = 1;
+    }
   }
 }
 

@@ -61,6 +61,8 @@ struct mgpu_ctx {
   int fbbt_variant = 0;
   int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L, 3 K3P
   int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)
+  int bnb_order = 0;           // mgpu_bnb_config: 0 depth-first stack, 1 best-first
+  int bnb_warm = 0;            // mgpu_bnb_config: 0 root basis, 1 parent basis
   DevBuf lp_slots;             // K3L: one B^-1 [m][m] per resident workgroup
   DevBuf lp_next;              // K3L: node counter of the dynamic schedule
   DevBuf pfi_ovf;              // K3P: overflow counter + node list

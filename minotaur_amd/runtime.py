@@ -29,7 +29,7 @@ EXPORTS = [
     'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
     'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
-    'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_strong_branch',
+    'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_bnb_config', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
 ]
 
@@ -38,7 +38,8 @@ class BnbStats(ctypes.Structure):
     """mgpu_bnb_stats (include/mgpu.h)."""
     _fields_ = [('rounds', ctypes.c_longlong), ('nodes', ctypes.c_longlong),
                 ('ndec', ctypes.c_longlong * 5), ('open', ctypes.c_int),
-                ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double)]
+                ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double),
+                ('pruned', ctypes.c_longlong)]
 
 _lib = None
 
@@ -89,6 +90,7 @@ def load_library():
     lib.mgpu_lp_bound.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
     lib.mgpu_lp_bound_dev.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
     lib.mgpu_bnb_init.argtypes = [_P, _I, _P, _P, _D]
+    lib.mgpu_bnb_config.argtypes = [_P, _I, _I]
     lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
     lib.mgpu_bnb_best.argtypes = [_P, _P, _P]
     lib.mgpu_bnb_shard.argtypes = [_P, _I, _I, _P]
@@ -422,6 +424,11 @@ class Context:
             _dp(iters), _dp(x)), 'mgpu_lp_bound_dev')
 
     # -- batched branch-and-bound ---------------------------------------------
+    def bnb_config(self, order=0, warm=0):
+        """Next tree: order 0 depth-first / 1 best-first; warm 0 root basis /
+        1 parent basis (mgpu_bnb_config)."""
+        self._chk(self.lib.mgpu_bnb_config(self.h, int(order), int(warm)), 'mgpu_bnb_config')
+
     def bnb_init(self, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
         p = self.problem
         lb = _np(p.vlb if root_lb is None else root_lb, np.float64)

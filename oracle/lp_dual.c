@@ -668,3 +668,32 @@ int orc_lp_bound_batch(int n, int m, const int *colptr, const int *rowidx, const
   }
   return 0;
 }
+
+/* Per-node warm starts in and out (the batched tree's parent warm starts,
+ * NodeIncRelaxer.cpp:146-150): node b starts from ws_*[b] (head [m], st
+ * [n+m], binv [m][m] row-major, d [n+m]) and leaves its final basis in
+ * wo_*[b]; dense explicit-inverse arithmetic (the K3 / K3L restatement). */
+int orc_dual_simplex_nodes(int n, int m, const int *colptr, const int *rowidx,
+                           const double *cval, const double *c, const double *rlo,
+                           const double *rhi, int B, const double *lb, const double *ub,
+                           const int *ws_head, const signed char *ws_st, const double *ws_binv,
+                           const double *ws_d, int iter_limit, int *status, double *obj,
+                           double *x, int *iters, int *wo_head, signed char *wo_st,
+                           double *wo_binv, double *wo_d, int nthreads)
+{
+  orc_lp P;
+  P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cval; P.c = c;
+  P.rlo = rlo; P.rhi = rhi;
+  if (nthreads < 1) nthreads = 1;
+  const size_t N = (size_t) (n + m), mm = (size_t) m * m;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 8)
+  for (int b = 0; b < B; ++b) {
+    status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n, ws_head + (size_t) b * m,
+                             ws_st + (size_t) b * N, ws_binv + (size_t) b * mm,
+                             ws_d + (size_t) b * N, 1, 1, iter_limit, obj + b,
+                             x ? x + (size_t) b * n : 0, iters + b, 0, wo_head + (size_t) b * m,
+                             wo_st + (size_t) b * N, wo_binv + (size_t) b * mm,
+                             wo_d + (size_t) b * N);
+  }
+  return 0;
+}

@@ -207,6 +207,35 @@ def dual_simplex(p, LB, UB, ws=None, iter_limit=10000, nthreads=1, want_x=False,
     return st, obj, it, x
 
 
+def dual_simplex_nodes(p, LB, UB, ws, iter_limit=10000, nthreads=1):
+    """Per-node warm starts in and out (dense arithmetic, K3/K3L): ws is a
+    WarmStart whose arrays carry a leading batch axis (binv row-major);
+    returns (status, obj incl. constant, iters, x, WarmStart out)."""
+    l = lib()
+    l.orc_dual_simplex_nodes.restype = _I
+    l.orc_dual_simplex_nodes.argtypes = [_I, _I] + [_P] * 6 + [_I] + [_P] * 6 + [_I] + \
+        [_P] * 8 + [_I]
+    LB = np.ascontiguousarray(LB, dtype=np.float64)
+    UB = np.ascontiguousarray(UB, dtype=np.float64)
+    B = LB.shape[0]
+    colptr, rowidx, cval = lp_csc(p)
+    h = np.ascontiguousarray(ws.head, dtype=np.int32)
+    s = np.ascontiguousarray(ws.st, dtype=np.int8)
+    bi = np.ascontiguousarray(ws.binv, dtype=np.float64)
+    dd = np.ascontiguousarray(ws.d, dtype=np.float64)
+    st = np.zeros(B, dtype=np.int32)
+    obj = np.zeros(B)
+    it = np.zeros(B, dtype=np.int32)
+    x = np.zeros((B, p.n))
+    wo = WarmStart(np.zeros_like(h), np.zeros_like(s), np.zeros_like(bi), np.zeros_like(dd))
+    l.orc_dual_simplex_nodes(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj),
+                             _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(h), _ptr(s),
+                             _ptr(bi), _ptr(dd), iter_limit, _ptr(st), _ptr(obj), _ptr(x),
+                             _ptr(it), _ptr(wo.head), _ptr(wo.st), _ptr(wo.binv), _ptr(wo.d),
+                             nthreads)
+    return st, obj + p.obj_const, it, x, wo
+
+
 def dual_simplex_root(p, lb=None, ub=None, iter_limit=100000):
     l = lib()
     _lp_sig(l)

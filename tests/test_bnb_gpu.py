@@ -131,3 +131,65 @@ def test_bnb_k3l_tree_matches_cpu_and_highs(ctx):
     assert og == oc
     assert hs == 0 and abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
     _check_solution(p, xg, og)
+
+
+@pytest.mark.parametrize('order,warm', [(1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize('k', range(4))
+def test_bnb_search_modes_match_cpu_and_highs(ctx, k, order, warm):
+    """Best-first selection (TreeManager bfs: lowest bound first, open nodes
+    pruned by the incumbent before evaluation) and parent warm starts
+    (NodeIncRelaxer.cpp:146-150: each node LP from its parent's optimal
+    basis, K3 / K3L per-node warm starts): the GPU tree is the CPU
+    restatement's tree (rounds, nodes, decisions, pruned-open counts) and
+    proves the HiGHS MILP optimum."""
+    import os
+    from bnb import CpuBnbContext
+    from minotaur_amd.problem import LinProblem
+    cases = [knapsack_oa(), random_mkp(6, 16, 3), random_mkp(1, 30, 4),
+             LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
+                                          'instances', 'nvs08_oa.npz'))]
+    p = cases[k]
+    hs, hobj = oracle.highs_milp(p)
+    ctx.load(p)
+    og, xg, sg, _ = bnb.solve(ctx, batch=64, capacity=1 << 15, order=order, warm=warm)
+    oc, xc, sc, _ = bnb.solve(CpuBnbContext(p, ctx.oracle_pfi()), batch=64, capacity=1 << 15,
+                              order=order, warm=warm)
+    assert sg.open == sc.open == 0
+    assert (sg.rounds, sg.nodes, list(sg.ndec), sg.pruned) == \
+        (sc.rounds, sc.nodes, list(sc.ndec), sc.pruned)
+    assert abs(og - oc) <= 1e-9 * max(1.0, abs(oc))
+    assert hs == 0 and abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
+    _check_solution(p, xg, og)
+
+
+def test_bnb_best_first_k3l_parent_warm(ctx):
+    """m > 64 (knapsack OA f = 17, K3L node LPs) with parent warm starts and
+    best-first selection: same tree as the CPU restatement, HiGHS optimum."""
+    from bnb import CpuBnbContext
+    p = knapsack_oa(f=17, N=64)
+    hs, hobj = oracle.highs_milp(p)
+    ctx.load(p)
+    og, xg, sg, _ = bnb.solve(ctx, batch=256, capacity=1 << 16, order=1, warm=1)
+    oc, _, sc, _ = bnb.solve(CpuBnbContext(p, ctx.oracle_pfi()), batch=256, capacity=1 << 16,
+                             order=1, warm=1)
+    assert (sg.rounds, sg.nodes, list(sg.ndec), sg.pruned) == \
+        (sc.rounds, sc.nodes, list(sc.ndec), sc.pruned)
+    assert og == oc
+    assert hs == 0 and abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
+
+
+def test_bnb_tls4_lin_root_is_integral(ctx):
+    """Config 2's tree: tls4-lin's root LP optimum is already integral (value
+    0, as HiGHS' MILP finds at its root node), so the branch-and-bound search
+    on it is one node in every search mode."""
+    import os
+    from minotaur_amd.problem import LinProblem
+    p = LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
+                                     'instances', 'tls4_lin.npz'))
+    hs, hobj = oracle.highs_milp(p)
+    ctx.load(p)
+    for order, warm in ((0, 0), (1, 0), (1, 1)):
+        og, xg, sg, _ = bnb.solve(ctx, batch=1024, capacity=1 << 12, order=order, warm=warm)
+        assert sg.nodes == 1 and sg.ndec[3] == 1
+        assert hs == 0 and abs(og - hobj) <= 1e-9
+        _check_solution(p, xg, og)
