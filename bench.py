@@ -162,17 +162,15 @@ def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
     }
 
 
-def tree_search(ctx, dev, rank, world, B, args):
-    """Supplementary: a COMPLETE branch-and-bound tree on a weak-bound MILP
-    (multi-dimensional knapsack n=60, m=8) with the batched driver
-    (mgpu_bnb_*), node-sharded across ranks with an incumbent all-reduce MIN
-    per round; the proven optimum is checked against the value HiGHS gives."""
+def run_tree(ctx, dev, rank, world, p, B, order, warm, cap):
+    """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
+    across ranks after the shared first rounds, incumbent all-reduce MIN per
+    round.  Returns (incumbent, nodes, LP solves, pivots, pruned-open,
+    rounds, seconds) — counts summed over ranks, seconds the max."""
     import torch
     import torch.distributed as dist
     from minotaur_amd import bnb
     from minotaur_amd import dist as mdist
-    from minotaur_amd.problem import random_boxes, random_mkp
-    p = random_mkp(1, 60, 8)
 
     def amin(v):
         t = torch.tensor([v], dtype=torch.float64, device=dev)
@@ -183,29 +181,122 @@ def tree_search(ctx, dev, rank, world, B, args):
         return float(mdist.allreduce_max(t).item())
 
     ctx.load(p)
-    bnb.solve_distributed(ctx, 1024, rank, world, amin, amax, capacity=1 << 16,
-                          max_rounds=3)                       # warm-up (kernel loads)
+    bnb.solve_distributed(ctx, 64, rank, world, amin, amax, capacity=1 << 14, max_rounds=2,
+                          order=order, warm=warm)            # warm-up (kernel loads)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, amin, amax,
-                                                     capacity=1 << 22)
+                                                     capacity=cap, order=order, warm=warm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    nd = torch.tensor([float(mine)], dtype=torch.float64, device=dev)
+    cnt = torch.tensor([float(mine[k]) for k in ('nodes', 'lps', 'pivots', 'pruned')],
+                       dtype=torch.float64, device=dev)
     mdist.allreduce_max(el)
-    mdist.allreduce_sum(nd)
-    el, nodes = float(el.item()), float(nd.item())
-    out = {"instance": p.name, "vars": p.n, "rows": p.m, "nodes": nodes, "seconds": el,
-           "nodes_per_s": nodes / el, "rounds": rounds, "batch_per_gpu": B,
-           "optimum": inc, "optimum_highs": -1915.0,
-           "search": "depth-first over batches, MaxVio branching, root-basis warm start"}
+    mdist.allreduce_sum(cnt)
+    c = [float(v) for v in cnt.tolist()]
+    return inc, c[0], c[1], c[2], c[3], rounds, float(el.item())
+
+
+# Complete trees in the bench line: config 2's own instance,
+# config 1's OA-LP, and a weak-bound MILP whose tree is large enough to time
+# the driver's throughput (multi-dimensional knapsack n = 60, m = 8).
+TREES = [("tls4_lin", "instance", 1, 0, 0.0),
+         ("nvs08_oa", "instance", 1, 0, None),
+         ("mkp-1-n60-m8", "mkp", 0, 0, -1915.0),
+         ("mkp-1-n60-m8", "mkp", 1, 0, -1915.0),
+         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0)]
+
+
+def tree_search(ctx, dev, rank, world, B, args):
+    """Supplementary: complete branch-and-bound trees (every node popped from
+    the HBM pool, children pushed, incumbent pruning) with their proven
+    optima checked against HiGHS' MILP value."""
+    from minotaur_amd.problem import LinProblem, random_boxes, random_mkp
+    out = []
+    for name, kind, order, warm, opt in TREES:
+        if kind == "mkp":
+            p = random_mkp(1, 60, 8)
+        else:
+            p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', f'{name}.npz'))
+        if opt is None:
+            sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+            import oracle
+            opt = oracle.highs_milp(p)[1]
+        inc, nodes, lps, piv, pruned, rounds, el = run_tree(ctx, dev, rank, world, p, B, order,
+                                                            warm, 1 << 22)
+        out.append({"instance": p.name, "vars": p.n, "rows": p.m,
+                    "search": ("best-first" if order else "depth-first over batches") +
+                              (", parent-basis warm starts" if warm else
+                               ", root-basis warm start") + ", MaxVio branching",
+                    "nodes": nodes, "lp_solves": lps, "pivots_per_lp": piv / max(lps, 1.0),
+                    "pruned_open": pruned, "rounds": rounds, "seconds": el,
+                    "nodes_per_s": nodes / el, "relaxations_per_s": lps / el,
+                    "batch_per_gpu": B, "optimum": inc, "optimum_highs": opt,
+                    "optimum_matches_highs": bool(abs(inc - opt) <= 1e-6 * max(1.0, abs(opt)))})
+        if kind == "mkp" and order == 0 and rank == 0 and world == 1 \
+                and not args.no_cpu_baseline:
+            LB, UB = random_boxes(p, 4096, 7)
+            out[-1]["cpu_baseline"] = cpu_baseline(p, LB, UB, 6.0, "mkp random-branching boxes")
+    return out
+
+
+def knapsack_nodes(ctx, dev, rank, world, args, reps=50):
+    """Supplementary (config 3): 1000 synthetic knapsack-MINLP
+    nodes (seeded boxes of [1, 64]^9, seed 7) of the examples/knapsack OA-LP
+    (f = 9, N = 64, 4 tangents per term: m = 37), batched FBBT + LP relaxation
+    from the root basis + decision, repeated `reps` times."""
+    import torch
+    from minotaur_amd import dist as mdist
+    from minotaur_amd.problem import knapsack_oa, random_boxes
+    from minotaur_amd.runtime import WarmStart
+    p = knapsack_oa()
+    ctx.load(p)
+    root, ws_h = ctx.root_solve()
+    ws = WarmStart(*(torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                     for a in (ws_h.head, ws_h.st, ws_h.d, ws_h.binv)))
+    LB, UB = random_boxes(p, 1000, mdist.shard_seed(7, rank))
+    B = LB.shape[0]
+    lb0, ub0 = torch.from_numpy(LB).to(dev), torch.from_numpy(UB).to(dev)
+    lb1, ub1 = torch.empty_like(lb0), torch.empty_like(ub0)
+    z32 = lambda: torch.zeros(B, dtype=torch.int32, device=dev)   # noqa: E731
+    inf, nm, st, it, dec = z32(), z32(), z32(), z32(), z32()
+    ob = torch.zeros(B, dtype=torch.float64, device=dev)
+    x = torch.zeros((B, p.n), dtype=torch.float64, device=dev)
+
+    def step():
+        ctx.fbbt_dev(lb0, ub0, lb1, ub1, inf, nm)
+        ctx.lp_solve_dev(lb1, ub1, st, ob, it, ws=ws, skip=inf, x=x)
+        ctx.node_decide_dev(st, ob, x, dec, fbbt_infeas=inf)
+
+    step()
+    torch.cuda.synchronize()
+    fb, lp = [], []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+        fb.append(ctx.last_kernel_ms('fbbt'))
+        lp.append(ctx.last_kernel_ms('lp'))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    solved = int((st != 12).sum().item())
+    piv = int(it.sum().item())
+    fbm, lpm = float(np.median(fb)), float(np.median(lp))
+    lpf = lp_flops(p, piv, solved)
+    out = {"instance": f"{p.name} ({p.m} rows, {p.n} cols)", "nodes": B, "reps": reps,
+           "nodes_per_s": B * reps / el, "relaxations_per_s": solved * reps / el,
+           "ms_per_batch": 1e3 * el / reps, "fbbt_ms": fbm, "lp_ms": lpm,
+           "pivots_per_lp": piv / max(solved, 1),
+           "roofline": {"kernel": "lp", "bound": "fp64", "unit": "TFLOP/s",
+                        "achieved": lpf / (lpm * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                        "frac": lpf / (lpm * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                        "note": "1000 LPs are a fraction of one wave per SIMD: launch- and "
+                                "latency-bound by construction"}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        LB, UB = random_boxes(p, 4096, 7)
-        out["cpu_baseline"] = cpu_baseline(p, LB, UB, 5.0, "mkp random-branching boxes")
+        out["cpu_baseline"] = cpu_baseline(p, LB, UB, 4.0, "knapsack boxes")
     return out
 
 
@@ -253,7 +344,7 @@ def convex_batch(ctx, dev, rank, world, B, args):
         if world > 1:
             torch.distributed.barrier()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        nd = torch.tensor([float(mine)], dtype=torch.float64, device=dev)
+        nd = torch.tensor([float(mine['nodes'])], dtype=torch.float64, device=dev)
         mdist.allreduce_max(el)
         mdist.allreduce_sum(nd)
         el, nodes = float(el.item()), float(nd.item())
@@ -344,6 +435,8 @@ def main():
                     help='skip the supplementary convex batch (config 5, knapsack OA trees)')
     ap.add_argument('--no-qp', action='store_true',
                     help='skip the supplementary QP relaxation batch (color_lab2, MFMA KKT)')
+    ap.add_argument('--no-knapsack', action='store_true',
+                    help='skip the supplementary config-3 batch (1000 knapsack nodes)')
     args = ap.parse_args()
 
     import torch
@@ -449,6 +542,7 @@ def main():
     tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, B, args)
     cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, B, args)
     qprel = None if args.no_qp else qp_relaxation(ctx, dev, rank, world, args)
+    ksn = None if args.no_knapsack else knapsack_nodes(ctx, dev, rank, world, args)
     ctx.load(p)
     nodes = float(B) * world * args.steps
     fbbt_ms = float(np.mean(acc["fbbt_ms"]))
@@ -509,9 +603,11 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": ("tls4-lin B&B node batch: K1 FBBT -> K3 warm-started dual-simplex "
-                             "LP (FBBT-infeasible nodes skipped) -> prune/integrality decision; "
-                             "incumbent all-reduce MIN per step"),
+                "workload": ("fixed-batch node throughput: one batch of tls4-lin B&B nodes per "
+                             "GPU re-evaluated every step (K1 FBBT -> K3P dual-simplex LP from "
+                             "the root basis, FBBT-infeasible nodes skipped -> prune/"
+                             "integrality decision; incumbent all-reduce MIN); no branching "
+                             "inside the timed region: complete trees are in tree_search"),
                 "instance": f"tls4-lin ({p.m} rows, {p.n} cols, {p.nnz} nnz)",
                 "nodes_per_gpu": B,
                 "global_batch": B * world,
@@ -526,6 +622,7 @@ def main():
             "tree_search": tree,
             "convex_batch": cvx,
             "qp_relaxation": qprel,
+            "knapsack_nodes": ksn,
         }
         if rehearse:
             line["rehearsal"] = "all ranks on device 0 over gloo (not a scaling number)"

@@ -223,6 +223,8 @@ typedef struct {
   long long pruned;             /* best-first: open nodes pruned by the
                                    incumbent before evaluation
                                    (TreeManager::getCandidate)            */
+  long long lps, pivots;        /* node LPs solved (OsiLPStats::calls) and
+                                   their simplex pivots                   */
 } mgpu_bnb_stats;
 
 /* Search options of the next mgpu_bnb_init (default 0, 0):

@@ -40,7 +40,9 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
     open nodes, then keeps nodes i = rank (mod world) (mgpu_bnb_shard) and
     searches its share; allreduce_min / allreduce_max(float) -> float are
     the collectives (minotaur_amd/dist.py over RCCL, or gloo in the CPU
-    tests).  Returns (incumbent, x or None, stats, rounds, nodes_this_rank)."""
+    tests).  Returns (incumbent, x or None, stats, rounds, mine) where
+    mine = {nodes, lps, pivots, pruned} evaluated by this rank, the shared
+    first rounds counted on rank 0 only (so sums over ranks are exact)."""
     cap = capacity or 64 * batch
     shard_at = shard_at or 4 * world
     ctx.bnb_config(order, warm)
@@ -49,18 +51,20 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
     sharded = world == 1
     st = None
     rounds = 0
-    shared_nodes = 0
+    shared = (0, 0, 0, 0)
     while rounds < max_rounds:
         st = ctx.bnb_round(batch, inc)
         rounds += 1
         open_now = st.open
         if not sharded and (open_now >= shard_at or open_now == 0):
-            shared_nodes = st.nodes          # evaluated identically on every rank
+            shared = (st.nodes, st.lps, st.pivots, st.pruned)   # identical on every rank
             open_now = ctx.bnb_shard(rank, world)
             sharded = True
         inc = allreduce_min(st.incumbent)
         if allreduce_max(float(open_now)) == 0.0:
             break
     obj, x = ctx.bnb_best()
-    mine = st.nodes - (shared_nodes if rank != 0 else 0)
+    sub = shared if rank != 0 else (0, 0, 0, 0)
+    mine = {k: v - w for k, v, w in zip(('nodes', 'lps', 'pivots', 'pruned'),
+                                         (st.nodes, st.lps, st.pivots, st.pruned), sub)}
     return inc, (x if obj == inc else None), st, rounds, mine

@@ -73,7 +73,7 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
   HIPCHK(c, s.bup.ensure((size_t)B));
   for (DevBuf *b : {&s.bsum, &s.bidx, &s.boff}) HIPCHK(c, b->ensure(nblk * 4));
   HIPCHK(c, s.bmin.ensure(nblk * 8));
-  HIPCHK(c, s.bcnt.ensure(nblk * 5 * 4));
+  HIPCHK(c, s.bcnt.ensure(nblk * 7 * 4));
   HIPCHK(c, s.out.ensure(sizeof(BnbOut)));
   if (s.warm) {
     const size_t N = n + m;
@@ -325,6 +325,8 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   io.nb = nb;
   io.base = base;
   io.decision = s.dec.as<int32_t>();
+  io.status = s.st.as<int32_t>();
+  io.iters = s.it.as<int32_t>();
   io.cand_obj = s.cand.as<double>();
   io.obj = s.obj.as<double>();
   io.bvar = s.bvar.as<int32_t>();
@@ -382,6 +384,8 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   s.tot.rounds += 1;
   s.tot.nodes += nb;
   for (int k = 0; k < 5; ++k) s.tot.ndec[k] += o.ndec[k];
+  s.tot.lps += o.lps;
+  s.tot.pivots += o.pivots;
   s.tot.open = s.count;
   s.tot.incumbent = s.inc;
   s.tot.last_batch = nb;

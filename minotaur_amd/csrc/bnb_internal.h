@@ -7,6 +7,7 @@ namespace mgpu {
 
 struct BnbOut {                 // per round, device -> host
   long long ndec[5];            // decision counts (mgpu.h decision codes)
+  long long lps, pivots;        // LPs solved (not pruned by FBBT) and their pivots
   int nbranched;                // nodes with decision 0 (2 children each)
   int best_idx;                 // batch index of the best integer-feasible node, -1 none
   double best;                  // its objective (+inf none)
@@ -32,6 +33,8 @@ struct BnbIO {
   int8_t *ws_st;                // [cap][N]
   double *ws_d, *ws_binv;       // [cap][N], [cap][m][m]
   const int32_t *decision;      // [nb]
+  const int32_t *status;        // [nb] LP status (12 = not solved: FBBT-infeasible)
+  const int32_t *iters;         // [nb] LP pivots
   const double *cand_obj;       // [nb]
   const double *obj;            // [nb] relaxation values (children's bound)
   const int32_t *bvar;          // [nb]

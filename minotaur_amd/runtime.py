@@ -39,7 +39,8 @@ class BnbStats(ctypes.Structure):
     _fields_ = [('rounds', ctypes.c_longlong), ('nodes', ctypes.c_longlong),
                 ('ndec', ctypes.c_longlong * 5), ('open', ctypes.c_int),
                 ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double),
-                ('pruned', ctypes.c_longlong)]
+                ('pruned', ctypes.c_longlong), ('lps', ctypes.c_longlong),
+                ('pivots', ctypes.c_longlong)]
 
 _lib = None
 

@@ -39,6 +39,7 @@ class _Stats:
         self.last_batch = 0
         self.incumbent = math.inf
         self.pruned = 0
+        self.lps = self.pivots = 0
 
 
 def _order_key(v):
@@ -131,15 +132,17 @@ class CpuBnbContext:
             if self.warm:
                 ws = oracle.WarmStart(*(np.stack([getattr(nodes[i].ws, k) for i in keep])
                                         for k in ('head', 'st', 'binv', 'd')))
-                s2, o2, _, x2, w2 = oracle.dual_simplex_nodes(p, f.lb[keep], f.ub[keep], ws)
+                s2, o2, i2, x2, w2 = oracle.dual_simplex_nodes(p, f.lb[keep], f.ub[keep], ws)
                 for t, i in enumerate(keep):
                     wo[i] = oracle.WarmStart(w2.head[t].copy(), w2.st[t].copy(),
                                              w2.binv[t].copy(), w2.d[t].copy())
             else:
-                s2, o2, _, x2 = oracle.dual_simplex(p, f.lb[keep], f.ub[keep], self.ws,
-                                                     want_x=True,
-                                                     pfi=self.pfi if self.ws is not None else 0)
+                s2, o2, i2, x2 = oracle.dual_simplex(p, f.lb[keep], f.ub[keep], self.ws,
+                                                      want_x=True,
+                                                      pfi=self.pfi if self.ws is not None else 0)
             status[keep], obj[keep], x[keep] = s2, o2, x2
+            self.tot.lps += int(keep.size)
+            self.tot.pivots += int(np.sum(i2))
         ints = np.isin(p.vtype, (0, 1))
         children = []
         best, best_i = math.inf, -1

@@ -155,8 +155,8 @@ def test_bnb_search_modes_match_cpu_and_highs(ctx, k, order, warm):
     oc, xc, sc, _ = bnb.solve(CpuBnbContext(p, ctx.oracle_pfi()), batch=64, capacity=1 << 15,
                               order=order, warm=warm)
     assert sg.open == sc.open == 0
-    assert (sg.rounds, sg.nodes, list(sg.ndec), sg.pruned) == \
-        (sc.rounds, sc.nodes, list(sc.ndec), sc.pruned)
+    assert (sg.rounds, sg.nodes, list(sg.ndec), sg.pruned, sg.lps, sg.pivots) == \
+        (sc.rounds, sc.nodes, list(sc.ndec), sc.pruned, sc.lps, sc.pivots)
     assert abs(og - oc) <= 1e-9 * max(1.0, abs(oc))
     assert hs == 0 and abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
     _check_solution(p, xg, og)
@@ -178,18 +178,25 @@ def test_bnb_best_first_k3l_parent_warm(ctx):
     assert hs == 0 and abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
 
 
-def test_bnb_tls4_lin_root_is_integral(ctx):
-    """Config 2's tree: tls4-lin's root LP optimum is already integral (value
-    0, as HiGHS' MILP finds at its root node), so the branch-and-bound search
-    on it is one node in every search mode."""
+def test_bnb_tls4_lin_tree(ctx):
+    """Config 2's own tree: tls4-lin's MILP optimum is 0 (HiGHS proves it at
+    its root node); the LP optimum is degenerate and our dual simplex's
+    root vertex is fractional, so the batched tree branches (a few hundred to
+    a few thousand nodes by search mode) and proves 0, evaluating the same
+    tree as the CPU restatement in every mode."""
     import os
+    from bnb import CpuBnbContext
     from minotaur_amd.problem import LinProblem
     p = LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
                                      'instances', 'tls4_lin.npz'))
     hs, hobj = oracle.highs_milp(p)
+    assert hs == 0 and hobj == 0.0
     ctx.load(p)
     for order, warm in ((0, 0), (1, 0), (1, 1)):
-        og, xg, sg, _ = bnb.solve(ctx, batch=1024, capacity=1 << 12, order=order, warm=warm)
-        assert sg.nodes == 1 and sg.ndec[3] == 1
-        assert hs == 0 and abs(og - hobj) <= 1e-9
+        og, xg, sg, _ = bnb.solve(ctx, batch=1024, capacity=1 << 14, order=order, warm=warm)
+        oc, _, sc, _ = bnb.solve(CpuBnbContext(p, ctx.oracle_pfi()), batch=1024,
+                                 capacity=1 << 14, order=order, warm=warm)
+        assert sg.open == 0 and abs(og - hobj) <= 1e-9
+        assert (sg.rounds, sg.nodes, list(sg.ndec), sg.pruned) == \
+            (sc.rounds, sc.nodes, list(sc.ndec), sc.pruned)
         _check_solution(p, xg, og)

@@ -96,7 +96,7 @@ def _bnb_worker(rank, world, port, out):
 
     inc, x, st, rounds, mine = bnb.solve_distributed(ctx, 8, rank, world, amin, amax,
                                                      capacity=1 << 14)
-    out[rank] = (inc, rounds, mine, st.nodes)
+    out[rank] = (inc, rounds, mine['nodes'], st.nodes)
     dist.destroy_process_group()
 
 
