@@ -57,8 +57,8 @@ def pmc_traffic(kernel, batch):
     (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3
     FETCH_SIZE/WRITE_SIZE passes of this same bench at the same batch)."""
     import glob
-    key = {'fbbt': 'fbbt_linear_kernel', 'lp_dual': 'lp_dual_kernel',
-           'lp_pfi': 'lp_pfi_kernel'}[kernel]
+    keys = {'fbbt': ('fbbt_linear_persist', 'fbbt_linear_kernel'), 'lp_dual': ('lp_dual_kernel',),
+            'lp_pfi': ('lp_pfi_kernel',)}[kernel]
     for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')), reverse=True):
         try:
             d = json.load(open(f))
@@ -66,9 +66,10 @@ def pmc_traffic(kernel, batch):
             continue
         args = d.get("bench_args", "").split()
         b = int(args[args.index('--batch') + 1]) if '--batch' in args else 65536
-        k = d.get("kernels", {}).get(key)
-        if b == batch and k and k.get("hbm_bytes_per_launch"):
-            return k["hbm_bytes_per_launch"], os.path.basename(f)
+        for key in keys:
+            k = d.get("kernels", {}).get(key)
+            if b == batch and k and k.get("hbm_bytes_per_launch"):
+                return k["hbm_bytes_per_launch"], os.path.basename(f)
     return None, None
 
 
@@ -425,8 +426,9 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=131072,
-                    help='open nodes per GPU per step (131072: two K1 waves per SIMD)')
+    ap.add_argument('--batch', type=int, default=524288,
+                    help='open nodes per GPU per step (524288: K1 persistent waves refill '
+                         'their lanes; 131072 = one node per resident lane)')
     ap.add_argument('--cpu-seconds', type=float, default=16.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-bnb', action='store_true',

@@ -58,6 +58,7 @@ struct mgpu_ctx {
   // workspaces
   DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_inf, io_nmods, io_mv, io_ml, io_mval;
   DevBuf scratch, flag_scratch;
+  DevBuf fbbt_next;            // K1 persistent variant: node queue head
   int fbbt_variant = 0;
   int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L, 3 K3P
   int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)

@@ -802,6 +802,171 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   }
 }
 
+// Persistent variant (global scratch, bit flags): a fixed grid of waves
+// takes nodes from a device queue.  A lane whose node ends its sweep loop
+// (simplePresolve's termination rule) writes the node out at the next sweep
+// boundary and takes the next node from the queue, which starts its first
+// sweep in that same wave sweep.  The rows and arithmetic per node are
+// unchanged (bit-exact); what changes is the packing: the one-node-per-lane
+// kernel keeps a whole wave looping until its slowest node's last sweep
+// (nodes need 1-6 sweeps, 2.3 on average on tls4-lin), this one refills the
+// lanes of the nodes that finished early.
+// kWG waves per workgroup share one LDS copy of the records (each wave has
+// its own scratch slot and node queue position; no barrier after staging).
+// (diagnostic builds: -DMGPU_FBBT_WPE=k asks the compiler for k waves per
+// SIMD, i.e. at most 512/k VGPRs)
+#ifdef MGPU_FBBT_WPE
+#define MGPU_K1P_ATTR __attribute__((amdgpu_waves_per_eu(MGPU_FBBT_WPE)))
+#else
+#define MGPU_K1P_ATTR
+#endif
+template <int kWG>
+__global__ MGPU_K1P_ATTR __launch_bounds__(kLanes * kWG) void fbbt_linear_persist(DevLP lp,
+                                                                                   FbbtIO io) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & (kLanes - 1);
+  const int wave = blockIdx.x * kWG + (int)(threadIdx.x / kLanes);
+  const int n = lp.n, m = lp.m;
+  NodeView<true, true> v;
+  v.lane = lane;
+  v.rowidx = lp.rowidx;
+  v.bits = 0ull;
+  v.stride = kLanes;
+  v.lb = io.scratch + (size_t)wave * 2 * n * kLanes;
+  v.ub = v.lb + (size_t)n * kLanes;
+  v.flag = nullptr;
+  // row and term records staged once into LDS
+  RowRec *s_rows = reinterpret_cast<RowRec *>(lds);
+  TermRec *s_trec = reinterpret_cast<TermRec *>(reinterpret_cast<char *>(lds) +
+                                                (size_t)m * sizeof(RowRec));
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(lp.rows);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_rows);
+    for (int i = threadIdx.x; i < 2 * m; i += kLanes * kWG) dst[i] = src[i];
+    src = reinterpret_cast<const uint4 *>(lp.trec);
+    dst = reinterpret_cast<uint4 *>(s_trec);
+    for (int i = threadIdx.x; i < 2 * lp.nnz; i += kLanes * kWG) dst[i] = src[i];
+  }
+  __syncthreads();
+  if (wave >= io.npw) return;   // the grid is rounded up to whole workgroups
+  const TermRec *trec = s_trec;
+  const RowRec *rows = s_rows;
+  const uint64_t all_rows = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+  const TermChunk opre = load_terms(lp.orec, lp.nobj < kLanes ? lp.nobj : kLanes, lane);
+  const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+
+  int node = -1;
+  bool has = false, changed = false, infeas = false, exhausted = false;
+  unsigned iters = 1;
+  NodeState s{0, 0u};
+  ModLog log{nullptr, nullptr, nullptr, io.mod_cap};
+  while (true) {
+    bool go = has && changed && iters <= 10u && (iters <= 2u || s.nintmods > 0u) && !infeas;
+    // retire: nodes whose sweep loop ended (checked at the sweep boundary,
+    // exactly where simplePresolve's loop test runs, LinearHandler.cpp:1625)
+    const bool fin = has && !go;
+    if (__any(fin)) {
+      if (fin) {
+        io.infeas[node] = infeas ? 1 : 0;
+        io.nmods[node] = s.nmods;
+        double *dst_l = io.lb_out + (size_t)node * n;
+        double *dst_u = io.ub_out + (size_t)node * n;
+        for (int j = 0; j < n; ++j) {
+          dst_l[j] = v.L(j);
+          dst_u[j] = v.U(j);
+        }
+        has = false;
+      }
+    }
+    // refill idle lanes from the queue (one atomic per wave)
+    if (!exhausted) {
+      const uint64_t idle = __ballot(!has);
+      if (idle) {
+        const int cnt = __popcll(idle);
+        int base = 0;
+        if (lane == (int)__builtin_ctzll(idle)) base = atomicAdd(io.next, cnt);
+        base = __shfl(base, (int)__builtin_ctzll(idle), kLanes);
+        if (base + cnt >= io.batch) exhausted = true;
+        if (!has) {
+          const int my = base + __popcll(idle & lt_mask);
+          if (my < io.batch) {
+            node = my;
+            has = true;
+            const double *src_l = io.lb_in + (size_t)node * n;
+            const double *src_u = io.ub_in + (size_t)node * n;
+            for (int j = 0; j < n; ++j) {
+              v.L(j) = src_l[j];
+              v.U(j) = src_u[j];
+            }
+            // simplePresolve: every constraint's BFlag set (:1618-1622)
+            v.bits = all_rows;
+            s.nmods = 0;
+            s.nintmods = 0u;
+            changed = true;
+            infeas = false;
+            iters = 1;
+            log = ModLog{nullptr, nullptr, nullptr, io.mod_cap};
+            if (io.mod_var != nullptr && io.mod_cap > 0) {
+              const size_t o = (size_t)node * io.mod_cap;
+              log.var = io.mod_var + o;
+              log.lu = io.mod_lu + o;
+              log.val = io.mod_val + o;
+            }
+            go = true;
+          }
+        }
+      }
+    }
+    if (!__any(go)) {
+      if (exhausted || !__any(has)) break;
+      continue;
+    }
+    if (go) {
+      s.nintmods = 0u;
+      changed = false;
+      ++iters;
+    }
+    bool cons_on = go;
+    for (int r0 = 0; r0 < m; r0 += kLanes) {
+      const int rcnt = m - r0 < kLanes ? m - r0 : kLanes;
+      RowRec rr{0.0, 0.0, 0, 0, 0, 0};
+      if (lane < rcnt) rr = rows[r0 + lane];
+      for (int q = 0; q < rcnt; ++q) {
+        const int r = r0 + q;
+        const bool mine = cons_on && v.flagged(r);
+        if (!__any(mine)) continue;
+        const int k0 = rl(rr.k0, q), nt = rl(rr.nt, q);
+        const TermChunk pre = load_terms(trec + k0, nt < kLanes ? nt : kLanes, lane);
+        if (mine) {
+          const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
+          bool tch;
+          v.clear(r);
+          bool inf;
+          if (nt <= 3) inf = rc_lin_bnd_tighten<3>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 5) inf = rc_lin_bnd_tighten<5>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 6) inf = rc_lin_bnd_tighten<6>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 11) inf = rc_lin_bnd_tighten<11>(nt, pre, rlo, rhi, v, s, log, tch);
+          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
+          else inf = lin_bnd_tighten(trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
+          if (inf) {
+            cons_on = false;
+          } else if (tch) {
+            changed = true;
+          }
+        }
+      }
+    }
+    if (go && io.has_inc && lp.nobj > 0) {
+      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
+      else bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
+    }
+    const bool bad = check_bounds_rest(lp, v, tighten_ints(lp, v, s, log, go, changed));
+    if (go) infeas = bad;
+  }
+}
+
 template <bool kLds, bool kBits, bool kTL>
 hipError_t launch_variant(const DevLP &lp, const FbbtIO &io, size_t lds, hipStream_t stream) {
   const int waves = (io.batch + io.npw - 1) / io.npw;
@@ -843,6 +1008,26 @@ hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
                 : launch_variant<true, false, false>(lp, io, lds, stream);
   }
   if (io.scratch == nullptr || (!bits && io.flag_scratch == nullptr)) return hipErrorInvalidValue;
+  if (variant == 3) {  // persistent refill (caller sized the grid in io.npw units)
+    if (!bits || io.next == nullptr || tab > 64 * 1024) return hipErrorInvalidValue;
+    static const int wg = getenv("MGPU_FBBT_WG") ? atoi(getenv("MGPU_FBBT_WG")) : 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+      for (const void *f : {(const void *)fbbt_linear_persist<1>,
+                            (const void *)fbbt_linear_persist<4>}) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+        if (e != hipSuccess) return e;
+      }
+      attr_set = true;
+    }
+    if (wg == 1)
+      hipLaunchKernelGGL(fbbt_linear_persist<1>, dim3(io.npw), dim3(kLanes), tab, stream, lp, io);
+    else
+      hipLaunchKernelGGL(fbbt_linear_persist<4>, dim3((io.npw + 3) / 4), dim3(4 * kLanes), tab,
+                         stream, lp, io);
+    return hipGetLastError();
+  }
   const bool tl = !no_tl && bits && tab <= 64 * 1024;
   if (tl) return launch_variant<false, true, true>(lp, io, tab, stream);
   return bits ? launch_variant<false, true, false>(lp, io, 0, stream)

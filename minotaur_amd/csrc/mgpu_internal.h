@@ -178,6 +178,7 @@ struct FbbtIO {
   int npw;                      // nodes per wave (64, or fewer for more waves)
   double *scratch;              // global-bounds variant: [waves][2][n][kLanes]
   uint8_t *flag_scratch;        // global-bounds variant: [waves][m][kLanes]
+  int32_t *next;                // persistent variant: zeroed node counter (queue head)
 };
 
 constexpr int kLanes = 64;      // wave64: one node per lane

@@ -60,7 +60,8 @@ int mgpu_destroy(mgpu_ctx *c) {
                     &c->lp_wb, &c->lp_st, &c->lp_obj, &c->lp_it, &c->lp_x, &c->lp_oh,
                     &c->lp_ost, &c->lp_od, &c->lp_ob, &c->lp_slots, &c->io_lb_in,
                     &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
-                    &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch})
+                    &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch,
+                    &c->fbbt_next})
     b->release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -251,7 +252,7 @@ int mgpu_set_lp_pfi(mgpu_ctx *c, int kmax) {
 static_assert(MGPU_LP_PFI_MAX == kPfiMax, "ABI eta-file cap = kernel's");
 
 int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
-  if (!c || variant < 0 || variant > 2) return MGPU_ERR_ARG;
+  if (!c || variant < 0 || variant > 3) return MGPU_ERR_ARG;
   c->fbbt_variant = variant;
   return MGPU_OK;
 }
@@ -341,14 +342,41 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   const int waves = (batch + npw - 1) / npw;
   const bool fits = fbbt_lds_bytes(c->lp.n, c->lp.m) <= 160 * 1024;
   // Auto: the LDS variant holds one wave per CU when the node bounds take
-  // most of the 160 KiB; once there are more waves than CUs the global-
-  // scratch variant (many waves per CU hiding latency) is faster (measured
-  // 2.9 vs 4.8 ms at 65536 tls4-lin nodes).
+  // most of the 160 KiB; beyond that, one node per lane with the bounds in a
+  // global scratch while the batch needs at most 8 waves per CU (131 072
+  // nodes on 256 CUs), and past that the persistent
+  // variant, whose lanes take the next node as soon as theirs finishes
+  // (measured on tls4-lin: 262 144 nodes 4.00 -> 3.45 ms, 524 288 nodes
+  // 6.67 -> 5.58 ms; at 131 072 the one-shot kernel is faster, 1.87 vs
+  // 2.17 ms; tools/fbbt_refill_probe.py).
   int variant = c->fbbt_variant;
-  if (variant == 0) variant = (fits && waves <= c->num_cus) ? 1 : 2;
-  if (variant == 2) {
-    HIPCHK(c, c->scratch.ensure((size_t)waves * 2 * c->lp.n * kLanes * sizeof(double)));
-    HIPCHK(c, c->flag_scratch.ensure((size_t)waves * (c->lp.m > 0 ? c->lp.m : 1) * kLanes));
+  if (variant == 0)
+    variant = (fits && waves <= c->num_cus) ? 1 : (waves > 8 * c->num_cus && npw == kLanes) ? 3 : 2;
+  // persistent path: bit flags (m <= 64) and records staged in 64 KiB of LDS
+  if (variant == 3 && (c->lp.m > 64 || (size_t)c->lp.m * sizeof(RowRec) +
+                                            (size_t)c->lp.nnz * sizeof(TermRec) > 64 * 1024))
+    variant = 2;
+  int grid = waves;
+  if (variant == 3) {
+    // persistent waves: 8 per CU (two per SIMD at the kernel's 177 VGPRs;
+    // more waves only enlarge the scratch working set, which already lives
+    // in the MALL: 3072-4096 waves measured slower), fewer for small
+    // batches; MGPU_FBBT_WAVES overrides
+    grid = c->num_cus * 8;
+    if (const char *e = getenv("MGPU_FBBT_WAVES")) {
+      const int v = atoi(e);
+      if (v >= 1) grid = v;
+    }
+    const int need = (batch + kLanes - 1) / kLanes;
+    if (grid > need) grid = need;
+    io.npw = grid;   // the persistent launch reads its grid from npw
+    HIPCHK(c, c->fbbt_next.ensure(sizeof(int32_t)));
+    HIPCHK(c, hipMemsetAsync(c->fbbt_next.p, 0, sizeof(int32_t), c->stream));
+    io.next = c->fbbt_next.as<int32_t>();
+  }
+  if (variant == 2 || variant == 3) {
+    HIPCHK(c, c->scratch.ensure((size_t)grid * 2 * c->lp.n * kLanes * sizeof(double)));
+    HIPCHK(c, c->flag_scratch.ensure((size_t)grid * (c->lp.m > 0 ? c->lp.m : 1) * kLanes));
     // (byte flags are only used when m > 64; bit flags live in VGPRs)
     io.scratch = c->scratch.as<double>();
     io.flag_scratch = c->flag_scratch.as<uint8_t>();

@@ -29,12 +29,15 @@ def _inc(g):
     return math.inf if g['incumbent'] is None else g['incumbent']
 
 
-@pytest.mark.parametrize('variant', [1, 2])
+@pytest.mark.parametrize('variant', [1, 2, 3])
 @pytest.mark.parametrize('name', cases())
-def test_fbbt_matches_reference_golden(ctx, name, variant):
+def test_fbbt_matches_reference_golden(ctx, name, variant, monkeypatch):
+    """variant 3 (persistent, lanes refilled from the node queue) runs on
+    two waves here, so nearly every lane processes several nodes."""
     p, g = load_fbbt(name)
     ctx.load(p)
     ctx.set_fbbt_variant(variant)
+    monkeypatch.setenv('MGPU_FBBT_WAVES', '2')
     try:
         r = ctx.fbbt(g['lb_in'], g['ub_in'], _inc(g), mod_cap=g['mod_cap'])
     finally:
@@ -53,13 +56,22 @@ def _tls4():
                                         'tls4_lin.npz'))
 
 
+@pytest.mark.parametrize('waves', [None, '7', '150'])
 @pytest.mark.parametrize('inc', [math.inf, 20.0])
-def test_fbbt_large_batch_vs_oracle(ctx, inc):
-    """Ragged last wave (B not a multiple of 64) and many waves."""
+def test_fbbt_large_batch_vs_oracle(ctx, inc, waves, monkeypatch):
+    """Ragged last wave (B not a multiple of 64) and many waves; with
+    `waves` set, the persistent variant on that many waves (node queue
+    refills)."""
     p = _tls4()
     LB, UB = random_boxes(p, 20001, 424242)
     ctx.load(p)
-    r = ctx.fbbt(LB, UB, inc)
+    if waves:
+        ctx.set_fbbt_variant(3)
+        monkeypatch.setenv('MGPU_FBBT_WAVES', waves)
+    try:
+        r = ctx.fbbt(LB, UB, inc)
+    finally:
+        ctx.set_fbbt_variant(0)
     o = oracle.linear_fbbt(p, LB, UB, None if math.isinf(inc) else inc, nthreads=8)
     assert bits_equal(r.lb, o.lb) and bits_equal(r.ub, o.ub)
     assert np.array_equal(r.infeasible, o.infeas)
