@@ -328,4 +328,105 @@ int integ_quad(int device, int hip, const QSpecI *sp, int has_inc, double inc, i
   return 0;
 }
 
+// The reference's own root OBBT, QuadHandler::postSolveRootNode (QuadHandler.
+// cpp:1397-1547) -> tightenLP_ (:2218-2297), with HipLPEngine as its bound-
+// tightening engine bte_ (setBTEngine, as SimpleTransformer.cpp:948-951
+// wires it in mglob) and as the root relaxation's engine.  The relaxation
+// is the one minotaur_amd/obbt.py relaxation_lp builds: the original
+// constraints with every product replaced by its aux y, then the secant /
+// McCormick rows of relaxInitInc, objective in the same form.
+// Outputs: p_'s variable bounds after OBBT; info[0] root LP status,
+// info[1] postSolveRootNode's return value, info[2] bound LPs solved by bte_.
+int integ_obbt(int device, const QSpecI *sp, int has_inc, double inc, double *out_lb,
+               double *out_ub, int *info) {
+  const QSpecI &s = *sp;
+  EnvPtr env = (EnvPtr) new Environment();
+  int err = 0;
+  env->startTimer(err);
+  ProblemPtr orig = (ProblemPtr) new Problem(env);
+  for (int j = 0; j < s.nv0; ++j) orig->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
+  for (int c = 0; c < s.ncon; ++c) orig->newConstraint(qfun(s, orig, c), s.clb[c], s.cub[c]);
+  if (s.has_obj) orig->newObjective(qfun(s, orig, s.ncon), s.obj_const, Minimize);
+  else orig->newObjective((FunctionPtr) new Function((LinearFunctionPtr) new LinearFunction()),
+                          s.obj_const, Minimize);
+  orig->calculateSize();
+  ProblemPtr p = (ProblemPtr) new Problem(env);
+  for (int j = 0; j < s.nv; ++j) p->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
+  QuadHandler *qh = new QuadHandler(env, p, orig);
+  auto add_aux = [&](int x0, int x1, int y) {
+    LinearFunctionPtr lf = (LinearFunctionPtr) new LinearFunction();
+    lf->addTerm(p->getVariable(y), -1.0);
+    QuadraticFunctionPtr qf = (QuadraticFunctionPtr) new QuadraticFunction();
+    qf->addTerm(p->getVariable(x0), p->getVariable(x1), 1.0);
+    qh->addConstraint(p->newConstraint((FunctionPtr) new Function(lf, qf), 0.0, 0.0));
+  };
+  for (int k = 0; k < s.nsq; ++k) add_aux(s.sq_x[k], s.sq_x[k], s.sq_y[k]);
+  for (int k = 0; k < s.nbil; ++k) add_aux(s.bil_x0[k], s.bil_x1[k], s.bil_y[k]);
+  p->calculateSize();
+  RelaxationPtr rel = (RelaxationPtr) new Relaxation(env);
+  for (int j = 0; j < s.nv; ++j) {
+    VariablePtr v = p->getVariable(j);
+    rel->newVariable(v->getLb(), v->getUb(), v->getType());
+  }
+  // original rows / objective with products replaced by their aux y
+  auto yof = [&](int a, int b) {
+    for (int k = 0; k < s.nsq; ++k)
+      if (a == s.sq_x[k] && b == s.sq_x[k]) return s.sq_y[k];
+    for (int k = 0; k < s.nbil; ++k)
+      if (a == s.bil_x0[k] && b == s.bil_x1[k]) return s.bil_y[k];
+    return -1;
+  };
+  auto ylin = [&](int c) {
+    LinearFunctionPtr lf = (LinearFunctionPtr) new LinearFunction();
+    for (int k = s.lptr[c]; k < s.lptr[c + 1]; ++k)
+      lf->incTerm(rel->getVariable(s.lvar[k]), s.lval[k]);
+    for (int k = s.qptr[c]; k < s.qptr[c + 1]; ++k)
+      lf->incTerm(rel->getVariable(yof(s.qv1[k], s.qv2[k])), s.qval[k]);
+    return lf;
+  };
+  for (int c = 0; c < s.ncon; ++c)
+    rel->newConstraint((FunctionPtr) new Function(ylin(c)), s.clb[c], s.cub[c]);
+  bool inf = false;
+  qh->relaxInitInc(rel, &inf);
+  if (s.has_obj) rel->newObjective((FunctionPtr) new Function(ylin(s.ncon)), s.obj_const, Minimize);
+  else rel->newObjective((FunctionPtr) new Function((LinearFunctionPtr) new LinearFunction()),
+                         s.obj_const, Minimize);
+  rel->calculateSize();
+  SolutionPoolPtr spool = (SolutionPoolPtr) new SolutionPool(env, p, 1);
+  if (has_inc) {
+    std::vector<double> x(s.nv, 0.0);
+    spool->addSolution(x.data(), inc);
+  }
+  HipLPEngine *root_e = new HipLPEngine(env, device);
+  HipLPEngine *bte = new HipLPEngine(env, device);
+  qh->setBTEngine(bte);
+  root_e->load(rel);
+  info[0] = (int)root_e->solve();
+  info[1] = -1;
+  info[2] = 0;
+  if (info[0] == ProvenOptimal) {
+    ModVector pm, rm;
+    info[1] = qh->postSolveRootNode(rel, spool, root_e->getSolution(), pm, rm) ? 1 : 0;
+    for (ModificationPtr m : pm) delete m;
+    for (ModificationPtr m : rm) delete m;
+    std::vector<double> st(6, 0.0);
+    bte->fillStats(st);
+    info[2] = (int)st[0];
+  }
+  for (int j = 0; j < s.nv; ++j) {
+    out_lb[j] = p->getVariable(j)->getLb();
+    out_ub[j] = p->getVariable(j)->getUb();
+  }
+  root_e->clear();
+  delete qh;
+  delete bte;
+  delete root_e;
+  delete spool;
+  delete rel;
+  delete p;
+  delete orig;
+  delete env;
+  return 0;
+}
+
 }  // extern "C"

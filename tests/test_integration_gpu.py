@@ -136,3 +136,40 @@ def test_hip_quad_handler_matches_reference(integ, seed, inc):
     assert np.array_equal(a_inf, b_inf) and np.array_equal(a_nm, b_nm)
     assert bits_equal(a_rows, b_rows)
     assert calls[0] == LB.shape[0] and calls[1] == 1   # only the root call on the CPU
+
+
+@pytest.mark.parametrize('seed', [0, 1, 2, 3, 4, 5])
+def test_reference_obbt_matches_batched_obbt(integ, seed):
+    """Root OBBT two ways on the same relaxation (original rows in aux form +
+    the secant / McCormick rows): the REFERENCE's own QuadHandler::
+    postSolveRootNode -> tightenLP_ with HipLPEngine as its bte_ (bound LPs
+    one after the other, each from the previous optimum), and the batched
+    path (minotaur_amd/obbt.py: every candidate bound LP in ONE K3 batch from
+    the root basis, tightenLP_'s loop replayed on the host).  Same tightened
+    bounds within 1e-6 and the same number of bound LPs used."""
+    import oracle
+    from minotaur_amd import obbt
+    from minotaur_amd.quad import random_qcqp
+    from minotaur_amd.runtime import Context
+    integ.integ_obbt.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_double, P, P, P]
+    qp = random_qcqp(seed, nv0=8, ncon=4)
+    spec = oracle.qspec(qp)
+    rlb, rub = np.zeros(qp.nv), np.zeros(qp.nv)
+    info = np.zeros(3, dtype=np.int32)
+    integ.integ_obbt(0, ctypes.byref(spec), 0, 0.0, _p(rlb), _p(rub), _p(info))
+    rows = oracle.quad_root_rows(qp)
+    p = obbt.relaxation_lp(qp, rows)
+    ctx = Context(0)
+    try:
+        ctx.load(p)
+        r, ws = ctx.root_solve()
+        assert r.status[0] == info[0]
+        if info[0] != 0:
+            pytest.skip('root relaxation not optimal')
+        inf, lb, ub, mods, nlp, used = obbt.obbt(ctx, qp, rows, r.x[0], ws)
+    finally:
+        ctx.close()
+    assert info[1] in (0, 1) and not inf
+    assert used == info[2]
+    assert np.allclose(lb, rlb, rtol=1e-6, atol=1e-6)
+    assert np.allclose(ub, rub, rtol=1e-6, atol=1e-6)
