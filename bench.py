@@ -165,31 +165,26 @@ def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
 
 def run_tree(ctx, dev, rank, world, p, B, order, warm, cap):
     """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
-    across ranks after the shared first rounds, incumbent all-reduce MIN per
-    round.  Returns (incumbent, nodes, LP solves, pivots, pruned-open,
-    rounds, seconds) — counts summed over ranks, seconds the max."""
+    across ranks after the shared first rounds: one packed all-reduce per
+    round (incumbent MIN + open counts), open nodes rebalanced every 8 rounds
+    or when a rank runs dry (dist.rebalance).  Returns (incumbent, nodes, LP
+    solves, pivots, pruned-open, rounds, seconds, nodes moved) — counts
+    summed over ranks, seconds the max."""
     import torch
     import torch.distributed as dist
     from minotaur_amd import bnb
     from minotaur_amd import dist as mdist
-
-    def amin(v):
-        t = torch.tensor([v], dtype=torch.float64, device=dev)
-        return float(mdist.allreduce_incumbent(t).item())
-
-    def amax(v):
-        t = torch.tensor([v], dtype=torch.float64, device=dev)
-        return float(mdist.allreduce_max(t).item())
-
+    comm = mdist.Comm(rank, world, dev)
     ctx.load(p)
-    bnb.solve_distributed(ctx, 64, rank, world, amin, amax, capacity=1 << 14, max_rounds=2,
-                          order=order, warm=warm)            # warm-up (kernel loads)
+    bnb.solve_distributed(ctx, 64, rank, world, capacity=1 << 14, max_rounds=2, order=order,
+                          warm=warm, comm=comm)                # warm-up (kernel loads)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, amin, amax,
-                                                     capacity=cap, order=order, warm=warm)
+    inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=cap,
+                                                     order=order, warm=warm, comm=comm,
+                                                     lb_every=8)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -199,7 +194,7 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap):
     mdist.allreduce_max(el)
     mdist.allreduce_sum(cnt)
     c = [float(v) for v in cnt.tolist()]
-    return inc, c[0], c[1], c[2], c[3], rounds, float(el.item())
+    return inc, c[0], c[1], c[2], c[3], rounds, float(el.item()), mine['moved']
 
 
 # Complete trees in the bench line: config 2's own instance,
@@ -227,14 +222,15 @@ def tree_search(ctx, dev, rank, world, B, args):
             sys.path.insert(0, os.path.join(ROOT, 'oracle'))
             import oracle
             opt = oracle.highs_milp(p)[1]
-        inc, nodes, lps, piv, pruned, rounds, el = run_tree(ctx, dev, rank, world, p, B, order,
-                                                            warm, 1 << 22)
+        inc, nodes, lps, piv, pruned, rounds, el, moved = run_tree(ctx, dev, rank, world, p, B,
+                                                                   order, warm, 1 << 22)
         out.append({"instance": p.name, "vars": p.n, "rows": p.m,
                     "search": ("best-first" if order else "depth-first over batches") +
                               (", parent-basis warm starts" if warm else
                                ", root-basis warm start") + ", MaxVio branching",
                     "nodes": nodes, "lp_solves": lps, "pivots_per_lp": piv / max(lps, 1.0),
                     "pruned_open": pruned, "rounds": rounds, "seconds": el,
+                    "nodes_migrated": moved,
                     "nodes_per_s": nodes / el, "relaxations_per_s": lps / el,
                     "batch_per_gpu": B, "optimum": inc, "optimum_highs": opt,
                     "optimum_matches_highs": bool(abs(inc - opt) <= 1e-6 * max(1.0, abs(opt)))})

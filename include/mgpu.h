@@ -270,6 +270,20 @@ int mgpu_strong_branch_dev(mgpu_ctx *ctx, const double *d_lb, const double *d_ub
  * i = rank (mod world), packed in order; *kept = nodes left. */
 int mgpu_bnb_shard(mgpu_ctx *ctx, int rank, int world, int *kept);
 
+/* Node migration between ranks (MpiBranchAndBound::LoadBalance_'s node
+ * send / receive, src/base/MpiBranchAndBound.cpp:78-195; Serializer.cpp:
+ * 26-112 carries the same content: the node's bound changes, lower bound and
+ * depth).  Host buffers, boxes [k][n].
+ *   mgpu_bnb_export: removes up to k open nodes (the stack's top k; in
+ *                    best-first order the first k live pool slots) and
+ *                    returns their boxes, bounds and depths; *got = count.
+ *   mgpu_bnb_import: adds k open nodes (with parent warm starts they start
+ *                    from the root basis). */
+int mgpu_bnb_export(mgpu_ctx *ctx, int k, double *lb, double *ub, double *nlb, int32_t *depth,
+                    int *got);
+int mgpu_bnb_import(mgpu_ctx *ctx, int k, const double *lb, const double *ub, const double *nlb,
+                    const int32_t *depth);
+
 /* ---- QP relaxation with an MFMA KKT block (K5) ---------------
  * Replaces BqpdEngine::solve (src/interfaces/BqpdEngine.cpp:449-534) on the
  * QP relaxation QPDRelaxer builds (examples/QPDRelaxer.cpp:56-126):

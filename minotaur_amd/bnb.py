@@ -33,16 +33,24 @@ def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
     return obj, x, st, time.perf_counter() - t0
 
 
-def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
-                      capacity=None, max_rounds=10**9, shard_at=None, order=0, warm=0):
+def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max=None,
+                      capacity=None, max_rounds=10**9, shard_at=None, order=0, warm=0,
+                      comm=None, lb_every=0):
     """Node-sharded tree search.  Every rank runs the same deterministic
     rounds until the pool holds at least ``shard_at`` (default 4 * world)
     open nodes, then keeps nodes i = rank (mod world) (mgpu_bnb_shard) and
-    searches its share; allreduce_min / allreduce_max(float) -> float are
-    the collectives (minotaur_amd/dist.py over RCCL, or gloo in the CPU
-    tests).  Returns (incumbent, x or None, stats, rounds, mine) where
-    mine = {nodes, lps, pivots, pruned} evaluated by this rank, the shared
-    first rounds counted on rank 0 only (so sums over ranks are exact)."""
+    searches its share.  After every round ONE collective carries the
+    incumbent (MIN) and the largest open count (the stop test): ``comm``
+    (minotaur_amd.dist.Comm over RCCL / gloo) packs both into one all-reduce;
+    without it the two callables allreduce_min / allreduce_max(float) ->
+    float are used.  With ``comm`` and lb_every > 0, every lb_every rounds
+    (and whenever some rank ran out of nodes while others hold more than a
+    batch) the open nodes are rebalanced across ranks (dist.rebalance:
+    MpiBranchAndBound::LoadBalance_).  Returns (incumbent, x or None, stats,
+    rounds, mine) where mine = {nodes, lps, pivots, pruned, moved} evaluated
+    by this rank, the shared first rounds counted on rank 0 only (so sums
+    over ranks are exact)."""
+    from . import dist as mdist
     cap = capacity or 64 * batch
     shard_at = shard_at or 4 * world
     ctx.bnb_config(order, warm)
@@ -51,7 +59,9 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
     sharded = world == 1
     st = None
     rounds = 0
+    moved = 0
     shared = (0, 0, 0, 0)
+    n = ctx.problem.n
     while rounds < max_rounds:
         st = ctx.bnb_round(batch, inc)
         rounds += 1
@@ -60,11 +70,22 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min, allreduce_max,
             shared = (st.nodes, st.lps, st.pivots, st.pruned)   # identical on every rank
             open_now = ctx.bnb_shard(rank, world)
             sharded = True
-        inc = allreduce_min(st.incumbent)
-        if allreduce_max(float(open_now)) == 0.0:
-            break
+        if comm is not None:
+            inc, most, least = comm.round_reduce(st.incumbent, open_now)
+            if most == 0.0:
+                break
+            # the trigger uses only all-reduced values: every rank agrees
+            if sharded and world > 1 and lb_every > 0 and (
+                    rounds % lb_every == 0 or (least == 0 and most > batch)):
+                open_now, k = mdist.rebalance(ctx, comm, open_now, n)
+                moved += k
+        else:
+            inc = allreduce_min(st.incumbent)
+            if allreduce_max(float(open_now)) == 0.0:
+                break
     obj, x = ctx.bnb_best()
     sub = shared if rank != 0 else (0, 0, 0, 0)
     mine = {k: v - w for k, v, w in zip(('nodes', 'lps', 'pivots', 'pruned'),
                                          (st.nodes, st.lps, st.pivots, st.pruned), sub)}
+    mine['moved'] = moved
     return inc, (x if obj == inc else None), st, rounds, mine

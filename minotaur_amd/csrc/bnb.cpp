@@ -525,6 +525,123 @@ int mgpu_strong_branch(mgpu_ctx *c, const double *lb, const double *ub, int ncan
   return MGPU_OK;
 }
 
+// Node migration for load balancing across ranks (MpiBranchAndBound::
+// LoadBalance_, MpiBranchAndBound.cpp:78-195: node boxes, bounds and depths
+// move between processes).  Host buffers; boxes [k][n].
+int mgpu_bnb_export(mgpu_ctx *c, int k, double *lb, double *ub, double *nlb, int32_t *depth,
+                    int *got) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_export: mgpu_bnb_init first");
+  if (k < 0 || (k > 0 && (!lb || !ub || !nlb || !depth)) || !got)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_export: bad argument");
+  BnbState &s = *c->bnb;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = s.n;
+  if (k > s.count) k = s.count;
+  *got = 0;
+  if (k == 0) return MGPU_OK;
+  if (s.order == 0) {
+    // the top k of the stack (contiguous): no compaction needed
+    const size_t o = (size_t)(s.count - k);
+    HIPCHK(c, hipMemcpyAsync(lb, s.plb.as<double>() + o * n, (size_t)k * n * 8,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ub, s.pub.as<double>() + o * n, (size_t)k * n * 8,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(nlb, s.pnlb.as<double>() + o, (size_t)k * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(depth, s.pdepth.as<int32_t>() + o, (size_t)k * 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  } else {
+    // best-first pool: the first k live slots
+    std::vector<uint8_t> live((size_t)s.hw);
+    HIPCHK(c, hipMemcpyAsync(live.data(), s.plive.p, (size_t)s.hw, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> slots;
+    for (int i = 0; i < s.hw && (int)slots.size() < k; ++i)
+      if (live[i]) slots.push_back((uint32_t)i);
+    k = (int)slots.size();
+    DevBuf dsl, tlb, tub, tdep;
+    HIPCHK(c, dsl.ensure((size_t)k * 4));
+    HIPCHK(c, tlb.ensure((size_t)k * n * 8));
+    HIPCHK(c, tub.ensure((size_t)k * n * 8));
+    HIPCHK(c, tdep.ensure((size_t)k * 4));
+    HIPCHK(c, hipMemcpyAsync(dsl.p, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice,
+                             c->stream));
+    BnbSelIO g{};
+    g.nb = k;
+    g.n = n;
+    g.slots = dsl.as<uint32_t>();
+    g.plb = s.plb.as<double>();
+    g.pub = s.pub.as<double>();
+    g.pdepth = s.pdepth.as<int32_t>();
+    g.plive = s.plive.as<uint8_t>();
+    g.wlb = tlb.as<double>();
+    g.wub = tub.as<double>();
+    g.depth_in = tdep.as<int32_t>();
+    HIPCHK(c, launch_bnb_gather(g, c->stream));
+    HIPCHK(c, hipMemcpyAsync(lb, tlb.p, (size_t)k * n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ub, tub.p, (size_t)k * n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(depth, tdep.p, (size_t)k * 4, hipMemcpyDeviceToHost, c->stream));
+    std::vector<double> all((size_t)s.hw);
+    HIPCHK(c, hipMemcpyAsync(all.data(), s.pnlb.p, (size_t)s.hw * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int t = 0; t < k; ++t) nlb[t] = all[slots[t]];
+  }
+  s.count -= k;
+  s.tot.open = s.count;
+  *got = k;
+  return MGPU_OK;
+}
+
+int mgpu_bnb_import(mgpu_ctx *c, int k, const double *lb, const double *ub, const double *nlb,
+                    const int32_t *depth) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_import: mgpu_bnb_init first");
+  if (k < 0 || (k > 0 && (!lb || !ub || !nlb || !depth)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_import: bad argument");
+  if (k == 0) return MGPU_OK;
+  BnbState &s = *c->bnb;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = s.n, m = c->lp.m, N = n + m;
+  // stack: on top; best-first: appended past the high-water mark
+  const int at = s.order == 0 ? s.count : s.hw;
+  if (at + k > s.cap) return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_import: node pool full");
+  HIPCHK(c, hipMemcpyAsync(s.plb.as<double>() + (size_t)at * n, lb, (size_t)k * n * 8,
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(s.pub.as<double>() + (size_t)at * n, ub, (size_t)k * n * 8,
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(s.pnlb.as<double>() + at, nlb, (size_t)k * 8, hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipMemcpyAsync(s.pdepth.as<int32_t>() + at, depth, (size_t)k * 4,
+                           hipMemcpyHostToDevice, c->stream));
+  if (s.order == 1) {
+    HIPCHK(c, hipMemsetAsync(s.plive.as<uint8_t>() + at, 1, (size_t)k, c->stream));
+    s.hw += k;
+  }
+  if (s.warm) {
+    // a migrated node starts from the root basis (its parent's stays with
+    // the rank that branched it)
+    for (int t = 0; t < k; ++t) {
+      const size_t o = (size_t)(at + t);
+      HIPCHK(c, hipMemcpyAsync(s.pws_head.as<int32_t>() + o * m, s.ws_head.p, (size_t)m * 4,
+                               hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(s.pws_st.as<int8_t>() + o * N, s.ws_st.p, (size_t)N,
+                               hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(s.pws_d.as<double>() + o * N, s.ws_d.p, (size_t)N * 8,
+                               hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(s.pws_binv.as<double>() + o * m * m, s.ws_binv.p,
+                               (size_t)m * m * 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s.count += k;
+  s.tot.open = s.count;
+  return MGPU_OK;
+}
+
 int mgpu_bnb_best(mgpu_ctx *c, double *obj, double *x) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_best: mgpu_bnb_init first");

@@ -29,7 +29,8 @@ EXPORTS = [
     'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
     'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
-    'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_bnb_config', 'mgpu_strong_branch',
+    'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_bnb_config', 'mgpu_bnb_export',
+    'mgpu_bnb_import', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
 ]
 
@@ -92,6 +93,8 @@ def load_library():
     lib.mgpu_lp_bound_dev.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
     lib.mgpu_bnb_init.argtypes = [_P, _I, _P, _P, _D]
     lib.mgpu_bnb_config.argtypes = [_P, _I, _I]
+    lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
+    lib.mgpu_bnb_import.argtypes = [_P, _I, _P, _P, _P, _P]
     lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
     lib.mgpu_bnb_best.argtypes = [_P, _P, _P]
     lib.mgpu_bnb_shard.argtypes = [_P, _I, _I, _P]
@@ -494,6 +497,23 @@ class Context:
         self._chk(self.lib.mgpu_bnb_shard(self.h, int(rank), int(world), ctypes.byref(k)),
                   'mgpu_bnb_shard')
         return k.value
+
+    def bnb_export(self, k):
+        """Remove up to k open nodes: (lb [k,n], ub [k,n], nlb [k], depth [k])."""
+        n = self.problem.n
+        lb, ub = np.empty((k, n)), np.empty((k, n))
+        nlb, dep = np.empty(k), np.empty(k, dtype=np.int32)
+        got = ctypes.c_int(0)
+        self._chk(self.lib.mgpu_bnb_export(self.h, int(k), _hp(lb), _hp(ub), _hp(nlb), _hp(dep),
+                                           ctypes.byref(got)), 'mgpu_bnb_export')
+        g = got.value
+        return lb[:g], ub[:g], nlb[:g], dep[:g]
+
+    def bnb_import(self, lb, ub, nlb, depth):
+        k = len(nlb)
+        self._chk(self.lib.mgpu_bnb_import(self.h, int(k), _hp(_np(lb, np.float64)),
+                                           _hp(_np(ub, np.float64)), _hp(_np(nlb, np.float64)),
+                                           _hp(_np(depth, np.int32))), 'mgpu_bnb_import')
 
     def bnb_best(self):
         x = np.empty(self.problem.n)

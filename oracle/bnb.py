@@ -216,5 +216,32 @@ class CpuBnbContext:
         self.tot.open = sum(nd is not None for nd in self.pool)
         return self.tot.open
 
+    def bnb_export(self, k):
+        """mgpu_bnb_export: the stack's top k, or the first k live slots."""
+        n = self.problem.n
+        if self.order == 0:
+            k = min(k, len(self.pool))
+            nodes = self.pool[len(self.pool) - k:]
+            del self.pool[len(self.pool) - k:]
+        else:
+            idx = [i for i, nd in enumerate(self.pool) if nd is not None][:k]
+            nodes = [self.pool[i] for i in idx]
+            for i in idx:
+                self.pool[i] = None
+        self.tot.open = sum(nd is not None for nd in self.pool)
+        if not nodes:
+            return np.empty((0, n)), np.empty((0, n)), np.empty(0), np.empty(0, np.int32)
+        return (np.stack([nd.lb for nd in nodes]), np.stack([nd.ub for nd in nodes]),
+                np.array([nd.nlb for nd in nodes]), np.array([nd.depth for nd in nodes],
+                                                             dtype=np.int32))
+
+    def bnb_import(self, lb, ub, nlb, depth):
+        """mgpu_bnb_import: on top of the stack / past the high-water mark;
+        with parent warm starts a migrated node starts from the root basis."""
+        for t in range(len(nlb)):
+            self.pool.append(_Node(np.array(lb[t]), np.array(ub[t]), float(nlb[t]),
+                                   int(depth[t]), self.ws))
+        self.tot.open = sum(nd is not None for nd in self.pool)
+
     def bnb_best(self):
         return self.inc, self.best_x.copy()

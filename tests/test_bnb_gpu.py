@@ -200,3 +200,39 @@ def test_bnb_tls4_lin_tree(ctx):
         assert (sg.rounds, sg.nodes, list(sg.ndec), sg.pruned) == \
             (sc.rounds, sc.nodes, list(sc.ndec), sc.pruned)
         _check_solution(p, xg, og)
+
+
+@pytest.mark.parametrize('order,warm', [(0, 0), (1, 0), (1, 1)])
+def test_bnb_export_import_between_contexts(ctx, order, warm):
+    """Node migration (mgpu_bnb_export / mgpu_bnb_import, the node send /
+    receive of MpiBranchAndBound::LoadBalance_) between two engine contexts
+    in one process: half of context A's open nodes move to context B after
+    a few rounds; both trees then run to the end with the incumbent MIN
+    exchanged each round and together prove the HiGHS optimum."""
+    from minotaur_amd.runtime import Context
+    p = random_mkp(5, 22, 3)
+    hs, hobj = oracle.highs_milp(p)
+    other = Context(0)
+    try:
+        ctx.load(p)
+        other.load(p)
+        for c in (ctx, other):
+            c.bnb_config(order, warm)
+        ctx.bnb_init(1 << 15)
+        other.bnb_init(1 << 15)
+        other.bnb_export(1 << 15)           # B starts with an empty pool
+        st = None
+        for _ in range(4):
+            st = ctx.bnb_round(16)
+        lb, ub, nlb, dep = ctx.bnb_export(st.open // 2)
+        assert len(nlb) == st.open // 2 > 0
+        other.bnb_import(lb, ub, nlb, dep)
+        inc, open_ = st.incumbent, [1, 1]
+        while max(open_) > 0:
+            sts = [c.bnb_round(16, inc) for c in (ctx, other)]
+            open_ = [s.open for s in sts]
+            inc = min(s.incumbent for s in sts)
+        assert abs(inc - hobj) <= 1e-6 * max(1.0, abs(hobj))
+        assert sts[1].nodes > 0
+    finally:
+        other.close()

@@ -126,3 +126,66 @@ def test_cpu_tree_step_matches_highs():
         hs, hobj = oracle.highs_milp(p)
         obj, x, st, _ = bnb.solve(CpuBnbContext(p), batch=16, capacity=1 << 14)
         assert st.open == 0 and abs(obj - hobj) <= 1e-6 * max(1.0, abs(hobj))
+
+
+def _lb_worker(rank, world, port, out, order):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from bnb import CpuBnbContext
+    from minotaur_amd import bnb
+    from minotaur_amd.dist import Comm
+    from minotaur_amd.problem import random_mkp
+
+    class Skewed(CpuBnbContext):
+        """An intentionally imbalanced split: rank 0 keeps every open node."""
+
+        def bnb_shard(self, r, w):
+            if r != 0:
+                self.pool = [] if self.order == 0 else [None] * len(self.pool)
+            self.tot.open = sum(nd is not None for nd in self.pool)
+            return self.tot.open
+
+    p = random_mkp(2, 18, 3)
+    ctx = Skewed(p)
+    inc, x, st, rounds, mine = bnb.solve_distributed(ctx, 8, rank, world, capacity=1 << 14,
+                                                     order=order, comm=Comm(rank, world),
+                                                     lb_every=3)
+    out[rank] = (inc, rounds, mine['nodes'], mine['moved'])
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('order', [0, 1])
+def test_rebalanced_sharded_tree_search(order):
+    """MpiBranchAndBound::LoadBalance_ semantics over gloo: the split after
+    the shared rounds leaves rank 1 without nodes; the periodic rebalance
+    (all-gather of open counts, common plan, nodes exported, sent, imported)
+    gives it work, both ranks evaluate nodes, and the run still proves the
+    HiGHS optimum with one packed all-reduce per round."""
+    import oracle
+    from minotaur_amd.problem import random_mkp
+    hs, hobj = oracle.highs_milp(random_mkp(2, 18, 3))
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_lb_worker, args=(world, _free_port(), out, order), nprocs=world, join=True)
+    (i0, r0, m0, mv0), (i1, r1, m1, mv1) = out[0], out[1]
+    assert i0 == i1 and abs(i0 - hobj) <= 1e-6 * max(1.0, abs(hobj))
+    assert r0 == r1
+    assert mv0 == mv1 > 0            # the plan is global: same count on every rank
+    assert m0 > 0 and m1 > 0         # rank 1 got work only through migration
+
+
+def test_balance_plan():
+    from minotaur_amd.dist import balance_plan
+    assert balance_plan([10, 0], 2) == [(0, 1, 5)]
+    plan = balance_plan([7, 0, 3, 10], 4)
+    after = [7, 0, 3, 10]
+    for s, d, k in plan:
+        after[s] -= k
+        after[d] += k
+    assert sorted(after) == [5, 5, 5, 5] and sum(k for _, _, k in plan) == 7
+    assert balance_plan([4, 4, 4], 3) == []
