@@ -278,6 +278,18 @@ EngineStatus HipLPEngine::solve() {
       sol_->setObjValue(INFINITY);
     }
   }
+  {
+    SolveRec r{-1, 0.0, (int)status_, sol_->getObjValue(), it};
+    int nz = 0;
+    for (int j = 0; j < n; ++j)
+      if (obj_[j] != 0.0) {
+        ++nz;
+        r.col = j;
+        r.sign = obj_[j];
+      }
+    if (nz != 1) r.col = -1;
+    log_.push_back(r);
+  }
   lastIters_ = it;
   stats_->iters += it;
   stats_->time += timer_->query();

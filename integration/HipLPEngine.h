@@ -95,6 +95,18 @@ class HipLPEngine : public LPEngine {
   void writeStats(std::ostream &out) const;
   void fillStats(std::vector<double> &lpStats);
 
+  /// One record per solve(): the objective's single column and sign when
+  /// the objective is +-x_j (the bound LPs of QuadHandler::tightenLP_),
+  /// else col = -1; the status and objective value returned.
+  struct SolveRec {
+    int col;
+    double sign;
+    int status;
+    double value;
+    int iters;
+  };
+  const std::vector<SolveRec> &solveLog() const { return log_; }
+
   // LPEngine extras used by drivers
   void getBasics(int *index);
   int getNumCols() { return n_; }
@@ -123,6 +135,7 @@ class HipLPEngine : public LPEngine {
   HipLPStats *stats_;
   Timer *timer_;
   std::vector<double> x_, y_, rc_;
+  std::vector<SolveRec> log_;
   static const std::string me_;
 };
 typedef HipLPEngine *HipLPEnginePtr;

@@ -336,9 +336,11 @@ int integ_quad(int device, int hip, const QSpecI *sp, int has_inc, double inc, i
 // constraints with every product replaced by its aux y, then the secant /
 // McCormick rows of relaxInitInc, objective in the same form.
 // Outputs: p_'s variable bounds after OBBT; info[0] root LP status,
-// info[1] postSolveRootNode's return value, info[2] bound LPs solved by bte_.
+// info[1] postSolveRootNode's return value, info[2] bound LPs solved by bte_;
+// log_*[k] (k < cap): bte_'s solves in order (column, sign, status, value).
 int integ_obbt(int device, const QSpecI *sp, int has_inc, double inc, double *out_lb,
-               double *out_ub, int *info) {
+               double *out_ub, int *info, int cap, int *log_col, double *log_sign,
+               int *log_st, double *log_val) {
   const QSpecI &s = *sp;
   EnvPtr env = (EnvPtr) new Environment();
   int err = 0;
@@ -412,14 +414,20 @@ int integ_obbt(int device, const QSpecI *sp, int has_inc, double inc, double *ou
     std::vector<double> st(6, 0.0);
     bte->fillStats(st);
     info[2] = (int)st[0];
+    const auto &lg = bte->solveLog();
+    for (size_t k = 0; k < lg.size() && (int)k < cap; ++k) {
+      log_col[k] = lg[k].col;
+      log_sign[k] = lg[k].sign;
+      log_st[k] = lg[k].status;
+      log_val[k] = lg[k].value;
+    }
   }
   for (int j = 0; j < s.nv; ++j) {
     out_lb[j] = p->getVariable(j)->getLb();
     out_ub[j] = p->getVariable(j)->getUb();
   }
   root_e->clear();
-  delete qh;
-  delete bte;
+  delete qh;          // QuadHandler's destructor deletes its bte_ (QuadHandler.cpp:118-120)
   delete root_e;
   delete spool;
   delete rel;
