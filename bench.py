@@ -223,7 +223,7 @@ def tree_search(ctx, dev, rank, world, B, args):
             import oracle
             opt = oracle.highs_milp(p)[1]
         inc, nodes, lps, piv, pruned, rounds, el, moved = run_tree(ctx, dev, rank, world, p, B,
-                                                                   order, warm, 1 << 22)
+                                                                   order, warm, 1 << 23)
         out.append({"instance": p.name, "vars": p.n, "rows": p.m,
                     "search": ("best-first" if order else "depth-first over batches") +
                               (", parent-basis warm starts" if warm else
@@ -425,6 +425,9 @@ def main():
     ap.add_argument('--batch', type=int, default=524288,
                     help='open nodes per GPU per step (524288: K1 persistent waves refill '
                          'their lanes; 131072 = one node per resident lane)')
+    ap.add_argument('--tree-batch', type=int, default=131072,
+                    help='open nodes per GPU per round of the complete trees (tree_search, '
+                         'convex_batch)')
     ap.add_argument('--cpu-seconds', type=float, default=16.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-bnb', action='store_true',
@@ -537,8 +540,9 @@ def main():
     mdist.allreduce_sum(cnt)
     elapsed = float(tot.item())
     solved, pivots, pfi_solved, pfi_pivots = (float(v) for v in cnt.tolist())
-    tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, B, args)
-    cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, B, args)
+    TB = args.tree_batch
+    tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, TB, args)
+    cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, TB, args)
     qprel = None if args.no_qp else qp_relaxation(ctx, dev, rank, world, args)
     ksn = None if args.no_knapsack else knapsack_nodes(ctx, dev, rank, world, args)
     ctx.load(p)
@@ -575,7 +579,7 @@ def main():
         dom = lp_kernel if lp_main_ms >= fbbt_ms else "fbbt"
         kd = kernels[dom]
         traffic, tsrc = pmc_traffic(dom, B)
-        roofline = {"kernel": dom, "bound": "hbm" if dom == "fbbt" else "mfma",
+        roofline = {"kernel": dom, "bound": "hbm" if dom == "fbbt" else "fp64",
                     "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
                     "frac": kd["frac"], "traffic": traffic}
         if tsrc:
