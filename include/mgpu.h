@@ -144,6 +144,39 @@ int mgpu_lp_solve_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double
                       int32_t *d_wo_head, int8_t *d_wo_st, double *d_wo_d,
                       double *d_wo_binv);
 
+/* ---- per-node rows (the glob path) ---------------------------------------
+ * QuadHandler rewrites the secant / McCormick rows of the relaxation at
+ * every node (upSqCon_ / upBilCon_, QuadHandler.cpp:3322-3419) and hands
+ * them to the engine through OsiLPEngine::changeConstraint (OsiLPEngine.cpp:
+ * 206-243), after which Clp refactors the kept basis.  Batched: the loaded
+ * relaxation fixes the sparsity pattern; node b brings a value record
+ * vals[b][stride] (e.g. mgpu_quad_fbbt's rows_out, zero-copy) from which
+ *   coef_pos[k] : an entry of the loaded CSR (index into colidx/val) whose
+ *                 value is vals[b][coef_src[k]]; |value| <= 1e-9 counts as
+ *                 the term's absence (LinearFunction::addTerm,
+ *                 LinearFunction.cpp:89-95);
+ *   row_idx[q]  : a row whose bounds are vals[b][lo_src[q]] / vals[b][hi_src[q]]
+ *                 (-1 keeps the loaded bound).
+ * mgpu_set_node_rows validates and uploads the map (cleared by mgpu_load_lp;
+ * ncoef = nrow = 0 clears it).  mgpu_lp_solve_rows[_dev] then solves every
+ * node's own LP: with a warm basis (head [m] + st [n+m], shared or per node)
+ * the basis is refactored for each node's matrix on the device (K3R: the
+ * oracle's Gauss-Jordan with partial pivoting; singular -> slack basis) and
+ * its reduced costs recomputed, then the dense dual simplex K3 runs from it
+ * (m <= 64).  Outputs as mgpu_lp_solve. */
+int mgpu_set_node_rows(mgpu_ctx *ctx, int stride, int ncoef, const int32_t *coef_pos,
+                       const int32_t *coef_src, int nrow, const int32_t *row_idx,
+                       const int32_t *lo_src, const int32_t *hi_src);
+int mgpu_lp_solve_rows(mgpu_ctx *ctx, int batch, const double *lb, const double *ub,
+                       const int32_t *skip, const double *vals, const int32_t *ws_head,
+                       const int8_t *ws_st, int ws_shared, int iter_limit, int32_t *status,
+                       double *obj, int32_t *iters, double *x);
+int mgpu_lp_solve_rows_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double *d_ub,
+                           const int32_t *d_skip, const double *d_vals,
+                           const int32_t *d_ws_head, const int8_t *d_ws_st, int ws_shared,
+                           int iter_limit, int32_t *d_status, double *d_obj, int32_t *d_iters,
+                           double *d_x);
+
 /* Node decision after the relaxation solve (device pointers, async): the
  * EngineStatus switch of PCBProcessor::shouldPrune_ (PCBProcessor.cpp:400-523)
  * plus IntVarHandler::isFeasible (IntVarHandler.cpp:54-84).
@@ -358,7 +391,8 @@ int mgpu_quad_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in, const do
                        int32_t *d_mod_idx, double *d_mod_v1, double *d_mod_v2);
 
 /* Device-side timing of the last launch of the named kernel family
- * ("fbbt", "lp", "quad", "qp"), measured with hipEvents on the context stream.
+ * ("fbbt", "lp", "quad", "qp", "refactor" = K3R of the last
+ * mgpu_lp_solve_rows), measured with hipEvents on the context stream.
  * "lp" is the whole LP call; "lp_main" its first kernel (K3P, or the only
  * one) and "lp_tail" the dense K3 re-solve of K3P's overflow list (0 when
  * K3P did not run). */

@@ -74,6 +74,14 @@ struct mgpu_ctx {
   hipEvent_t ev8 = nullptr;    // between K3P and its dense overflow re-solve
   bool last_lp_pfi = false;    // the last LP call ran K3P
   double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0, last_qp_ms = 0.0;
+  // per-node rows (mgpu_set_node_rows): device maps csc_pos, csr_pos,
+  // coef_src, row, lo_src, hi_src; K3R's per-node warm starts; host-path
+  // staging of the node records
+  bool nr_set = false;
+  int nr_stride = 0, nr_ncoef = 0, nr_nrow = 0;
+  DevBuf nr_map, nr_ws, nr_vals;
+  hipEvent_t ev9 = nullptr, ev10 = nullptr;  // around K3R
+  double last_refac_ms = 0.0;
   QuadState *quad = nullptr;   // K2 problem (mgpu_load_quad)
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
   QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)

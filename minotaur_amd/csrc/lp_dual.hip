@@ -78,6 +78,11 @@ __host__ __device__ inline size_t shared_ws_bytes(int n, int m) {
 __host__ __device__ inline size_t wave_bytes(int N) {
   return 6 * al16((size_t)N * 8) + 2 * al16((size_t)N) + 2 * 64 * 8;
 }
+// per-node rows: the wave's copy of the matrix values (CSC, CSR) and row
+// bounds, with the node's entries written over the loaded ones
+__host__ __device__ inline size_t rows_wave_bytes(int m, int nnz) {
+  return 2 * al16((size_t)nnz * 8) + 2 * al16((size_t)m * 8);
+}
 
 __device__ __forceinline__ double art_lo(double thi, double ab) {
   return (thi < kInfB ? thi : 0.0) - ab;
@@ -272,7 +277,9 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     // loop-invariant B^-1 init values / LDS addresses out of the node loop
     int lane = lane0;
     asm volatile("" : "+v"(lane));
-    unsigned char *wp = p + (size_t)wave * wave_bytes(N);
+    const bool nrows = io.nr.vals != nullptr;
+    unsigned char *wp =
+        p + (size_t)wave * (wave_bytes(N) + (nrows ? rows_wave_bytes(m, nnz) : 0));
     Ctx C;
     C.colptr = s_colptr; C.rowidx = s_rowidx; C.cval = s_cval;
     C.rowptr = s_rowptr; C.ccol = s_ccol; C.rval = s_rval;
@@ -285,7 +292,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     C.st = (int8_t *)wp;  wp += al16((size_t)N);
     C.art = (int8_t *)wp; wp += al16((size_t)N);
     C.rho = (double *)wp; wp += 64 * 8;
-    C.aq = (double *)wp;
+    C.aq = (double *)wp;  wp += 64 * 8;
     C.n = n; C.m = m; C.N = N;
     C.nlb = io.lb + (size_t)b * io.box_stride;
     C.nub = io.ub + (size_t)b * io.box_stride;
@@ -301,6 +308,40 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         io.iters[b] = 0;
       }
       continue;
+    }
+    if (nrows) {
+      // the node's matrix and row bounds: the loaded values, then its own
+      // entries (OsiLPEngine::changeConstraint of the rewritten rows)
+      double *wc = (double *)wp;  wp += al16((size_t)nnz * 8);
+      double *wr = (double *)wp;  wp += al16((size_t)nnz * 8);
+      double *wlo = (double *)wp; wp += al16((size_t)m * 8);
+      double *whi = (double *)wp;
+      for (int t = lane; t < nnz; t += 64) {
+        wc[t] = s_cval[t];
+        wr[t] = s_rval[t];
+      }
+      for (int i = lane; i < m; i += 64) {
+        wlo[i] = lp.rlo[i];
+        whi[i] = lp.rhi[i];
+      }
+      wave_sync();
+      const double *rec = io.nr.vals + (size_t)b * io.nr.stride;
+      for (int q = lane; q < io.nr.ncoef; q += 64) {
+        double v = rec[io.nr.coef_src[q]];
+        if (fabs(v) <= kLfTol) v = 0.0;
+        wc[io.nr.csc_pos[q]] = v;
+        wr[io.nr.csr_pos[q]] = v;
+      }
+      for (int q = lane; q < io.nr.nrow; q += 64) {
+        const int r = io.nr.row[q];
+        if (io.nr.lo_src[q] >= 0) wlo[r] = rec[io.nr.lo_src[q]];
+        if (io.nr.hi_src[q] >= 0) whi[r] = rec[io.nr.hi_src[q]];
+      }
+      wave_sync();
+      C.cval = wc;
+      C.rval = wr;
+      C.rlo = wlo;
+      C.rhi = whi;
     }
 
     // ---- working bounds; an empty box is infeasible before any pivot ----
@@ -661,6 +702,10 @@ size_t lp_lds_bytes(int n, int m, int nnz) {
   return shared_a_bytes(n, m, nnz) + (size_t)kLpWaves * wave_bytes(n + m);
 }
 
+size_t lp_lds_bytes_rows(int n, int m, int nnz) {
+  return lp_lds_bytes(n, m, nnz) + (size_t)kLpWaves * rows_wave_bytes(m, nnz);
+}
+
 static size_t lp_lds_bytes_shared(int n, int m, int nnz) {
   return lp_lds_bytes(n, m, nnz) + shared_ws_bytes(n, m);
 }
@@ -668,11 +713,13 @@ static size_t lp_lds_bytes_shared(int n, int m, int nnz) {
 hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, int num_cus, hipStream_t stream) {
   if (io.batch <= 0) return hipSuccess;
   if (lp.m > kLpMaxM) return hipErrorInvalidValue;
-  const bool shared = io.ws.head != nullptr && io.ws.s_head == 0 && io.ws.s_st == 0 &&
-                      io.ws.s_d == 0 && io.ws.s_binv == 0 &&
+  const bool nrows = io.nr.vals != nullptr;
+  const bool shared = !nrows && io.ws.head != nullptr && io.ws.s_head == 0 &&
+                      io.ws.s_st == 0 && io.ws.s_d == 0 && io.ws.s_binv == 0 &&
                       lp_lds_bytes_shared(lp.n, lp.m, lp.nnz) <= 160 * 1024;
-  const size_t lds = shared ? lp_lds_bytes_shared(lp.n, lp.m, lp.nnz)
-                            : lp_lds_bytes(lp.n, lp.m, lp.nnz);
+  const size_t lds = shared  ? lp_lds_bytes_shared(lp.n, lp.m, lp.nnz)
+                     : nrows ? lp_lds_bytes_rows(lp.n, lp.m, lp.nnz)
+                             : lp_lds_bytes(lp.n, lp.m, lp.nnz);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {

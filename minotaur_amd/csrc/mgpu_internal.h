@@ -78,8 +78,31 @@ struct LpWarm {
   long s_head, s_st, s_d, s_binv;   // per-node strides in elements (0 = shared)
 };
 
+// Per-node rows (the glob path: QuadHandler::upSqCon_/upBilCon_ rewrite the
+// secant and McCormick rows at every node, QuadHandler.cpp:3322-3419, and
+// OsiLPEngine::changeConstraint hands them to the LP, OsiLPEngine.cpp:
+// 206-243).  The sparsity pattern is the loaded one; node b overrides the
+// values of `ncoef` matrix entries and the bounds of `nrow` rows from its
+// value record vals[b * stride ...] (e.g. K2's row state, zero-copy).
+struct NodeRowsIO {
+  const double *vals;           // [B][stride]; null = no per-node rows
+  long stride;
+  int ncoef;
+  const int32_t *csc_pos;       // [ncoef] entry position in the CSC arrays
+  const int32_t *csr_pos;       // [ncoef] entry position in the CSR arrays
+  const int32_t *coef_src;      // [ncoef] offset in a node record
+  int nrow;
+  const int32_t *row;           // [nrow] row index
+  const int32_t *lo_src;        // [nrow] offset of the row's lower bound, -1 = loaded
+  const int32_t *hi_src;        // [nrow] offset of the row's upper bound, -1 = loaded
+};
+// LinearFunction::addTerm keeps only |a| > 1e-9 (LinearFunction.cpp:22,
+// 89-95): a smaller node coefficient is the term's absence, i.e. 0.
+constexpr double kLfTol = 1e-9;
+
 struct LpIO {
   int batch;
+  NodeRowsIO nr;                // K3 only: per-node matrix values / row bounds
   const double *lb, *ub;        // [B][n] node boxes
   long box_stride;              // elements between boxes (n; 0 = one shared box)
   const int32_t *obj_col;       // [B] or null: LP b minimises obj_sign[b] * x[obj_col[b]]
@@ -155,6 +178,31 @@ struct DecideIO {
 hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t stream);
 
 size_t lp_lds_bytes(int n, int m, int nnz);
+// K3 with per-node rows: each wave also keeps its node's matrix values and
+// row bounds in LDS
+size_t lp_lds_bytes_rows(int n, int m, int nnz);
+
+// K3R (lp_rows.hip): the warm basis refactored for each node's own matrix
+// (OsiLPEngine::changeConstraint then Clp's factorisation of the kept
+// basis): the oracle's invert_basis (Gauss-Jordan, partial pivoting, a
+// pivot below 1e-12 = singular -> slack basis) and compute_duals, bit for
+// bit.  Writes a per-node warm start (head, st, d, binv column-major).
+struct RefacIO {
+  int batch;
+  NodeRowsIO nr;
+  const int32_t *skip;          // [B] or null
+  const int32_t *head;          // warm basis in: [m] (s_head 0) or [B][m]
+  const int8_t *st;             // [n+m] or [B][n+m]
+  long s_head, s_st;
+  int32_t *o_head;              // [B][m]
+  int8_t *o_st;                 // [B][n+m]
+  double *o_d;                  // [B][n+m]
+  double *o_binv;               // [B][m][m] column-major
+  int32_t *o_sing;              // [B] 1: singular, slack basis (or null)
+};
+size_t lp_refactor_lds_bytes(int n, int m, int nnz);
+hipError_t launch_lp_refactor(const DevLP &lp, const RefacIO &io, hipStream_t stream);
+
 hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, int num_cus, hipStream_t stream);
 // K3L (lp_large.hip): one node per 256-thread workgroup, B^-1 in HBM slots
 size_t lp_large_lds_bytes(int n, int m);

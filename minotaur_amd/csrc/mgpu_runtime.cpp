@@ -37,7 +37,8 @@ int mgpu_create(int device, mgpu_ctx **out) {
       hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess ||
       hipEventCreate(&c->ev4) != hipSuccess || hipEventCreate(&c->ev5) != hipSuccess ||
       hipEventCreate(&c->ev6) != hipSuccess || hipEventCreate(&c->ev7) != hipSuccess ||
-      hipEventCreate(&c->ev8) != hipSuccess) {
+      hipEventCreate(&c->ev8) != hipSuccess || hipEventCreate(&c->ev9) != hipSuccess ||
+      hipEventCreate(&c->ev10) != hipSuccess) {
     delete c;
     return MGPU_ERR_HIP;
   }
@@ -61,7 +62,7 @@ int mgpu_destroy(mgpu_ctx *c) {
                     &c->lp_ost, &c->lp_od, &c->lp_ob, &c->lp_slots, &c->io_lb_in,
                     &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
                     &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch,
-                    &c->fbbt_next})
+                    &c->fbbt_next, &c->nr_map, &c->nr_ws, &c->nr_vals})
     b->release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -72,6 +73,8 @@ int mgpu_destroy(mgpu_ctx *c) {
   if (c->ev6) (void)hipEventDestroy(c->ev6);
   if (c->ev7) (void)hipEventDestroy(c->ev7);
   if (c->ev8) (void)hipEventDestroy(c->ev8);
+  if (c->ev9) (void)hipEventDestroy(c->ev9);
+  if (c->ev10) (void)hipEventDestroy(c->ev10);
   quad_state_free(c);
   bnb_state_free(c);
   qp_state_free(c);
@@ -127,6 +130,7 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   bnb_state_free(c);  // a tree belongs to the problem it was started on
+  c->nr_set = false;  // so do per-node rows (positions in its CSR)
   c->lp = DevLP{};
   // CSR terms, packed
   c->h_terms.resize(nnz > 0 ? nnz : 1);
@@ -265,6 +269,13 @@ double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
         hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess)
       c->last_fbbt_ms = ms;
     return c->last_fbbt_ms;
+  }
+  if (!strcmp(which, "refactor")) {  // K3R of the last mgpu_lp_solve_rows
+    float ms = 0.f;
+    if (hipEventSynchronize(c->ev10) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev9, c->ev10) == hipSuccess)
+      c->last_refac_ms = ms;
+    return c->last_refac_ms;
   }
   if (!strcmp(which, "lp")) {
     float ms = 0.f;

@@ -324,3 +324,114 @@ def random_quad_boxes(qp: QuadProblem, B: int, seed: int, max_depth: int = 8,
                 else:
                     LB[b, j] = t
     return LB, UB
+
+
+@dataclass
+class NodeRows:
+    """Per-node rows of an LP relaxation (``mgpu_set_node_rows``): entry
+    ``coef_pos[k]`` of the loaded CSR takes a node record's value
+    ``coef_src[k]``; row ``row_idx[q]`` takes bounds ``lo_src[q]`` /
+    ``hi_src[q]`` of it (-1: the loaded bound).  ``stride`` = record length."""
+    stride: int
+    coef_pos: np.ndarray
+    coef_src: np.ndarray
+    row_idx: np.ndarray
+    lo_src: np.ndarray
+    hi_src: np.ndarray
+
+    def node_problem(self, p, rec):
+        """The LP of one node (a copy of ``p`` with the record applied;
+        |a| <= 1e-9 dropped as LinearFunction::addTerm does)."""
+        import copy
+        q = copy.copy(p)
+        val = p.val.copy()
+        v = np.asarray(rec, dtype=np.float64)[self.coef_src]
+        val[self.coef_pos] = np.where(np.abs(v) <= LF_TOL, 0.0, v)
+        q.val = val
+        q.rlo = p.rlo.copy()
+        q.rhi = p.rhi.copy()
+        for r, lo, hi in zip(self.row_idx, self.lo_src, self.hi_src):
+            if lo >= 0:
+                q.rlo[r] = rec[lo]
+            if hi >= 0:
+                q.rhi[r] = rec[hi]
+        return q
+
+
+def relaxation_lp(qp: QuadProblem, rows=None):
+    """The LP relaxation of ``p_`` that mglob's engine solves at a node
+    (QuadHandler::relax_, QuadHandler.cpp:1549-1592, plus the linear rows):
+
+    * rows 0..ncon-1: the original constraints with every product replaced by
+      its auxiliary (SimpleTransformer), bounds clb/cub;
+    * one secant row per square, ``y + a_x x <= rhs`` (upSqCon_ rewrites a_x
+      and rhs), then four McCormick rows per bilinear, ``-y + a0 x0 + a1 x1
+      <= rhs`` (types 0, 1) and ``y + a0 x0 + a1 x1 <= rhs`` (types 2, 3)
+      (upBilCon_ rewrites a0, a1, rhs);
+    * objective: the original objective with products replaced (0 if none).
+
+    ``rows``: the row state at the root (``Context.quad_rows()`` layout,
+    ``QuadProblem.nrow_state`` values).  Returns ``(LinProblem, NodeRows)``;
+    the NodeRows map reads a node's K2 row state (``rows_out``) directly.
+    The rewritten entries are always in the pattern (value 0 when dropped)."""
+    from .problem import LinProblem
+    nsq, nbil = qp.nsq, qp.nbil
+    rows = np.zeros(qp.nrow_state) if rows is None else np.asarray(rows, dtype=np.float64)
+    aux = {}
+    for k in range(nsq):
+        aux[(int(qp.sq_x[k]), int(qp.sq_x[k]))] = int(qp.sq_y[k])
+    for k in range(nbil):
+        aux[(int(qp.bil_x0[k]), int(qp.bil_x1[k]))] = int(qp.bil_y[k])
+
+    def linearize(f):
+        d = {}
+        for t in range(qp.lptr[f], qp.lptr[f + 1]):
+            d[int(qp.lvar[t])] = d.get(int(qp.lvar[t]), 0.0) + float(qp.lval[t])
+        for t in range(qp.qptr[f], qp.qptr[f + 1]):
+            y = aux[(int(qp.qv1[t]), int(qp.qv2[t]))]
+            d[y] = d.get(y, 0.0) + float(qp.qval[t])
+        return [(j, d[j]) for j in sorted(d) if abs(d[j]) > LF_TOL]
+
+    rowptr, colidx, val, rlo, rhi = [0], [], [], [], []
+    coef_pos, coef_src, row_idx, hi_src = [], [], [], []
+
+    def add_row(terms, lo, hi, varying=()):
+        # terms ascending by column; varying: {col: record offset}
+        for j, a in terms:
+            if j in varying:
+                coef_pos.append(len(colidx))
+                coef_src.append(varying[j])
+            colidx.append(j)
+            val.append(a)
+        rowptr.append(len(colidx))
+        rlo.append(lo)
+        rhi.append(hi)
+
+    for c in range(qp.ncon):
+        add_row(linearize(c), float(qp.clb[c]), float(qp.cub[c]))
+    for k in range(nsq):
+        x, y = int(qp.sq_x[k]), int(qp.sq_y[k])
+        row_idx.append(len(rlo))
+        hi_src.append(2 * k + 1)
+        add_row([(x, rows[2 * k]), (y, 1.0)], -np.inf, rows[2 * k + 1], {x: 2 * k})
+    for k in range(nbil):
+        x0, x1, y = int(qp.bil_x0[k]), int(qp.bil_x1[k]), int(qp.bil_y[k])
+        for t in range(4):
+            o = 2 * nsq + 12 * k + 3 * t
+            row_idx.append(len(rlo))
+            hi_src.append(o + 2)
+            add_row([(x0, rows[o]), (x1, rows[o + 1]), (y, -1.0 if t < 2 else 1.0)],
+                    -np.inf, rows[o + 2], {x0: o, x1: o + 1})
+    obj = np.zeros(qp.nv)
+    if qp.has_obj:
+        for j, a in linearize(qp.ncon):
+            obj[j] = a
+    i32 = lambda a: np.asarray(a, dtype=np.int32)
+    p = LinProblem(name=f'{qp.name}-relax', n=qp.nv, m=len(rlo), rowptr=i32(rowptr),
+                   colidx=i32(colidx), val=np.asarray(val, dtype=np.float64),
+                   rlo=np.asarray(rlo, dtype=np.float64), rhi=np.asarray(rhi, dtype=np.float64),
+                   vlb=qp.vlb.copy(), vub=qp.vub.copy(), vtype=qp.vtype.copy(), obj=obj,
+                   obj_const=float(qp.obj_const) if qp.has_obj else 0.0).validate()
+    nr = NodeRows(stride=qp.nrow_state, coef_pos=i32(coef_pos), coef_src=i32(coef_src),
+                  row_idx=i32(row_idx), lo_src=i32([-1] * len(row_idx)), hi_src=i32(hi_src))
+    return p, nr

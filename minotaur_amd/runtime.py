@@ -32,6 +32,7 @@ EXPORTS = [
     'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_bnb_config', 'mgpu_bnb_export',
     'mgpu_bnb_import', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
+    'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev',
 ]
 
 
@@ -103,6 +104,9 @@ def load_library():
     lib.mgpu_load_qp.argtypes = [_P, _I, _I, _P, _P, _D, _P, _P]
     lib.mgpu_qp_solve.argtypes = [_P, _I, _P, _P, _I, _P, _P, _P, _P]
     lib.mgpu_qp_solve_dev.argtypes = [_P, _I, _P, _P, _I, _P, _P, _P, _P]
+    lib.mgpu_set_node_rows.argtypes = [_P, _I, _I, _P, _P, _I, _P, _P, _P]
+    lib.mgpu_lp_solve_rows.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
+    lib.mgpu_lp_solve_rows_dev.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -395,6 +399,56 @@ class Context:
             _dp(status), _dp(obj), _dp(iters), _dp(x),
             _dp(wo.head) if wo else None, _dp(wo.st) if wo else None,
             _dp(wo.d) if wo else None, _dp(wo.binv) if wo else None), 'mgpu_lp_solve_dev')
+
+    # -- per-node rows (glob path) ---------------------------------------------
+    def set_node_rows(self, nr):
+        """``nr``: a ``quad.NodeRows`` map (or None to clear)."""
+        if nr is None:
+            self._chk(self.lib.mgpu_set_node_rows(self.h, 0, 0, None, None, 0, None, None, None),
+                      'mgpu_set_node_rows')
+            return
+        cp, cs = _np(nr.coef_pos, np.int32), _np(nr.coef_src, np.int32)
+        ri, lo, hi = (_np(nr.row_idx, np.int32), _np(nr.lo_src, np.int32),
+                      _np(nr.hi_src, np.int32))
+        self._keep_rows = (cp, cs, ri, lo, hi)
+        self._chk(self.lib.mgpu_set_node_rows(self.h, int(nr.stride), int(cp.size), _hp(cp),
+                                              _hp(cs), int(ri.size), _hp(ri), _hp(lo), _hp(hi)),
+                  'mgpu_set_node_rows')
+
+    def lp_solve_rows(self, lb, ub, vals, ws=None, skip=None, iter_limit=0, want_x=False):
+        """Every node's own LP (node rows from ``vals`` [B, stride]); ``ws``:
+        a WarmStart whose head/st (1-D shared or per node) are refactored for
+        each node's matrix; None = slack basis."""
+        p = self.problem
+        lb = _np(lb, np.float64)
+        ub = _np(ub, np.float64)
+        vals = _np(vals, np.float64)
+        B = lb.shape[0]
+        st = np.zeros(B, dtype=np.int32)
+        obj = np.zeros(B)
+        it = np.zeros(B, dtype=np.int32)
+        x = np.zeros((B, p.n)) if want_x else None
+        wh = wst = None
+        shared = 1
+        if ws is not None:
+            wh = _np(ws.head, np.int32)
+            wst = _np(ws.st, np.int8)
+            shared = 1 if wh.ndim == 1 else 0
+        sk = None if skip is None else _np(skip, np.int32)
+        self._chk(self.lib.mgpu_lp_solve_rows(
+            self.h, B, _hp(lb), _hp(ub), _hp(sk), _hp(vals), _hp(wh), _hp(wst), shared,
+            int(iter_limit), _hp(st), _hp(obj), _hp(it), _hp(x)), 'mgpu_lp_solve_rows')
+        return LpOut(st, obj, it, x, None)
+
+    def lp_solve_rows_dev(self, lb, ub, vals, status, obj, iters, ws=None, skip=None,
+                          iter_limit=0, x=None):
+        """Torch CUDA tensors (``vals`` e.g. quad_fbbt_dev's rows_out)."""
+        B = int(lb.shape[0])
+        shared = 1 if (ws is None or ws.head.dim() == 1) else 0
+        self._chk(self.lib.mgpu_lp_solve_rows_dev(
+            self.h, B, _dp(lb), _dp(ub), _dp(skip), _dp(vals),
+            _dp(ws.head) if ws else None, _dp(ws.st) if ws else None, shared, int(iter_limit),
+            _dp(status), _dp(obj), _dp(iters), _dp(x)), 'mgpu_lp_solve_rows_dev')
 
     def lp_bound(self, cols, signs, lb=None, ub=None, ws=None, iter_limit=0, want_x=False):
         """Bound LPs min sign_b * x[col_b] on one box (host arrays); ws: the

@@ -697,3 +697,61 @@ int orc_dual_simplex_nodes(int n, int m, const int *colptr, const int *rowidx,
   }
   return 0;
 }
+
+/* Per-node rows (mgpu_lp_solve_rows, the glob path: QuadHandler::upSqCon_ /
+ * upBilCon_ rewrite rows at every node, QuadHandler.cpp:3322-3419, and
+ * OsiLPEngine::changeConstraint loads them, OsiLPEngine.cpp:206-243): node b
+ * solves the loaded LP with matrix entries csc_pos[k] (CSC order) set to
+ * vals[b][coef_src[k]] (|v| <= 1e-9 -> 0, LinearFunction::addTerm) and the
+ * bounds of rows row[q] from vals[b][lo_src[q]] / vals[b][hi_src[q]] (-1 =
+ * loaded), from the warm basis head/st (shared when ws_shared, else per node)
+ * with the inverse rebuilt for the node's matrix (invert_basis, singular ->
+ * slack basis) and compute_duals; dense arithmetic (K3R + K3). */
+int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
+                          const double *cval, const double *c, const double *rlo,
+                          const double *rhi, int B, const double *lb, const double *ub,
+                          const double *vals, int stride, int ncoef, const int *csc_pos,
+                          const int *coef_src, int nrow, const int *row, const int *lo_src,
+                          const int *hi_src, const int *ws_head, const signed char *ws_st,
+                          int ws_shared, int iter_limit, int *status, double *obj, double *x,
+                          int *iters, int nthreads)
+{
+  const int nnz = colptr[n];
+  const size_t N = (size_t) (n + m);
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+  {
+    double *cv = (double *) malloc(sizeof(double) * (size_t) (nnz + 1));
+    double *lo = (double *) malloc(sizeof(double) * (size_t) (m + 1));
+    double *hi = (double *) malloc(sizeof(double) * (size_t) (m + 1));
+    int *h = (int *) malloc(sizeof(int) * (size_t) (m + 1));
+    signed char *s = (signed char *) malloc(N + 1);
+    double *bi = (double *) malloc(sizeof(double) * (size_t) m * m + 8);
+    orc_lp P;
+    P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cv; P.c = c;
+    P.rlo = lo; P.rhi = hi;
+#pragma omp for schedule(dynamic, 8)
+    for (int b = 0; b < B; ++b) {
+      const double *rec = vals + (size_t) b * stride;
+      memcpy(cv, cval, sizeof(double) * (size_t) nnz);
+      memcpy(lo, rlo, sizeof(double) * (size_t) m);
+      memcpy(hi, rhi, sizeof(double) * (size_t) m);
+      for (int k = 0; k < ncoef; ++k) {
+        double v = rec[coef_src[k]];
+        cv[csc_pos[k]] = fabs(v) <= 1e-9 ? 0.0 : v;
+      }
+      for (int q = 0; q < nrow; ++q) {
+        if (lo_src[q] >= 0) lo[row[q]] = rec[lo_src[q]];
+        if (hi_src[q] >= 0) hi[row[q]] = rec[hi_src[q]];
+      }
+      const int have = ws_head != 0;
+      const size_t wb = ws_shared ? 0 : (size_t) b;
+      status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n,
+                               have ? ws_head + wb * m : 0, have ? ws_st + wb * N : 0, 0, 0, have,
+                               0, iter_limit, obj + b, x ? x + (size_t) b * n : 0, iters + b, 0, h,
+                               s, bi, 0);
+    }
+    free(cv); free(lo); free(hi); free(h); free(s); free(bi);
+  }
+  return 0;
+}

@@ -551,3 +551,49 @@ def node_decide(vtype, status, obj, x, incumbent=math.inf, fbbt_infeas=None, abs
                 dec[b] = (DEC_ENGINE if st not in (0, 1, 6, 7, 9) else
                           DEC_BRANCH if frac else DEC_FEASIBLE)
     return dec, meas
+
+
+def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1,
+                      want_x=False):
+    """Per-node rows (mgpu_lp_solve_rows): node b solves ``p`` with the entries
+    and row bounds of ``nr`` (a quad.NodeRows) taken from ``vals[b]``, from
+    the warm basis ``ws`` (head/st; 1-D shared or per node) refactored for
+    its matrix.  Returns (status, obj incl. constant, iters, x)."""
+    l = lib()
+    l.orc_dual_simplex_rows.restype = _I
+    l.orc_dual_simplex_rows.argtypes = ([_I, _I] + [_P] * 6 + [_I] + [_P] * 3 + [_I, _I]
+                                        + [_P] * 2 + [_I] + [_P] * 5 + [_I, _I] + [_P] * 4
+                                        + [_I])
+    LB = np.ascontiguousarray(LB, dtype=np.float64)
+    UB = np.ascontiguousarray(UB, dtype=np.float64)
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    B = LB.shape[0]
+    colptr, rowidx, cval = lp_csc(p)
+    # CSR entry -> CSC position (lp_csc fills in CSR order)
+    csc_of = np.empty(p.nnz, dtype=np.int32)
+    fill = colptr[:-1].copy()
+    for k in range(p.nnz):
+        j = p.colidx[k]
+        csc_of[k] = fill[j]
+        fill[j] += 1
+    cpos = np.ascontiguousarray(csc_of[nr.coef_pos], dtype=np.int32)
+    csrc = np.ascontiguousarray(nr.coef_src, dtype=np.int32)
+    row = np.ascontiguousarray(nr.row_idx, dtype=np.int32)
+    lo = np.ascontiguousarray(nr.lo_src, dtype=np.int32)
+    hi = np.ascontiguousarray(nr.hi_src, dtype=np.int32)
+    h = s = None
+    shared = 1
+    if ws is not None:
+        h = np.ascontiguousarray(ws.head, dtype=np.int32)
+        s = np.ascontiguousarray(ws.st, dtype=np.int8)
+        shared = 1 if h.ndim == 1 else 0
+    st = np.zeros(B, dtype=np.int32)
+    obj = np.zeros(B)
+    it = np.zeros(B, dtype=np.int32)
+    x = np.zeros((B, p.n)) if want_x else None
+    l.orc_dual_simplex_rows(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj),
+                            _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(vals),
+                            int(nr.stride), int(cpos.size), _ptr(cpos), _ptr(csrc), int(row.size),
+                            _ptr(row), _ptr(lo), _ptr(hi), _ptr(h), _ptr(s), shared, iter_limit,
+                            _ptr(st), _ptr(obj), _ptr(x), _ptr(it), nthreads)
+    return st, obj + p.obj_const, it, x
