@@ -258,6 +258,11 @@ typedef struct {
                                    (TreeManager::getCandidate)            */
   long long lps, pivots;        /* node LPs solved (OsiLPStats::calls) and
                                    their simplex pivots                   */
+  long long sb_lps, sb_pivots;  /* reliability branching: strong-branching
+                                   LPs (also OsiLPStats::calls) and pivots */
+  long long sb_pruned;          /* nodes PrunedByBrancher                 */
+  long long sb_modified;        /* nodes ModifiedByBrancher (re-queued
+                                   with the one-sided bound change)       */
 } mgpu_bnb_stats;
 
 /* Search options of the next mgpu_bnb_init (default 0, 0):
@@ -275,6 +280,20 @@ typedef struct {
  *            146-150); the basis lives with the node in HBM, m*4 + (n+m)*9 +
  *            m*m*8 bytes per pool slot (K3 / K3L per-node warm starts). */
 int mgpu_bnb_config(mgpu_ctx *ctx, int order, int warm);
+
+/* Brancher of the next mgpu_bnb_init: 0 MaxVioBrancher (default), 1
+ * ReliabilityBrancher (the reference's default, ReliabilityBrancher.cpp) with
+ * its defaults: pseudocosts, reliability threshold 4 observations per side,
+ * node distance 50, at most 20 unreliable candidates strong-branched per
+ * node with an iteration limit of 25, pruning / one-sided bound changes
+ * from strong branching (trustCutoff).  Batched semantics: the nodes of a
+ * round see the pseudocost state of the round's start (plus each node's own
+ * updateAfterSolve observation); the round's observations are folded in
+ * node order after it, so batch 1 is the reference's sequence.  All the
+ * round's strong-branching LPs run in one K3 / K3L batch, each from its
+ * node's optimal basis.  Pseudocosts stay with the rank (MpiBranchAndBound
+ * keeps one brancher per process). */
+int mgpu_bnb_brancher(mgpu_ctx *ctx, int kind);
 
 int mgpu_bnb_init(mgpu_ctx *ctx, int capacity, const double *root_lb, const double *root_ub,
                   double incumbent);

@@ -28,6 +28,9 @@ struct BnbState {
   std::vector<double> best_x;
   mgpu_bnb_stats tot{};
   int order = 0, warm = 0;     // mgpu_bnb_config at init
+  int rel = 0;                 // mgpu_bnb_brancher at init: 1 = reliability branching
+  long long calls = 0;         // ReliabilityBrancher stats_->calls (findBranches calls)
+  int maxsb = 0;               // strong-branching LP capacity of the child buffers
   int hw = 0;                  // best-first: pool high-water mark
   size_t sort_bytes = 0;
   DevBuf plb, pub, pnlb, pdepth;
@@ -39,13 +42,21 @@ struct BnbState {
   // parent warm starts: per pool slot, per batch (gathered in) and out
   DevBuf pws_head, pws_st, pws_d, pws_binv, bws_head, bws_st, bws_d, bws_binv, wo_head, wo_st,
       wo_d, wo_binv;
+  // reliability branching: pseudocost state [n], parent branching data per
+  // pool slot, per-batch and strong-branching child workspaces
+  DevBuf pc_up, pc_dn, cnt_up, cnt_dn, last, last_new, ppvar, ppval, bnlb, bpvar, bpval, rflag, rrank,
+      nsb, sb_off, sb_var, sb_val, dec2, nev, ev_var, ev_side, ev_cost, rcnt, clb, cub, cnode,
+      cst, cobj, cit;
   void release() {
     for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
                       &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
                       &bmin, &bcnt, &out, &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj,
                       &r_it, &plive, &keys, &keys2, &vals, &vals2, &sort_tmp, &counts,
                       &pws_head, &pws_st, &pws_d, &pws_binv, &bws_head, &bws_st, &bws_d,
-                      &bws_binv, &wo_head, &wo_st, &wo_d, &wo_binv})
+                      &bws_binv, &wo_head, &wo_st, &wo_d, &wo_binv, &pc_up, &pc_dn, &cnt_up,
+                      &cnt_dn, &last, &last_new, &ppvar, &ppval, &bnlb, &bpvar, &bpval, &rflag, &rrank,
+                      &nsb, &sb_off, &sb_var, &sb_val, &dec2, &nev, &ev_var, &ev_side, &ev_cost,
+                      &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit})
       b->release();
   }
 };
@@ -75,6 +86,23 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
   HIPCHK(c, s.bmin.ensure(nblk * 8));
   HIPCHK(c, s.bcnt.ensure(nblk * 7 * 4));
   HIPCHK(c, s.out.ensure(sizeof(BnbOut)));
+  if (s.rel) {
+    for (DevBuf *b : {&s.bpvar, &s.rflag, &s.rrank, &s.nsb, &s.sb_off, &s.dec2, &s.nev})
+      HIPCHK(c, b->ensure((size_t)B * 4));
+    for (DevBuf *b : {&s.bnlb, &s.bpval}) HIPCHK(c, b->ensure((size_t)B * 8));
+    HIPCHK(c, s.sb_var.ensure((size_t)B * kRelMaxCands * 4));
+    HIPCHK(c, s.sb_val.ensure((size_t)B * kRelMaxCands * 8));
+    HIPCHK(c, s.ev_var.ensure((size_t)B * kRelEvents * 4));
+    HIPCHK(c, s.ev_side.ensure((size_t)B * kRelEvents));
+    HIPCHK(c, s.ev_cost.ensure((size_t)B * kRelEvents * 8));
+  }
+  if (s.warm || s.rel) {  // reliability branching needs each node's optimal basis
+    const size_t N = n + m;
+    HIPCHK(c, s.wo_head.ensure((size_t)B * m * 4 + 4));
+    HIPCHK(c, s.wo_st.ensure((size_t)B * N + 4));
+    HIPCHK(c, s.wo_d.ensure((size_t)B * N * 8));
+    HIPCHK(c, s.wo_binv.ensure((size_t)B * m * m * 8 + 8));
+  }
   if (s.warm) {
     const size_t N = n + m;
     HIPCHK(c, s.bws_head.ensure((size_t)B * m * 4 + 4));
@@ -90,6 +118,93 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
   return MGPU_OK;
 }
 
+// Reliability branching for the round's nodes (bnb_rel.hip): candidates
+// and strong-branching lists, the strong-branching LPs in one K3/K3L batch
+// (each from its node's optimal basis, iteration limit 25), the choice, and
+// the pseudocost update.  Leaves the final decisions in s.dec2 and the
+// choice / bound change in s.bvar / s.bval / s.bup.
+int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
+  const int n = s.n, m = c->lp.m, N = n + m;
+  HIPCHK(c, launch_rel_gather(nb, base, bfs ? s.vals2.as<uint32_t>() : nullptr,
+                              s.pnlb.as<double>(), s.ppvar.as<int32_t>(), s.ppval.as<double>(),
+                              s.bnlb.as<double>(), s.bpvar.as<int32_t>(), s.bpval.as<double>(),
+                              c->stream));
+  int32_t *tot = reinterpret_cast<int32_t *>(s.rcnt.as<char>() + 32);  // [2] after counters
+  HIPCHK(c, hipMemsetAsync(s.rcnt.p, 0, 48, c->stream));
+  RelIO r{};
+  r.nb = nb;
+  r.n = n;
+  r.vtype = c->lp.vtype;
+  r.decision = s.dec.as<int32_t>();
+  r.x = s.x.as<double>();
+  r.obj = s.obj.as<double>();
+  r.nlb = s.bnlb.as<double>();
+  r.pvar = s.bpvar.as<int32_t>();
+  r.pval = s.bpval.as<double>();
+  r.pc_up = s.pc_up.as<double>();
+  r.pc_dn = s.pc_dn.as<double>();
+  r.cnt_up = s.cnt_up.as<int32_t>();
+  r.cnt_dn = s.cnt_dn.as<int32_t>();
+  r.last = s.last.as<int32_t>();
+  r.last_new = s.last_new.as<int32_t>();
+  HIPCHK(c, hipMemsetAsync(s.last_new.p, 0xFF, (size_t)n * 4, c->stream));
+  r.calls0 = s.calls;
+  r.rank = s.rrank.as<int32_t>();
+  r.cutoff = s.inc;
+  r.nsb = s.nsb.as<int32_t>();
+  r.sb_var = s.sb_var.as<int32_t>();
+  r.sb_val = s.sb_val.as<double>();
+  r.sb_off = s.sb_off.as<int32_t>();
+  r.dec_out = s.dec2.as<int32_t>();
+  r.bvar = s.bvar.as<int32_t>();
+  r.bval = s.bval.as<double>();
+  r.bup = s.bup.as<int8_t>();
+  r.nev = s.nev.as<int32_t>();
+  r.ev_var = s.ev_var.as<int32_t>();
+  r.ev_side = s.ev_side.as<int8_t>();
+  r.ev_cost = s.ev_cost.as<double>();
+  r.counters = s.rcnt.as<unsigned long long>();
+  HIPCHK(c, launch_rel_rank(r, s.rflag.as<int32_t>(), s.rrank.as<int32_t>(), tot, c->stream));
+  HIPCHK(c, launch_rel_prepare(r, s.sb_off.as<int32_t>(), tot + 1, c->stream));
+  int32_t h_tot[2] = {0, 0};
+  HIPCHK(c, hipMemcpyAsync(h_tot, tot, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int nchild = 2 * h_tot[1];
+  if (nchild > 0) {
+    if (nchild > s.maxsb) {
+      HIPCHK(c, s.clb.ensure((size_t)nchild * n * 8));
+      HIPCHK(c, s.cub.ensure((size_t)nchild * n * 8));
+      for (DevBuf *b : {&s.cnode, &s.cst, &s.cit}) HIPCHK(c, b->ensure((size_t)nchild * 4));
+      HIPCHK(c, s.cobj.ensure((size_t)nchild * 8));
+      s.maxsb = nchild;
+    }
+    HIPCHK(c, launch_rel_children(r, s.wlb.as<double>(), s.wub.as<double>(), s.clb.as<double>(),
+                                  s.cub.as<double>(), s.cnode.as<int32_t>(), c->stream));
+    // the strong-branching LPs: child -> its node's optimal basis (strides
+    // per node, indexed through ws_index), ReliabilityBrancher's iteration cap
+    LpIO io{};
+    io.batch = nchild;
+    io.lb = s.clb.as<double>();
+    io.ub = s.cub.as<double>();
+    io.box_stride = n;
+    io.ws = LpWarm{s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), s.wo_d.as<double>(),
+                   s.wo_binv.as<double>(), m, N, N, (long)m * m};
+    io.ws_index = s.cnode.as<int32_t>();
+    io.iter_limit = kRelIterLimit;
+    io.status = s.cst.as<int32_t>();
+    io.obj = s.cobj.as<double>();
+    io.iters = s.cit.as<int32_t>();
+    const int lrc = launch_lp_nodes(c, io);
+    if (lrc != MGPU_OK) return lrc;
+    r.c_status = s.cst.as<int32_t>();
+    r.c_obj = s.cobj.as<double>();
+    r.c_iters = s.cit.as<int32_t>();
+  }
+  HIPCHK(c, launch_rel_decide(r, c->stream));
+  s.calls += h_tot[0];
+  return MGPU_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -100,6 +215,14 @@ int mgpu_bnb_config(mgpu_ctx *c, int order, int warm) {
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_config: order and warm are 0 or 1");
   c->bnb_order = order;
   c->bnb_warm = warm;
+  return MGPU_OK;
+}
+
+int mgpu_bnb_brancher(mgpu_ctx *c, int kind) {
+  if (!c) return MGPU_ERR_ARG;
+  if (kind < 0 || kind > 1)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_brancher: 0 (MaxVio) or 1 (reliability)");
+  c->bnb_brancher = kind;
   return MGPU_OK;
 }
 
@@ -119,7 +242,27 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   s->inc = incumbent;
   s->order = c->bnb_order;
   s->warm = c->bnb_warm;
+  s->rel = c->bnb_brancher;
   s->tot.incumbent = incumbent;
+  if (s->rel) {
+    if (m > kLpMaxM && !(lp_large_lds_bytes(n, m) <= (size_t)kLargeLdsMax))
+      return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: reliability branching needs K3 or K3L");
+    // ReliabilityBrancher::initialize (:384-398): pseudocosts 0, counts 0,
+    // lastStrBranched_ 20000
+    for (DevBuf *b : {&s->pc_up, &s->pc_dn}) HIPCHK(c, b->ensure((size_t)n * 8));
+    for (DevBuf *b : {&s->cnt_up, &s->cnt_dn, &s->last, &s->last_new})
+      HIPCHK(c, b->ensure((size_t)n * 4));
+    for (DevBuf *b : {&s->pc_up, &s->pc_dn, &s->cnt_up, &s->cnt_dn})
+      HIPCHK(c, hipMemsetAsync(b->p, 0, b->bytes, c->stream));
+    std::vector<int32_t> l20k(n, 20000);
+    HIPCHK(c, hipMemcpyAsync(s->last.p, l20k.data(), (size_t)n * 4, hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, s->ppvar.ensure((size_t)capacity * 4));
+    HIPCHK(c, s->ppval.ensure((size_t)capacity * 8));
+    HIPCHK(c, hipMemsetAsync(s->ppvar.p, 0xFF, (size_t)capacity * 4, c->stream));  // -1: root
+    HIPCHK(c, s->rcnt.ensure(64));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   HIPCHK(c, s->plb.ensure((size_t)capacity * n * 8));
   HIPCHK(c, s->pub.ensure((size_t)capacity * n * 8));
   HIPCHK(c, s->pnlb.ensure((size_t)capacity * 8));
@@ -295,13 +438,18 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
                            s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), s.wo_d.as<double>(),
                            s.wo_binv.as<double>());
   } else {
+    // reliability branching strong-branches from each node's optimal basis:
+    // the node LPs give it back (dense K3 instead of K3P)
     rc = mgpu_lp_solve_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(),
                            s.root_ok ? s.ws_head.as<int32_t>() : nullptr,
                            s.root_ok ? s.ws_st.as<int8_t>() : nullptr,
                            s.root_ok ? s.ws_d.as<double>() : nullptr,
                            s.root_ok ? s.ws_binv.as<double>() : nullptr, 1, 0,
                            s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
-                           s.x.as<double>(), nullptr, nullptr, nullptr, nullptr);
+                           s.x.as<double>(), s.rel ? s.wo_head.as<int32_t>() : nullptr,
+                           s.rel ? s.wo_st.as<int8_t>() : nullptr,
+                           s.rel ? s.wo_d.as<double>() : nullptr,
+                           s.rel ? s.wo_binv.as<double>() : nullptr);
   }
   if (rc != MGPU_OK) return rc;
   DecideIO d{};
@@ -321,10 +469,21 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   d.bval = s.bval.as<double>();
   d.bup = s.bup.as<int8_t>();
   HIPCHK(c, launch_node_decide(c->lp, d, c->stream));
+  const int32_t *decision = s.dec.as<int32_t>();
+  unsigned long long rcnt[4] = {0, 0, 0, 0};
+  if (s.rel) {
+    rc = rel_round(c, s, nb, base, bfs);
+    if (rc != MGPU_OK) return rc;
+    decision = s.dec2.as<int32_t>();
+  }
   BnbIO io{};
   io.nb = nb;
   io.base = base;
-  io.decision = s.dec.as<int32_t>();
+  io.decision = decision;
+  if (s.rel) {
+    io.ppvar = s.ppvar.as<int32_t>();
+    io.ppval = s.ppval.as<double>();
+  }
   io.status = s.st.as<int32_t>();
   io.iters = s.it.as<int32_t>();
   io.cand_obj = s.cand.as<double>();
@@ -352,7 +511,7 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     io.hw = s.hw;
     io.plive = s.plive.as<uint8_t>();
   }
-  if (s.warm) {
+  if (s.warm) {  // (reliability alone: children keep the root warm start)
     io.m = m;
     io.N = N;
     io.wo_head = s.wo_head.as<int32_t>();
@@ -368,14 +527,20 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   HIPCHK(c, launch_bnb_tail(io, n, c->stream));
   BnbOut o;
   HIPCHK(c, hipMemcpyAsync(&o, s.out.p, sizeof o, hipMemcpyDeviceToHost, c->stream));
+  if (s.rel)
+    HIPCHK(c, hipMemcpyAsync(rcnt, s.rcnt.p, sizeof rcnt, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (!bfs) {
-    s.count = base + 2 * o.nbranched;
+    s.count = base + o.nchild;
   } else {
-    s.count = live - nb + 2 * o.nbranched;
-    const long grow = 2L * o.nbranched - nb - holes;
+    s.count = live - nb + o.nchild;
+    const long grow = (long)o.nchild - nb - holes;
     if (grow > 0) s.hw += (int)grow;
   }
+  s.tot.sb_lps += (long long)rcnt[0];
+  s.tot.sb_pruned += (long long)rcnt[1];
+  s.tot.sb_modified += (long long)rcnt[2];
+  s.tot.sb_pivots += (long long)rcnt[3];
   if (o.best_idx >= 0 && o.best < s.inc) {
     s.inc = o.best;
     HIPCHK(c, hipMemcpy(s.best_x.data(), s.x.as<double>() + (size_t)o.best_idx * n,
@@ -442,6 +607,9 @@ int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
   tnlb.release();
   tdep.release();
   HIPCHK(c, e);
+  // the packed pool no longer matches the parent branching data: the kept
+  // nodes make no pseudocost observation on their first solve
+  if (s.rel) HIPCHK(c, hipMemset(s.ppvar.p, 0xFF, s.ppvar.bytes));
   s.count = k;
   s.tot.open = k;
   if (kept) *kept = k;
@@ -621,6 +789,8 @@ int mgpu_bnb_import(mgpu_ctx *c, int k, const double *lb, const double *ub, cons
     HIPCHK(c, hipMemsetAsync(s.plive.as<uint8_t>() + at, 1, (size_t)k, c->stream));
     s.hw += k;
   }
+  if (s.rel)  // migrated nodes carry no parent branching data
+    HIPCHK(c, hipMemsetAsync(s.ppvar.as<int32_t>() + at, 0xFF, (size_t)k * 4, c->stream));
   if (s.warm) {
     // a migrated node starts from the root basis (its parent's stays with
     // the rank that branched it)

@@ -11,8 +11,10 @@
 //   bnb_children    : one wave per branched node writes its two children
 //                     (IntVarHandler::getBranches, IntVarHandler.cpp:125-175:
 //                     down ub = floor(x_j), up lb = ceil(x_j)) at
-//                     base + 2 * prefix, the preferred direction on top of
-//                     the stack so it is popped first.
+//                     base + prefix (prefix counts 2 children per branched
+//                     node, 1 per node reliability branching modified), the
+//                     preferred direction on top of the stack so it is
+//                     popped first.
 // Children inherit the node's FBBT-tightened box, as the reference keeps a
 // node's presolve mods (PCBProcessor::presolveNode_, :134-175).
 #include "bnb_internal.h"
@@ -36,11 +38,13 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
   const int dec = live ? io.decision[i] : -1;
   // stack mode: depth before children overwrite the slots (best-first: gathered)
   if (live && io.slots == nullptr) io.depth_in[i] = io.pdepth[io.base + i];
-  const int f = dec == 0 ? 1 : 0;
+  // children: two per branched node, one per node modified by the brancher
+  // (reliability branching's one-sided bound change, decision 5)
+  const int f = dec == 0 ? 2 : dec == 5 ? 1 : 0;
   s_pos[t] = f;
   s_min[t] = live ? io.cand_obj[i] : INFINITY;
   s_idx[t] = live ? i : INT_MAX;
-  for (int k = 0; k < 5; ++k) s_cnt[t][k] = dec == k ? 1 : 0;
+  for (int k = 0; k < 5; ++k) s_cnt[t][k] = (dec == k || (k == 0 && dec == 5)) ? 1 : 0;
   const bool lp = live && io.status[i] != 12;
   s_cnt[t][5] = lp ? 1 : 0;
   s_cnt[t][6] = lp ? io.iters[i] : 0;
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
   if (cnt[6]) atomicAdd(reinterpret_cast<unsigned long long *>(&io.out->pivots),
                         (unsigned long long)cnt[6]);
   if (t == 0) {
-    io.out->nbranched = s_carry;
+    io.out->nchild = s_carry;
     io.out->best = s_min[0];
     io.out->best_idx = s_idx[0] == INT_MAX ? -1 : s_idx[0];
   }
@@ -146,31 +150,63 @@ __global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
 __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= io.nb || io.decision[i] != 0) return;
-  const int p = io.boff[i / kScanBlock] + io.pos[i];
+  const int dec = i < io.nb ? io.decision[i] : -1;
+  if (dec != 0 && dec != 5) return;
+  const long p = io.boff[i / kScanBlock] + io.pos[i];  // first child index of the node
   const int j = io.bvar[i];
   const double v = io.bval[i];
   const bool up_first = io.bup[i] != 0;
+  // free list F of best-first mode
+  auto slot_of = [&](long c) -> size_t {
+    if (c < io.nb) return io.slots[c];
+    const long h = c - io.nb, holes = io.hw - io.live;
+    if (h < holes) return io.slots[io.live + h];
+    return (size_t)(io.hw + (h - holes));
+  };
+  const double *sl = io.wlb + (size_t)i * n, *su = io.wub + (size_t)i * n;
+  if (dec == 5) {
+    // the node itself again with the brancher's bound change (up: lb = ceil,
+    // else ub = floor), same depth, its LP value as bound, no pseudocost
+    // observation when it is solved again (updateAfterSolve only runs on a
+    // node's first solve, PCBProcessor.cpp:245-248)
+    const size_t c = io.slots == nullptr ? (size_t)io.base + p : slot_of(p);
+    double *cl = io.plb + c * n, *cu = io.pub + c * n;
+    for (int k = lane; k < n; k += 64) {
+      const double l = sl[k], u = su[k];
+      cl[k] = (k == j && up_first) ? ceil(v) : l;
+      cu[k] = (k == j && !up_first) ? floor(v) : u;
+    }
+    if (io.ws_head != nullptr) {
+      const int m = io.m, N = io.N;
+      const size_t mm = (size_t)m * m;
+      for (int k = lane; k < m; k += 64) io.ws_head[c * m + k] = io.wo_head[(size_t)i * m + k];
+      for (int k = lane; k < N; k += 64) {
+        io.ws_st[c * N + k] = io.wo_st[(size_t)i * N + k];
+        io.ws_d[c * N + k] = io.wo_d[(size_t)i * N + k];
+      }
+      for (size_t k = lane; k < mm; k += 64) io.ws_binv[c * mm + k] = io.wo_binv[(size_t)i * mm + k];
+    }
+    if (lane == 0) {
+      io.pnlb[c] = io.obj[i];
+      io.pdepth[c] = io.depth_in[i];
+      if (io.plive != nullptr) io.plive[c] = 1;
+      if (io.ppvar != nullptr) io.ppvar[c] = -1;
+    }
+    return;
+  }
   size_t c_down, c_up;
   if (io.slots == nullptr) {
-    // stack order: slot base + 2p + 1 is popped first
-    const size_t c_first = (size_t)io.base + 2 * (size_t)p + 1;
+    // stack order: slot base + p + 1 is popped first
+    const size_t c_first = (size_t)io.base + (size_t)p + 1;
     const size_t c_second = c_first - 1;
     c_down = up_first ? c_second : c_first;
     c_up = up_first ? c_first : c_second;
   } else {
-    // free list F: the preferred child takes the lower child index 2p
-    auto slot_of = [&](long c) -> size_t {
-      if (c < io.nb) return io.slots[c];
-      const long h = c - io.nb, holes = io.hw - io.live;
-      if (h < holes) return io.slots[io.live + h];
-      return (size_t)(io.hw + (h - holes));
-    };
-    const size_t c_first = slot_of(2L * p), c_second = slot_of(2L * p + 1);
+    // the preferred child takes the lower child index p
+    const size_t c_first = slot_of(p), c_second = slot_of(p + 1);
     c_down = up_first ? c_second : c_first;
     c_up = up_first ? c_first : c_second;
   }
-  const double *sl = io.wlb + (size_t)i * n, *su = io.wub + (size_t)i * n;
   double *dl = io.plb + c_down * n, *du = io.pub + c_down * n;
   double *ul = io.plb + c_up * n, *uu = io.pub + c_up * n;
   for (int k = lane; k < n; k += 64) {
@@ -211,6 +247,12 @@ __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
     if (io.plive != nullptr) {
       io.plive[c_down] = 1;
       io.plive[c_up] = 1;
+    }
+    if (io.ppvar != nullptr) {  // Branch::getActivity: x_j at the branching
+      io.ppvar[c_down] = j;
+      io.ppvar[c_up] = j;
+      io.ppval[c_down] = v;
+      io.ppval[c_up] = v;
     }
   }
 }

@@ -8,7 +8,7 @@ namespace mgpu {
 struct BnbOut {                 // per round, device -> host
   long long ndec[5];            // decision counts (mgpu.h decision codes)
   long long lps, pivots;        // LPs solved (not pruned by FBBT) and their pivots
-  int nbranched;                // nodes with decision 0 (2 children each)
+  int nchild;                   // children written (2 per decision 0, 1 per decision 5)
   int best_idx;                 // batch index of the best integer-feasible node, -1 none
   double best;                  // its objective (+inf none)
 };
@@ -32,7 +32,9 @@ struct BnbIO {
   int32_t *ws_head;             // [cap][m]
   int8_t *ws_st;                // [cap][N]
   double *ws_d, *ws_binv;       // [cap][N], [cap][m][m]
-  const int32_t *decision;      // [nb]
+  const int32_t *decision;      // [nb] (5: one child with the bound change bvar/bval/bup)
+  int32_t *ppvar;               // [cap] or null: the children's parent branching variable
+  double *ppval;                //   and its value (reliability branching's pseudocosts)
   const int32_t *status;        // [nb] LP status (12 = not solved: FBBT-infeasible)
   const int32_t *iters;         // [nb] LP pivots
   const double *cand_obj;       // [nb]
@@ -68,6 +70,59 @@ struct BnbSelIO {
   int8_t *bws_st;
   double *bws_d, *bws_binv;
 };
+
+// Batched reliability branching (bnb_rel.hip).  ReliabilityBrancher
+// defaults (ReliabilityBrancher.cpp:43-58): maxStrongCands_ 20,
+// maxIterations_ 25, thresh_ 4, minNodeDist_ 50, eTol_ 1e-6, trustCutoff_.
+constexpr int kRelMaxCands = 20;
+constexpr int kRelIterLimit = 25;
+constexpr int kRelThresh = 4;
+constexpr int kRelMinDist = 50;
+constexpr double kRelETol = 1e-6;
+constexpr int kRelEvents = 1 + 2 * kRelMaxCands;   // pseudocost observations per node
+struct RelIO {
+  int nb, n;
+  const uint8_t *vtype;         // [n]
+  const int32_t *decision;      // [nb] node_decide's decisions
+  const double *x, *obj;        // [nb][n], [nb] node LP solution
+  const double *nlb;            // [nb] node bound (the parent's LP value)
+  const int32_t *pvar;          // [nb] parent's branching variable (-1: none)
+  const double *pval;           // [nb] its value in the parent's LP solution
+  double *pc_up, *pc_dn;        // [n] pseudocosts (pseudoUp_ / pseudoDown_)
+  int32_t *cnt_up, *cnt_dn;     // [n] timesUp_ / timesDown_
+  int32_t *last;                // [n] lastStrBranched_
+  int32_t *last_new;            // [n] this round's last writer (-1 none): the largest
+                                //   call number that strong-branched the variable
+  long long calls0;             // findBranches calls before this round
+  int32_t *rank;                // [nb] rank among the round's branching nodes
+  double cutoff;                // incumbent value (s_pool best, +inf none)
+  int32_t *nsb;                 // [nb] strong-branched candidates
+  int32_t *sb_var;              // [nb][kRelMaxCands]
+  double *sb_val;
+  int32_t *sb_off;              // [nb] exclusive prefix of nsb
+  const int32_t *c_status;      // strong-branching LPs [2 * total]: down, up per candidate
+  const double *c_obj;
+  const int32_t *c_iters;
+  int32_t *dec_out;             // [nb] 0 branch, 1 pruned by brancher, 5 modified, else as in
+  int32_t *bvar;                // [nb] choice (decision 0) / bound change (decision 5)
+  double *bval;
+  int8_t *bup;                  // 1: up branch first / the up branch's bound change
+  int32_t *nev;                 // [nb] observations
+  int32_t *ev_var;              // [nb][kRelEvents]
+  int8_t *ev_side;              // 0 down, 1 up
+  double *ev_cost;
+  unsigned long long *counters; // [4] strong-branching LPs, pruned, modified, their pivots
+};
+hipError_t launch_rel_rank(const RelIO &io, int32_t *flag, int32_t *rank, int32_t *total,
+                           hipStream_t stream);
+hipError_t launch_rel_prepare(const RelIO &io, int32_t *sb_off, int32_t *total,
+                              hipStream_t stream);
+hipError_t launch_rel_children(const RelIO &io, const double *wlb, const double *wub,
+                               double *clb, double *cub, int32_t *cnode, hipStream_t stream);
+hipError_t launch_rel_decide(const RelIO &io, hipStream_t stream);
+hipError_t launch_rel_gather(int nb, int base, const uint32_t *slots, const double *pnlb,
+                             const int32_t *ppvar, const double *ppval, double *bnlb,
+                             int32_t *bpvar, double *bpval, hipStream_t stream);
 
 hipError_t launch_bnb_tail(const BnbIO &io, int n, hipStream_t stream);
 hipError_t launch_bnb_keys(const double *pnlb, uint8_t *plive, int hw, double cutoff, double ub,

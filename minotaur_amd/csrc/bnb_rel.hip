@@ -1,0 +1,465 @@
+// Batched reliability branching (ReliabilityBrancher, src/base/
+// ReliabilityBrancher.cpp, the reference's default brancher), gfx950.
+//
+// The reference runs findBranches node by node: pseudocost state is updated
+// after every node solve (updateAfterSolve, :508-530) and after every
+// strong-branched candidate (useStrongBranchInfo_, :539-576).  A batched
+// round processes B nodes at once, so here every node of a round sees the
+// pseudocost state of the round's start plus its OWN updateAfterSolve
+// observation; the round's observations are then folded into the state in
+// node order (the reference's order).  With one node per round this is the
+// reference's sequence exactly.
+//
+// Kernels of one round (bnb.cpp drives them after node_decide):
+//   rel_flags / excl_scan : rank of each branching node among the round's
+//                           (findBranches call number = calls0 + rank + 1);
+//   rel_prepare           : per node, the IntVarHandler candidates
+//                           (IntVarHandler.cpp:86-108), the reliable test
+//                           (findCandidates_, :238-320) and the first
+//                           maxStrongCands_ (20) unreliable ones in
+//                           CompareScore order (score, then index);
+//   excl_scan             : offsets of the nodes' strong-branching LPs;
+//   rel_children          : their child boxes (getBrMod: down ub = floor x,
+//                           up lb = ceil x) and warm-start index (the node's
+//                           own optimal basis);
+//   (K3: all children in one batch, iteration limit 25, :101)
+//   rel_decide            : findBestCandidate_ (:75-159) per node: reliable
+//                           pseudocost scores, the strong-branching results
+//                           (shouldPrune_, useStrongBranchInfo_: prune / one-
+//                           sided bound change / pseudocost observation),
+//                           the remaining unreliable candidates; direction
+//                           = down first when change_up > change_down;
+//   pc_fold               : the round's observations into the pseudocosts,
+//                           per variable in node order (updatePCost_).
+// One thread per node in rel_prepare / rel_decide: the logic is a short
+// serial scan over the integer columns with data-dependent exits, not
+// arithmetic that rewards lanes.
+#include "bnb_internal.h"
+
+#include <climits>
+
+namespace mgpu {
+namespace {
+
+__device__ __forceinline__ bool is_int(uint8_t t) { return t == kBinary || t == kInteger; }
+
+// IntVarHandler::getBranchingCandidates: |floor(x + 0.5) - x| > intTol
+__device__ __forceinline__ bool fractional(double v) {
+  return fabs(floor(v + 0.5) - v) > kIntTol;
+}
+
+// ReliabilityBrancher::getScore_ (:368-377)
+__device__ __forceinline__ double rel_score(double up, double down) {
+  return up > down ? down * 0.8 + up * 0.2 : up * 0.8 + down * 0.2;
+}
+
+// updateAfterSolve's observation of this node (:508-530): cost of the
+// parent's branching, (lb - parent lb) / (|x_j - x_j(parent)| + eTol), 0 when
+// negative / inf / nan; side 0 down (x_j decreased), 1 up.
+__device__ __forceinline__ bool after_solve_obs(const RelIO &io, int b, int &var, int &side,
+                                                double &cost) {
+  const int dec = io.decision[b];
+  var = io.pvar[b];
+  if (var < 0 || !(dec == 0 || dec == 3)) return false;
+  const double oldval = io.pval[b], newval = io.x[(size_t)b * io.n + var];
+  double c = (io.obj[b] - io.nlb[b]) / (fabs(newval - oldval) + kRelETol);
+  if (c < 0.0 || isinf(c) || isnan(c)) c = 0.0;
+  cost = c;
+  side = newval < oldval ? 0 : 1;
+  return true;
+}
+
+// the state of variable j as this node sees it: the round's start plus its
+// own updateAfterSolve observation (updatePCost_, :532-537)
+struct PcView {
+  double pu, pd;
+  int cu, cd;
+};
+__device__ __forceinline__ PcView pc_view(const RelIO &io, int j, bool own, int ov, int os,
+                                          double oc) {
+  PcView v{io.pc_up[j], io.pc_dn[j], io.cnt_up[j], io.cnt_dn[j]};
+  if (own && j == ov) {
+    if (os == 0) {
+      v.pd = (v.pd * v.cd + oc) / (v.cd + 1);
+      v.cd += 1;
+    } else {
+      v.pu = (v.pu * v.cu + oc) / (v.cu + 1);
+      v.cu += 1;
+    }
+  }
+  return v;
+}
+
+__device__ __forceinline__ long long calls_of(const RelIO &io, int b) {
+  return io.calls0 + io.rank[b] + 1;
+}
+
+// findCandidates_ reliable test (:297-300).  calls and lastStrBranched_
+// are UInt: their difference wraps around as the reference's does.
+__device__ __forceinline__ bool reliable(const RelIO &io, int j, long long calls, const PcView &v) {
+  const unsigned d = (unsigned)calls - (unsigned)io.last[j];
+  return (double)kRelMinDist > fabs((double)d) || (v.cu >= kRelThresh && v.cd >= kRelThresh);
+}
+
+// unreliable score (:301-304): times - s_wt * (pseudo up + down) - i_wt * max(dd, ud)
+__device__ __forceinline__ double unrel_score(const PcView &v, double dd, double ud) {
+  return (double)(v.cu + v.cd) - 1e-5 * (v.pu + v.pd) - 1e-6 * fmax(dd, ud);
+}
+
+__global__ __launch_bounds__(256) void rel_flags(RelIO io, int32_t *flag) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b < io.nb) flag[b] = io.decision[b] == 0 ? 1 : 0;
+}
+
+// exclusive scan of in[0, nb) into out, total into *total (one workgroup)
+__global__ __launch_bounds__(1024) void excl_scan(const int32_t *in, int32_t *out, int nb,
+                                                  int32_t *total) {
+  __shared__ int s[1024];
+  __shared__ int carry;
+  const int t = threadIdx.x;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < nb; c0 += 1024) {
+    const int i = c0 + t;
+    const int v = i < nb ? in[i] : 0;
+    s[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int u = t >= o ? s[t - o] : 0;
+      __syncthreads();
+      s[t] += u;
+      __syncthreads();
+    }
+    if (i < nb) out[i] = carry + s[t] - v;
+    __syncthreads();
+    if (t == 1023) carry += s[1023];
+    __syncthreads();
+  }
+  if (t == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb) return;
+  int nsb = 0;
+  if (io.decision[b] == 0) {
+    const double *x = io.x + (size_t)b * io.n;
+    int ov = -1, os = 0;
+    double oc = 0.0;
+    const bool own = after_solve_obs(io, b, ov, os, oc);
+    const long long calls = calls_of(io, b);
+    // the first kRelMaxCands unreliable candidates in (score, index) order:
+    // repeated selection of the next larger key
+    double ps = -INFINITY;
+    int pj = -1;
+    for (int k = 0; k < kRelMaxCands; ++k) {
+      double bs = INFINITY;
+      int bj = INT_MAX;
+      for (int j = 0; j < io.n; ++j) {
+        if (!is_int(io.vtype[j])) continue;
+        const double v = x[j];
+        if (!fractional(v)) continue;
+        const PcView pv = pc_view(io, j, own, ov, os, oc);
+        if (reliable(io, j, calls, pv)) continue;
+        const double sc = unrel_score(pv, v - floor(v), ceil(v) - v);
+        const bool after = sc > ps || (sc == ps && j > pj);
+        if (after && (sc < bs || (sc == bs && j < bj))) {
+          bs = sc;
+          bj = j;
+        }
+      }
+      if (bj == INT_MAX) break;
+      io.sb_var[(size_t)b * kRelMaxCands + k] = bj;
+      io.sb_val[(size_t)b * kRelMaxCands + k] = x[bj];
+      ++nsb;
+      ps = bs;
+      pj = bj;
+    }
+  }
+  io.nsb[b] = nsb;
+}
+
+// one wave per strong-branching child: the node's (FBBT-tightened) box with
+// the candidate's bound change
+__global__ __launch_bounds__(256) void rel_children(RelIO io, const double *wlb, const double *wub,
+                                                    double *clb, double *cub, int32_t *cnode) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= io.nb) return;
+  const int k2 = 2 * io.nsb[b];
+  const size_t off = 2 * (size_t)io.sb_off[b];
+  for (int ch = 0; ch < k2; ++ch) {
+    const int j = io.sb_var[(size_t)b * kRelMaxCands + (ch >> 1)];
+    const double v = io.sb_val[(size_t)b * kRelMaxCands + (ch >> 1)];
+    const bool up = ch & 1;
+    double *dl = clb + (off + ch) * io.n, *du = cub + (off + ch) * io.n;
+    for (int k = lane; k < io.n; k += 64) {
+      double l = wlb[(size_t)b * io.n + k], u = wub[(size_t)b * io.n + k];
+      if (k == j) {
+        if (up) l = ceil(v);
+        else u = floor(v);
+      }
+      dl[k] = l;
+      du[k] = u;
+    }
+    if (lane == 0) cnode[off + ch] = b;
+  }
+}
+
+// ReliabilityBrancher::shouldPrune_ (:430-467) for one strong-branching LP
+__device__ __forceinline__ bool sb_prune(double chcutoff, double change, int st, bool &is_rel) {
+  switch (st) {
+    case 3:   // ProvenLocalInfeasible
+    case 2:   // ProvenInfeasible
+    case 5:   // ProvenObjectiveCutOff
+      return true;
+    case 1:   // ProvenLocalOptimal
+    case 0:   // ProvenOptimal (trustCutoff_)
+      return change > chcutoff - kRelETol;
+    case 6:   // EngineIterationLimit
+      return false;
+    case 7:   // ProvenFailedCQFeas / Infeas
+    case 8:
+      is_rel = false;
+      return false;
+    default:  // unexpected status (engProbs)
+      is_rel = false;
+      return false;
+  }
+}
+
+__global__ __launch_bounds__(256) void rel_decide(RelIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb) return;
+  const size_t e0 = (size_t)b * kRelEvents;
+  int ov = -1, os = 0, nev = 0;
+  double oc = 0.0;
+  const bool own = after_solve_obs(io, b, ov, os, oc);
+  if (own) {  // updateAfterSolve comes first (PCBProcessor.cpp:245-248)
+    io.ev_var[e0] = ov;
+    io.ev_side[e0] = (int8_t)os;
+    io.ev_cost[e0] = oc;
+    nev = 1;
+  }
+  int dec = io.decision[b];
+  if (dec == 0) {
+    const double *x = io.x + (size_t)b * io.n;
+    const long long calls = calls_of(io, b);
+    const double objval = io.obj[b];
+    double best = -INFINITY;
+    int bj = -1;
+    bool down_first = false;
+    // reliable candidates, ascending index (:84-96)
+    for (int j = 0; j < io.n; ++j) {
+      if (!is_int(io.vtype[j])) continue;
+      const double v = x[j];
+      if (!fractional(v)) continue;
+      const PcView pv = pc_view(io, j, own, ov, os, oc);
+      if (!reliable(io, j, calls, pv)) continue;
+      const double cd = (v - floor(v)) * pv.pd, cu = (ceil(v) - v) * pv.pu;
+      const double sc = rel_score(cu, cd);
+      if (sc > best) {
+        best = sc;
+        bj = j;
+        down_first = cu > cd;
+      }
+    }
+    // strong-branched candidates (:98-128)
+    const double maxchange = io.cutoff - objval;
+    const int nsb = io.nsb[b];
+    const size_t off = 2 * (size_t)io.sb_off[b];
+    int status = 0;   // 0 NotModified, 1 Pruned, 2 Modified
+    int mvar = -1, mup = 0;
+    for (int k = 0; k < nsb; ++k) {
+      const int j = io.sb_var[(size_t)b * kRelMaxCands + k];
+      const double v = io.sb_val[(size_t)b * kRelMaxCands + k];
+      const double dd = v - floor(v), ud = ceil(v) - v;
+      const int sd = io.c_status[off + 2 * k], su = io.c_status[off + 2 * k + 1];
+      double cd = fmax(io.c_obj[off + 2 * k] - objval, 0.0);
+      double cu = fmax(io.c_obj[off + 2 * k + 1] - objval, 0.0);
+      bool is_rel = true;
+      const bool pd = sb_prune(maxchange, cd, sd, is_rel);
+      const bool pu = sb_prune(maxchange, cu, su, is_rel);
+      if (!is_rel) {
+        cu = 0.0;
+        cd = 0.0;
+      } else if (pu && pd) {
+        status = 1;
+      } else if (pu) {
+        status = 2;       // the down branch's bound change
+        mvar = j;
+        mup = 0;
+      } else if (pd) {
+        status = 2;       // the up branch's bound change
+        mvar = j;
+        mup = 1;
+      } else if (nev + 2 <= kRelEvents) {
+        io.ev_var[e0 + nev] = j;
+        io.ev_side[e0 + nev] = 0;
+        io.ev_cost[e0 + nev] = fabs(cd) / (fabs(dd) + kRelETol);
+        io.ev_var[e0 + nev + 1] = j;
+        io.ev_side[e0 + nev + 1] = 1;
+        io.ev_cost[e0 + nev + 1] = fabs(cu) / (fabs(ud) + kRelETol);
+        nev += 2;
+      }
+      const double sc = rel_score(cu, cd);
+      // lastStrBranched_ = calls: within the round the last writer is the
+      // largest call number (pc_fold stores it)
+      atomicMax(&io.last_new[j], (int)calls);
+      if (status != 0) break;
+      if (sc > best) {
+        best = sc;
+        bj = j;
+        down_first = cu > cd;
+      }
+    }
+    if (status == 0) {
+      // the remaining unreliable candidates by pseudocost (:129-147), in
+      // CompareScore order after the first nsb
+      double ps = -INFINITY;
+      int pj = -1;
+      for (int k = 0;; ++k) {
+        double bs = INFINITY;
+        int kj = INT_MAX;
+        for (int j = 0; j < io.n; ++j) {
+          if (!is_int(io.vtype[j])) continue;
+          const double v = x[j];
+          if (!fractional(v)) continue;
+          const PcView pv = pc_view(io, j, own, ov, os, oc);
+          if (reliable(io, j, calls, pv)) continue;
+          const double sc = unrel_score(pv, v - floor(v), ceil(v) - v);
+          const bool after = sc > ps || (sc == ps && j > pj);
+          if (after && (sc < bs || (sc == bs && j < kj))) {
+            bs = sc;
+            kj = j;
+          }
+        }
+        if (kj == INT_MAX) break;
+        ps = bs;
+        pj = kj;
+        if (k < nsb) continue;   // strong-branched above
+        const double v = x[kj];
+        const PcView pv = pc_view(io, kj, own, ov, os, oc);
+        const double cd = (v - floor(v)) * pv.pd, cu = (ceil(v) - v) * pv.pu;
+        const double sc = rel_score(cu, cd);
+        if (sc > best) {
+          best = sc;
+          bj = kj;
+          down_first = cu > cd;
+        }
+      }
+      io.bvar[b] = bj;
+      io.bval[b] = x[bj];
+      io.bup[b] = down_first ? 0 : 1;
+    } else if (status == 1) {
+      dec = 1;   // PrunedByBrancher -> NodeInfeasible (PCBProcessor.cpp:284-294)
+      atomicAdd(&io.counters[1], 1ull);
+    } else {
+      // ModifiedByBrancher: the node again with the one-sided bound change
+      // (PCBProcessor.cpp:295-305); the tail writes it as a single child
+      dec = 5;
+      io.bvar[b] = mvar;
+      io.bval[b] = x[mvar];
+      io.bup[b] = (int8_t)mup;
+      atomicAdd(&io.counters[2], 1ull);
+    }
+    if (nsb > 0) {
+      unsigned long long piv = 0;
+      for (int c = 0; c < 2 * nsb; ++c) piv += (unsigned long long)io.c_iters[off + c];
+      atomicAdd(&io.counters[0], (unsigned long long)(2 * nsb));
+      atomicAdd(&io.counters[3], piv);
+    }
+  }
+  io.dec_out[b] = dec;
+  io.nev[b] = nev;
+}
+
+// updatePCost_ over the round's observations, per variable in node order
+__global__ __launch_bounds__(64) void pc_fold(RelIO io) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= io.n) return;
+  double pu = io.pc_up[j], pd = io.pc_dn[j];
+  int cu = io.cnt_up[j], cd = io.cnt_dn[j];
+  for (int b = 0; b < io.nb; ++b) {
+    const int k = io.nev[b];
+    for (int e = 0; e < k; ++e) {
+      const size_t i = (size_t)b * kRelEvents + e;
+      if (io.ev_var[i] != j) continue;
+      const double c = io.ev_cost[i];
+      if (io.ev_side[i] == 0) {
+        pd = (pd * cd + c) / (cd + 1);
+        cd += 1;
+      } else {
+        pu = (pu * cu + c) / (cu + 1);
+        cu += 1;
+      }
+    }
+  }
+  if (io.last_new[j] >= 0) io.last[j] = io.last_new[j];
+  io.pc_up[j] = pu;
+  io.pc_dn[j] = pd;
+  io.cnt_up[j] = cu;
+  io.cnt_dn[j] = cd;
+}
+
+}  // namespace
+
+hipError_t launch_rel_rank(const RelIO &io, int32_t *flag, int32_t *rank, int32_t *total,
+                           hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_flags, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io, flag);
+  hipLaunchKernelGGL(excl_scan, dim3(1), dim3(1024), 0, stream, flag, rank, io.nb, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_rel_prepare(const RelIO &io, int32_t *sb_off, int32_t *total,
+                              hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_prepare, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  hipLaunchKernelGGL(excl_scan, dim3(1), dim3(1024), 0, stream, io.nsb, sb_off, io.nb, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_rel_children(const RelIO &io, const double *wlb, const double *wub,
+                               double *clb, double *cub, int32_t *cnode, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io, wlb, wub,
+                     clb, cub, cnode);
+  return hipGetLastError();
+}
+
+hipError_t launch_rel_decide(const RelIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_decide, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  hipLaunchKernelGGL(pc_fold, dim3((io.n + 63) / 64), dim3(64), 0, stream, io);
+  return hipGetLastError();
+}
+
+}  // namespace mgpu
+
+namespace mgpu {
+namespace {
+// per-batch parent data of the popped nodes: node bound, parent branching
+// variable and value (stack: slot base + i; best-first: the selected slots)
+__global__ __launch_bounds__(256) void rel_gather(int nb, int base, const uint32_t *slots,
+                                                  const double *pnlb, const int32_t *ppvar,
+                                                  const double *ppval, double *bnlb,
+                                                  int32_t *bpvar, double *bpval) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nb) return;
+  const size_t s = slots != nullptr ? (size_t)slots[i] : (size_t)base + i;
+  bnlb[i] = pnlb[s];
+  bpvar[i] = ppvar[s];
+  bpval[i] = ppval[s];
+}
+}  // namespace
+
+hipError_t launch_rel_gather(int nb, int base, const uint32_t *slots, const double *pnlb,
+                             const int32_t *ppvar, const double *ppval, double *bnlb,
+                             int32_t *bpvar, double *bpval, hipStream_t stream) {
+  if (nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_gather, dim3((nb + 255) / 256), dim3(256), 0, stream, nb, base, slots,
+                     pnlb, ppvar, ppval, bnlb, bpvar, bpval);
+  return hipGetLastError();
+}
+}  // namespace mgpu

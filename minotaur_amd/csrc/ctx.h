@@ -64,6 +64,7 @@ struct mgpu_ctx {
   int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)
   int bnb_order = 0;           // mgpu_bnb_config: 0 depth-first stack, 1 best-first
   int bnb_warm = 0;            // mgpu_bnb_config: 0 root basis, 1 parent basis
+  int bnb_brancher = 0;        // mgpu_bnb_brancher: 0 MaxVio, 1 reliability
   DevBuf lp_slots;             // K3L: one B^-1 [m][m] per resident workgroup
   DevBuf lp_next;              // K3L: node counter of the dynamic schedule
   DevBuf pfi_ovf;              // K3P: overflow counter + node list
@@ -124,3 +125,6 @@ hipError_t upload(DevBuf &b, const T *src, size_t count) {
 void quad_state_free(mgpu_ctx *c);  // quad_runtime.cpp
 void bnb_state_free(mgpu_ctx *c);   // bnb.cpp
 void qp_state_free(mgpu_ctx *c);    // qp_runtime.cpp
+// an LP batch with per-node warm starts through the K3 / K3L selection of
+// mgpu_lp_solve (mgpu_runtime.cpp); io.next is set here
+int launch_lp_nodes(mgpu_ctx *c, const LpIO &io);

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     }
     if (bi >= nsolve) break;
     const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
-    const int bw = io.list_ws ? bi : b;  // warm-start index
+    const int bw = io.ws_index != nullptr ? io.ws_index[b] : io.list_ws ? bi : b;  // warm start
 
     // lane index made opaque per node: otherwise LICM hoists the 64
     // loop-invariant B^-1 init values / LDS addresses out of the node loop
@@ -652,10 +652,14 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     if (status == 0 || status == 6) {
       if (lane < m) C.z[h] = zB;
       wave_sync();
-      double s = 0.0;
-      for (int j = lane; j < n; j += 64) s += C.cj(j) * C.z[j];
-      s = wave_sum(s);
-      if (lane == 0) io.obj[b] = C.ocol < 0 ? s + lp.objoff : s;
+      // objective as the oracle sums it: sequentially over the columns, so
+      // the value is the oracle's bit for bit (the batched tree's reliability
+      // branching compares strong-branching values and pseudocosts exactly)
+      if (lane == 0) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += C.cj(j) * C.z[j];
+        io.obj[b] = C.ocol < 0 ? s + lp.objoff : s;
+      }
       if (io.x != nullptr)
         for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = C.z[j];
       if (io.wo_head != nullptr) {

@@ -292,9 +292,10 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
     // ---- basis: warm start or slack basis (B = -I) ----
     const bool warm = io.ws.head != nullptr;
     if (warm) {
-      const int32_t *wh = io.ws.head + (size_t)b * io.ws.s_head;
-      const int8_t *wst = io.ws.st + (size_t)b * io.ws.s_st;
-      const double *wb = io.ws.binv + (size_t)b * io.ws.s_binv;
+      const size_t bw = io.ws_index != nullptr ? (size_t)io.ws_index[b] : (size_t)b;
+      const int32_t *wh = io.ws.head + bw * io.ws.s_head;
+      const int8_t *wst = io.ws.st + bw * io.ws.s_st;
+      const double *wb = io.ws.binv + bw * io.ws.s_binv;
       for (int j = tid; j < N; j += kT) {
         const int8_t v = wst[j];
         s.st[j] = v == ST_BASIC ? ST_LB : v;
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
       for (int i = tid; i < m; i += kT) s.st[s.head[i]] = ST_BASIC;
       __syncthreads();
       if (s.ocol < 0) {
-        const double *wd = io.ws.d + (size_t)b * io.ws.s_d;
+        const double *wd = io.ws.d + bw * io.ws.s_d;
         for (int j = tid; j < N; j += kT) s.d[j] = s.st[j] == ST_BASIC ? 0.0 : wd[j];
       } else {
         // bound LP (oracle compute_duals): y = c_B' B^-1 = osign * row r of

@@ -109,6 +109,8 @@ struct LpIO {
   const double *obj_sign;       //   (bound LPs, QuadHandler::tightenLP_)
   const int32_t *skip;          // [B] nonzero = node already infeasible (FBBT)
   LpWarm ws;                    // ws.head == nullptr: slack basis
+  const int32_t *ws_index;      // [B] or null: LP b starts from warm start ws_index[b]
+                                //   (strong-branching children -> their node's basis)
   int iter_limit;
   int32_t *status;              // [B] EngineStatus numerics
   double *obj;                  // [B] objective incl. constant

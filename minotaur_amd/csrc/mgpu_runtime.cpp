@@ -473,7 +473,7 @@ bool use_large_lp(const mgpu_ctx *c) {
 bool use_pfi(const mgpu_ctx *c, const LpIO &io) {
   if (c->lp_variant != 0 && c->lp_variant != 3) return false;
   const bool shared = io.ws.head != nullptr && io.ws.s_head == 0 && io.ws.s_st == 0 &&
-                      io.ws.s_d == 0 && io.ws.s_binv == 0;
+                      io.ws.s_d == 0 && io.ws.s_binv == 0 && io.ws_index == nullptr;
   const int kmax = c->lp_variant == 3 && c->lp_pfi == 0 ? kPfiMax : c->lp_pfi;
   return shared && io.wo_head == nullptr && kmax > 0 &&
          lp_pfi_fits(c->lp.n, c->lp.m, c->lp.nnz) &&
@@ -559,6 +559,10 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
   return MGPU_OK;
 }
 }  // namespace
+
+extern "C++" int launch_lp_nodes(mgpu_ctx *c, const LpIO &io) {
+  return launch_lp(c, io, "lp batch");
+}
 
 int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub,
                       const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,

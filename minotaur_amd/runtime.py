@@ -32,7 +32,7 @@ EXPORTS = [
     'mgpu_bnb_round', 'mgpu_bnb_best', 'mgpu_bnb_shard', 'mgpu_bnb_config', 'mgpu_bnb_export',
     'mgpu_bnb_import', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
-    'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev',
+    'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
 ]
 
 
@@ -42,7 +42,9 @@ class BnbStats(ctypes.Structure):
                 ('ndec', ctypes.c_longlong * 5), ('open', ctypes.c_int),
                 ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double),
                 ('pruned', ctypes.c_longlong), ('lps', ctypes.c_longlong),
-                ('pivots', ctypes.c_longlong)]
+                ('pivots', ctypes.c_longlong), ('sb_lps', ctypes.c_longlong),
+                ('sb_pivots', ctypes.c_longlong), ('sb_pruned', ctypes.c_longlong),
+                ('sb_modified', ctypes.c_longlong)]
 
 _lib = None
 
@@ -94,6 +96,7 @@ def load_library():
     lib.mgpu_lp_bound_dev.argtypes = [_P, _I] + [_P] * 7 + [_I] + [_P] * 4
     lib.mgpu_bnb_init.argtypes = [_P, _I, _P, _P, _D]
     lib.mgpu_bnb_config.argtypes = [_P, _I, _I]
+    lib.mgpu_bnb_brancher.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
     lib.mgpu_bnb_import.argtypes = [_P, _I, _P, _P, _P, _P]
     lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
@@ -486,6 +489,10 @@ class Context:
         """Next tree: order 0 depth-first / 1 best-first; warm 0 root basis /
         1 parent basis (mgpu_bnb_config)."""
         self._chk(self.lib.mgpu_bnb_config(self.h, int(order), int(warm)), 'mgpu_bnb_config')
+
+    def bnb_brancher(self, kind):
+        """Next tree's brancher: 0 MaxVio, 1 reliability (mgpu_bnb_brancher)."""
+        self._chk(self.lib.mgpu_bnb_brancher(self.h, int(kind)), 'mgpu_bnb_brancher')
 
     def bnb_init(self, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
         p = self.problem

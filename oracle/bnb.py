@@ -13,7 +13,11 @@ children), same pool order:
   to the free slots in the engine's order (the slots just taken, the older
   holes ascending, then new slots);
 * warm 0: node LPs from the root optimum (shared); warm 1: from the parent's
-  optimal basis, whose own optimum is handed to both children.
+  optimal basis, whose own optimum is handed to both children;
+* brancher 0: MaxVioBrancher; brancher 1: the batched ReliabilityBrancher of
+  bnb_rel.hip (pseudocosts frozen at the round's start plus each node's own
+  updateAfterSolve observation, strong-branching LPs from each node's optimal
+  basis with iteration limit 25, observations folded in node order).
 
 ``CpuBnbContext`` exposes the engine's bnb_* methods so minotaur_amd.bnb's
 drivers run unchanged on it (gloo tests of the multi-rank control flow, and
@@ -40,6 +44,7 @@ class _Stats:
         self.incumbent = math.inf
         self.pruned = 0
         self.lps = self.pivots = 0
+        self.sb_lps = self.sb_pivots = self.sb_pruned = self.sb_modified = 0
 
 
 def _order_key(v):
@@ -50,20 +55,38 @@ def _order_key(v):
 
 
 class _Node:
-    __slots__ = ('lb', 'ub', 'nlb', 'depth', 'ws')
+    __slots__ = ('lb', 'ub', 'nlb', 'depth', 'ws', 'pvar', 'pval')
 
-    def __init__(self, lb, ub, nlb, depth, ws=None):
+    def __init__(self, lb, ub, nlb, depth, ws=None, pvar=-1, pval=0.0):
         self.lb, self.ub, self.nlb, self.depth, self.ws = lb, ub, nlb, depth, ws
+        self.pvar, self.pval = pvar, pval
+
+
+# ReliabilityBrancher defaults (ReliabilityBrancher.cpp:43-58)
+REL_MAX_CANDS, REL_ITER, REL_THRESH, REL_MIN_DIST, REL_ETOL = 20, 25, 4, 50, 1e-6
+
+
+def _rel_score(up, down):
+    """ReliabilityBrancher::getScore_ (:368-377)."""
+    return down * 0.8 + up * 0.2 if up > down else up * 0.8 + down * 0.2
+
+
+def _fractional(v):
+    return abs(math.floor(v + 0.5) - v) > INT_TOL
 
 
 class CpuBnbContext:
-    def __init__(self, p, pfi=0, order=0, warm=0):
+    def __init__(self, p, pfi=0, order=0, warm=0, brancher=0):
         self.problem = p
         self.pfi = pfi   # node LPs in K3P's product form (Context.oracle_pfi())
         self.order, self.warm = order, warm
+        self.brancher = brancher
 
     def bnb_config(self, order=0, warm=0):
         self.order, self.warm = int(order), int(warm)
+
+    def bnb_brancher(self, kind):
+        self.brancher = int(kind)
 
     # -- mgpu_bnb_init ------------------------------------------------------
     def bnb_init(self, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
@@ -78,6 +101,13 @@ class CpuBnbContext:
         self.best_x = np.full(p.n, np.nan)
         self.tot = _Stats()
         self.tot.incumbent = incumbent
+        self.rel = self.brancher == 1
+        if self.rel:   # ReliabilityBrancher::initialize (:384-398)
+            n = p.n
+            self.pc_up, self.pc_dn = [0.0] * n, [0.0] * n
+            self.cnt_up, self.cnt_dn = [0] * n, [0] * n
+            self.last = [20000] * n
+            self.calls = 0
 
     # -- mgpu_bnb_round -----------------------------------------------------
     def _select(self, batch):
@@ -129,7 +159,16 @@ class CpuBnbContext:
         wo = [None] * nb
         keep = np.nonzero(f.infeas == 0)[0]
         if keep.size:
-            if self.warm:
+            if self.rel and not self.warm:
+                # the node's optimal basis is needed: dense solve from the root
+                k = keep.size
+                ws = oracle.WarmStart(*(np.stack([getattr(self.ws, a)] * k)
+                                        for a in ('head', 'st', 'binv', 'd')))
+                s2, o2, i2, x2, w2 = oracle.dual_simplex_nodes(p, f.lb[keep], f.ub[keep], ws)
+                for t, i in enumerate(keep):
+                    wo[i] = oracle.WarmStart(w2.head[t].copy(), w2.st[t].copy(),
+                                             w2.binv[t].copy(), w2.d[t].copy())
+            elif self.warm:
                 ws = oracle.WarmStart(*(np.stack([getattr(nodes[i].ws, k) for i in keep])
                                         for k in ('head', 'st', 'binv', 'd')))
                 s2, o2, i2, x2, w2 = oracle.dual_simplex_nodes(p, f.lb[keep], f.ub[keep], ws)
@@ -146,18 +185,33 @@ class CpuBnbContext:
         ints = np.isin(p.vtype, (0, 1))
         children = []
         best, best_i = math.inf, -1
+        decs = [self._decide(f.infeas[i], status[i], obj[i], x[i], ints) for i in range(nb)]
+        if self.rel:
+            choice = self._rel_round(nodes, decs, obj, x, f, wo)
         for i in range(nb):
-            dec = self._decide(f.infeas[i], status[i], obj[i], x[i], ints)
-            self.tot.ndec[dec] += 1
+            dec = decs[i]
+            self.tot.ndec[0 if dec == 5 else dec] += 1
             if dec == 3 and (obj[i] < best):
                 best, best_i = obj[i], i
-            if dec != 0:
+            if dec not in (0, 5):
                 continue
-            j, v, up_first = self._branch(x[i], ints)
+            if self.rel:
+                j, v, up_first = choice[i]
+            else:
+                j, v, up_first = self._branch(x[i], ints)
             w = wo[i] if self.warm else self.ws
-            down = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w)
+            if dec == 5:
+                # ModifiedByBrancher: the node again with the bound change
+                nd = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth, w)
+                if up_first:
+                    nd.lb[j] = math.ceil(v)
+                else:
+                    nd.ub[j] = math.floor(v)
+                children.append(nd)
+                continue
+            down = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w, j, v)
             down.ub[j] = math.floor(v)
-            up = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w)
+            up = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w, j, v)
             up.lb[j] = math.ceil(v)
             if self.order == 0:
                 children += [down, up] if up_first else [up, down]   # preferred on top
@@ -181,6 +235,171 @@ class CpuBnbContext:
         self.tot.last_batch = nb
         self.tot.incumbent = self.inc
         return self.tot
+
+    # -- batched reliability branching (bnb_rel.hip) ----------------------------
+    def _rel_round(self, nodes, decs, obj, x, f, wo):
+        """Restates rel_prepare / the strong-branching LP batch / rel_decide /
+        pc_fold over the round; updates ``decs`` in place (1 pruned by the
+        brancher, 5 modified) and returns {node: (var, value, up_first)}."""
+        p = self.problem
+        nb = len(nodes)
+        ints = [j for j in range(p.n) if p.vtype[j] in (0, 1)]
+        obs, calls, sb = {}, {}, {}
+        rank = 0
+        for i in range(nb):
+            if decs[i] == 0:
+                calls[i] = self.calls + rank + 1
+                rank += 1
+            nd = nodes[i]
+            if nd.pvar >= 0 and decs[i] in (0, 3):
+                newval, oldval = x[i][nd.pvar], nd.pval
+                c = (obj[i] - nd.nlb) / (abs(newval - oldval) + REL_ETOL)
+                if c < 0.0 or math.isinf(c) or math.isnan(c):
+                    c = 0.0
+                obs[i] = (nd.pvar, 0 if newval < oldval else 1, c)
+
+        def view(i, j):
+            pu, pd, cu, cd = self.pc_up[j], self.pc_dn[j], self.cnt_up[j], self.cnt_dn[j]
+            o = obs.get(i)
+            if o is not None and o[0] == j:
+                if o[1] == 0:
+                    pd = (pd * cd + o[2]) / (cd + 1)
+                    cd += 1
+                else:
+                    pu = (pu * cu + o[2]) / (cu + 1)
+                    cu += 1
+            return pu, pd, cu, cd
+
+        def reliable(i, j, v):
+            d = (calls[i] - self.last[j]) & 0xFFFFFFFF
+            return float(REL_MIN_DIST) > abs(float(d)) or (v[2] >= REL_THRESH and
+                                                           v[3] >= REL_THRESH)
+
+        def unrel_sorted(i):
+            out = []
+            for j in ints:
+                v = x[i][j]
+                if not _fractional(v):
+                    continue
+                pv = view(i, j)
+                if reliable(i, j, pv):
+                    continue
+                dd, ud = v - math.floor(v), math.ceil(v) - v
+                out.append(((pv[2] + pv[3]) - 1e-5 * (pv[0] + pv[1]) - 1e-6 * max(dd, ud), j))
+            return [j for _, j in sorted(out)]
+
+        kids_lb, kids_ub, kids_ws = [], [], []
+        for i in range(nb):
+            if decs[i] != 0:
+                continue
+            sb[i] = unrel_sorted(i)[:REL_MAX_CANDS]
+            for j in sb[i]:
+                v = x[i][j]
+                for up in (False, True):
+                    lb, ub = f.lb[i].copy(), f.ub[i].copy()
+                    if up:
+                        lb[j] = math.ceil(v)
+                    else:
+                        ub[j] = math.floor(v)
+                    kids_lb.append(lb)
+                    kids_ub.append(ub)
+                    kids_ws.append(wo[i])
+        cst = cobj = cit = None
+        if kids_lb:
+            ws = oracle.WarmStart(*(np.stack([getattr(w, a) for w in kids_ws])
+                                    for a in ('head', 'st', 'binv', 'd')))
+            cst, cobj, cit, _, _ = oracle.dual_simplex_nodes(
+                p, np.stack(kids_lb), np.stack(kids_ub), ws, iter_limit=REL_ITER)
+            self.tot.sb_lps += len(kids_lb)
+            self.tot.sb_pivots += int(np.sum(cit))
+        choice, events = {}, []
+        last_upd = {}
+        off = 0
+
+        def sb_prune(chcut, change, st):
+            if st in (3, 2, 5):
+                return True, True
+            if st in (1, 0):
+                return change > chcut - REL_ETOL, True
+            if st == 6:
+                return False, True
+            return False, False
+
+        for i in range(nb):
+            if i in obs:
+                events.append(obs[i])
+            if decs[i] != 0:
+                continue
+            xi = x[i]
+            objval = obj[i]
+            best, bj, down_first = -math.inf, -1, False
+            for j in ints:
+                v = xi[j]
+                if not _fractional(v):
+                    continue
+                pv = view(i, j)
+                if not reliable(i, j, pv):
+                    continue
+                cd, cu = (v - math.floor(v)) * pv[1], (math.ceil(v) - v) * pv[0]
+                sc = _rel_score(cu, cd)
+                if sc > best:
+                    best, bj, down_first = sc, j, cu > cd
+            maxchange = self.inc - objval
+            status = 0
+            mod = None
+            for k, j in enumerate(sb[i]):
+                v = xi[j]
+                dd, ud = v - math.floor(v), math.ceil(v) - v
+                sd, su = int(cst[off + 2 * k]), int(cst[off + 2 * k + 1])
+                cd = max(cobj[off + 2 * k] - objval, 0.0)
+                cu = max(cobj[off + 2 * k + 1] - objval, 0.0)
+                pd_, rel_d = sb_prune(maxchange, cd, sd)
+                pu_, rel_u = sb_prune(maxchange, cu, su)
+                if not (rel_d and rel_u):
+                    cu = cd = 0.0
+                elif pu_ and pd_:
+                    status = 1
+                elif pu_:
+                    status, mod = 2, (j, v, False)
+                elif pd_:
+                    status, mod = 2, (j, v, True)
+                else:
+                    events.append((j, 0, abs(cd) / (abs(dd) + REL_ETOL)))
+                    events.append((j, 1, abs(cu) / (abs(ud) + REL_ETOL)))
+                sc = _rel_score(cu, cd)
+                last_upd[j] = max(last_upd.get(j, -1), calls[i])
+                if status != 0:
+                    break
+                if sc > best:
+                    best, bj, down_first = sc, j, cu > cd
+            if status == 0:
+                for j in unrel_sorted(i)[len(sb[i]):]:
+                    v = xi[j]
+                    pv = view(i, j)
+                    cd, cu = (v - math.floor(v)) * pv[1], (math.ceil(v) - v) * pv[0]
+                    sc = _rel_score(cu, cd)
+                    if sc > best:
+                        best, bj, down_first = sc, j, cu > cd
+                choice[i] = (bj, xi[bj], not down_first)
+            elif status == 1:
+                decs[i] = 1
+                self.tot.sb_pruned += 1
+            else:
+                decs[i] = 5
+                choice[i] = mod
+                self.tot.sb_modified += 1
+            off += 2 * len(sb[i])
+        for j, c in last_upd.items():   # the round's last writer (largest call number)
+            self.last[j] = c
+        for j, side, c in events:      # updatePCost_ in node order
+            if side == 0:
+                self.pc_dn[j] = (self.pc_dn[j] * self.cnt_dn[j] + c) / (self.cnt_dn[j] + 1)
+                self.cnt_dn[j] += 1
+            else:
+                self.pc_up[j] = (self.pc_up[j] * self.cnt_up[j] + c) / (self.cnt_up[j] + 1)
+                self.cnt_up[j] += 1
+        self.calls += rank
+        return choice
 
     def _decide(self, finf, st, solval, x, ints):
         dec, _ = oracle.node_decide(self.problem.vtype, [st], [solval], x[None], self.inc,
