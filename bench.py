@@ -127,18 +127,23 @@ def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
     def sample(S):
         if S <= LB.shape[0]:
             return LB[:S], UB[:S], f"first {S} of the rank-0 node boxes"
-        from minotaur_amd.problem import random_boxes
-        XL, XU = random_boxes(p, S - LB.shape[0], 99991)
-        return (np.concatenate([LB, XL]), np.concatenate([UB, XU]),
-                f"the {LB.shape[0]} rank-0 node boxes + {XL.shape[0]} more of the same generator")
+        # more work than the batch holds: the batch again, cyclically (the
+        # host code keeps no state between boxes; generating millions of new
+        # boxes in Python would take minutes)
+        idx = np.arange(S) % LB.shape[0]
+        return (LB[idx], UB[idx],
+                f"{S} boxes: the {LB.shape[0]} rank-0 node boxes cycled")
 
     def leg(threads, ref, budget):
         probe = min(256 * threads, LB.shape[0])
         a, b, _ = run(LB[:probe], UB[:probe], threads, ref)
         per = (a + b) / probe
         S = int(min(64 * LB.shape[0], max(probe, budget / max(per, 1e-9))))
+        progress(0, f"cpu baseline leg ({threads} threads, ref={ref}): probe {probe} nodes "
+                    f"{a + b:.2f}s -> sample {S}")
         lb, ub, what = sample(S)
         tf, tl, solved = run(lb, ub, threads, ref)
+        progress(0, f"cpu baseline leg done: {tf + tl:.2f}s")
         return S, tf, tl, solved, what
 
     S, tf, tl, solved, what = leg(T, False, 0.5 * budget_s)
@@ -163,13 +168,13 @@ def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
     }
 
 
-def run_tree(ctx, dev, rank, world, p, B, order, warm, cap):
+def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0):
     """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
     across ranks after the shared first rounds: one packed all-reduce per
     round (incumbent MIN + open counts), open nodes rebalanced every 8 rounds
     or when a rank runs dry (dist.rebalance).  Returns (incumbent, nodes, LP
-    solves, pivots, pruned-open, rounds, seconds, nodes moved) — counts
-    summed over ranks, seconds the max."""
+    solves, pivots, pruned-open, rounds, seconds, nodes moved, strong-branching
+    LPs, their pivots) — counts summed over ranks, seconds the max."""
     import torch
     import torch.distributed as dist
     from minotaur_amd import bnb
@@ -177,34 +182,39 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap):
     comm = mdist.Comm(rank, world, dev)
     ctx.load(p)
     bnb.solve_distributed(ctx, 64, rank, world, capacity=1 << 14, max_rounds=2, order=order,
-                          warm=warm, comm=comm)                # warm-up (kernel loads)
+                          warm=warm, comm=comm, brancher=brancher)   # warm-up (kernel loads)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=cap,
                                                      order=order, warm=warm, comm=comm,
-                                                     lb_every=8)
+                                                     lb_every=8, brancher=brancher)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    cnt = torch.tensor([float(mine[k]) for k in ('nodes', 'lps', 'pivots', 'pruned')],
+    cnt = torch.tensor([float(mine[k]) for k in ('nodes', 'lps', 'pivots', 'pruned', 'sb_lps',
+                                                  'sb_pivots')],
                        dtype=torch.float64, device=dev)
     mdist.allreduce_max(el)
     mdist.allreduce_sum(cnt)
     c = [float(v) for v in cnt.tolist()]
-    return inc, c[0], c[1], c[2], c[3], rounds, float(el.item()), mine['moved']
+    return inc, c[0], c[1], c[2], c[3], rounds, float(el.item()), mine['moved'], c[4], c[5]
 
 
 # Complete trees in the bench line: config 2's own instance,
 # config 1's OA-LP, and a weak-bound MILP whose tree is large enough to time
 # the driver's throughput (multi-dimensional knapsack n = 60, m = 8).
-TREES = [("tls4_lin", "instance", 1, 0, 0.0),
-         ("nvs08_oa", "instance", 1, 0, None),
-         ("mkp-1-n60-m8", "mkp", 0, 0, -1915.0),
-         ("mkp-1-n60-m8", "mkp", 1, 0, -1915.0),
-         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0)]
+# (name, kind, order, warm, optimum, brancher): brancher 1 = the reference's
+# default ReliabilityBrancher (strong-branching LPs count as relaxations).
+TREES = [("tls4_lin", "instance", 1, 0, 0.0, 0),
+         ("tls4_lin", "instance", 1, 0, 0.0, 1),
+         ("nvs08_oa", "instance", 1, 0, None, 0),
+         ("mkp-1-n60-m8", "mkp", 0, 0, -1915.0, 0),
+         ("mkp-1-n60-m8", "mkp", 1, 0, -1915.0, 0),
+         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0, 0),
+         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0, 1)]
 
 
 def tree_search(ctx, dev, rank, world, B, args):
@@ -213,7 +223,7 @@ def tree_search(ctx, dev, rank, world, B, args):
     optima checked against HiGHS' MILP value."""
     from minotaur_amd.problem import LinProblem, random_boxes, random_mkp
     out = []
-    for name, kind, order, warm, opt in TREES:
+    for name, kind, order, warm, opt, br in TREES:
         if kind == "mkp":
             p = random_mkp(1, 60, 8)
         else:
@@ -222,16 +232,21 @@ def tree_search(ctx, dev, rank, world, B, args):
             sys.path.insert(0, os.path.join(ROOT, 'oracle'))
             import oracle
             opt = oracle.highs_milp(p)[1]
-        inc, nodes, lps, piv, pruned, rounds, el, moved = run_tree(ctx, dev, rank, world, p, B,
-                                                                   order, warm, 1 << 23)
+        inc, nodes, lps, piv, pruned, rounds, el, moved, sbl, sbp = run_tree(
+            ctx, dev, rank, world, p, B, order, warm, 1 << 23, br)
+        progress(rank, f"tree {p.name} order {order} warm {warm} brancher {br}: "
+                       f"{nodes:.0f} nodes in {el:.2f}s")
         out.append({"instance": p.name, "vars": p.n, "rows": p.m,
                     "search": ("best-first" if order else "depth-first over batches") +
                               (", parent-basis warm starts" if warm else
-                               ", root-basis warm start") + ", MaxVio branching",
+                               ", root-basis warm start") +
+                              (", reliability branching (strong branching + pseudocosts)"
+                               if br else ", MaxVio branching"),
                     "nodes": nodes, "lp_solves": lps, "pivots_per_lp": piv / max(lps, 1.0),
+                    "strong_branching_lps": sbl,
                     "pruned_open": pruned, "rounds": rounds, "seconds": el,
                     "nodes_migrated": moved,
-                    "nodes_per_s": nodes / el, "relaxations_per_s": lps / el,
+                    "nodes_per_s": nodes / el, "relaxations_per_s": (lps + sbl) / el,
                     "batch_per_gpu": B, "optimum": inc, "optimum_highs": opt,
                     "optimum_matches_highs": bool(abs(inc - opt) <= 1e-6 * max(1.0, abs(opt)))})
         if kind == "mkp" and order == 0 and rank == 0 and world == 1 \
@@ -359,6 +374,72 @@ def convex_batch(ctx, dev, rank, world, B, args):
                       "node-sharded after the shared first rounds"}
 
 
+def glob_batch(ctx, dev, rank, world, args, B=65536, reps=10):
+    """Supplementary (the batched glob path): node boxes of
+    a random QCQP (seeded; 14 original variables, 8 quadratic rows -> 31
+    columns, 52 LP rows with 40 McCormick / secant rows rewritten per node)
+    through K2 (QuadHandler::presolveNode: bounds + row rewrite), then every
+    node's own LP (mgpu_lp_solve_rows: K3R refactors the root basis for the
+    node's rows, K3 solves), device-resident, repeated `reps` times."""
+    import torch
+    from minotaur_amd import dist as mdist
+    from minotaur_amd.quad import random_qcqp, random_quad_boxes, relaxation_lp
+    from minotaur_amd.runtime import WarmStart
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle
+    qp = random_qcqp(7, nv0=14, ncon=8)
+    ctx.load_quad(qp)
+    rows0 = ctx.quad_rows()
+    p, nr = relaxation_lp(qp, rows0)
+    st0, _, _, _, _, ws = oracle.dual_simplex_root(p)
+    ctx.load(p)
+    ctx.set_node_rows(nr)
+    LB, UB = random_quad_boxes(qp, B, mdist.shard_seed(23, rank))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    lb, ub, rows = t(LB), t(UB), t(np.tile(rows0, (B, 1)))
+    lb2, ub2, rows2 = torch.empty_like(lb), torch.empty_like(ub), torch.empty_like(rows)
+    z32 = lambda: torch.zeros(B, dtype=torch.int32, device=dev)   # noqa: E731
+    inf, nm, st, it = z32(), z32(), z32(), z32()
+    ob = torch.zeros(B, dtype=torch.float64, device=dev)
+    wsd = WarmStart(t(ws.head.astype(np.int32)), t(ws.st.astype(np.int8)), None, None)
+
+    def step():
+        ctx.quad_fbbt_dev(lb, ub, rows, lb2, ub2, rows2, inf, nm, qt=1)
+        ctx.lp_solve_rows_dev(lb2, ub2, rows2, st, ob, it, ws=wsd, skip=inf)
+
+    step()
+    torch.cuda.synchronize()
+    k2, rf, lp = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+        k2.append(ctx.last_kernel_ms('quad'))
+        rf.append(ctx.last_kernel_ms('refactor'))
+        lp.append(ctx.last_kernel_ms('lp'))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    solved = int((st != 12).sum().item())
+    out = {"instance": f"{qp.name} relaxation ({p.n} cols, {p.m} rows, "
+                       f"{nr.row_idx.size} rows rewritten per node)",
+           "nodes_per_gpu": B, "reps": reps, "nodes_per_s": B * reps * world / el,
+           "relaxations_per_s": solved * reps * world / el,
+           "k2_ms": float(np.median(k2)), "refactor_ms": float(np.median(rf)),
+           "lp_ms": float(np.median(lp)), "pivots_per_lp": float(it.sum().item()) / max(solved, 1),
+           "root_lp_status": int(st0)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        S = 2048
+        t0 = time.perf_counter()
+        o = oracle.quad_fbbt(qp, LB[:S], UB[:S], None, 1, rows0)
+        oracle.dual_simplex_rows(p, o.lb, o.ub, nr, o.rows, ws=WarmStart(ws.head, ws.st, None,
+                                                                          None))
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": S / dt, "unit": "nodes/s", "cores": 1, "kind": "port",
+                               "sample": f"first {S} node boxes: K2 by the C restatement "
+                                         "(bit-identical to the reference QuadHandler), node "
+                                         f"LPs by the dual-simplex restatement, {dt:.2f}s"}
+    return out
+
+
 def qp_relaxation(ctx, dev, rank, world, args, B=1024, reps=3):
     """Supplementary (config 4): QP relaxations of color_lab2_4x0 node boxes
     (300 vars relaxed to [0,1] with random fixings, 61 equality rows, dense
@@ -417,6 +498,12 @@ def qp_relaxation(ctx, dev, rank, world, args, B=1024, reps=3):
     return out
 
 
+def progress(rank, msg):
+    """One line per phase on stderr (the JSON line stays alone on stdout)."""
+    if rank == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -436,6 +523,8 @@ def main():
                     help='skip the supplementary convex batch (config 5, knapsack OA trees)')
     ap.add_argument('--no-qp', action='store_true',
                     help='skip the supplementary QP relaxation batch (color_lab2, MFMA KKT)')
+    ap.add_argument('--no-glob', action='store_true',
+                    help='skip the supplementary glob batch (QCQP: K2 -> per-node rows LP)')
     ap.add_argument('--no-knapsack', action='store_true',
                     help='skip the supplementary config-3 batch (1000 knapsack nodes)')
     args = ap.parse_args()
@@ -541,10 +630,17 @@ def main():
     elapsed = float(tot.item())
     solved, pivots, pfi_solved, pfi_pivots = (float(v) for v in cnt.tolist())
     TB = args.tree_batch
+    progress(rank, f"headline done: {1e3 * elapsed / args.steps:.2f} ms/step")
     tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, TB, args)
+    progress(rank, "tree_search done")
     cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, TB, args)
+    progress(rank, "convex_batch done")
     qprel = None if args.no_qp else qp_relaxation(ctx, dev, rank, world, args)
+    progress(rank, "qp_relaxation done")
     ksn = None if args.no_knapsack else knapsack_nodes(ctx, dev, rank, world, args)
+    progress(rank, "knapsack_nodes done")
+    glob = None if args.no_glob else glob_batch(ctx, dev, rank, world, args)
+    progress(rank, "glob_batch done")
     ctx.load(p)
     nodes = float(B) * world * args.steps
     fbbt_ms = float(np.mean(acc["fbbt_ms"]))
@@ -625,6 +721,7 @@ def main():
             "convex_batch": cvx,
             "qp_relaxation": qprel,
             "knapsack_nodes": ksn,
+            "glob_batch": glob,
         }
         if rehearse:
             line["rehearsal"] = "all ranks on device 0 over gloo (not a scaling number)"

@@ -48,7 +48,8 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
     (and whenever some rank ran out of nodes while others hold more than a
     batch) the open nodes are rebalanced across ranks (dist.rebalance:
     MpiBranchAndBound::LoadBalance_).  Returns (incumbent, x or None, stats,
-    rounds, mine) where mine = {nodes, lps, pivots, pruned, moved} evaluated
+    rounds, mine) where mine = {nodes, lps, pivots, pruned, sb_lps, sb_pivots,
+    moved} evaluated
     by this rank, the shared first rounds counted on rank 0 only (so sums
     over ranks are exact)."""
     from . import dist as mdist
@@ -62,14 +63,15 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
     st = None
     rounds = 0
     moved = 0
-    shared = (0, 0, 0, 0)
+    shared = (0, 0, 0, 0, 0, 0)
     n = ctx.problem.n
     while rounds < max_rounds:
         st = ctx.bnb_round(batch, inc)
         rounds += 1
         open_now = st.open
         if not sharded and (open_now >= shard_at or open_now == 0):
-            shared = (st.nodes, st.lps, st.pivots, st.pruned)   # identical on every rank
+            shared = (st.nodes, st.lps, st.pivots, st.pruned, st.sb_lps,
+                      st.sb_pivots)                           # identical on every rank
             open_now = ctx.bnb_shard(rank, world)
             sharded = True
         if comm is not None:
@@ -86,8 +88,10 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
             if allreduce_max(float(open_now)) == 0.0:
                 break
     obj, x = ctx.bnb_best()
-    sub = shared if rank != 0 else (0, 0, 0, 0)
-    mine = {k: v - w for k, v, w in zip(('nodes', 'lps', 'pivots', 'pruned'),
-                                         (st.nodes, st.lps, st.pivots, st.pruned), sub)}
+    sub = shared if rank != 0 else (0, 0, 0, 0, 0, 0)
+    mine = {k: v - w for k, v, w in zip(('nodes', 'lps', 'pivots', 'pruned', 'sb_lps',
+                                         'sb_pivots'),
+                                        (st.nodes, st.lps, st.pivots, st.pruned, st.sb_lps,
+                                         st.sb_pivots), sub)}
     mine['moved'] = moved
     return inc, (x if obj == inc else None), st, rounds, mine

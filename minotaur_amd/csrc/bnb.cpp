@@ -46,7 +46,7 @@ struct BnbState {
   // pool slot, per-batch and strong-branching child workspaces
   DevBuf pc_up, pc_dn, cnt_up, cnt_dn, last, last_new, ppvar, ppval, bnlb, bpvar, bpval, rflag, rrank,
       nsb, sb_off, sb_var, sb_val, dec2, nev, ev_var, ev_side, ev_cost, rcnt, clb, cub, cnode,
-      cst, cobj, cit;
+      cst, cobj, cit, ev_off, cv_var, cv_side, cv_cost;
   void release() {
     for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
                       &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
@@ -56,7 +56,8 @@ struct BnbState {
                       &bws_binv, &wo_head, &wo_st, &wo_d, &wo_binv, &pc_up, &pc_dn, &cnt_up,
                       &cnt_dn, &last, &last_new, &ppvar, &ppval, &bnlb, &bpvar, &bpval, &rflag, &rrank,
                       &nsb, &sb_off, &sb_var, &sb_val, &dec2, &nev, &ev_var, &ev_side, &ev_cost,
-                      &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit})
+                      &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit, &ev_off, &cv_var, &cv_side,
+                      &cv_cost})
       b->release();
   }
 };
@@ -87,8 +88,12 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
   HIPCHK(c, s.bcnt.ensure(nblk * 7 * 4));
   HIPCHK(c, s.out.ensure(sizeof(BnbOut)));
   if (s.rel) {
-    for (DevBuf *b : {&s.bpvar, &s.rflag, &s.rrank, &s.nsb, &s.sb_off, &s.dec2, &s.nev})
+    for (DevBuf *b : {&s.bpvar, &s.rflag, &s.rrank, &s.nsb, &s.sb_off, &s.dec2, &s.nev,
+                      &s.ev_off})
       HIPCHK(c, b->ensure((size_t)B * 4));
+    HIPCHK(c, s.cv_var.ensure((size_t)B * kRelEvents * 4));
+    HIPCHK(c, s.cv_side.ensure((size_t)B * kRelEvents));
+    HIPCHK(c, s.cv_cost.ensure((size_t)B * kRelEvents * 8));
     for (DevBuf *b : {&s.bnlb, &s.bpval}) HIPCHK(c, b->ensure((size_t)B * 8));
     HIPCHK(c, s.sb_var.ensure((size_t)B * kRelMaxCands * 4));
     HIPCHK(c, s.sb_val.ensure((size_t)B * kRelMaxCands * 8));
@@ -163,6 +168,11 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
   r.ev_var = s.ev_var.as<int32_t>();
   r.ev_side = s.ev_side.as<int8_t>();
   r.ev_cost = s.ev_cost.as<double>();
+  r.ev_off = s.ev_off.as<int32_t>();
+  r.ev_total = tot + 2;
+  r.cv_var = s.cv_var.as<int32_t>();
+  r.cv_side = s.cv_side.as<int8_t>();
+  r.cv_cost = s.cv_cost.as<double>();
   r.counters = s.rcnt.as<unsigned long long>();
   HIPCHK(c, launch_rel_rank(r, s.rflag.as<int32_t>(), s.rrank.as<int32_t>(), tot, c->stream));
   HIPCHK(c, launch_rel_prepare(r, s.sb_off.as<int32_t>(), tot + 1, c->stream));

@@ -111,6 +111,11 @@ struct RelIO {
   int32_t *ev_var;              // [nb][kRelEvents]
   int8_t *ev_side;              // 0 down, 1 up
   double *ev_cost;
+  int32_t *ev_off;              // [nb] packed offsets of the nodes' observations
+  int32_t *ev_total;            // device: number of observations
+  int32_t *cv_var;              // packed observations [nb * kRelEvents] in node order
+  int8_t *cv_side;
+  double *cv_cost;
   unsigned long long *counters; // [4] strong-branching LPs, pruned, modified, their pivots
 };
 hipError_t launch_rel_rank(const RelIO &io, int32_t *flag, int32_t *rank, int32_t *total,

@@ -374,32 +374,55 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
   io.nev[b] = nev;
 }
 
-// updatePCost_ over the round's observations, per variable in node order
+// the round's observations packed in node order (offsets: excl_scan of nev)
+__global__ __launch_bounds__(256) void rel_compact(RelIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb) return;
+  const int k = io.nev[b];
+  const size_t o = (size_t)io.ev_off[b];
+  for (int e = 0; e < k; ++e) {
+    const size_t i = (size_t)b * kRelEvents + e;
+    io.cv_var[o + e] = io.ev_var[i];
+    io.cv_side[o + e] = io.ev_side[i];
+    io.cv_cost[o + e] = io.ev_cost[i];
+  }
+}
+
+// updatePCost_ over the round's observations, per variable in node order:
+// one wave per variable walks the packed list 64 at a time (one coalesced
+// load, a ballot of this variable's entries, then their costs in order)
 __global__ __launch_bounds__(64) void pc_fold(RelIO io) {
-  const int j = blockIdx.x * 64 + threadIdx.x;
-  if (j >= io.n) return;
+  const int j = blockIdx.x;
+  const int lane = threadIdx.x;
   double pu = io.pc_up[j], pd = io.pc_dn[j];
   int cu = io.cnt_up[j], cd = io.cnt_dn[j];
-  for (int b = 0; b < io.nb; ++b) {
-    const int k = io.nev[b];
-    for (int e = 0; e < k; ++e) {
-      const size_t i = (size_t)b * kRelEvents + e;
-      if (io.ev_var[i] != j) continue;
-      const double c = io.ev_cost[i];
-      if (io.ev_side[i] == 0) {
-        pd = (pd * cd + c) / (cd + 1);
+  const int E = *io.ev_total;
+  for (int c0 = 0; c0 < E; c0 += 64) {
+    const int i = c0 + lane;
+    const int v = i < E ? io.cv_var[i] : -1;
+    const double c = i < E ? io.cv_cost[i] : 0.0;
+    const int sd = i < E ? io.cv_side[i] : 0;
+    uint64_t mine = __ballot(v == j);
+    while (mine) {
+      const int k = __builtin_ctzll(mine);
+      mine &= mine - 1;
+      const double x = __shfl(c, k, 64);
+      if (__shfl(sd, k, 64) == 0) {
+        pd = (pd * cd + x) / (cd + 1);
         cd += 1;
       } else {
-        pu = (pu * cu + c) / (cu + 1);
+        pu = (pu * cu + x) / (cu + 1);
         cu += 1;
       }
     }
   }
-  if (io.last_new[j] >= 0) io.last[j] = io.last_new[j];
-  io.pc_up[j] = pu;
-  io.pc_dn[j] = pd;
-  io.cnt_up[j] = cu;
-  io.cnt_dn[j] = cd;
+  if (lane == 0) {
+    if (io.last_new[j] >= 0) io.last[j] = io.last_new[j];
+    io.pc_up[j] = pu;
+    io.pc_dn[j] = pd;
+    io.cnt_up[j] = cu;
+    io.cnt_dn[j] = cd;
+  }
 }
 
 }  // namespace
@@ -431,7 +454,10 @@ hipError_t launch_rel_children(const RelIO &io, const double *wlb, const double 
 hipError_t launch_rel_decide(const RelIO &io, hipStream_t stream) {
   if (io.nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(rel_decide, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
-  hipLaunchKernelGGL(pc_fold, dim3((io.n + 63) / 64), dim3(64), 0, stream, io);
+  hipLaunchKernelGGL(excl_scan, dim3(1), dim3(1024), 0, stream, io.nev, io.ev_off, io.nb,
+                     io.ev_total);
+  hipLaunchKernelGGL(rel_compact, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  hipLaunchKernelGGL(pc_fold, dim3(io.n), dim3(64), 0, stream, io);
   return hipGetLastError();
 }
 

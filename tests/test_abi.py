@@ -65,3 +65,22 @@ def test_pfi_cap_matches_header():
     hdr = open(os.path.join(ROOT, 'include', 'mgpu.h')).read()
     m = re.search(r'#define MGPU_LP_PFI_MAX (\d+)', hdr)
     assert m and int(m.group(1)) == runtime.LP_PFI_MAX
+
+
+def test_reference_libraries_coexist_in_one_process():
+    """The two test libraries that carry the reference objects (oracle/_ref:
+    libref_fbbt.so and the integration library, loaded RTLD_GLOBAL by the
+    integration tests) are linked -Bsymbolic: loading both and exiting must
+    not destroy one copy of the reference's static objects twice."""
+    import subprocess
+    import sys
+    ref = os.path.join(ROOT, 'oracle', '_ref')
+    a, b = os.path.join(ref, 'libminotaur_hip_integ.so'), os.path.join(ref, 'libref_fbbt.so')
+    if not (os.path.exists(a) and os.path.exists(b)):
+        import pytest
+        pytest.skip('oracle/_ref not built')
+    code = ("import ctypes, os\n"
+            f"ctypes.CDLL({a!r}, mode=os.RTLD_LAZY | os.RTLD_GLOBAL)\n"
+            f"ctypes.CDLL({b!r}, mode=os.RTLD_LAZY)\n")
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()[-500:]
