@@ -226,14 +226,18 @@ hipError_t launch_m(const DevLP &lp, const RefacIO &io, hipStream_t stream) {
 
 }  // namespace
 
+// register rows sized to the basis: M <= 56 keeps the two rows of B and I
+// under 256 VGPRs (two waves per SIMD), M = 64 needs AGPRs (one wave)
 size_t lp_refactor_lds_bytes(int n, int m, int nnz) {
-  return m <= 32 ? refactor_lds<32>(n, m, nnz) : refactor_lds<64>(n, m, nnz);
+  return m <= 32 ? refactor_lds<32>(n, m, nnz)
+       : m <= 56 ? refactor_lds<56>(n, m, nnz) : refactor_lds<64>(n, m, nnz);
 }
 
 hipError_t launch_lp_refactor(const DevLP &lp, const RefacIO &io, hipStream_t stream) {
   if (io.batch <= 0) return hipSuccess;
   if (lp.m > kLpMaxM || lp.m <= 0) return hipErrorInvalidValue;
-  return lp.m <= 32 ? launch_m<32>(lp, io, stream) : launch_m<64>(lp, io, stream);
+  return lp.m <= 32 ? launch_m<32>(lp, io, stream)
+       : lp.m <= 56 ? launch_m<56>(lp, io, stream) : launch_m<64>(lp, io, stream);
 }
 
 }  // namespace mgpu
