@@ -177,6 +177,16 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const d
                            int iter_limit, int32_t *d_status, double *d_obj, int32_t *d_iters,
                            double *d_x);
 
+/* The warm basis refactored for the LOADED matrix (host pointers, one
+ * basis): what Clp does with the kept basis after OsiLPEngine::
+ * changeConstraint / addConstraint / removeCons (OsiLPEngine.cpp:152-262).
+ * K3R on the device: the oracle's Gauss-Jordan with partial pivoting and
+ * compute_duals.  In: head [m], st [n+m]; out: head, st, reduced costs d
+ * [n+m], B^-1 [m][m] column-major; *singular = 1 when the basis was
+ * singular and the slack basis was returned instead.  m <= 64. */
+int mgpu_lp_refactor(mgpu_ctx *ctx, const int32_t *head, const int8_t *st, int32_t *o_head,
+                     int8_t *o_st, double *o_d, double *o_binv, int *singular);
+
 /* Node decision after the relaxation solve (device pointers, async): the
  * EngineStatus switch of PCBProcessor::shouldPrune_ (PCBProcessor.cpp:400-523)
  * plus IntVarHandler::isFeasible (IntVarHandler.cpp:54-84).

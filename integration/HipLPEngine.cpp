@@ -139,13 +139,33 @@ int HipLPEngine::upload_() {
                       chi_.data(), ctype_.data(), obj_.data(), 0.0);
 }
 
-// Gauss-Jordan inverse of the kept basis after the matrix changed (rows
-// edited / added / removed).  Falls back to the slack basis if singular.
+// Inverse of the kept basis after the matrix changed (rows edited / added /
+// removed), as Clp refactors it after OsiLPEngine::changeConstraint: on the
+// device (mgpu_lp_refactor, K3R: Gauss-Jordan with partial pivoting plus the
+// reduced costs) for m <= 64, else the same Gauss-Jordan on the host.  A
+// singular basis is dropped for the slack basis.
 void HipLPEngine::refactor_() {
   const int m = m_, n = n_;
   if ((int)ws_.head.size() != m) {
     wsValid_ = false;
     return;
+  }
+  {
+    HipLPWarmStart out;
+    out.head.resize(m);
+    out.st.resize(n + m);
+    out.d.resize(n + m);
+    out.binv.resize((size_t)m * m);
+    int sing = 0;
+    if (mgpu_lp_refactor(ctx_, ws_.head.data(), ws_.st.data(), out.head.data(), out.st.data(),
+                         out.d.data(), out.binv.data(), &sing) == MGPU_OK) {
+      if (sing) {
+        wsValid_ = false;
+      } else {
+        ws_ = out;
+      }
+      return;
+    }
   }
   std::vector<double> B((size_t)m * m, 0.0), I((size_t)m * m, 0.0);
   for (int i = 0; i < m; ++i) {

@@ -215,4 +215,45 @@ int mgpu_lp_solve_rows(mgpu_ctx *c, int batch, const double *lb, const double *u
   return MGPU_OK;
 }
 
+int mgpu_lp_refactor(mgpu_ctx *c, const int32_t *head, const int8_t *st, int32_t *o_head,
+                     int8_t *o_st, double *o_d, double *o_binv, int *singular) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_refactor: no problem loaded");
+  if (!head || !st || !o_head || !o_st || !o_d || !o_binv)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_refactor: bad argument");
+  const int n = c->lp.n, m = c->lp.m, N = n + m;
+  if (m > kLpMaxM || m == 0 || lp_refactor_lds_bytes(n, m, c->lp.nnz) > 160 * 1024)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_refactor: needs 0 < m <= %d (m=%d)", kLpMaxM, m);
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t s_h = al16h((size_t)m * 4), s_s = al16h((size_t)N), s_d = al16h((size_t)N * 8),
+               s_b = al16h((size_t)m * m * 8);
+  // in: head, st; out: head, st, d, binv, singular flag
+  HIPCHK(c, c->nr_vals.ensure(2 * s_h + 2 * s_s + s_d + s_b + 16));
+  char *w = c->nr_vals.as<char>();
+  int32_t *d_head = (int32_t *)w;
+  int8_t *d_st = (int8_t *)(w + s_h);
+  RefacIO rf{};
+  rf.batch = 1;
+  rf.head = d_head;
+  rf.st = d_st;
+  rf.o_head = (int32_t *)(w + s_h + s_s);
+  rf.o_st = (int8_t *)(w + 2 * s_h + s_s);
+  rf.o_d = (double *)(w + 2 * s_h + 2 * s_s);
+  rf.o_binv = (double *)(w + 2 * s_h + 2 * s_s + s_d);
+  rf.o_sing = (int32_t *)(w + 2 * s_h + 2 * s_s + s_d + s_b);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_head, head, (size_t)m * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_st, st, (size_t)N, hipMemcpyHostToDevice, s));
+  HIPCHK(c, launch_lp_refactor(c->lp, rf, s));
+  int32_t sing = 0;
+  HIPCHK(c, hipMemcpyAsync(o_head, rf.o_head, (size_t)m * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(o_st, rf.o_st, (size_t)N, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(o_d, rf.o_d, (size_t)N * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(o_binv, rf.o_binv, (size_t)m * m * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(&sing, rf.o_sing, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (singular) *singular = sing;
+  return MGPU_OK;
+}
+
 }  // extern "C"

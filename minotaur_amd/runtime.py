@@ -33,6 +33,7 @@ EXPORTS = [
     'mgpu_bnb_import', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
     'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
+    'mgpu_lp_refactor',
 ]
 
 
@@ -108,6 +109,7 @@ def load_library():
     lib.mgpu_qp_solve.argtypes = [_P, _I, _P, _P, _I, _P, _P, _P, _P]
     lib.mgpu_qp_solve_dev.argtypes = [_P, _I, _P, _P, _I, _P, _P, _P, _P]
     lib.mgpu_set_node_rows.argtypes = [_P, _I, _I, _P, _P, _I, _P, _P, _P]
+    lib.mgpu_lp_refactor.argtypes = [_P] + [_P] * 7
     lib.mgpu_lp_solve_rows.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
     lib.mgpu_lp_solve_rows_dev.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
@@ -402,6 +404,21 @@ class Context:
             _dp(status), _dp(obj), _dp(iters), _dp(x),
             _dp(wo.head) if wo else None, _dp(wo.st) if wo else None,
             _dp(wo.d) if wo else None, _dp(wo.binv) if wo else None), 'mgpu_lp_solve_dev')
+
+    def lp_refactor(self, head, st):
+        """The basis (head [m], st [n+m]) refactored for the loaded matrix:
+        (WarmStart with binv column-major, singular flag)."""
+        p = self.problem
+        h = _np(head, np.int32)
+        s = _np(st, np.int8)
+        oh = np.zeros(p.m, np.int32)
+        ost = np.zeros(p.n + p.m, np.int8)
+        od = np.zeros(p.n + p.m)
+        ob = np.zeros((p.m, p.m))
+        sing = ctypes.c_int(0)
+        self._chk(self.lib.mgpu_lp_refactor(self.h, _hp(h), _hp(s), _hp(oh), _hp(ost), _hp(od),
+                                            _hp(ob), ctypes.byref(sing)), 'mgpu_lp_refactor')
+        return WarmStart(oh, ost, od, ob), int(sing.value)
 
     # -- per-node rows (glob path) ---------------------------------------------
     def set_node_rows(self, nr):

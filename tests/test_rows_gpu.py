@@ -172,3 +172,43 @@ def test_rows_errors(ctx):
     ctx.load(p)                                # a reload clears the map
     with pytest.raises(MgpuError):
         ctx.lp_solve_rows(p.vlb[None], p.vub[None], rows0[None])
+
+
+def test_lp_refactor_single_basis(ctx):
+    """mgpu_lp_refactor (what HipLPEngine runs after changeConstraint): the
+    kept basis refactored for the loaded matrix equals numpy's inverse of the
+    basis matrix and the oracle LP from that basis takes the same pivots;
+    a singular basis comes back as the slack basis."""
+    from minotaur_amd.problem import random_problem
+    from minotaur_amd.runtime import WarmStart
+    p = random_problem(5, n=30, m=20)
+    ctx.load(p)
+    _, ws = ctx.root_solve()
+    q = random_problem(5, n=30, m=20)
+    q.val = q.val * (1.0 + 0.05 * np.sin(np.arange(q.nnz)))   # rows changed
+    ctx.load(q)
+    w, sing = ctx.lp_refactor(ws.head, ws.st)
+    assert sing == 0
+    A = np.hstack([q.dense(), -np.eye(q.m)])
+    Bm = A[:, w.head]
+    binv = w.binv.T                      # column-major -> (B^-1)[i, k]
+    assert np.allclose(binv @ Bm, np.eye(q.m), atol=1e-9)
+    y = np.array([q.obj[h] if h < q.n else 0.0 for h in w.head]) @ binv
+    cfull = np.concatenate([q.obj, np.zeros(q.m)])
+    d = cfull - A.T @ y
+    nb = w.st != 3
+    assert np.allclose(w.d[nb], d[nb], atol=1e-9)
+    # the solve from the refactored basis = the oracle's from (head, st)
+    r = ctx.lp_solve(q.vlb[None], q.vub[None], ws=WarmStart(w.head, w.st, w.d, w.binv))
+    from minotaur_amd.quad import NodeRows
+    none = NodeRows(1, np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int32),
+                    np.zeros(0, np.int32), np.zeros(0, np.int32))
+    so, oo, io, _ = oracle.dual_simplex_rows(q, q.vlb[None], q.vub[None], none, np.zeros((1, 1)),
+                                             ws=WarmStart(ws.head, ws.st, None, None))
+    assert r.status[0] == so[0] and r.iters[0] == io[0]
+    assert abs(r.obj[0] - oo[0]) <= 1e-9 * max(1.0, abs(oo[0]))
+    # singular: two basis positions on the same slack column
+    h2 = ws.head.copy()
+    h2[1] = h2[0]
+    w2, sing2 = ctx.lp_refactor(h2, ws.st)
+    assert sing2 == 1 and np.array_equal(w2.head, np.arange(q.n, q.n + q.m))
