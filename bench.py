@@ -586,7 +586,10 @@ def main():
         ctx.fbbt_dev(lb0, ub0, lb1, ub1, infeas, nmods, inc)
         ctx.lp_solve_dev(lb1, ub1, status, obj, iters, ws=ws, skip=infeas, x=x)
         ctx.node_decide_dev(status, obj, x, decision, inc, fbbt_infeas=infeas, cand_obj=cand)
-        best = mdist.allreduce_incumbent(cand.min().reshape(1))
+        cmin = cand.min().reshape(1)
+        acc["ev"][0].record()
+        best = mdist.allreduce_incumbent(cmin)
+        acc["ev"][1].record()
         acc["solved"] += (status != 12).sum()
         acc["pivots"] += iters.sum()
         # LPs finished by K3P itself (the rest went to its dense overflow re-solve)
@@ -599,13 +602,15 @@ def main():
         acc["lp_ms"].append(ctx.last_kernel_ms('lp'))
         acc["lp_main_ms"].append(ctx.last_kernel_ms('lp_main'))
         acc["lp_tail_ms"].append(ctx.last_kernel_ms('lp_tail'))
+        acc["rccl_ms"].append(acc["ev"][0].elapsed_time(acc["ev"][1]))
 
     def new_acc():
         return {"solved": torch.zeros((), dtype=torch.int64, device=dev),
                 "pivots": torch.zeros((), dtype=torch.int64, device=dev),
                 "pfi_solved": torch.zeros((), dtype=torch.int64, device=dev),
                 "pfi_pivots": torch.zeros((), dtype=torch.int64, device=dev),
-                "fbbt_ms": [], "lp_ms": [], "lp_main_ms": [], "lp_tail_ms": []}
+                "fbbt_ms": [], "lp_ms": [], "lp_main_ms": [], "lp_tail_ms": [], "rccl_ms": [],
+                "ev": (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))}
 
     # warm-up runs the exact timed step (also loads torch's lazily-loaded
     # reduction kernels, which otherwise land in the first timed step)
@@ -713,6 +718,11 @@ def main():
                 "parallelism": f"node-sharded x{world}",
             },
             "relaxations_per_s": solved / elapsed,
+            "fbbt_node_passes_per_s": float(B) * world / (fbbt_ms * 1e-3),
+            "collectives": {"incumbent_syncs": args.steps,
+                            "rccl_ms_total": float(np.sum(acc["rccl_ms"])),
+                            "note": "one all-reduce MIN of the incumbent per step (timed with "
+                                    "events on the engine stream; 0 at one GPU)"},
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,
