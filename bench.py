@@ -364,7 +364,9 @@ def convex_batch(ctx, dev, rank, world, B, args):
         ok &= good
         tot_nodes += nodes
         tot_s += el
-        per.append({"f": f, "rows": p.m, "lp_kernel": "K3L" if p.m > 64 else "K3",
+        kern = (("K3P + K3 overflow" if p.m <= 64 else "K3PW + K3L overflow")
+                if ctx.oracle_pfi() > 0 else ("K3" if p.m <= 64 else "K3L"))
+        per.append({"f": f, "rows": p.m, "lp_kernel": kern,
                     "nodes": nodes, "seconds": el, "rounds": rounds, "optimum": inc,
                     "optimum_highs": opt})
     return {"instances": per, "nodes": tot_nodes, "seconds": tot_s,

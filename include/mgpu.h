@@ -206,10 +206,11 @@ int mgpu_node_decide_dev(mgpu_ctx *ctx, int batch, const int32_t *d_fbbt_infeas,
  * (large n). For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
 
-/* Which LP kernel the next LP calls use: 0 auto, 1 K3, 2 K3L, 3 K3P.
- * Auto: K3P (product form against the shared inverse) for a batch that
- * shares one warm start and wants no warm start back, when m <= 64 and
- * n + m <= 256; else K3 when m <= 64 and the matrix fits LDS; else K3L.
+/* Which LP kernel the next LP calls use: 0 auto, 1 K3, 2 K3L, 3 product
+ * form (K3P / K3PW).  Auto: K3P (product form against the shared inverse)
+ * for a batch that shares one warm start and wants no warm start back, when
+ * m <= 64 and n + m <= 256, K3PW for such a batch when 64 < m <= 128 and
+ * B0^{-1} fits LDS; else K3 when m <= 64 and the matrix fits LDS; else K3L.
  * K3 and K3L restate oracle/lp_dual.c pivot for pivot, K3P its product-form
  * mode (oracle dual_simplex(..., pfi=k)).  For tests/benchmarks. */
 int mgpu_set_lp_variant(mgpu_ctx *ctx, int variant);
@@ -219,6 +220,18 @@ int mgpu_set_lp_variant(mgpu_ctx *ctx, int variant);
  * (default MGPU_LP_PFI_MAX). */
 #define MGPU_LP_PFI_MAX 16
 int mgpu_set_lp_pfi(mgpu_ctx *ctx, int kmax);
+
+/* K3PW (64 < m <= 128 rows, two basis rows per lane) eta-file cap: a node
+ * that needs more pivots is continued by K3L from its basis and explicit
+ * inverse.  0 keeps auto mode off K3PW; 1..MGPU_LP_PFI_WIDE_MAX (default
+ * MGPU_LP_PFI_WIDE_MAX). */
+#define MGPU_LP_PFI_WIDE_MAX 32
+int mgpu_set_lp_pfi_wide(mgpu_ctx *ctx, int kmax);
+
+/* The eta-file cap the LP calls use for a batch that shares one warm start
+ * and wants no warm start back (K3P or K3PW, the oracle's dual_simplex(...,
+ * pfi=k)); 0 when such a batch runs a dense kernel (K3 / K3L). */
+int mgpu_lp_pfi_cap(mgpu_ctx *ctx);
 
 /* Batched bound LPs: LP b minimises obj_sign[b] * x[obj_col[b]] over the
  * loaded relaxation on ONE box lb/ub [n] (the relaxation's), warm-started

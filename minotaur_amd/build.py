@@ -14,7 +14,7 @@ HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 
 SOURCES = ['mgpu_runtime.cpp', 'quad_runtime.cpp', 'bnb.cpp', 'fbbt_linear.hip',
-           'lp_dual.hip', 'lp_pfi.hip', 'lp_large.hip', 'node_decide.hip', 'quad_fbbt.hip', 'bnb.hip',
+           'lp_dual.hip', 'lp_pfi.hip', 'lp_pfi_wide.hip', 'lp_large.hip', 'node_decide.hip', 'quad_fbbt.hip', 'bnb.hip',
            'bnb_select.hip', 'qp_runtime.cpp', 'rows_runtime.cpp', 'lp_rows.hip', 'bnb_rel.hip',
            'qp_kkt.hip']
 # -ffp-contract=off: no fused multiply-add anywhere (bit-exact FBBT sums,

@@ -62,6 +62,7 @@ struct mgpu_ctx {
   int fbbt_variant = 0;
   int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L, 3 K3P
   int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)
+  int lp_pfi_wide = kPfiWideMax;  // K3PW eta-file cap (0: auto never picks K3PW)
   int bnb_order = 0;           // mgpu_bnb_config: 0 depth-first stack, 1 best-first
   int bnb_warm = 0;            // mgpu_bnb_config: 0 root basis, 1 parent basis
   int bnb_brancher = 0;        // mgpu_bnb_brancher: 0 MaxVio, 1 reliability
@@ -73,7 +74,7 @@ struct mgpu_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr,
             ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;
   hipEvent_t ev8 = nullptr;    // between K3P and its dense overflow re-solve
-  bool last_lp_pfi = false;    // the last LP call ran K3P
+  bool last_lp_pfi = false;    // the last LP call ran K3P or K3PW
   double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0, last_qp_ms = 0.0;
   // per-node rows (mgpu_set_node_rows): device maps csc_pos, csr_pos,
   // coef_src, row, lo_src, hi_src; K3R's per-node warm starts; host-path

@@ -248,17 +248,26 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
   s.n = n; s.m = m; s.N = N;
   const size_t mm = (size_t)m * m;
 
+  // node list (the product-form kernels' overflow re-solve, as K3's):
+  // positions list_lo .. min(*node_count, list_hi) of node_list
+  const int lo = io.node_list != nullptr ? io.list_lo : 0;
+  int nsolve = io.batch;
+  if (io.node_list != nullptr) {
+    nsolve = *io.node_count;
+    if (nsolve > io.list_hi) nsolve = io.list_hi;
+  }
   // nodes from a device counter when the host gives one (dynamic schedule:
   // a workgroup that finishes early takes the next node), else a static stride
   __shared__ int s_next;
-  for (int b = blockIdx.x;; b += gridDim.x) {
+  for (int bi = lo + blockIdx.x;; bi += gridDim.x) {
     __syncthreads();  // the previous node's LDS state is dead
     if (io.next != nullptr) {
       if (tid == 0) s_next = atomicAdd(io.next, 1);
       __syncthreads();
-      b = s_next;
+      bi = lo + s_next;
     }
-    if (b >= io.batch) break;
+    if (bi >= nsolve) break;
+    const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
     s.nlb = io.lb + (size_t)b * io.box_stride;
     s.nub = io.ub + (size_t)b * io.box_stride;
     s.ocol = io.obj_col != nullptr ? io.obj_col[b] : -1;
@@ -292,7 +301,8 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
     // ---- basis: warm start or slack basis (B = -I) ----
     const bool warm = io.ws.head != nullptr;
     if (warm) {
-      const size_t bw = io.ws_index != nullptr ? (size_t)io.ws_index[b] : (size_t)b;
+      const size_t bw = io.ws_index != nullptr ? (size_t)io.ws_index[b]
+                        : io.list_ws ? (size_t)bi : (size_t)b;
       const int32_t *wh = io.ws.head + bw * io.ws.s_head;
       const int8_t *wst = io.ws.st + bw * io.ws.s_st;
       const double *wb = io.ws.binv + bw * io.ws.s_binv;
@@ -567,7 +577,7 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
     }
     if (tid == 0) {
       io.status[b] = status;
-      io.iters[b] = iters;
+      io.iters[b] = iters + io.iter_base;
     }
   }
 }

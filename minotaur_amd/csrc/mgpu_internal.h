@@ -120,8 +120,8 @@ struct LpIO {
   int8_t *wo_st;                // [B][n+m]
   double *wo_d;                 // [B][n+m]
   double *wo_binv;              // [B][m][m]
-  // K3 only: solve just the nodes node_list[list_lo .. min(*node_count,
-  // list_hi)) (device memory; the overflow list of K3P), null = every node
+  // K3 and K3L: solve just the nodes node_list[list_lo .. min(*node_count,
+  // list_hi)) (device memory; the overflow list of K3P / K3PW), null = every node
   // of the batch.  list_ws: the per-node warm start is indexed by list
   // position (K3P's continuation slots), not by node.  iter_base is added to
   // the reported iteration counts (the pivots K3P already made).
@@ -158,6 +158,13 @@ size_t lp_pfi_lds_bytes(int n, int m, int nnz);
 bool lp_pfi_fits(int n, int m, int nnz);
 hipError_t launch_lp_pfi(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
                          hipStream_t stream);
+// K3PW (lp_pfi_wide.hip): K3P for 64 < m <= 128 (two basis rows per lane),
+// n + m <= 256, at most kPfiWideMax etas; its overflow list goes to K3L.
+constexpr int kPfiWideMax = 32;
+size_t lp_pfiw_lds_bytes(int n, int m, int nnz);
+bool lp_pfiw_fits(int n, int m, int nnz);
+hipError_t launch_lp_pfiw(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
+                          hipStream_t stream);
 
 struct DecideIO {
   int batch;

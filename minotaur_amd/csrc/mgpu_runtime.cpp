@@ -253,7 +253,14 @@ int mgpu_set_lp_pfi(mgpu_ctx *c, int kmax) {
   return MGPU_OK;
 }
 
+int mgpu_set_lp_pfi_wide(mgpu_ctx *c, int kmax) {
+  if (!c || kmax < 0 || kmax > MGPU_LP_PFI_WIDE_MAX) return MGPU_ERR_ARG;
+  c->lp_pfi_wide = kmax;
+  return MGPU_OK;
+}
+
 static_assert(MGPU_LP_PFI_MAX == kPfiMax, "ABI eta-file cap = kernel's");
+static_assert(MGPU_LP_PFI_WIDE_MAX == kPfiWideMax, "ABI eta-file cap = kernel's");
 
 int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
   if (!c || variant < 0 || variant > 3) return MGPU_ERR_ARG;
@@ -468,23 +475,39 @@ bool use_large_lp(const mgpu_ctx *c) {
   return c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024;
 }
 
-// K3P serves a batch that shares one warm start and asks for no warm start
-// back; in auto mode whenever the problem fits it, variant 3 insists.
+// Product form serves a batch that shares one warm start and asks for no
+// warm start back: K3P for m <= 64 (dense continuation K3), K3PW for
+// 64 < m <= 128 (continuation K3L); in auto mode whenever the problem fits,
+// variant 3 insists.  Returns the eta-file cap (0: a dense kernel) and which
+// kernel in *wide.
+int pfi_cap(const mgpu_ctx *c, bool *wide) {
+  *wide = false;
+  if (!c->loaded || (c->lp_variant != 0 && c->lp_variant != 3)) return 0;
+  const int n = c->lp.n, m = c->lp.m, nnz = c->lp.nnz;
+  if (lp_pfi_fits(n, m, nnz) && lp_lds_bytes(n, m, nnz) <= 160 * 1024)
+    return c->lp_variant == 3 && c->lp_pfi == 0 ? kPfiMax : c->lp_pfi;
+  if (lp_pfiw_fits(n, m, nnz) && lp_large_lds_bytes(n, m) <= (size_t)kLargeLdsMax) {
+    *wide = true;
+    return c->lp_variant == 3 && c->lp_pfi_wide == 0 ? kPfiWideMax : c->lp_pfi_wide;
+  }
+  return 0;
+}
+
 bool use_pfi(const mgpu_ctx *c, const LpIO &io) {
-  if (c->lp_variant != 0 && c->lp_variant != 3) return false;
   const bool shared = io.ws.head != nullptr && io.ws.s_head == 0 && io.ws.s_st == 0 &&
                       io.ws.s_d == 0 && io.ws.s_binv == 0 && io.ws_index == nullptr;
-  const int kmax = c->lp_variant == 3 && c->lp_pfi == 0 ? kPfiMax : c->lp_pfi;
-  return shared && io.wo_head == nullptr && kmax > 0 &&
-         lp_pfi_fits(c->lp.n, c->lp.m, c->lp.nnz) &&
-         lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) <= 160 * 1024;
+  bool wide;
+  return shared && io.wo_head == nullptr && pfi_cap(c, &wide) > 0;
 }
 
 int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
   if (use_pfi(c, io)) {
-    // K3P, then the dense K3 on exactly the nodes that filled the eta file:
-    // it continues from K3P's basis and explicit inverse (continuation
-    // slots), or restarts from the shared warm start past the slot capacity
+    // K3P / K3PW, then the dense K3 / K3L on exactly the nodes that filled
+    // the eta file: it continues from the product form's basis and explicit
+    // inverse (continuation slots), or restarts from the shared warm start
+    // past the slot capacity
+    bool wide = false;
+    const int kcap = pfi_cap(c, &wide);
     const int m = c->lp.m, N = c->lp.n + c->lp.m;
     const int cap = io.batch < kPfiOvfSlots ? io.batch : kPfiOvfSlots;
     HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 4) * sizeof(int32_t)));
@@ -495,7 +518,7 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     int32_t *cnt = c->pfi_ovf.as<int32_t>();
     HIPCHK(c, hipMemsetAsync(cnt, 0, 4 * sizeof(int32_t), c->stream));
     PfiIO px{};
-    px.kmax = c->lp_pfi > 0 ? c->lp_pfi : kPfiMax;
+    px.kmax = kcap;
     px.ovf_count = cnt;
     px.next = cnt + 1;
     px.ovf_list = cnt + 4;
@@ -505,8 +528,23 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     px.c_st = (int8_t *)(cp + sb_head);
     px.c_d = (double *)(cp + sb_head + sb_st);
     px.c_binv = (double *)(cp + sb_head + sb_st + sb_d);
-    HIPCHK(c, launch_lp_pfi(c->lp, io, px, c->num_cus, c->stream));
+    if (wide) {
+      HIPCHK(c, launch_lp_pfiw(c->lp, io, px, c->num_cus, c->stream));
+    } else {
+      HIPCHK(c, launch_lp_pfi(c->lp, io, px, c->num_cus, c->stream));
+    }
     HIPCHK(c, hipEventRecord(c->ev8, c->stream));
+    // K3L continuation: one HBM inverse slot per resident workgroup
+    int lgrid = 0;
+    if (wide) {
+      lgrid = lp_large_grid(io.batch < cap ? io.batch : cap, c->lp.n, m, c->num_cus);
+      HIPCHK(c, c->lp_slots.ensure((size_t)lgrid * m * m * sizeof(double) + 8));
+      HIPCHK(c, lp_large_prepare());
+    }
+    auto dense = [&](const LpIO &d) -> hipError_t {
+      return wide ? launch_lp_large(c->lp, d, c->lp_slots.as<double>(), lgrid, c->stream)
+                  : launch_lp_dual(c->lp, d, c->num_cus, c->stream);
+    };
     c->last_lp_pfi = true;
     LpIO io2 = io;
     io2.node_list = px.ovf_list;
@@ -518,7 +556,7 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     io2.iter_limit = io.iter_limit - px.kmax;  // K3P only overflows below the limit
     io2.ws = LpWarm{px.c_head, px.c_st, px.c_d, px.c_binv, m, N, N, (long)m * m};
     io2.next = cnt + 2;
-    HIPCHK(c, launch_lp_dual(c->lp, io2, c->num_cus, c->stream));
+    HIPCHK(c, dense(io2));
     if (io.batch > cap) {  // overflow beyond the slots: restart from the shared warm start
       LpIO io3 = io;
       io3.node_list = px.ovf_list;
@@ -526,14 +564,14 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
       io3.list_lo = cap;
       io3.list_hi = 0x7fffffff;
       io3.next = cnt + 3;
-      HIPCHK(c, launch_lp_dual(c->lp, io3, c->num_cus, c->stream));
+      HIPCHK(c, dense(io3));
     }
     return MGPU_OK;
   }
   c->last_lp_pfi = false;
   if (c->lp_variant == 3)
-    return fail(c, MGPU_ERR_ARG, "%s: K3P needs a shared warm start, no warm-start output, "
-                "m <= 64 and n + m <= %d", who, 64 * kPfiSlots);
+    return fail(c, MGPU_ERR_ARG, "%s: K3P/K3PW need a shared warm start, no warm-start "
+                "output, m <= 128 and n + m <= %d", who, 64 * kPfiSlots);
   if (!use_large_lp(c)) {
     if (c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
       return fail(c, MGPU_ERR_ARG, "%s: problem too large for K3 (m=%d)", who, c->lp.m);
@@ -562,6 +600,12 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
 
 extern "C++" int launch_lp_nodes(mgpu_ctx *c, const LpIO &io) {
   return launch_lp(c, io, "lp batch");
+}
+
+int mgpu_lp_pfi_cap(mgpu_ctx *c) {
+  if (!c) return MGPU_ERR_ARG;
+  bool wide;
+  return pfi_cap(c, &wide);
 }
 
 int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub,

@@ -20,6 +20,7 @@ _I = ctypes.c_int
 _D = ctypes.c_double
 
 LP_PFI_MAX = 16  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
+LP_PFI_WIDE_MAX = 32  # MGPU_LP_PFI_WIDE_MAX: K3PW eta-file cap
 
 # Every entry point declared in include/mgpu.h (checked by the CPU tests).
 EXPORTS = [
@@ -33,7 +34,7 @@ EXPORTS = [
     'mgpu_bnb_import', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
     'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
-    'mgpu_lp_refactor',
+    'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap',
 ]
 
 
@@ -84,6 +85,8 @@ def load_library():
     lib.mgpu_set_fbbt_variant.argtypes = [_P, _I]
     lib.mgpu_set_lp_variant.argtypes = [_P, _I]
     lib.mgpu_set_lp_pfi.argtypes = [_P, _I]
+    lib.mgpu_set_lp_pfi_wide.argtypes = [_P, _I]
+    lib.mgpu_lp_pfi_cap.argtypes = [_P]
     lib.mgpu_lp_solve.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_lp_solve_dev.argtypes = [_P, _I] + [_P] * 7 + [_I, _I] + [_P] * 8
     lib.mgpu_node_decide_dev.argtypes = [_P, _I] + [_P] * 4 + [_D] * 5 + [_P] * 3
@@ -225,17 +228,21 @@ class Context:
         self._chk(self.lib.mgpu_set_lp_pfi(self.h, int(kmax)), 'mgpu_set_lp_pfi')
         self.lp_pfi = int(kmax)
 
+    def set_lp_pfi_wide(self, kmax: int):
+        """K3PW eta-file cap (64 < m <= 128; 0: auto mode never picks K3PW)."""
+        self._chk(self.lib.mgpu_set_lp_pfi_wide(self.h, int(kmax)), 'mgpu_set_lp_pfi_wide')
+
     def oracle_pfi(self, shared_ws=True, want_ws=False):
         """The ``pfi`` argument under which oracle.dual_simplex / lp_bound
-        restate what this context runs for such a batch (0 = dense K3/K3L)."""
-        p = self.problem
-        v, k = getattr(self, 'lp_variant', 0), getattr(self, 'lp_pfi', LP_PFI_MAX)
-        if v == 3:
-            k = k or LP_PFI_MAX
-        elif v != 0:
+        restate what this context runs for such a batch (0 = dense K3/K3L):
+        the eta-file cap of K3P / K3PW for the loaded problem
+        (mgpu_lp_pfi_cap)."""
+        if not shared_ws or want_ws:
             return 0
-        fits = p is not None and p.m <= 64 and p.n + p.m <= 256
-        return k if (shared_ws and not want_ws and fits) else 0
+        k = self.lib.mgpu_lp_pfi_cap(self.h)
+        if k < 0:
+            raise MgpuError(f"mgpu_lp_pfi_cap failed ({k})")
+        return int(k)
 
     def set_fbbt_variant(self, v: int):
         self._chk(self.lib.mgpu_set_fbbt_variant(self.h, int(v)), 'mgpu_set_fbbt_variant')

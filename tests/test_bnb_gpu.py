@@ -124,8 +124,13 @@ def test_bnb_k3l_tree_matches_cpu_and_highs(ctx):
     assert p.m > 64
     hs, hobj = oracle.highs_milp(p)
     ctx.load(p)
-    og, xg, sg, _ = bnb.solve(ctx, batch=512, capacity=1 << 17)
-    oc, xc, sc, _ = bnb.solve(CpuBnbContext(p, ctx.oracle_pfi()), batch=512, capacity=1 << 17)
+    ctx.set_lp_variant(2)   # K3L (auto picks the product-form K3PW for this batch)
+    try:
+        og, xg, sg, _ = bnb.solve(ctx, batch=512, capacity=1 << 17)
+        assert ctx.oracle_pfi() == 0
+    finally:
+        ctx.set_lp_variant(0)
+    oc, xc, sc, _ = bnb.solve(CpuBnbContext(p, 0), batch=512, capacity=1 << 17)
     assert sg.open == sc.open == 0
     assert (sg.rounds, sg.nodes, list(sg.ndec)) == (sc.rounds, sc.nodes, list(sc.ndec))
     assert og == oc
