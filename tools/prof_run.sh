@@ -5,7 +5,7 @@
 #   wide stream -> doubled when converted to bytes).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/prof
+OUT=${OUT:-$R/gpurun_out/prof}
 ARGS=${BENCH_ARGS:---steps 5 --warmup 1 --batch 524288 --no-cpu-baseline --no-bnb --no-qp --no-convex --no-knapsack}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
