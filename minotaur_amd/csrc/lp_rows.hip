@@ -18,8 +18,16 @@
 // register 0: each elimination step shifts the B row left by one (columns
 // already pivoted are unit vectors that are never read again), so the
 // dynamic step loop indexes registers only with compile-time constants.
-// The pivot row is broadcast through LDS.  Steps whose column has no other
-// nonzero (slack columns) skip the elimination with a wave-uniform branch.
+// The I part is kept in PIVOT order: register k holds the column of the row
+// pivoted at step k, and a row's own identity entry (exactly 1 until that
+// row is pivoted) is implicit.  At step c only registers 0..c of I and
+// 0..m-c-1 of B can be nonzero, so both updates run over 8-register chunks
+// below those bounds (wave-uniform branches): half the work of the dense
+// [B | I] sweep.  The values are the oracle's (the skipped entries are the
+// zeros it updates); only the sign of a zero entry of B^-1 can differ, which
+// no consumer distinguishes.  The pivot row is broadcast through LDS.  Steps
+// whose column has no other nonzero (slack columns) skip the elimination with
+// a wave-uniform branch.
 #include "mgpu_internal.h"
 #include "wave.h"
 
@@ -43,6 +51,7 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
   double *wc = (double *)p;   p += al16r((size_t)nnz * 8);      // node CSC values
   double *Ls = (double *)p;   p += al16r((size_t)m * ld * 8);   // dense B, then B^-1 rows
   double *prow = (double *)p; p += al16r((size_t)2 * M * 8);    // pivot row broadcast
+  int32_t *pord = (int32_t *)p; p += al16r((size_t)M * 4);       // row pivoted at step k
   double *y = (double *)p;    p += al16r((size_t)m * 8);
   int32_t *hd = (int32_t *)p; p += al16r((size_t)m * 4);
   int8_t *st = (int8_t *)p;
@@ -80,11 +89,14 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
   wave_sync();
 
   const bool row = lane < m;
-  double Bv[M], Iv[M];
+  constexpr int kC = 8;          // register chunk of the skipped updates
+  constexpr int NQ = M / kC;
+  static_assert(M % kC == 0, "register rows are whole chunks");
+  double Bv[M], Iv[M];  // Iv[k]: the column of the row pivoted at step k
 #pragma unroll
   for (int k = 0; k < M; ++k) {
     Bv[k] = (row && k < m) ? Ls[(size_t)lane * ld + k] : 0.0;
-    Iv[k] = (row && k == lane) ? 1.0 : 0.0;
+    Iv[k] = 0.0;
   }
   int lpos = lane;  // logical row (row swaps move logical positions, not data)
   bool sing = false;
@@ -110,18 +122,25 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
     const int lp_P = rl(lpos, P);
     if (lane == Q) lpos = lp_P;  // swap rows c and piv
     if (lane == P) lpos = c;
-    // scale the pivot row by 1 / pivot (a product, as the oracle)
+    // scale the pivot row by 1 / pivot (a product, as the oracle); its own
+    // identity entry (1) becomes inv at pivot position c
     const double inv = 1.0 / rld(Bv[0], P);
+    if (lane == 0) pord[c] = P;
     if (lane == P) {
 #pragma unroll
-      for (int k = 0; k < M; ++k) {
-        Bv[k] *= inv;
-        Iv[k] *= inv;
-      }
+      for (int k = 0; k < M; ++k) Bv[k] *= inv;
 #pragma unroll
       for (int k = 1; k < M; ++k) prow[k] = Bv[k];
 #pragma unroll
-      for (int k = 0; k < M; ++k) prow[M + k] = Iv[k];
+      for (int q = 0; q < NQ; ++q) {
+        if (q * kC <= c) {
+#pragma unroll
+          for (int k = q * kC; k < q * kC + kC; ++k) {
+            Iv[k] = k < c ? Iv[k] * inv : k == c ? inv : Iv[k];
+            prow[M + k] = Iv[k];
+          }
+        }
+      }
     }
     wave_sync();
     // eliminate column c from every other row with f = B_rc != 0
@@ -134,9 +153,14 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
         Bv[k] = upd ? t : Bv[k + 1];
       }
 #pragma unroll
-      for (int k = 0; k < M; ++k) {
-        const double t = Iv[k] - f * prow[M + k];
-        Iv[k] = upd ? t : Iv[k];
+      for (int q = 0; q < NQ; ++q) {
+        if (q * kC <= c) {
+#pragma unroll
+          for (int k = q * kC; k < q * kC + kC; ++k) {
+            const double t = Iv[k] - f * prow[M + k];
+            Iv[k] = upd ? t : Iv[k];
+          }
+        }
       }
     } else {
 #pragma unroll
@@ -164,11 +188,12 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
       for (int i = lane; i < m; i += 64) ob[(size_t)k * m + i] = i == k ? -1.0 : 0.0;
     return;
   }
-  // row lpos of B^-1 (basis position lpos) to LDS, row-major
+  // row lpos of B^-1 (basis position lpos) to LDS, row-major: pivot
+  // position k is column pord[k] of the identity part
   if (row) {
 #pragma unroll
     for (int k = 0; k < M; ++k)
-      if (k < m) Ls[(size_t)lpos * ld + k] = Iv[k];
+      if (k < m) Ls[(size_t)lpos * ld + pord[k]] = Iv[k];
   }
   wave_sync();
   // column-major B^-1: column k is one coalesced store over the lanes
@@ -206,7 +231,8 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
 template <int M>
 size_t refactor_lds(int n, int m, int nnz) {
   return al16r((size_t)nnz * 8) + al16r((size_t)m * (m + 1) * 8) + al16r((size_t)2 * M * 8) +
-         al16r((size_t)m * 8) + al16r((size_t)m * 4) + al16r((size_t)(n + m));
+         al16r((size_t)M * 4) + al16r((size_t)m * 8) + al16r((size_t)m * 4) +
+         al16r((size_t)(n + m));
 }
 
 template <int M>
