@@ -137,6 +137,50 @@ struct NodeView {
   }
 };
 
+// bounds loaded per batch in the column loops (tightenInts_, checkBounds_,
+// staging, write-out): loads issued together, one memory round trip
+constexpr int kBnd = 8;
+
+// box in (row-major [node][var] in HBM) -> this lane's node view, and back;
+// kBnd loads in flight before the stores (src and dst may alias as far as
+// the compiler knows, which would make every column its own round trip)
+template <class V>
+__device__ __forceinline__ void box_in(V &v, const double *src_l, const double *src_u, int n) {
+  for (int j0 = 0; j0 < n; j0 += kBnd) {
+    double a[kBnd], b[kBnd];
+#pragma unroll
+    for (int e = 0; e < kBnd; ++e) {
+      const int j = j0 + e < n ? j0 + e : j0;
+      a[e] = src_l[j];
+      b[e] = src_u[j];
+    }
+#pragma unroll
+    for (int e = 0; e < kBnd; ++e)
+      if (j0 + e < n) {
+        v.L(j0 + e) = a[e];
+        v.U(j0 + e) = b[e];
+      }
+  }
+}
+template <class V>
+__device__ __forceinline__ void box_out(const V &v, double *dst_l, double *dst_u, int n) {
+  for (int j0 = 0; j0 < n; j0 += kBnd) {
+    double a[kBnd], b[kBnd];
+#pragma unroll
+    for (int e = 0; e < kBnd; ++e) {
+      const int j = j0 + e < n ? j0 + e : j0;
+      a[e] = v.L(j);
+      b[e] = v.U(j);
+    }
+#pragma unroll
+    for (int e = 0; e < kBnd; ++e)
+      if (j0 + e < n) {
+        dst_l[j0 + e] = a[e];
+        dst_u[j0 + e] = b[e];
+      }
+  }
+}
+
 struct NodeState {
   int nmods;
   unsigned nintmods;
@@ -588,10 +632,24 @@ __device__ __forceinline__ bool tighten_ints(const DevLP &lp, V &v, NodeState &s
   for (int c0 = 0; c0 < lp.nint; c0 += kLanes) {
     const int cnt = lp.nint - c0 < kLanes ? lp.nint - c0 : kLanes;
     const TermChunk ch = load_terms(lp.irec + c0, cnt, v.lane);
-    for (int k = 0; k < cnt; ++k) {
+    // the columns are distinct, so the bounds of 8 of them are loaded before
+    // any is written: one memory round trip per 8 columns instead of one per
+    // column (the compiler cannot prove the stores do not alias later loads)
+    for (int k0 = 0; k0 < cnt; k0 += kBnd) {
+      double lv[kBnd], uv[kBnd];
+#pragma unroll
+      for (int e = 0; e < kBnd; ++e) {
+        const int jj = rl(ch.j, k0 + e < cnt ? k0 + e : k0);
+        lv[e] = v.L(jj);
+        uv[e] = v.U(jj);
+      }
+#pragma unroll
+      for (int e = 0; e < kBnd; ++e) {
+      const int k = k0 + e;
+      if (k >= cnt) break;
       const Term1 t{0.0, rlu64(ch.cmask, k), rl(ch.j, k), rl(ch.cs, k), rl(ch.ce, k), 1};
       const int j = t.j;
-      const double l = v.L(j), u = v.U(j);
+      const double l = lv[e], u = uv[e];
       if (act && l > -kInfty && fabs(l - floor(l + 0.5)) > kIntTol) {
         const double nv = ceil(l);
         v.change_bflag(t);
@@ -610,6 +668,7 @@ __device__ __forceinline__ bool tighten_ints(const DevLP &lp, V &v, NodeState &s
         u2 = nv;
       }
       bad |= l2 > u2 + kETol;
+      }
     }
   }
   return bad;
@@ -625,9 +684,17 @@ __device__ __forceinline__ bool check_bounds_rest(const DevLP &lp, const V &v, b
   for (int c0 = 0; c0 < lp.ncont; c0 += kLanes) {
     const int cnt = lp.ncont - c0 < kLanes ? lp.ncont - c0 : kLanes;
     const int jl = v.lane < cnt ? lp.ccont[c0 + v.lane] : 0;
-    for (int k = 0; k < cnt; ++k) {
-      const int j = rl(jl, k);
-      bad |= v.L(j) > v.U(j) + kETol;
+    for (int k0 = 0; k0 < cnt; k0 += kBnd) {
+      double lv[kBnd], uv[kBnd];
+#pragma unroll
+      for (int e = 0; e < kBnd; ++e) {
+        const int j = rl(jl, k0 + e < cnt ? k0 + e : k0);
+        lv[e] = v.L(j);
+        uv[e] = v.U(j);
+      }
+#pragma unroll
+      for (int e = 0; e < kBnd; ++e)
+        if (k0 + e < cnt) bad |= lv[e] > uv[e] + kETol;
     }
   }
   return bad || lp.cons_bad != 0;
@@ -682,14 +749,8 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   // node's row (consecutive vars share cache lines) and every store is one
   // coalesced 512-B scratch row.  LDS variant: node-outer, coalesced reads.
   if constexpr (!kLds) {
-    if (lane < nb) {
-      const double *src_l = io.lb_in + (size_t)(b0 + lane) * n;
-      const double *src_u = io.ub_in + (size_t)(b0 + lane) * n;
-      for (int j = 0; j < n; ++j) {
-        v.L(j) = src_l[j];
-        v.U(j) = src_u[j];
-      }
-    }
+    if (lane < nb)
+      box_in(v, io.lb_in + (size_t)(b0 + lane) * n, io.ub_in + (size_t)(b0 + lane) * n, n);
   }
   for (int nd = 0; nd < (kLds ? nb : 0); ++nd) {
     const double *src_l = io.lb_in + (size_t)(b0 + nd) * n;
@@ -783,14 +844,8 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   }
   __syncthreads();
   if constexpr (!kLds) {  // var-outer: coalesced scratch reads (as the staging)
-    if (kFbbtOutVarOuter && lane < nb) {
-      double *dst_l = io.lb_out + (size_t)(b0 + lane) * n;
-      double *dst_u = io.ub_out + (size_t)(b0 + lane) * n;
-      for (int j = 0; j < n; ++j) {
-        dst_l[j] = v.L(j);
-        dst_u[j] = v.U(j);
-      }
-    }
+    if (kFbbtOutVarOuter && lane < nb)
+      box_out(v, io.lb_out + (size_t)(b0 + lane) * n, io.ub_out + (size_t)(b0 + lane) * n, n);
   }
   for (int nd = 0; nd < (kLds || !kFbbtOutVarOuter ? nb : 0); ++nd) {
     double *dst_l = io.lb_out + (size_t)(b0 + nd) * n;
@@ -869,12 +924,7 @@ __global__ MGPU_K1P_ATTR __launch_bounds__(kLanes * kWG) void fbbt_linear_persis
       if (fin) {
         io.infeas[node] = infeas ? 1 : 0;
         io.nmods[node] = s.nmods;
-        double *dst_l = io.lb_out + (size_t)node * n;
-        double *dst_u = io.ub_out + (size_t)node * n;
-        for (int j = 0; j < n; ++j) {
-          dst_l[j] = v.L(j);
-          dst_u[j] = v.U(j);
-        }
+        box_out(v, io.lb_out + (size_t)node * n, io.ub_out + (size_t)node * n, n);
         has = false;
       }
     }
@@ -892,12 +942,7 @@ __global__ MGPU_K1P_ATTR __launch_bounds__(kLanes * kWG) void fbbt_linear_persis
           if (my < io.batch) {
             node = my;
             has = true;
-            const double *src_l = io.lb_in + (size_t)node * n;
-            const double *src_u = io.ub_in + (size_t)node * n;
-            for (int j = 0; j < n; ++j) {
-              v.L(j) = src_l[j];
-              v.U(j) = src_u[j];
-            }
+            box_in(v, io.lb_in + (size_t)node * n, io.ub_in + (size_t)node * n, n);
             // simplePresolve: every constraint's BFlag set (:1618-1622)
             v.bits = all_rows;
             s.nmods = 0;
