@@ -931,7 +931,7 @@ __global__ MGPU_K1P_ATTR __launch_bounds__(kLanes * kWG) void fbbt_linear_persis
     // refill idle lanes from the queue (one atomic per wave)
     if (!exhausted) {
       const uint64_t idle = __ballot(!has);
-      if (idle) {
+      if (idle && (__popcll(idle) >= io.refill_min || idle == ~0ull)) {
         const int cnt = __popcll(idle);
         int base = 0;
         if (lane == (int)__builtin_ctzll(idle)) base = atomicAdd(io.next, cnt);

@@ -236,6 +236,7 @@ struct FbbtIO {
   double *scratch;              // global-bounds variant: [waves][2][n][kLanes]
   uint8_t *flag_scratch;        // global-bounds variant: [waves][m][kLanes]
   int32_t *next;                // persistent variant: zeroed node counter (queue head)
+  int refill_min;               // persistent variant: idle lanes before a refill (1 = any)
 };
 
 constexpr int kLanes = 64;      // wave64: one node per lane
