@@ -1,20 +1,28 @@
 #!/usr/bin/env python
-"""Headline benchmark: batched branch-and-bound node processing on MI355X.
+"""Headline benchmark: batched branch-and-bound tree rounds on MI355X.
 
 BASELINE.json metric: "B&B nodes/sec + relaxations solved/sec at 1/2/4/8
 MI355X", quoted on configs[1] ("tls4.nl glob solver, batched FBBT + LP
-relaxation on 1 MI355X").  One STEP processes one batch of open nodes per
-GPU through the whole hot path, device resident:
+relaxation on 1 MI355X").  Config 2's instance is tls4.nl itself as a MINLP:
+its outer-approximation LP (minotaur_amd/instances/tls4_oa.npz: the four
+convex sqrt rows as tangent rows, the 60 linear rows).  One STEP is one round
+of the batched tree per GPU, device resident (mgpu_bnb_round):
 
+  select       pop the top B open nodes of the HBM node stack (TreeManager)
   K1 FBBT      LinearHandler::presolveNode      (LinearHandler.cpp:1592-1653)
-  K3 LP        OsiLPEngine::solve, warm basis   (OsiLPEngine.cpp:571-652)
-  decision     PCBProcessor::shouldPrune_ + IntVarHandler::isFeasible
-  incumbent    all-reduce MIN over ranks        (MpiBranchAndBound.cpp:387-389)
+  K3P LP       OsiLPEngine::solve, root basis   (OsiLPEngine.cpp:571-652)
+  decision     PCBProcessor::shouldPrune_ + IntVarHandler::isFeasible +
+               MaxVioBrancher's choice
+  branch       IntVarHandler::getBranches: both children written to the stack
+  incumbent    one packed all-reduce (MIN incumbent, open counts) over ranks
+               (MpiBranchAndBound.cpp:387-389)
 
 Nodes pruned by FBBT are not LP-solved (as in PCBProcessor::process), so
-relaxations/s <= nodes/s.  Node boxes are synthetic: seeded random branching
-from the tls4-lin root, a different seed per rank (weak scaling,
-node-sharded, no data-path collective besides the incumbent all-reduce).
+relaxations/s <= nodes/s.  The stack starts as the root plus B synthetic
+boxes (seeded random branching from the root), a different seed
+per rank (weak scaling, node-sharded); later rounds pop their descendants.
+Supplementary objects: the round-1/2 fixed batch (tls4-lin), complete trees
+from the root, configs 3/4/5, the glob batch.
 
 Run: python bench.py [--gpus N --steps K --warmup W --batch B]
      (N>1 through torch.distributed.run; one process per GPU over RCCL).
@@ -52,10 +60,11 @@ def lp_flops(p, pivots, solves):
     return pivots * per_pivot + solves * per_solve
 
 
-def pmc_traffic(kernel, batch):
+def pmc_traffic(kernel, batch, tree=False):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3
-    FETCH_SIZE/WRITE_SIZE passes of this same bench at the same batch)."""
+    FETCH_SIZE/WRITE_SIZE passes of this same bench at the same batch; tree:
+    summaries of the tree-round headline, marked "workload": "tree_rounds")."""
     import glob
     keys = {'fbbt': ('fbbt_linear_persist', 'fbbt_linear_kernel'), 'lp_dual': ('lp_dual_kernel',),
             'lp_pfi': ('lp_pfi_kernel',)}[kernel]
@@ -63,6 +72,8 @@ def pmc_traffic(kernel, batch):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
+            continue
+        if (d.get("workload") == "tree_rounds") != tree:
             continue
         args = d.get("bench_args", "").split()
         b = int(args[args.index('--batch') + 1]) if '--batch' in args else 65536
@@ -203,12 +214,17 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0):
     return inc, c[0], c[1], c[2], c[3], rounds, float(el.item()), mine['moved'], c[4], c[5]
 
 
-# Complete trees in the bench line: config 2's own instance,
-# config 1's OA-LP, and a weak-bound MILP whose tree is large enough to time
-# the driver's throughput (multi-dimensional knapsack n = 60, m = 8).
+# Complete trees in the bench line: config 2's instance as a
+# MINLP (tls4's OA-LP: 10^5-node MaxVio trees, OA-MILP optimum 3.2 = HiGHS),
+# its linear rows alone (tls4-lin, trivial: LP bound = optimum 0), config 1's
+# OA-LP, and a weak-bound MILP whose tree is large enough to time the
+# driver's throughput (multi-dimensional knapsack n = 60, m = 8).
 # (name, kind, order, warm, optimum, brancher): brancher 1 = the reference's
 # default ReliabilityBrancher (strong-branching LPs count as relaxations).
-TREES = [("tls4_lin", "instance", 1, 0, 0.0, 0),
+TREES = [("tls4_oa", "instance", 0, 0, 3.2, 0),
+         ("tls4_oa", "instance", 1, 0, 3.2, 0),
+         ("tls4_oa", "instance", 1, 1, 3.2, 0),
+         ("tls4_oa", "instance", 1, 0, 3.2, 1),
          ("tls4_lin", "instance", 1, 0, 0.0, 1),
          ("nvs08_oa", "instance", 1, 0, None, 0),
          ("mkp-1-n60-m8", "mkp", 0, 0, -1915.0, 0),
@@ -500,6 +516,176 @@ def qp_relaxation(ctx, dev, rank, world, args, B=1024, reps=3):
     return out
 
 
+def lp_flops_tableau(p, pivots):
+    """SURVEY 8(d)'s LP flop count: the tableau rank-1 update, 2 m (n + m)
+    per pivot (tls4: 19.8 kflop per pivot)."""
+    return pivots * 2.0 * p.m * (p.n + p.m)
+
+
+def kernel_entries(p, nb, fbbt_ms, lp_main_ms, lp_ms, lp_tail_ms, lps, lp_pivots, pfi_pivots):
+    """Per-launch roofline entries of K1 and K3P (algorithmic bytes / flops of
+    one launch over its HIP-event time).  K3P's work: the pivots it ran itself
+    (an LP that overflows its eta file runs its first pfi_cap pivots in K3P,
+    the rest in the dense continuation, timed apart as overflow_resolve_ms)."""
+    fb = fbbt_bytes(p, nb)
+    tab = lp_flops_tableau(p, pfi_pivots)
+    rev = lp_flops(p, pfi_pivots, lps)
+    k = {
+        "fbbt": {"ms": fbbt_ms, "bound": "hbm", "achieved": fb / (fbbt_ms * 1e-3) / 1e9,
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "bytes_per_launch": fb,
+                 "nodes_per_launch": nb},
+        "lp_pfi": {"ms": lp_main_ms, "bound": "fp64", "unit": "TFLOP/s",
+                   "achieved": tab / (lp_main_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                   "flops_per_launch": tab,
+                   "flop_count": "SURVEY 8(d): 2 m (n + m) per pivot",
+                   "revised_flops_per_launch": rev,
+                   "revised_achieved": rev / (lp_main_ms * 1e-3) / 1e12,
+                   "revised_flop_count": "per pivot 2m^2 + 2 nnz + 2 m nnz / n, per solve "
+                                         "2m^2 + 2 nnz (explicit-inverse revised simplex)",
+                   "solves_per_launch": lps, "pivots_in_launch": pfi_pivots,
+                   "pivots_per_solve": lp_pivots / max(lps, 1),
+                   "lp_call_ms": lp_ms, "overflow_resolve_ms": lp_tail_ms},
+    }
+    for e in k.values():
+        e["frac"] = e["achieved"] / e["peak"]
+    k["lp_pfi"]["revised_frac"] = k["lp_pfi"]["revised_achieved"] / FP64_PEAK_TFLOPS
+    return k
+
+
+def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
+    """The headline: rounds of the batched tree (mgpu_bnb_round) over an HBM
+    node stack that starts as the root plus the B seeded boxes; every step is
+    ONE round (pop B nodes, K1, K3P, decide + MaxVio choice, children pushed)
+    and one packed all-reduce of the incumbent and open counts.  Returns the
+    aggregate counts (summed over ranks), the max elapsed time and rank 0's
+    per-launch kernel entries."""
+    import torch
+    from minotaur_amd import dist as mdist
+    B = LB.shape[0]
+    ctx.load(p)
+    cap = B * (max(1, args.warmup) + args.steps + 2) + 2
+    ctx.bnb_config(0, 0)
+    ctx.bnb_brancher(0)
+    ctx.bnb_init(cap)
+    ctx.bnb_import(LB, UB, np.full(B, -math.inf), np.zeros(B, dtype=np.int32))
+    comm = mdist.Comm(rank, world, dev)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    state = {"inc": math.inf, "prev": None}
+    keys = ("nodes", "lps", "pivots", "pfi_pivots")
+
+    def step(acc):
+        st = ctx.bnb_round(B, state["inc"])
+        ev[0].record()
+        inc, most, _ = comm.round_reduce(st.incumbent, st.open)
+        ev[1].record()
+        ev[1].synchronize()
+        state["inc"] = min(state["inc"], inc)
+        cur = {k: getattr(st, k) for k in keys}
+        if acc is not None:
+            prev = state["prev"]
+            for k in keys:
+                acc[k] += cur[k] - prev[k]
+            acc["fbbt_ms"].append(ctx.last_kernel_ms('fbbt'))
+            acc["lp_ms"].append(ctx.last_kernel_ms('lp'))
+            acc["lp_main_ms"].append(ctx.last_kernel_ms('lp_main'))
+            acc["lp_tail_ms"].append(ctx.last_kernel_ms('lp_tail'))
+            acc["batch"].append(st.last_batch)
+            acc["rccl_ms"].append(ev[0].elapsed_time(ev[1]))
+            acc["open"] = st.open
+        state["prev"] = cur
+        return most
+
+    for _ in range(max(1, args.warmup)):
+        step(None)
+    acc = {k: 0 for k in keys}
+    acc.update({"fbbt_ms": [], "lp_ms": [], "lp_main_ms": [], "lp_tail_ms": [], "batch": [],
+                "rccl_ms": [], "open": 0})
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(acc)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    tot = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    cnt = torch.tensor([float(acc[k]) for k in keys], dtype=torch.float64, device=dev)
+    mdist.allreduce_max(tot)
+    mdist.allreduce_sum(cnt)
+    nodes, lps, pivots, pfi_pivots = (float(v) for v in cnt.tolist())
+    S = args.steps
+    nb = float(np.mean(acc["batch"]))
+    kernels = kernel_entries(p, nb, float(np.mean(acc["fbbt_ms"])),
+                             float(np.mean(acc["lp_main_ms"])), float(np.mean(acc["lp_ms"])),
+                             float(np.mean(acc["lp_tail_ms"])), acc["lps"] / S,
+                             acc["pivots"] / S, acc["pfi_pivots"] / S)
+    summary = {"nodes": nodes, "lp_solves": lps, "pivots_per_lp": pivots / max(lps, 1.0),
+               "nodes_per_round_per_gpu": nb, "open_after_rank0": acc["open"],
+               "search": "depth-first over batches (HBM stack), MaxVio branching, root-basis "
+                         "warm start (K3P)",
+               "incumbent": state["inc"]}
+    return {"elapsed": float(tot.item()), "nodes": nodes, "lps": lps, "kernels": kernels,
+            "summary": summary, "incumbent": state["inc"],
+            "rccl_ms": float(np.sum(acc["rccl_ms"]))}
+
+
+def fixed_batch(ctx, dev, rank, world, args, reps=10):
+    """Supplementary (round 1-2 headline, kept for continuity): one FIXED
+    batch of tls4-lin node boxes re-evaluated every step — K1 FBBT -> K3P LP
+    from the root basis -> prune/integrality decision — with no branching,
+    no selection and no child writes (the kernel-only throughput of the node
+    pipeline)."""
+    import torch
+    from minotaur_amd import dist as mdist
+    from minotaur_amd.problem import LinProblem, random_boxes
+    from minotaur_amd.runtime import WarmStart
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_lin.npz'))
+    B = args.batch
+    LB, UB = random_boxes(p, B, mdist.shard_seed(20261015, rank))
+    ctx.load(p)
+    root, ws_h = ctx.root_solve()
+    assert root.status[0] == 0, "root LP not optimal"
+    ws = WarmStart(*(torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                     for a in (ws_h.head, ws_h.st, ws_h.d, ws_h.binv)))
+    lb0, ub0 = torch.from_numpy(LB).to(dev), torch.from_numpy(UB).to(dev)
+    lb1, ub1 = torch.empty_like(lb0), torch.empty_like(ub0)
+    z32 = lambda: torch.zeros(B, dtype=torch.int32, device=dev)   # noqa: E731
+    infeas, nmods, status, iters, decision = z32(), z32(), z32(), z32(), z32()
+    obj = torch.zeros(B, dtype=torch.float64, device=dev)
+    cand = torch.zeros(B, dtype=torch.float64, device=dev)
+    x = torch.zeros((B, p.n), dtype=torch.float64, device=dev)
+    cap = ctx.oracle_pfi()
+
+    def step():
+        ctx.fbbt_dev(lb0, ub0, lb1, ub1, infeas, nmods)
+        ctx.lp_solve_dev(lb1, ub1, status, obj, iters, ws=ws, skip=infeas, x=x)
+        ctx.node_decide_dev(status, obj, x, decision, fbbt_infeas=infeas, cand_obj=cand)
+
+    step()
+    torch.cuda.synchronize()
+    fb, lp, lpm, lpt = [], [], [], []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+        fb.append(ctx.last_kernel_ms('fbbt'))
+        lp.append(ctx.last_kernel_ms('lp'))
+        lpm.append(ctx.last_kernel_ms('lp_main'))
+        lpt.append(ctx.last_kernel_ms('lp_tail'))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    solved = float((status != 12).sum().item())
+    piv = float(iters.sum().item())
+    pfi_piv = float(torch.where(status != 12, torch.clamp(iters, max=cap), 0).sum().item())
+    k = kernel_entries(p, B, float(np.mean(fb)), float(np.mean(lpm)), float(np.mean(lp)),
+                       float(np.mean(lpt)), solved, piv, pfi_piv)
+    return {"instance": f"tls4-lin ({p.m} rows, {p.n} cols, {p.nnz} nnz)",
+            "nodes_per_gpu": B, "reps": reps, "nodes_per_s": B * reps * world / el,
+            "relaxations_per_s": solved * reps * world / el, "ms_per_batch": 1e3 * el / reps,
+            "kernels": k}
+
+
 def progress(rank, msg):
     """One line per phase on stderr (the JSON line stays alone on stdout)."""
     if rank == 0:
@@ -527,6 +713,8 @@ def main():
                     help='skip the supplementary QP relaxation batch (color_lab2, MFMA KKT)')
     ap.add_argument('--no-glob', action='store_true',
                     help='skip the supplementary glob batch (QCQP: K2 -> per-node rows LP)')
+    ap.add_argument('--no-fixed', action='store_true',
+                    help='skip the supplementary fixed batch (K1 + K3P on tls4-lin boxes)')
     ap.add_argument('--no-knapsack', action='store_true',
                     help='skip the supplementary config-3 batch (1000 knapsack nodes)')
     args = ap.parse_args()
@@ -535,7 +723,7 @@ def main():
     import torch.distributed as dist
     from minotaur_amd import dist as mdist
     from minotaur_amd.problem import LinProblem, random_boxes
-    from minotaur_amd.runtime import Context, WarmStart
+    from minotaur_amd.runtime import Context
 
     rank, world, local = mdist.env_ranks()
     # MGPU_BENCH_REHEARSAL=1 (test hook): every rank on device 0 over gloo, to
@@ -551,93 +739,23 @@ def main():
         else:
             dist.init_process_group('nccl', device_id=dev)
 
-    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_lin.npz'))
-    B = args.batch
-    LB, UB = random_boxes(p, B, mdist.shard_seed(20261015, rank))
-
     ctx = Context(local)
-    ctx.load(p)
-    root, ws_h = ctx.root_solve()
-    assert root.status[0] == 0, "root LP not optimal"
     # one dedicated stream for the engine AND the torch glue (the legacy null
     # stream would not order against the engine's non-blocking stream)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    ws = WarmStart(*(torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-                     for a in (ws_h.head, ws_h.st, ws_h.d, ws_h.binv)))
 
-    lb0 = torch.from_numpy(LB).to(dev)
-    ub0 = torch.from_numpy(UB).to(dev)
-    lb1 = torch.empty_like(lb0)
-    ub1 = torch.empty_like(ub0)
-    infeas = torch.zeros(B, dtype=torch.int32, device=dev)
-    nmods = torch.zeros(B, dtype=torch.int32, device=dev)
-    status = torch.zeros(B, dtype=torch.int32, device=dev)
-    obj = torch.zeros(B, dtype=torch.float64, device=dev)
-    iters = torch.zeros(B, dtype=torch.int32, device=dev)
-    x = torch.zeros((B, p.n), dtype=torch.float64, device=dev)
-    decision = torch.zeros(B, dtype=torch.int32, device=dev)
-    cand = torch.zeros(B, dtype=torch.float64, device=dev)
-    torch.cuda.synchronize()
-
-    state = {"incumbent": math.inf}
-
-    def step(acc):
-        inc = state["incumbent"]
-        ctx.fbbt_dev(lb0, ub0, lb1, ub1, infeas, nmods, inc)
-        ctx.lp_solve_dev(lb1, ub1, status, obj, iters, ws=ws, skip=infeas, x=x)
-        ctx.node_decide_dev(status, obj, x, decision, inc, fbbt_infeas=infeas, cand_obj=cand)
-        cmin = cand.min().reshape(1)
-        acc["ev"][0].record()
-        best = mdist.allreduce_incumbent(cmin)
-        acc["ev"][1].record()
-        acc["solved"] += (status != 12).sum()
-        acc["pivots"] += iters.sum()
-        # LPs finished by K3P itself (the rest went to its dense overflow re-solve)
-        mine = (status != 12) & (iters <= PFI_CAP)
-        acc["pfi_solved"] += mine.sum()
-        acc["pfi_pivots"] += torch.where(mine, iters, 0).sum()
-        b = float(best.item())          # one host sync per step
-        state["incumbent"] = min(inc, b)
-        acc["fbbt_ms"].append(ctx.last_kernel_ms('fbbt'))
-        acc["lp_ms"].append(ctx.last_kernel_ms('lp'))
-        acc["lp_main_ms"].append(ctx.last_kernel_ms('lp_main'))
-        acc["lp_tail_ms"].append(ctx.last_kernel_ms('lp_tail'))
-        acc["rccl_ms"].append(acc["ev"][0].elapsed_time(acc["ev"][1]))
-
-    def new_acc():
-        return {"solved": torch.zeros((), dtype=torch.int64, device=dev),
-                "pivots": torch.zeros((), dtype=torch.int64, device=dev),
-                "pfi_solved": torch.zeros((), dtype=torch.int64, device=dev),
-                "pfi_pivots": torch.zeros((), dtype=torch.int64, device=dev),
-                "fbbt_ms": [], "lp_ms": [], "lp_main_ms": [], "lp_tail_ms": [], "rccl_ms": [],
-                "ev": (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))}
-
-    # warm-up runs the exact timed step (also loads torch's lazily-loaded
-    # reduction kernels, which otherwise land in the first timed step)
-    for _ in range(max(1, args.warmup)):
-        step(new_acc())
-    acc = new_acc()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(acc)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    tot = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    cnt = torch.stack([acc["solved"].double(), acc["pivots"].double(),
-                       acc["pfi_solved"].double(), acc["pfi_pivots"].double()])
-    mdist.allreduce_max(tot)
-    mdist.allreduce_sum(cnt)
-    elapsed = float(tot.item())
-    solved, pivots, pfi_solved, pfi_pivots = (float(v) for v in cnt.tolist())
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
+    B = args.batch
+    LB, UB = random_boxes(p, B, mdist.shard_seed(20261017, rank))
+    h = tree_rounds(ctx, dev, rank, world, p, LB, UB, args)
+    elapsed, nodes, lps = h["elapsed"], h["nodes"], h["lps"]
+    progress(rank, f"headline done: {1e3 * elapsed / args.steps:.2f} ms/step, "
+                   f"{nodes / elapsed / 1e6:.2f} M nodes/s")
     TB = args.tree_batch
-    progress(rank, f"headline done: {1e3 * elapsed / args.steps:.2f} ms/step")
+    fixed = None if args.no_fixed else fixed_batch(ctx, dev, rank, world, args)
+    progress(rank, "fixed_batch done")
     tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, TB, args)
     progress(rank, "tree_search done")
     cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, TB, args)
@@ -648,52 +766,25 @@ def main():
     progress(rank, "knapsack_nodes done")
     glob = None if args.no_glob else glob_batch(ctx, dev, rank, world, args)
     progress(rank, "glob_batch done")
-    ctx.load(p)
-    nodes = float(B) * world * args.steps
-    fbbt_ms = float(np.mean(acc["fbbt_ms"]))
-    lp_ms = float(np.mean(acc["lp_ms"]))
-    lp_main_ms = float(np.mean(acc["lp_main_ms"]))
-    lp_tail_ms = float(np.mean(acc["lp_tail_ms"]))
-    lp_kernel = "lp_pfi" if lp_tail_ms > 0.0 else "lp_dual"
 
     if rank == 0:
-        # per-launch algorithmic work of rank 0's kernels
-        solved_r0 = solved / world / args.steps
-        pivots_r0 = pivots / world / args.steps
-        fb = fbbt_bytes(p, B)
-        if lp_kernel == "lp_pfi":   # K3P's own LPs; its overflow list goes to K3 (tail)
-            lp_solves, lp_pivots = pfi_solved / world / args.steps, pfi_pivots / world / args.steps
-        else:
-            lp_solves, lp_pivots = solved_r0, pivots_r0
-        lpf = lp_flops(p, lp_pivots, lp_solves)
-        kernels = {
-            "fbbt": {"ms": fbbt_ms, "bound": "hbm", "achieved": fb / (fbbt_ms * 1e-3) / 1e9,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "bytes_per_launch": fb},
-            lp_kernel: {"ms": lp_main_ms, "bound": "fp64", "unit": "TFLOP/s",
-                        "achieved": lpf / (lp_main_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
-                        "flops_per_launch": lpf, "solves_per_launch": lp_solves,
-                        "pivots_per_solve": lp_pivots / max(lp_solves, 1),
-                        "lp_call_ms": lp_ms, "overflow_resolve_ms": lp_tail_ms,
-                        "overflow_lps_per_launch": solved_r0 - lp_solves},
-        }
-        for k in kernels.values():
-            k["frac"] = k["achieved"] / k["peak"]
-        dom = lp_kernel if lp_main_ms >= fbbt_ms else "fbbt"
+        kernels = h["kernels"]
+        dom = max(("fbbt", "lp_pfi"), key=lambda k: kernels[k]["ms"])
         kd = kernels[dom]
-        traffic, tsrc = pmc_traffic(dom, B)
+        traffic, tsrc = pmc_traffic(dom, B, tree=True)
         roofline = {"kernel": dom, "bound": "hbm" if dom == "fbbt" else "fp64",
                     "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
                     "frac": kd["frac"], "traffic": traffic}
         if tsrc:
             roofline["traffic_source"] = f"profiles/{tsrc} (PMC, bytes per launch)"
         if dom != "fbbt":
-            roofline["note"] = ("FP64 VALU kernel (no MFMA: per-node pivots); achieved = the "
-                                "dual simplex's algorithmic flops (DESIGN.md §5) / kernel time; "
-                                "peak = MI355X FP64 dense rate 78.6 TF/s")
+            roofline["note"] = ("FP64 VALU kernel (no MFMA: per-node pivots); achieved = "
+                                "SURVEY 8(d)'s tableau flops 2m(n+m) per pivot over the pivots "
+                                "K3P ran itself / its HIP-event time; the revised-simplex count "
+                                "is kernels.lp_pfi.revised_*; peak = MI355X FP64 dense 78.6 TF/s")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(p, LB, UB, args.cpu_seconds)
+            cpu = cpu_baseline(p, LB, UB, args.cpu_seconds, "tls4-oa")
         line = {
             "metric": "B&B nodes/sec + relaxations solved/sec at 1/2/4/8 MI355X",
             "value": nodes / elapsed,
@@ -708,27 +799,33 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": ("fixed-batch node throughput: one batch of tls4-lin B&B nodes per "
-                             "GPU re-evaluated every step (K1 FBBT -> K3P dual-simplex LP from "
-                             "the root basis, FBBT-infeasible nodes skipped -> prune/"
-                             "integrality decision; incumbent all-reduce MIN); no branching "
-                             "inside the timed region: complete trees are in tree_search"),
-                "instance": f"tls4-lin ({p.m} rows, {p.n} cols, {p.nnz} nnz)",
+                "workload": ("branch-and-bound tree rounds on config 2 (tls4.nl as a MINLP: its "
+                             "outer-approximation LP): every step is one mgpu_bnb_round per GPU "
+                             "- pop the top B open nodes of the HBM node stack, K1 FBBT with the "
+                             "incumbent, K3P dual-simplex LP from the root basis (FBBT-"
+                             "infeasible nodes skipped), prune/integrality decision with the "
+                             "MaxVio branching choice, children written back to the stack - "
+                             "then one packed all-reduce (incumbent MIN, open counts); the pool "
+                             "starts as the root plus B seeded random-branching boxes"),
+                "instance": f"tls4-oa ({p.m} rows, {p.n} cols, {p.nnz} nnz)",
                 "nodes_per_gpu": B,
                 "global_batch": B * world,
-                "node_boxes": "seeded random branching from the root, depth 1-20 (SURVEY 8d)",
+                "node_boxes": "seeded random branching from the root, depth 1-20 (SURVEY 8d), "
+                              "then their descendants",
                 "parallelism": f"node-sharded x{world}",
             },
-            "relaxations_per_s": solved / elapsed,
-            "fbbt_node_passes_per_s": float(B) * world / (fbbt_ms * 1e-3),
+            "relaxations_per_s": lps / elapsed,
+            "fbbt_node_passes_per_s": float(B) * world / (kernels["fbbt"]["ms"] * 1e-3),
+            "tree_rounds": h["summary"],
             "collectives": {"incumbent_syncs": args.steps,
-                            "rccl_ms_total": float(np.sum(acc["rccl_ms"])),
-                            "note": "one all-reduce MIN of the incumbent per step (timed with "
-                                    "events on the engine stream; 0 at one GPU)"},
+                            "rccl_ms_total": h["rccl_ms"],
+                            "note": "one packed all-reduce (incumbent MIN, open max/min) per "
+                                    "round, timed with events on the engine stream"},
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,
-            "incumbent": state["incumbent"],
+            "incumbent": h["incumbent"],
+            "fixed_batch": fixed,
             "tree_search": tree,
             "convex_batch": cvx,
             "qp_relaxation": qprel,

@@ -215,10 +215,13 @@ int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
  * mode (oracle dual_simplex(..., pfi=k)).  For tests/benchmarks. */
 int mgpu_set_lp_variant(mgpu_ctx *ctx, int variant);
 
-/* K3P eta-file cap: a node that needs more pivots is re-solved by K3 from
- * the same warm start.  0 keeps auto mode off K3P; 1..MGPU_LP_PFI_MAX
- * (default MGPU_LP_PFI_MAX). */
-#define MGPU_LP_PFI_MAX 16
+/* K3P eta-file cap: a node that needs more pivots is continued by K3 from
+ * its basis and explicit inverse (one continuation slot per LP of the batch,
+ * up to 24 GB; past that it restarts in K3 from the shared warm start).  The
+ * eta file lives in VGPRs: caps <= 16 run the 16-eta build (4 waves per
+ * SIMD), larger caps the 32-eta build (3 waves per SIMD).  0 keeps auto mode
+ * off K3P; 1..MGPU_LP_PFI_MAX (default MGPU_LP_PFI_MAX). */
+#define MGPU_LP_PFI_MAX 32
 int mgpu_set_lp_pfi(mgpu_ctx *ctx, int kmax);
 
 /* K3PW (64 < m <= 128 rows, two basis rows per lane) eta-file cap: a node
@@ -286,6 +289,9 @@ typedef struct {
   long long sb_pruned;          /* nodes PrunedByBrancher                 */
   long long sb_modified;        /* nodes ModifiedByBrancher (re-queued
                                    with the one-sided bound change)       */
+  long long pfi_pivots;         /* node-LP pivots run by the product-form
+                                   kernel itself (K3P / K3PW: at most its
+                                   eta cap per LP; 0 for dense kernels)   */
 } mgpu_bnb_stats;
 
 /* Search options of the next mgpu_bnb_init (default 0, 0):

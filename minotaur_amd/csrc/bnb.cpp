@@ -85,7 +85,7 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
   HIPCHK(c, s.bup.ensure((size_t)B));
   for (DevBuf *b : {&s.bsum, &s.bidx, &s.boff}) HIPCHK(c, b->ensure(nblk * 4));
   HIPCHK(c, s.bmin.ensure(nblk * 8));
-  HIPCHK(c, s.bcnt.ensure(nblk * 7 * 4));
+  HIPCHK(c, s.bcnt.ensure(nblk * 8 * 4));
   HIPCHK(c, s.out.ensure(sizeof(BnbOut)));
   if (s.rel) {
     for (DevBuf *b : {&s.bpvar, &s.rflag, &s.rrank, &s.nsb, &s.sb_off, &s.dec2, &s.nev,
@@ -144,6 +144,8 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
   r.x = s.x.as<double>();
   r.obj = s.obj.as<double>();
   r.nlb = s.bnlb.as<double>();
+  // node depths: gathered for best-first; the stack's popped slice in place
+  r.depth = bfs ? s.depth_in.as<int32_t>() : s.pdepth.as<int32_t>() + base;
   r.pvar = s.bpvar.as<int32_t>();
   r.pval = s.bpval.as<double>();
   r.pc_up = s.pc_up.as<double>();
@@ -496,6 +498,9 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   }
   io.status = s.st.as<int32_t>();
   io.iters = s.it.as<int32_t>();
+  // the shared-root-basis node LPs ran the product form (K3P / K3PW) when the
+  // context selects it; per-node bases (warm 1, reliability) run K3 / K3L
+  io.pfi_cap = (!s.warm && !s.rel && s.root_ok) ? mgpu_lp_pfi_cap(c) : 0;
   io.cand_obj = s.cand.as<double>();
   io.obj = s.obj.as<double>();
   io.bvar = s.bvar.as<int32_t>();
@@ -561,6 +566,7 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   for (int k = 0; k < 5; ++k) s.tot.ndec[k] += o.ndec[k];
   s.tot.lps += o.lps;
   s.tot.pivots += o.pivots;
+  s.tot.pfi_pivots += o.pfi_pivots;
   s.tot.open = s.count;
   s.tot.incumbent = s.inc;
   s.tot.last_batch = nb;

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
   __shared__ int s_pos[kScanBlock];
   __shared__ double s_min[kScanBlock];
   __shared__ int s_idx[kScanBlock];
-  __shared__ int s_cnt[kScanBlock][7];   // decisions 0..4, LPs, pivots
+  __shared__ int s_cnt[kScanBlock][8];   // decisions 0..4, LPs, pivots, K3P pivots
   const int t = threadIdx.x;
   const int i = blockIdx.x * kScanBlock + t;
   const bool live = i < io.nb;
@@ -48,6 +48,9 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
   const bool lp = live && io.status[i] != 12;
   s_cnt[t][5] = lp ? 1 : 0;
   s_cnt[t][6] = lp ? io.iters[i] : 0;
+  // pivots the product-form kernel ran itself (an overflowing LP's first
+  // pfi_cap pivots; the rest ran in the dense continuation)
+  s_cnt[t][7] = lp ? min(io.iters[i], io.pfi_cap) : 0;
   __syncthreads();
   // Hillis-Steele inclusive scan of the flags
   for (int o = 1; o < kScanBlock; o <<= 1) {
@@ -66,7 +69,7 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
         s_min[t] = b;
         s_idx[t] = ib;
       }
-      for (int k = 0; k < 7; ++k) s_cnt[t][k] += s_cnt[t + o][k];
+      for (int k = 0; k < 8; ++k) s_cnt[t][k] += s_cnt[t + o][k];
     }
     __syncthreads();
   }
@@ -74,7 +77,7 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
     io.bsum[blockIdx.x] = s_pos[kScanBlock - 1];
     io.bmin[blockIdx.x] = s_min[0];
     io.bidx[blockIdx.x] = s_idx[0];
-    for (int k = 0; k < 7; ++k) io.bcnt[blockIdx.x * 7 + k] = s_cnt[0][k];
+    for (int k = 0; k < 8; ++k) io.bcnt[blockIdx.x * 8 + k] = s_cnt[0][k];
   }
 }
 
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
   if (t == 0) s_carry = 0;
   double my_min = INFINITY;
   int my_idx = INT_MAX;
-  long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+  long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int c0 = 0; c0 < nblk; c0 += 1024) {
     const int b = c0 + t;
     const int v = b < nblk ? io.bsum[b] : 0;
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
         my_min = m;
         my_idx = ix;
       }
-      for (int k = 0; k < 7; ++k) cnt[k] += io.bcnt[b * 7 + k];
+      for (int k = 0; k < 8; ++k) cnt[k] += io.bcnt[b * 8 + k];
     }
     s[t] = v;
     __syncthreads();
@@ -137,6 +140,8 @@ __global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
                         (unsigned long long)cnt[5]);
   if (cnt[6]) atomicAdd(reinterpret_cast<unsigned long long *>(&io.out->pivots),
                         (unsigned long long)cnt[6]);
+  if (cnt[7]) atomicAdd(reinterpret_cast<unsigned long long *>(&io.out->pfi_pivots),
+                        (unsigned long long)cnt[7]);
   if (t == 0) {
     io.out->nchild = s_carry;
     io.out->best = s_min[0];

@@ -8,6 +8,7 @@ namespace mgpu {
 struct BnbOut {                 // per round, device -> host
   long long ndec[5];            // decision counts (mgpu.h decision codes)
   long long lps, pivots;        // LPs solved (not pruned by FBBT) and their pivots
+  long long pfi_pivots;         // of those, run by the product-form kernel (<= pfi_cap per LP)
   int nchild;                   // children written (2 per decision 0, 1 per decision 5)
   int best_idx;                 // batch index of the best integer-feasible node, -1 none
   double best;                  // its objective (+inf none)
@@ -37,6 +38,7 @@ struct BnbIO {
   double *ppval;                //   and its value (reliability branching's pseudocosts)
   const int32_t *status;        // [nb] LP status (12 = not solved: FBBT-infeasible)
   const int32_t *iters;         // [nb] LP pivots
+  int pfi_cap;                  // product-form eta cap of the round's LP call (0: dense)
   const double *cand_obj;       // [nb]
   const double *obj;            // [nb] relaxation values (children's bound)
   const int32_t *bvar;          // [nb]
@@ -50,7 +52,7 @@ struct BnbIO {
   int32_t *pos;                 // [nb] in-block exclusive prefix
   int32_t *bsum, *bidx, *boff;  // [nblk]
   double *bmin;                 // [nblk]
-  int32_t *bcnt;                // [nblk][5]
+  int32_t *bcnt;                // [nblk][8]
   BnbOut *out;
 };
 
@@ -79,6 +81,7 @@ constexpr int kRelIterLimit = 25;
 constexpr int kRelThresh = 4;
 constexpr int kRelMinDist = 50;
 constexpr double kRelETol = 1e-6;
+constexpr int kRelMaxDepth = 1000;   // maxDepth_: deeper nodes are not strong-branched (:105)
 constexpr int kRelEvents = 1 + 2 * kRelMaxCands;   // pseudocost observations per node
 struct RelIO {
   int nb, n;
@@ -86,6 +89,7 @@ struct RelIO {
   const int32_t *decision;      // [nb] node_decide's decisions
   const double *x, *obj;        // [nb][n], [nb] node LP solution
   const double *nlb;            // [nb] node bound (the parent's LP value)
+  const int32_t *depth;         // [nb] node depth (Node::getDepth)
   const int32_t *pvar;          // [nb] parent's branching variable (-1: none)
   const double *pval;           // [nb] its value in the parent's LP solution
   double *pc_up, *pc_dn;        // [n] pseudocosts (pseudoUp_ / pseudoDown_)

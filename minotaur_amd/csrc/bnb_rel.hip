@@ -149,10 +149,12 @@ __global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
     const bool own = after_solve_obs(io, b, ov, os, oc);
     const long long calls = calls_of(io, b);
     // the first kRelMaxCands unreliable candidates in (score, index) order:
-    // repeated selection of the next larger key
+    // repeated selection of the next larger key; none below maxDepth_
+    // (findBestCandidate_: maxcnt = depth > maxDepth_ ? 0 : maxStrongCands_)
+    const int maxcnt = io.depth[b] > kRelMaxDepth ? 0 : kRelMaxCands;
     double ps = -INFINITY;
     int pj = -1;
-    for (int k = 0; k < kRelMaxCands; ++k) {
+    for (int k = 0; k < maxcnt; ++k) {
       double bs = INFINITY;
       int bj = INT_MAX;
       for (int j = 0; j < io.n; ++j) {

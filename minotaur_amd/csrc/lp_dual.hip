@@ -461,10 +461,14 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         else if (zB > ubB + kPTol) inf = zB - ubB;
       }
       double best = fabs(inf);
-      const int r = wave_argmax_lane(best);  // used only when best > 0
+      int r = wave_argmax_lane(best);  // used only when best > 0
       // keep the (wave-uniform) result in a VGPR: as an SGPR value it lets
       // LLVM re-schedule the pivot around it at +100 VGPRs
       asm volatile("" : "+v"(best));
+      // anti-cycling (oracle STALL_PIVOTS): past kStallPivots pivots of the
+      // solve, Bland's rule: the infeasible row with the lowest basic column,
+      // and below the exact minimum ratio with the lowest column on ties
+      const bool bland = iters + io.iter_base >= kStallPivots;
       if (best == 0.0) {
         if (!fresh) {
           zB = compute_primals(C, binv);
@@ -494,6 +498,12 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       if (iters >= io.iter_limit) {
         status = 6;
         break;
+      }
+      if (bland) {
+        double key = (lane < m && inf != 0.0) ? -(double)h : -INFINITY;
+        int rr = lane;
+        wave_argmax_idx(key, rr);
+        r = rr;
       }
       const double delta = rld(inf, r);
       STAMP(1);
@@ -561,16 +571,29 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       // ---- Harris pass 2: largest |alpha| among ratios <= tmax ----
       double qa = 0.0;
       int q = INT_MAX;
-      for (int j = lane; j < N; j += 64) {
-        if (C.t2[j] <= tmax) {
-          const double fa = fabs(C.al[j]);
-          if (fa > qa) {
-            qa = fa;
+      if (!bland) {
+        for (int j = lane; j < N; j += 64) {
+          if (C.t2[j] <= tmax) {
+            const double fa = fabs(C.al[j]);
+            if (fa > qa) {
+              qa = fa;
+              q = j;
+            }
+          }
+        }
+        wave_argmax_idx(qa, q);
+      } else {
+        double key = -INFINITY;
+        for (int j = lane; j < N; j += 64) {
+          const double t2 = C.t2[j];
+          if (t2 != INFINITY && -t2 > key) {
+            key = -t2;
             q = j;
           }
         }
+        wave_argmax_idx(key, q);
+        qa = q != INT_MAX ? fabs(C.al[q]) : 0.0;
       }
-      wave_argmax_idx(qa, q);
       if (qa == 0.0) {
         status = 2;
         break;

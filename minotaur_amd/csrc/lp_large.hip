@@ -368,8 +368,11 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
     int status = kUnknownStatus, iters = 0;
     bool fresh = true;
     for (;;) {
-      // ---- pricing: most infeasible basic row, lowest row on ties ----
-      double best = 0.0;
+      // ---- pricing: most infeasible basic row, lowest row on ties; past
+      // kStallPivots pivots (oracle STALL_PIVOTS) Bland's rule: the
+      // infeasible row with the lowest basic column ----
+      const bool bland = iters + io.iter_base >= kStallPivots;
+      double best = 0.0, key = -INFINITY;
       int r = INT_MAX;
       for (int i = tid; i < m; i += kT) {
         const int h = s.head[i];
@@ -377,12 +380,22 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
         double inf = 0.0;
         if (v < s.blo[h] - kPTol) inf = v - s.blo[h];
         else if (v > s.bhi[h] + kPTol) inf = v - s.bhi[h];
-        if (fabs(inf) > best) {
+        if (bland) {
+          if (inf != 0.0 && -(double)h > key) {
+            key = -(double)h;
+            r = i;
+          }
+        } else if (fabs(inf) > best) {
           best = fabs(inf);
           r = i;
         }
       }
-      blk_argmax(best, r, s);
+      if (bland) {
+        blk_argmax(key, r, s);
+        best = key == -INFINITY ? 0.0 : 1.0;   // only "some row is infeasible" is used
+      } else {
+        blk_argmax(best, r, s);
+      }
       if (best == 0.0) {
         if (!fresh) {
           compute_primals(s);
@@ -466,16 +479,29 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
       // ---- Harris pass 2: largest |alpha| among ratios <= tmax ----
       double qa = 0.0;
       int q = INT_MAX;
-      for (int j = tid; j < N; j += kT) {
-        if (s.t2[j] <= tmax) {
-          const double fa = fabs(s.al[j]);
-          if (fa > qa) {
-            qa = fa;
+      if (!bland) {
+        for (int j = tid; j < N; j += kT) {
+          if (s.t2[j] <= tmax) {
+            const double fa = fabs(s.al[j]);
+            if (fa > qa) {
+              qa = fa;
+              q = j;
+            }
+          }
+        }
+        blk_argmax(qa, q, s);
+      } else {  // Bland: the exact minimum ratio, lowest column on ties
+        double key = -INFINITY;
+        for (int j = tid; j < N; j += kT) {
+          const double t2 = s.t2[j];
+          if (t2 != INFINITY && -t2 > key) {
+            key = -t2;
             q = j;
           }
         }
+        blk_argmax(key, q, s);
+        qa = q != INT_MAX ? fabs(s.al[q]) : 0.0;
       }
-      blk_argmax(qa, q, s);
       if (qa == 0.0) {
         status = 2;
         break;

@@ -69,12 +69,14 @@ constexpr double kPivTol = 1e-9;
 constexpr double kArt0 = 1e7;
 constexpr double kInfB = 1e30;
 constexpr int kUnknownStatus = 12;
-// waves per workgroup (one workgroup per CU): 16 = 4 per SIMD (<= 128 VGPRs)
-// up to 3 column slots; the 4-slot build keeps 12 (3 per SIMD) rather than
-// spilling.  A/B on tls4-lin (S = 3): 12 waves with a 24-eta file 2.12 ms,
-// 16 waves with a 16-eta file 1.75 ms + a longer overflow tail (0.16 ms).
-template <int S>
-constexpr int waves_for() { return S <= 3 ? 16 : 12; }
+// waves per workgroup (one workgroup per CU): with a 16-eta file 16 = 4 per
+// SIMD (<= 128 VGPRs) up to 3 column slots; the 4-slot build keeps 12 (3 per
+// SIMD) rather than spilling.  The 32-eta file (deep tree nodes are 15-20
+// pivots from the root basis) costs 32 more VGPRs: 12 waves (3 per SIMD).
+// A/B on tls4-lin (S = 3): 12 waves with a 24-eta file 2.12 ms, 16 waves
+// with a 16-eta file 1.75 ms + a longer overflow tail (0.16 ms).
+template <int S, int K>
+constexpr int waves_for() { return (S <= 3 && K <= 16) ? 16 : 12; }
 __host__ __device__ inline int slots_for(int N) { return (N + 63) / 64; }
 
 // packed column status: bits 0-1 status, 2-3 artificial-bound flags, 4 fixed
@@ -82,6 +84,7 @@ enum : int { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
 constexpr int kArtLo = 4, kArtHi = 8, kFixed = 16;
 
 static_assert(kPfiMax < 64, "K3P never reaches K3's 64-pivot primal refresh");
+constexpr int kPfiSmall = 16;   // the 16-eta build (4 waves per SIMD)
 
 __host__ __device__ constexpr size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
 
@@ -145,10 +148,11 @@ struct Prob {
 
 // v <- E_{k-1} ... E_0 v (oracle pfi_apply_etas); lanes >= m hold eta 0;
 // the pivot row of eta t is lane t of prow
-__device__ __forceinline__ double apply_etas(double v, const double (&eta)[kPfiMax], int prow,
+template <int K>
+__device__ __forceinline__ double apply_etas(double v, const double (&eta)[K], int prow,
                                              int k, int lane) {
 #pragma unroll
-  for (int t = 0; t < kPfiMax; ++t) {
+  for (int t = 0; t < K; ++t) {
     if (t < k) {
       const int p = rl(prow, t);
       const double vp = rld(v, p);
@@ -158,9 +162,10 @@ __device__ __forceinline__ double apply_etas(double v, const double (&eta)[kPfiM
   return v;
 }
 
-template <int S>
-__global__ __launch_bounds__(64 * waves_for<S>()) void lp_pfi_kernel(DevLP lp, LpIO io, PfiIO px) {
-  constexpr int kWaves = waves_for<S>();
+template <int S, int K>
+__global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP lp, LpIO io,
+                                                                       PfiIO px) {
+  constexpr int kWaves = waves_for<S, K>();
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz, ld = m + 1;
   const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -351,9 +356,9 @@ __global__ __launch_bounds__(64 * waves_for<S>()) void lp_pfi_kernel(DevLP lp, L
       sa[s] = st | art | (lo_j == hi_j ? kFixed : 0);
     }
 
-    double eta[kPfiMax];
+    double eta[K];
 #pragma unroll
-    for (int t = 0; t < kPfiMax; ++t) eta[t] = 0.0;
+    for (int t = 0; t < K; ++t) eta[t] = 0.0;
     int prow = 0;  // lane t: pivot row of eta t
     int iters = 0;
 
@@ -462,7 +467,7 @@ __global__ __launch_bounds__(64 * waves_for<S>()) void lp_pfi_kernel(DevLP lp, L
       // ---- BTRAN: u = e_r' E_{k-1} ... E_0 over the nonzeros of u ----
       double u = lane == r ? 1.0 : 0.0;
 #pragma unroll
-      for (int t = kPfiMax - 1; t >= 0; --t) {
+      for (int t = K - 1; t >= 0; --t) {
         if (t < iters) {
           uint64_t mask = __ballot(u != 0.0);
           const double pr = u * eta[t];  // the oracle's products, lane-parallel
@@ -644,7 +649,7 @@ __global__ __launch_bounds__(64 * waves_for<S>()) void lp_pfi_kernel(DevLP lp, L
       const double inv = 1.0 / arq;
       const double e = lane == r ? inv : -alq * inv;
 #pragma unroll
-      for (int t = 0; t < kPfiMax; ++t)
+      for (int t = 0; t < K; ++t)
         if (t == iters) eta[t] = e;
       if (lane == iters) prow = r;
       ++iters;
@@ -687,10 +692,14 @@ __global__ __launch_bounds__(64 * waves_for<S>()) void lp_pfi_kernel(DevLP lp, L
       wave_sync();
       if (lane < m) zc[h] = zB;
       wave_sync();
-      double sum = 0.0;
-      for (int j = lane; j < n; j += 64) sum += P.cj(j) * zc[j];
-      sum = wave_sum(sum);
-      if (lane == 0) io.obj[b] = P.ocol < 0 ? sum + lp.objoff : sum;
+      // objective as the oracle sums it: sequentially over the columns, so
+      // the value is the oracle's bit for bit (best-first search orders nodes
+      // by these bounds; a last-bit difference reorders ties)
+      if (lane == 0) {
+        double sum = 0.0;
+        for (int j = 0; j < n; ++j) sum += P.cj(j) * zc[j];
+        io.obj[b] = P.ocol < 0 ? sum + lp.objoff : sum;
+      }
       if (io.x != nullptr)
         for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = zc[j];
     } else if (lane == 0) {
@@ -706,23 +715,34 @@ __global__ __launch_bounds__(64 * waves_for<S>()) void lp_pfi_kernel(DevLP lp, L
   PSTAMP_FLUSH
 }
 
-template <int S>
+template <int S, int K>
 hipError_t launch_s(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
                     hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)lp_pfi_kernel<S>,
+    hipError_t e = hipFuncSetAttribute((const void *)lp_pfi_kernel<S, K>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  constexpr int kWaves = waves_for<S>();
-  const size_t lds = lp_pfi_lds_bytes(lp.n, lp.m, lp.nnz);
+  constexpr int kWaves = waves_for<S, K>();
+  const size_t lds = lp_pfi_lds_bytes(lp.n, lp.m, lp.nnz, px.kmax);
   const int want = (io.batch + kWaves - 1) / kWaves;
   const int blocks = want < num_cus ? want : num_cus;
-  hipLaunchKernelGGL((lp_pfi_kernel<S>), dim3(blocks), dim3(64 * kWaves), lds, stream, lp, io,
-                     px);
+  hipLaunchKernelGGL((lp_pfi_kernel<S, K>), dim3(blocks), dim3(64 * kWaves), lds, stream, lp,
+                     io, px);
   return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_k(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
+                    hipStream_t stream) {
+  switch ((lp.n + lp.m + 63) / 64) {
+    case 1: return launch_s<1, K>(lp, io, px, num_cus, stream);
+    case 2: return launch_s<2, K>(lp, io, px, num_cus, stream);
+    case 3: return launch_s<3, K>(lp, io, px, num_cus, stream);
+    default: return launch_s<4, K>(lp, io, px, num_cus, stream);
+  }
 }
 
 }  // namespace
@@ -740,13 +760,18 @@ extern "C" int mgpu_debug_pfi_stamps(unsigned long long *out, int reset) {
 }
 #endif
 
-size_t lp_pfi_lds_bytes(int n, int m, int nnz) {
-  const int waves = slots_for(n + m) <= 3 ? waves_for<3>() : waves_for<4>();
+size_t lp_pfi_lds_bytes(int n, int m, int nnz, int kmax) {
+  const bool small = kmax <= kPfiSmall;
+  const int waves = slots_for(n + m) <= 3 ? (small ? waves_for<3, kPfiSmall>()
+                                                   : waves_for<3, kPfiMax>())
+                                          : waves_for<4, kPfiMax>();
   return pfi_shared_bytes(n, m, nnz) + (size_t)waves * pfi_wave_bytes(n + m);
 }
 
 bool lp_pfi_fits(int n, int m, int nnz) {
-  return m <= kLpMaxM && n + m <= 64 * kPfiSlots && lp_pfi_lds_bytes(n, m, nnz) <= 160 * 1024;
+  return m <= kLpMaxM && n + m <= 64 * kPfiSlots &&
+         lp_pfi_lds_bytes(n, m, nnz, kPfiSmall) <= 160 * 1024 &&
+         lp_pfi_lds_bytes(n, m, nnz, kPfiMax) <= 160 * 1024;
 }
 
 hipError_t launch_lp_pfi(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
@@ -755,13 +780,10 @@ hipError_t launch_lp_pfi(const DevLP &lp, const LpIO &io, const PfiIO &px, int n
   if (!lp_pfi_fits(lp.n, lp.m, lp.nnz) || io.ws.head == nullptr || px.kmax < 1 ||
       px.kmax > kPfiMax)
     return hipErrorInvalidValue;
-  const int S = (lp.n + lp.m + 63) / 64;
-  switch (S) {
-    case 1: return launch_s<1>(lp, io, px, num_cus, stream);
-    case 2: return launch_s<2>(lp, io, px, num_cus, stream);
-    case 3: return launch_s<3>(lp, io, px, num_cus, stream);
-    default: return launch_s<4>(lp, io, px, num_cus, stream);
-  }
+  // the eta file in VGPRs is sized at compile time: 16 (4 waves per SIMD)
+  // when the cap allows, else 32 (3 waves per SIMD)
+  return px.kmax <= kPfiSmall ? launch_k<kPfiSmall>(lp, io, px, num_cus, stream)
+                              : launch_k<kPfiMax>(lp, io, px, num_cus, stream);
 }
 
 }  // namespace mgpu

@@ -134,10 +134,17 @@ struct LpIO {
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
 constexpr int kLpDefaultIterLimit = 10000;  // OsiLPEngine maxIterLimit_ (OsiLPEngine.cpp:99)
+// Anti-cycling: a solve that has made this many pivots (counted across the
+// product-form / dense continuation split) switches to Bland's rule — the
+// infeasible row with the lowest basic column, the exact minimum ratio with
+// the lowest column on ties (oracle/lp_dual.c STALL_PIVOTS).  Degenerate
+// deep-tree node LPs otherwise cycle to the iteration limit.
+constexpr int kStallPivots = 128;
 
 // K3P (lp_pfi.hip): product-form dual simplex for a batch that shares its
 // warm start.  At most kPfiMax eta columns per node, n + m <= 64*kPfiSlots.
-constexpr int kPfiMax = 16;
+constexpr int kPfiMax = 32;
+static_assert(kPfiMax < kStallPivots, "K3P never reaches the Bland switch");
 constexpr int kPfiSlots = 4;
 struct PfiIO {
   int kmax;                     // eta-file cap for this launch (1..kPfiMax)
@@ -152,15 +159,18 @@ struct PfiIO {
   int8_t *c_st;
   double *c_d, *c_binv;
 };
-// continuation slots per LP call (K3P overflow beyond this restarts in K3)
-constexpr int kPfiOvfSlots = 16384;
-size_t lp_pfi_lds_bytes(int n, int m, int nnz);
+// continuation slots per LP call: one per LP of the batch, up to this many
+// bytes of HBM (K3P overflow beyond the slots restarts in K3 from the shared
+// warm start)
+constexpr size_t kPfiOvfBytes = 24ull << 30;
+size_t lp_pfi_lds_bytes(int n, int m, int nnz, int kmax);
 bool lp_pfi_fits(int n, int m, int nnz);
 hipError_t launch_lp_pfi(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
                          hipStream_t stream);
 // K3PW (lp_pfi_wide.hip): K3P for 64 < m <= 128 (two basis rows per lane),
 // n + m <= 256, at most kPfiWideMax etas; its overflow list goes to K3L.
 constexpr int kPfiWideMax = 32;
+static_assert(kPfiWideMax < kStallPivots, "K3PW never reaches the Bland switch");
 size_t lp_pfiw_lds_bytes(int n, int m, int nnz);
 bool lp_pfiw_fits(int n, int m, int nnz);
 hipError_t launch_lp_pfiw(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,

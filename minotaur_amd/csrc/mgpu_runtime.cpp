@@ -518,7 +518,9 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     bool wide = false;
     const int kcap = pfi_cap(c, &wide);
     const int m = c->lp.m, N = c->lp.n + c->lp.m;
-    const int cap = io.batch < kPfiOvfSlots ? io.batch : kPfiOvfSlots;
+    const size_t slot_bytes = (size_t)m * 4 + (size_t)N * 9 + (size_t)m * m * 8 + 48;
+    const size_t max_slots = kPfiOvfBytes / slot_bytes;
+    const int cap = (size_t)io.batch < max_slots ? io.batch : (int)max_slots;
     HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 4) * sizeof(int32_t)));
     const size_t sb_head = al16h((size_t)cap * m * 4), sb_st = al16h((size_t)cap * N),
                  sb_d = al16h((size_t)cap * N * 8), sb_binv = (size_t)cap * m * m * 8;

@@ -310,6 +310,62 @@ def random_mkp(seed: int, n: int = 40, m: int = 5, tight: float = 0.5):
                      np.zeros(n), np.ones(n), np.full(n, BINARY, dtype=np.int32), -c)
 
 
+def tls4_oa(model, ntan=1, seed=2, ratio_lo=0.5, ratio_hi=20.0):
+    """Outer-approximation LP of test_instances/tls4.nl (BASELINE config 2,
+    the MINLP itself rather than its linear rows only).
+
+    tls4 has four nonlinear rows (tls4.nl:203-222, expression o16 o54 of four
+    o39 o2 terms):
+
+      C_i:  - sum_{k<4} sqrt(x_{4i+k} * y_k) + a_i' z <= b_i,   i = 0..3,
+
+    with x_{4i+k} = column 4i+k (continuous, [1, inf)) and y_k = column 16+k
+    (integer, [1, 100]); the linear part a_i' z is the row's own linear terms
+    in the file.  -sqrt(x y) is convex on the positive orthant (sqrt(x y) is
+    the geometric mean, concave), so every tangent plane under-estimates it
+    and g(p) + grad g(p)'(x - p) <= b_i is a valid cut.  -sqrt(x y) is
+    positively homogeneous of degree 1, so g(p) = grad g(p)'p (Euler) and the
+    tangent at a point with ratio r = x/y is simply
+
+      -1/2 (x / sqrt(r) + y sqrt(r)) + a_i' z <= b_i,
+
+    exact on the ray x = r y.  Each nonlinear row becomes ``ntan`` tangent
+    rows, each with its own seeded ratio per term (log-uniform in
+    [ratio_lo, ratio_hi]); they take the place of C_i (rows 0..4*ntan-1), and
+    the 60 linear rows follow in file order.  With ntan = 1 the LP keeps
+    tls4's 64 rows (the K3P / K3 row range).
+
+    The OA-MILP optimum is a lower bound on tls4's MINLP optimum (8.3,
+    MINLPLib): 3.2 for the default seed (HiGHS, tools/make_instances.py)."""
+    import math as _m
+    assert model.n == 105 and model.m == 64, 'tls4 has 105 columns and 64 rows'
+    rng = np.random.default_rng(seed)
+    rows, rlo, rhi = [], [], []
+    nl_rows = [i for i in range(model.m) if model.con_nonlinear[i]]
+    assert nl_rows == [0, 1, 2, 3], nl_rows
+    for i in nl_rows:
+        lin = [(j, a) for j, a in model.rows[i] if a != 0.0]
+        for _ in range(ntan):
+            r = np.exp(rng.uniform(_m.log(ratio_lo), _m.log(ratio_hi), 4))
+            extra = []
+            for k in range(4):
+                extra += [(4 * i + k, -0.5 / _m.sqrt(r[k])), (16 + k, -0.5 * _m.sqrt(r[k]))]
+            rows.append(lin + extra)
+            rlo.append(model.con_lb[i])
+            rhi.append(model.con_ub[i])
+    for i in model.linear_rows():
+        rows.append(model.rows[i])
+        rlo.append(model.con_lb[i])
+        rhi.append(model.con_ub[i])
+    obj = np.zeros(model.n)
+    for j, a in model.obj_grad:
+        obj[j] += a
+    if model.obj_sense == 1:
+        obj = -obj
+    return from_rows('tls4-oa' if ntan == 1 else f'tls4-oa{ntan}', model.n, rows, rlo, rhi,
+                     model.var_lb, model.var_ub, model.var_type, obj, model.obj_const)
+
+
 def nvs08_oa(model, npts=4, nobj=8, seed=20261016):
     """Outer-approximation LP of test_instances/nvs08.nl (BASELINE config 1,
     SURVEY §0.1 / §8d: "OA-LP with tangent rows at seeded points").

@@ -19,7 +19,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _D = ctypes.c_double
 
-LP_PFI_MAX = 16  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
+LP_PFI_MAX = 32  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
 LP_PFI_WIDE_MAX = 32  # MGPU_LP_PFI_WIDE_MAX: K3PW eta-file cap
 
 # Every entry point declared in include/mgpu.h (checked by the CPU tests).
@@ -46,7 +46,7 @@ class BnbStats(ctypes.Structure):
                 ('pruned', ctypes.c_longlong), ('lps', ctypes.c_longlong),
                 ('pivots', ctypes.c_longlong), ('sb_lps', ctypes.c_longlong),
                 ('sb_pivots', ctypes.c_longlong), ('sb_pruned', ctypes.c_longlong),
-                ('sb_modified', ctypes.c_longlong)]
+                ('sb_modified', ctypes.c_longlong), ('pfi_pivots', ctypes.c_longlong)]
 
 _lib = None
 

@@ -45,6 +45,7 @@ class _Stats:
         self.pruned = 0
         self.lps = self.pivots = 0
         self.sb_lps = self.sb_pivots = self.sb_pruned = self.sb_modified = 0
+        self.pfi_pivots = 0
 
 
 def _order_key(v):
@@ -64,6 +65,7 @@ class _Node:
 
 # ReliabilityBrancher defaults (ReliabilityBrancher.cpp:43-58)
 REL_MAX_CANDS, REL_ITER, REL_THRESH, REL_MIN_DIST, REL_ETOL = 20, 25, 4, 50, 1e-6
+REL_MAX_DEPTH = 1000   # maxDepth_: no strong branching below it (:105)
 
 
 def _rel_score(up, down):
@@ -179,6 +181,8 @@ class CpuBnbContext:
                 s2, o2, i2, x2 = oracle.dual_simplex(p, f.lb[keep], f.ub[keep], self.ws,
                                                       want_x=True,
                                                       pfi=self.pfi if self.ws is not None else 0)
+                if self.ws is not None and self.pfi > 0:
+                    self.tot.pfi_pivots += int(np.minimum(i2, self.pfi).sum())
             status[keep], obj[keep], x[keep] = s2, o2, x2
             self.tot.lps += int(keep.size)
             self.tot.pivots += int(np.sum(i2))
@@ -292,7 +296,8 @@ class CpuBnbContext:
         for i in range(nb):
             if decs[i] != 0:
                 continue
-            sb[i] = unrel_sorted(i)[:REL_MAX_CANDS]
+            maxcnt = 0 if nodes[i].depth > REL_MAX_DEPTH else REL_MAX_CANDS
+            sb[i] = unrel_sorted(i)[:maxcnt]
             for j in sb[i]:
                 v = x[i][j]
                 for up in (False, True):

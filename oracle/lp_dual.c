@@ -28,6 +28,9 @@
 #define PIV_TOL 1e-9    /* smallest acceptable |alpha_rq| in the ratio test  */
 #define ART_BOUND 1e7   /* first artificial box for free / half-free columns */
 #define INF_B 1e30
+/* pivots after which a solve switches to Bland's rule (anti-cycling; the GPU
+ * kernels K3 / K3L use the same constant, kStallPivots in mgpu_internal.h) */
+#define STALL_PIVOTS 128
 
 enum { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
 
@@ -292,7 +295,8 @@ static int invert_basis(lpw *W) {
 static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub,
                              int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
                              int have_ws, int have_binv, int iter_limit, double *obj_out,
-                             double *x_out, double *y_out, int *iters_out, int pfi)
+                             double *x_out, double *y_out, int *iters_out, int pfi,
+                             int iter_base)
 {
   int n = P->n, m = P->m, N = n + m;
   lpw W;
@@ -369,7 +373,12 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
   compute_primals(&W);
 
   for (;;) {
-    /* ---- pricing: most infeasible basic row (Dantzig) ---- */
+    /* anti-cycling: past STALL_PIVOTS pivots of the solve (counted across
+     * the product-form / dense split) Bland's rule replaces Dantzig pricing
+     * and the Harris ratio test */
+    const int bland = iter_base + iters >= STALL_PIVOTS;
+    /* ---- pricing: most infeasible basic row (Dantzig); Bland: the
+     * infeasible row whose basic column has the lowest index ---- */
     int r = -1;
     double best = 0.0, delta = 0.0;
     for (int i = 0; i < m; ++i) {
@@ -377,7 +386,11 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       double v = W.z[h], inf = 0.0;
       if (v < W.blo[h] - P_TOL) inf = v - W.blo[h];
       else if (v > W.bhi[h] + P_TOL) inf = v - W.bhi[h];
-      if (fabs(inf) > best) { best = fabs(inf); r = i; delta = inf; }
+      if (bland) {
+        if (inf != 0.0 && (r < 0 || h < W.head[r])) { best = fabs(inf); r = i; delta = inf; }
+      } else if (fabs(inf) > best) {
+        best = fabs(inf); r = i; delta = inf;
+      }
     }
     if (r < 0 && !fresh) {
       /* confirm against freshly recomputed primal values */
@@ -448,7 +461,7 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       continue;
     }
     int q = -1;
-    double qa = 0.0;
+    double qa = 0.0, tb = INFINITY;
     for (int j = 0; j < N; ++j) {
       if (W.st[j] == ST_BASIC || W.blo[j] == W.bhi[j]) continue;
       double at = sigma * W.alpha_r[j], dj = W.d[j], t;
@@ -456,7 +469,11 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       else if (W.st[j] == ST_UB && at < -PIV_TOL) t = fmin(dj, 0.0) / at;
       else if (W.st[j] == ST_FREE && fabs(at) > PIV_TOL) t = 0.0;
       else continue;
-      if (t <= tmax && fabs(at) > qa) { qa = fabs(at); q = j; }
+      if (bland) {   /* the exact minimum ratio, lowest column on ties */
+        if (t < tb) { tb = t; q = j; }
+      } else if (t <= tmax && fabs(at) > qa) {
+        qa = fabs(at); q = j;
+      }
     }
     if (q < 0) { status = 2; break; }
     /* ---- column q, steps ---- */
@@ -552,7 +569,7 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
                      double *x_out, double *y_out, int *iters_out)
 {
   return dual_simplex_impl(P, lb, ub, ws_head, ws_st, ws_binv, ws_d, have_ws, have_binv,
-                           iter_limit, obj_out, x_out, y_out, iters_out, 0);
+                           iter_limit, obj_out, x_out, y_out, iters_out, 0, 0);
 }
 
 /* What the GPU runs for one LP of a batch that shares its warm start: K3P
@@ -573,13 +590,13 @@ static int solve_shared(const orc_lp *P, const double *lb, const double *ub, con
   }
   if (!(pfi > 0 && have_ws && have_binv))
     return dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, have_ws, have_binv, iter_limit,
-                             obj, x, 0, iters, 0);
+                             obj, x, 0, iters, 0, 0);
   st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, 1, 1, iter_limit, obj, x, 0, iters,
-                         pfi);
+                         pfi, 0);
   if (st == -1) {
     int it2 = 0;
     st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, 1, 1, iter_limit - pfi, obj, x, 0,
-                           &it2, 0);
+                           &it2, 0, pfi);
     *iters = pfi + it2;
   }
   return st;

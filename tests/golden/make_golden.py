@@ -58,6 +58,14 @@ def main():
     # root box (the node every tree starts from) and a tight incumbent
     dump('tls4_root', tls4, tls4.vlb[None, :].copy(), tls4.vub[None, :].copy(), None)
     dump('tls4_inc8', tls4, LB[:64], UB[:64], 8.0)
+    # config 2 as a MINLP: tls4's outer-approximation LP (tangent rows for
+    # its four convex sqrt rows); OA-MILP optimum 3.2, so incumbent 3.5 drives
+    # varBndsFromObj_ and the root box is the tree's first node
+    oa = LinProblem.load(os.path.join(inst, 'tls4_oa.npz'))
+    LB, UB = random_boxes(oa, 256, 20261017)
+    LB, UB = np.vstack([oa.vlb[None], LB]), np.vstack([oa.vub[None], UB])
+    dump('tls4_oa_noinc', oa, LB, UB, None)
+    dump('tls4_oa_inc3p5', oa, LB, UB, 3.5)
     # config 1: the nvs08 outer-approximation LP (root + seeded boxes)
     nv = LinProblem.load(os.path.join(inst, 'nvs08_oa.npz'))
     LB, UB = random_boxes(nv, 255, 808)

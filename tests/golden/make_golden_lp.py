@@ -59,6 +59,9 @@ def main():
     tls4 = LinProblem.load(os.path.join(inst, 'tls4_lin.npz'))
     LB, UB = random_boxes(tls4, 200, 20261015)
     dump('tls4', tls4, np.vstack([tls4.vlb[None], LB]), np.vstack([tls4.vub[None], UB]))
+    oa = LinProblem.load(os.path.join(inst, 'tls4_oa.npz'))
+    LB, UB = random_boxes(oa, 200, 20261017)
+    dump('tls4_oa', oa, np.vstack([oa.vlb[None], LB]), np.vstack([oa.vub[None], UB]))
     nv = LinProblem.load(os.path.join(inst, 'nvs08_oa.npz'))
     LB, UB = random_boxes(nv, 200, 808)
     dump('nvs08_oa', nv, np.vstack([nv.vlb[None], LB]), np.vstack([nv.vub[None], UB]))

@@ -3,10 +3,10 @@ warm start, repo:minotaur_amd/csrc/lp_pfi.hip) through the C ABI.
 
 K3P restates oracle/lp_dual.c's product-form mode (``pfi=k``: B^{-1} kept as
 k eta columns on the shared root inverse; an LP that needs more than k pivots
-is re-solved by the dense K3 from the same warm start).  So statuses and pivot
-counts equal the oracle's exactly and objectives agree to ~1e-9 (K3P's
-objective is a wave tree sum); against HiGHS the north-star bar of 1e-6
-holds.  Covered: the bench's node boxes (tls4-lin, column slots S = 3), the
+is continued by the dense K3 from its basis and explicit inverse).  So
+statuses, pivot counts and objective bits equal the oracle's (the objective is
+summed sequentially, as the oracle does); against HiGHS the north-star bar of
+1e-6 holds.  Covered: the bench's node boxes (tls4-lin, column slots S = 3), the
 golden warm-start cases, the overflow path (small eta caps force most LPs
 through the dense re-solve), iteration limits, skips, bound LPs (OBBT
 objectives), primal vectors, and instances with S = 1 and S = 4.
@@ -82,6 +82,8 @@ def _check(ctx, p, LB, UB, kmax, iter_limit=0, want_x=False):
     assert np.array_equal(r.status, st)
     assert np.array_equal(r.iters, its)
     assert _close(r.obj, obj)
+    ok = st == 0
+    assert np.array_equal(r.obj[ok].view(np.int64), obj[ok].view(np.int64))   # oracle bits
     if want_x:
         ok = st == 0
         assert np.allclose(r.x[ok], x[ok], rtol=1e-9, atol=1e-9)
@@ -104,6 +106,20 @@ def test_k3p_bench_boxes_vs_oracle(ctx, kmax):
     for b in np.nonzero(r.status == 0)[0][:40]:
         hs, ho = oracle.highs(p, f.lb[keep][b], f.ub[keep][b])
         assert hs == 0 and abs(ho - r.obj[b]) <= 1e-6 * max(1.0, abs(ho))
+
+
+@pytest.mark.parametrize('kmax', [KCAP, 24, 16, 9])
+def test_k3p_tls4_oa_deep_boxes_vs_oracle(ctx, kmax):
+    """Config 2's OA-LP boxes: 10.7 pivots from the root basis on average,
+    18 % above 16 (the 32-eta build for caps > 16, the 16-eta build below)."""
+    p = LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
+                                     'instances', 'tls4_oa.npz'))
+    ctx.load(p)
+    LB, UB = random_boxes(p, 6007, 20261017)
+    f = oracle.linear_fbbt(p, LB, UB, 3.5)
+    keep = f.infeas == 0
+    _, its = _check(ctx, p, f.lb[keep], f.ub[keep], kmax)
+    assert (its > 16).any()
 
 
 @pytest.mark.parametrize('name', ['tls4', 'knapsack', 'random0', 'random3', 'random5'])

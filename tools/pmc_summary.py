@@ -47,7 +47,9 @@ def main(src, tag, bench_args):
             k = short(r['Kernel_Name'])
             if k and str(r['Grid_Size']) == str(grid.get(k)):
                 ctr[k][r['Counter_Name']].append(float(r['Counter_Value']))
-    res = {"bench_args": bench_args, "kernels": {}}
+    # the bench's headline since round 3 is the tree round (bench.py
+    # tree_rounds); bench.pmc_traffic matches summaries by this key
+    res = {"bench_args": bench_args, "workload": "tree_rounds", "kernels": {}}
     for k in sorted(set(dur) | set(ctr)):
         d = dur.get(k, [])
         fe = ctr[k].get('FETCH_SIZE', [])

@@ -3,7 +3,7 @@
 # the default bench line, rocprof kernel stats of the same bench, and the
 # headline's PMC passes (tools/prof_run.sh).  Output under gpurun_out/$TAG.
 set -o pipefail
-TAG=${TAG:-r02c}
+TAG=${TAG:-r03a}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
