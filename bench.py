@@ -248,8 +248,11 @@ def tree_search(ctx, dev, rank, world, B, args):
             sys.path.insert(0, os.path.join(ROOT, 'oracle'))
             import oracle
             opt = oracle.highs_milp(p)[1]
+        # pool capacity: parent warm starts keep a basis per slot (m*m*8 B:
+        # 32 KB for tls4-oa), so those pools are sized to the tree
+        cap = 1 << 19 if warm and p.m > 16 else 1 << 23
         inc, nodes, lps, piv, pruned, rounds, el, moved, sbl, sbp = run_tree(
-            ctx, dev, rank, world, p, B, order, warm, 1 << 23, br)
+            ctx, dev, rank, world, p, B, order, warm, cap, br)
         progress(rank, f"tree {p.name} order {order} warm {warm} brancher {br}: "
                        f"{nodes:.0f} nodes in {el:.2f}s")
         out.append({"instance": p.name, "vars": p.n, "rows": p.m,
