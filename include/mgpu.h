@@ -144,6 +144,45 @@ int mgpu_lp_solve_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double
                       int32_t *d_wo_head, int8_t *d_wo_st, double *d_wo_d,
                       double *d_wo_binv);
 
+/* ---- path warm starts (the batched tree's warm mode 2) --------------------
+ * NodeIncRelaxer::createNodeRelaxation loads each child with its parent's
+ * optimal basis (NodeIncRelaxer.cpp:146-150; TreeManager::branch hands both
+ * children the parent's warm start, TreeManager.cpp:97-136).  A dense basis
+ * inverse per open node (32 KB at m = 64) is too much to keep and move for
+ * millions of nodes; a node's basis is kept instead as its PATH from the
+ * shared root basis: the pivots (entering column q, row r; packed
+ * q | r << 16) that led there, plus its column statuses (n+m bytes).  K3P
+ * rebuilds the etas by FTRAN in path order (bit for bit the arithmetic of
+ * the solves that made them), recomputes the reduced costs of that basis and
+ * continues with its own pivots in the same eta file.
+ *   k_in[b] <= 0      : node b starts from the shared warm start itself;
+ *   path_in [batch][MGPU_PATH_MAX], st_in [batch][n+m] (0 lb, 1 ub, 2 free,
+ *                       3 basic);
+ *   k_out / path_out / st_out (optional): node b's final path for its
+ *                       children — its replayed plus its own pivots — when
+ *                       it is optimal in the product form with at most
+ *                       `inherit` etas, else k_out[b] = 0 (children restart
+ *                       from the shared warm start);
+ *   iters             : the node's own pivots.
+ * Runs K3P only (m <= 64, n + m <= 256, eta cap <= MGPU_PATH_MAX; an LP that
+ * fills the eta file is continued by K3).  oracle/lp_dual.c
+ * orc_dual_simplex_path_batch restates it. */
+#define MGPU_PATH_MAX 32
+int mgpu_lp_solve_path(mgpu_ctx *ctx, int batch, const double *lb, const double *ub,
+                       const int32_t *ws_head, const int8_t *ws_st, const double *ws_d,
+                       const double *ws_binv, const int32_t *k_in, const uint32_t *path_in,
+                       const int8_t *st_in, int inherit, int iter_limit, int32_t *status,
+                       double *obj, int32_t *iters, double *x, int32_t *k_out,
+                       uint32_t *path_out, int8_t *st_out);
+int mgpu_lp_solve_path_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double *d_ub,
+                           const int32_t *d_skip, const int32_t *d_ws_head,
+                           const int8_t *d_ws_st, const double *d_ws_d,
+                           const double *d_ws_binv, const int32_t *d_k_in,
+                           const uint32_t *d_path_in, const int8_t *d_st_in, int inherit,
+                           int iter_limit, int32_t *d_status, double *d_obj,
+                           int32_t *d_iters, double *d_x, int32_t *d_k_out,
+                           uint32_t *d_path_out, int8_t *d_st_out);
+
 /* ---- per-node rows (the glob path) ---------------------------------------
  * QuadHandler rewrites the secant / McCormick rows of the relaxation at
  * every node (upSqCon_ / upBilCon_, QuadHandler.cpp:3322-3419) and hands

@@ -16,6 +16,7 @@
 // exchange the incumbent with an RCCL all-reduce MIN between rounds.
 #include <cmath>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "bnb_internal.h"
@@ -47,6 +48,9 @@ struct BnbState {
   DevBuf pc_up, pc_dn, cnt_up, cnt_dn, last, last_new, ppvar, ppval, bnlb, bpvar, bpval, rflag, rrank,
       nsb, sb_off, sb_var, sb_val, dec2, nev, ev_var, ev_side, ev_cost, rcnt, clb, cub, cnode,
       cst, cobj, cit, ev_off, cv_var, cv_side, cv_cost;
+  // path warm starts (warm 2): per pool slot, per batch (gathered in) and out
+  DevBuf ppk, ppath, ppst, bpk, bppath, bpst, opk, oppath, opst;
+  int inherit = 0;             // longest path handed to children (<= the eta cap)
   void release() {
     for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
                       &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
@@ -57,7 +61,7 @@ struct BnbState {
                       &cnt_dn, &last, &last_new, &ppvar, &ppval, &bnlb, &bpvar, &bpval, &rflag, &rrank,
                       &nsb, &sb_off, &sb_var, &sb_val, &dec2, &nev, &ev_var, &ev_side, &ev_cost,
                       &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit, &ev_off, &cv_var, &cv_side,
-                      &cv_cost})
+                      &cv_cost, &ppk, &ppath, &ppst, &bpk, &bppath, &bpst, &opk, &oppath, &opst})
       b->release();
   }
 };
@@ -101,14 +105,20 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
     HIPCHK(c, s.ev_side.ensure((size_t)B * kRelEvents));
     HIPCHK(c, s.ev_cost.ensure((size_t)B * kRelEvents * 8));
   }
-  if (s.warm || s.rel) {  // reliability branching needs each node's optimal basis
+  if (s.warm == 1 || s.rel) {  // reliability branching needs each node's optimal basis
     const size_t N = n + m;
     HIPCHK(c, s.wo_head.ensure((size_t)B * m * 4 + 4));
     HIPCHK(c, s.wo_st.ensure((size_t)B * N + 4));
     HIPCHK(c, s.wo_d.ensure((size_t)B * N * 8));
     HIPCHK(c, s.wo_binv.ensure((size_t)B * m * m * 8 + 8));
   }
-  if (s.warm) {
+  if (s.warm == 2) {
+    const size_t N = n + m;
+    for (DevBuf *b : {&s.bpk, &s.opk}) HIPCHK(c, b->ensure((size_t)B * 4));
+    for (DevBuf *b : {&s.bppath, &s.oppath}) HIPCHK(c, b->ensure((size_t)B * kPathMax * 4));
+    for (DevBuf *b : {&s.bpst, &s.opst}) HIPCHK(c, b->ensure((size_t)B * N + 16));
+  }
+  if (s.warm == 1) {
     const size_t N = n + m;
     HIPCHK(c, s.bws_head.ensure((size_t)B * m * 4 + 4));
     HIPCHK(c, s.bws_st.ensure((size_t)B * N + 4));
@@ -223,8 +233,8 @@ extern "C" {
 
 int mgpu_bnb_config(mgpu_ctx *c, int order, int warm) {
   if (!c) return MGPU_ERR_ARG;
-  if (order < 0 || order > 1 || warm < 0 || warm > 1)
-    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_config: order and warm are 0 or 1");
+  if (order < 0 || order > 1 || warm < 0 || warm > 2)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_config: order 0/1, warm 0/1/2");
   c->bnb_order = order;
   c->bnb_warm = warm;
   return MGPU_OK;
@@ -256,6 +266,15 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   s->warm = c->bnb_warm;
   s->rel = c->bnb_brancher;
   s->tot.incumbent = incumbent;
+  if (s->warm == 2) {
+    // path warm starts run on K3P's eta file: the tree hands children paths
+    // of at most min(kPathInherit, eta cap) pivots
+    const int kcap = mgpu_lp_pfi_cap(c);
+    if (s->rel || m > kLpMaxM || kcap <= 0 || kcap > kPathMax)
+      return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: path warm starts (warm 2) need MaxVio "
+                  "branching and K3P (m <= 64, eta cap 1..%d)", kPathMax);
+    s->inherit = kcap < kPathInherit ? kcap : kPathInherit;
+  }
   if (s->rel) {
     if (m > kLpMaxM && !(lp_large_lds_bytes(n, m) <= (size_t)kLargeLdsMax))
       return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: reliability branching needs K3 or K3L");
@@ -324,7 +343,17 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
     s->sort_bytes = tb;
     s->hw = 1;
   }
-  if (s->warm) {
+  if (s->warm == 2) {
+    if (!s->root_ok)
+      return fail(c, MGPU_ERR_STATE, "mgpu_bnb_init: path warm starts need an optimal root");
+    // per pool slot: path length (0: the root basis), pivots, column statuses
+    HIPCHK(c, s->ppk.ensure((size_t)capacity * 4));
+    HIPCHK(c, s->ppath.ensure((size_t)capacity * kPathMax * 4));
+    HIPCHK(c, s->ppst.ensure((size_t)capacity * N + 16));
+    HIPCHK(c, hipMemsetAsync(s->ppk.p, 0, (size_t)capacity * 4, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  if (s->warm == 1) {
     if (!s->root_ok)
       return fail(c, MGPU_ERR_STATE, "mgpu_bnb_init: parent warm starts need an optimal root");
     // every pool slot keeps its node's warm start (the parent's optimal basis)
@@ -397,7 +426,7 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   if (!bfs) {
     lb = s.plb.as<double>() + (size_t)base * n;
     ub = s.pub.as<double>() + (size_t)base * n;
-    if (s.warm) {  // the popped nodes are contiguous: their bases are read in place
+    if (s.warm == 1) {  // the popped nodes are contiguous: their bases are read in place
       w_head = s.pws_head.as<int32_t>() + (size_t)base * m;
       w_st = s.pws_st.as<int8_t>() + (size_t)base * N;
       w_d = s.pws_d.as<double>() + (size_t)base * N;
@@ -420,7 +449,15 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     g.wlb = s.wlb.as<double>();
     g.wub = s.wub.as<double>();
     g.depth_in = s.depth_in.as<int32_t>();
-    if (s.warm) {
+    if (s.warm == 2) {
+      g.pk = s.ppk.as<int32_t>();
+      g.ppath = s.ppath.as<uint32_t>();
+      g.pst = s.ppst.as<int8_t>();
+      g.bpk = s.bpk.as<int32_t>();
+      g.bppath = s.bppath.as<uint32_t>();
+      g.bpst = s.bpst.as<int8_t>();
+    }
+    if (s.warm == 1) {
       g.ws_head = s.pws_head.as<int32_t>();
       g.ws_st = s.pws_st.as<int8_t>();
       g.ws_d = s.pws_d.as<double>();
@@ -441,7 +478,22 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   rc = mgpu_fbbt_dev(c, nb, lb, ub, s.inc, s.wlb.as<double>(), s.wub.as<double>(),
                      s.inf.as<int32_t>(), s.nm.as<int32_t>(), 0, nullptr, nullptr, nullptr);
   if (rc != MGPU_OK) return rc;
-  if (s.warm) {
+  if (s.warm == 2) {
+    // each node from its parent's optimal basis (NodeIncRelaxer.cpp:146-150)
+    // kept as its pivot path from the root basis; its own final path comes
+    // back for its children
+    const int32_t *pk = bfs ? s.bpk.as<int32_t>() : s.ppk.as<int32_t>() + base;
+    const uint32_t *pp = bfs ? s.bppath.as<uint32_t>()
+                             : s.ppath.as<uint32_t>() + (size_t)base * kPathMax;
+    const int8_t *ps = bfs ? s.bpst.as<int8_t>() : s.ppst.as<int8_t>() + (size_t)base * N;
+    rc = mgpu_lp_solve_path_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(),
+                                s.inf.as<int32_t>(), s.ws_head.as<int32_t>(),
+                                s.ws_st.as<int8_t>(), s.ws_d.as<double>(),
+                                s.ws_binv.as<double>(), pk, pp, ps, s.inherit, 0,
+                                s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
+                                s.x.as<double>(), s.opk.as<int32_t>(), s.oppath.as<uint32_t>(),
+                                s.opst.as<int8_t>());
+  } else if (s.warm) {
     // each node from its parent's optimal basis (NodeIncRelaxer.cpp:146-150);
     // its own optimal basis comes back for its children
     rc = mgpu_lp_solve_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(),
@@ -500,7 +552,7 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   io.iters = s.it.as<int32_t>();
   // the shared-root-basis node LPs ran the product form (K3P / K3PW) when the
   // context selects it; per-node bases (warm 1, reliability) run K3 / K3L
-  io.pfi_cap = (!s.warm && !s.rel && s.root_ok) ? mgpu_lp_pfi_cap(c) : 0;
+  io.pfi_cap = ((s.warm == 0 || s.warm == 2) && !s.rel && s.root_ok) ? mgpu_lp_pfi_cap(c) : 0;
   io.cand_obj = s.cand.as<double>();
   io.obj = s.obj.as<double>();
   io.bvar = s.bvar.as<int32_t>();
@@ -526,7 +578,16 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     io.hw = s.hw;
     io.plive = s.plive.as<uint8_t>();
   }
-  if (s.warm) {  // (reliability alone: children keep the root warm start)
+  if (s.warm == 2) {  // children inherit the node's final path
+    io.N = N;
+    io.opk = s.opk.as<int32_t>();
+    io.oppath = s.oppath.as<uint32_t>();
+    io.opst = s.opst.as<int8_t>();
+    io.ppk = s.ppk.as<int32_t>();
+    io.ppath = s.ppath.as<uint32_t>();
+    io.ppst = s.ppst.as<int8_t>();
+  }
+  if (s.warm == 1) {  // (reliability alone: children keep the root warm start)
     io.m = m;
     io.N = N;
     io.wo_head = s.wo_head.as<int32_t>();
@@ -617,15 +678,38 @@ int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
                                   s.pdepth.as<int32_t>(), tlb.as<double>(), tub.as<double>(),
                                   tnlb.as<double>(), tdep.as<int32_t>(), s.count, s.n, rank,
                                   world, &k, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  // every other per-slot array moves with its node (parent warm starts,
+  // parent branching data, paths): slot k <- slot rank + k * world
+  if (e == hipSuccess && k > 0) {
+    const int m = c->lp.m, N = s.n + m;
+    std::vector<std::pair<DevBuf *, size_t>> rows;
+    if (s.warm == 1)
+      rows = {{&s.pws_head, (size_t)m * 4}, {&s.pws_st, (size_t)N}, {&s.pws_d, (size_t)N * 8},
+              {&s.pws_binv, (size_t)m * m * 8}};
+    if (s.warm == 2)
+      rows = {{&s.ppk, 4}, {&s.ppath, (size_t)kPathMax * 4}, {&s.ppst, (size_t)N}};
+    if (s.rel) {
+      rows.push_back({&s.ppvar, 4});
+      rows.push_back({&s.ppval, 8});
+    }
+    size_t most = 0;
+    for (auto &r : rows) most = r.second > most ? r.second : most;
+    DevBuf tmp;
+    if (most > 0) e = tmp.ensure((size_t)k * most);
+    for (auto &r : rows)
+      if (e == hipSuccess)
+        e = launch_bnb_shard_rows(r.first->as<unsigned char>(), tmp.as<unsigned char>(), r.second,
+                                  k, rank, world, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    tmp.release();
+  } else if (e == hipSuccess) {
+    e = hipStreamSynchronize(c->stream);
+  }
   tlb.release();
   tub.release();
   tnlb.release();
   tdep.release();
   HIPCHK(c, e);
-  // the packed pool no longer matches the parent branching data: the kept
-  // nodes make no pseudocost observation on their first solve
-  if (s.rel) HIPCHK(c, hipMemset(s.ppvar.p, 0xFF, s.ppvar.bytes));
   s.count = k;
   s.tot.open = k;
   if (kept) *kept = k;
@@ -807,7 +891,9 @@ int mgpu_bnb_import(mgpu_ctx *c, int k, const double *lb, const double *ub, cons
   }
   if (s.rel)  // migrated nodes carry no parent branching data
     HIPCHK(c, hipMemsetAsync(s.ppvar.as<int32_t>() + at, 0xFF, (size_t)k * 4, c->stream));
-  if (s.warm) {
+  if (s.warm == 2)  // a migrated node starts from the root basis
+    HIPCHK(c, hipMemsetAsync(s.ppk.as<int32_t>() + at, 0, (size_t)k * 4, c->stream));
+  if (s.warm == 1) {
     // a migrated node starts from the root basis (its parent's stays with
     // the rank that branched it)
     for (int t = 0; t < k; ++t) {

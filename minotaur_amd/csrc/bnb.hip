@@ -243,6 +243,25 @@ __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
       io.ws_binv[c_up * mm + k] = b;
     }
   }
+  if (io.opk != nullptr) {
+    const int kp = io.opk[i];
+    const int N = io.N;
+    if (lane < kp) {
+      const uint32_t v = io.oppath[(size_t)i * kPathMax + lane];
+      io.ppath[c_down * kPathMax + lane] = v;
+      io.ppath[c_up * kPathMax + lane] = v;
+    }
+    if (kp > 0)
+      for (int k = lane; k < N; k += 64) {
+        const int8_t v = io.opst[(size_t)i * N + k];
+        io.ppst[c_down * N + k] = v;
+        io.ppst[c_up * N + k] = v;
+      }
+    if (lane == 0) {
+      io.ppk[c_down] = kp;
+      io.ppk[c_up] = kp;
+    }
+  }
   if (lane == 0) {
     const double bound = io.obj[i];
     io.pnlb[c_down] = bound;
@@ -301,7 +320,39 @@ __global__ __launch_bounds__(256) void bnb_shard_copy(const double *slb, const d
   }
 }
 
+// Generic per-slot row compaction for the depth-first shard: row k of dst =
+// row (rank + k * world) of src (to_tmp) or row k of src (back), one wave
+// per row, 4-byte words when the row allows, bytes otherwise.
+__global__ __launch_bounds__(256) void bnb_rows_copy(const unsigned char *src, unsigned char *dst,
+                                                     size_t row_bytes, int kept, int rank,
+                                                     int world, int to_tmp) {
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= kept) return;
+  const size_t from = to_tmp ? (size_t)rank + (size_t)k * world : (size_t)k;
+  const unsigned char *a = src + from * row_bytes;
+  unsigned char *b = dst + (size_t)k * row_bytes;
+  if ((row_bytes & 3) == 0) {
+    const uint32_t *a4 = reinterpret_cast<const uint32_t *>(a);
+    uint32_t *b4 = reinterpret_cast<uint32_t *>(b);
+    for (size_t t = lane; t < row_bytes / 4; t += 64) b4[t] = a4[t];
+  } else {
+    for (size_t t = lane; t < row_bytes; t += 64) b[t] = a[t];
+  }
+}
+
 }  // namespace
+
+hipError_t launch_bnb_shard_rows(unsigned char *rows, unsigned char *tmp, size_t row_bytes,
+                                 int kept, int rank, int world, hipStream_t stream) {
+  if (kept <= 0 || row_bytes == 0) return hipSuccess;
+  const dim3 grid((kept + 3) / 4), blk(256);
+  hipLaunchKernelGGL(bnb_rows_copy, grid, blk, 0, stream, rows, tmp, row_bytes, kept, rank, world,
+                     1);
+  hipLaunchKernelGGL(bnb_rows_copy, grid, blk, 0, stream, tmp, rows, row_bytes, kept, rank, world,
+                     0);
+  return hipGetLastError();
+}
 
 hipError_t launch_bnb_shard(double *plb, double *pub, double *pnlb, int32_t *pdep, double *tlb,
                             double *tub, double *tnlb, int32_t *tdep, int count, int n,

@@ -33,6 +33,14 @@ struct BnbIO {
   int32_t *ws_head;             // [cap][m]
   int8_t *ws_st;                // [cap][N]
   double *ws_d, *ws_binv;       // [cap][N], [cap][m][m]
+  // path warm starts (opk != null): the node's final path (batch-indexed)
+  // is copied to both children's slots
+  const int32_t *opk;           // [nb]
+  const uint32_t *oppath;       // [nb][kPathMax]
+  const int8_t *opst;           // [nb][N]
+  int32_t *ppk;                 // [cap]
+  uint32_t *ppath;              // [cap][kPathMax]
+  int8_t *ppst;                 // [cap][N]
   const int32_t *decision;      // [nb] (5: one child with the bound change bvar/bval/bup)
   int32_t *ppvar;               // [cap] or null: the children's parent branching variable
   double *ppval;                //   and its value (reliability branching's pseudocosts)
@@ -71,6 +79,12 @@ struct BnbSelIO {
   int32_t *bws_head;            // [nb] batch bases
   int8_t *bws_st;
   double *bws_d, *bws_binv;
+  const int32_t *pk;            // pool paths (null: none)
+  const uint32_t *ppath;
+  const int8_t *pst;
+  int32_t *bpk;                 // [nb] batch paths
+  uint32_t *bppath;
+  int8_t *bpst;
 };
 
 // Batched reliability branching (bnb_rel.hip).  ReliabilityBrancher
@@ -143,6 +157,8 @@ hipError_t launch_bnb_gather(const BnbSelIO &io, hipStream_t stream);
 hipError_t launch_sb_boxes(const double *plb, const double *pub, const int32_t *var,
                            const double *val, int ncand, int n, double *clb, double *cub,
                            hipStream_t stream);
+hipError_t launch_bnb_shard_rows(unsigned char *rows, unsigned char *tmp, size_t row_bytes,
+                                 int kept, int rank, int world, hipStream_t stream);
 hipError_t launch_bnb_shard(double *plb, double *pub, double *pnlb, int32_t *pdep, double *tlb,
                             double *tub, double *tnlb, int32_t *tdep, int count, int n,
                             int rank, int world, int *kept, hipStream_t stream);

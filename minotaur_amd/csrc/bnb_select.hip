@@ -78,6 +78,13 @@ __global__ __launch_bounds__(256) void bnb_gather(BnbSelIO io) {
     const size_t mm = (size_t)m * m;
     for (size_t j = lane; j < mm; j += 64) io.bws_binv[k * mm + j] = io.ws_binv[s * mm + j];
   }
+  if (io.pk != nullptr) {
+    const int kp = io.pk[s];
+    if (lane == 0) io.bpk[k] = kp;
+    if (lane < kp) io.bppath[(size_t)k * kPathMax + lane] = io.ppath[s * kPathMax + lane];
+    if (kp > 0)
+      for (int j = lane; j < io.N; j += 64) io.bpst[(size_t)k * io.N + j] = io.pst[s * io.N + j];
+  }
   if (lane == 0) {
     io.depth_in[k] = io.pdepth[s];
     io.plive[s] = 0;

@@ -271,6 +271,9 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     }
     if (bi >= nsolve) break;
     const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
+    // pivots already made by K3P / K3PW (continuation): counted by the
+    // iteration limit, the Bland switch and the reported total
+    const int ib = io.iter_base_list != nullptr ? io.iter_base_list[bi] : io.iter_base;
     const int bw = io.ws_index != nullptr ? io.ws_index[b] : io.list_ws ? bi : b;  // warm start
 
     // lane index made opaque per node: otherwise LICM hoists the 64
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       // anti-cycling (oracle STALL_PIVOTS): past kStallPivots pivots of the
       // solve, Bland's rule: the infeasible row with the lowest basic column,
       // and below the exact minimum ratio with the lowest column on ties
-      const bool bland = iters + io.iter_base >= kStallPivots;
+      const bool bland = iters + ib >= kStallPivots;
       if (best == 0.0) {
         if (!fresh) {
           zB = compute_primals(C, binv);
@@ -495,7 +498,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         fresh = true;
         continue;
       }
-      if (iters >= io.iter_limit) {
+      if (iters + ib >= io.iter_limit) {
         status = 6;
         break;
       }
@@ -703,7 +706,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     }
     if (lane == 0) {
       io.status[b] = status;
-      io.iters[b] = iters + io.iter_base;
+      io.iters[b] = iters + ib;
     }
     STAMP(9);
   }

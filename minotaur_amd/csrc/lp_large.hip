@@ -268,6 +268,9 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
     }
     if (bi >= nsolve) break;
     const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
+    // pivots already made by K3P / K3PW (continuation): counted by the
+    // iteration limit, the Bland switch and the reported total
+    const int ib = io.iter_base_list != nullptr ? io.iter_base_list[bi] : io.iter_base;
     s.nlb = io.lb + (size_t)b * io.box_stride;
     s.nub = io.ub + (size_t)b * io.box_stride;
     s.ocol = io.obj_col != nullptr ? io.obj_col[b] : -1;
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
       // ---- pricing: most infeasible basic row, lowest row on ties; past
       // kStallPivots pivots (oracle STALL_PIVOTS) Bland's rule: the
       // infeasible row with the lowest basic column ----
-      const bool bland = iters + io.iter_base >= kStallPivots;
+      const bool bland = iters + ib >= kStallPivots;
       double best = 0.0, key = -INFINITY;
       int r = INT_MAX;
       for (int i = tid; i < m; i += kT) {
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
         fresh = true;
         continue;
       }
-      if (iters >= io.iter_limit) {
+      if (iters + ib >= io.iter_limit) {
         status = 6;
         break;
       }
@@ -603,7 +606,7 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
     }
     if (tid == 0) {
       io.status[b] = status;
-      io.iters[b] = iters + io.iter_base;
+      io.iters[b] = iters + ib;
     }
   }
 }

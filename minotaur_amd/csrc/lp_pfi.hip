@@ -162,6 +162,79 @@ __device__ __forceinline__ double apply_etas(double v, const double (&eta)[K], i
   return v;
 }
 
+// B0^{-1} a_q (oracle ftran_col, product form, before the etas): four CSC
+// entries' loads in flight, adds in CSC order; lanes >= m give 0
+__device__ __forceinline__ double ftran_b0(const Prob &P, int q, int lane) {
+  const int li = lane < P.m ? lane : 0, ld = P.ld;
+  double alq = 0.0;
+  if (q < P.n) {
+    int t = P.colptr[q];
+    const int e = P.colptr[q + 1];
+    for (; t + 4 <= e; t += 4) {
+      const int r0 = P.rowidx[t], r1 = P.rowidx[t + 1], r2 = P.rowidx[t + 2],
+                r3 = P.rowidx[t + 3];
+      const double c0 = P.cval[t], c1 = P.cval[t + 1], c2 = P.cval[t + 2], c3 = P.cval[t + 3];
+      const double b0 = P.b0[(size_t)r0 * ld + li], b1 = P.b0[(size_t)r1 * ld + li];
+      const double b2 = P.b0[(size_t)r2 * ld + li], b3 = P.b0[(size_t)r3 * ld + li];
+      alq += b0 * c0;
+      alq += b1 * c1;
+      alq += b2 * c2;
+      alq += b3 * c3;
+    }
+    for (; t < e; ++t) alq += P.b0[(size_t)P.rowidx[t] * ld + li] * P.cval[t];
+  } else {
+    alq = -P.b0[(size_t)(q - P.n) * ld + li];
+  }
+  return lane < P.m ? alq : 0.0;
+}
+
+// u <- u' E_{k-1} ... E_0 (oracle pfi_btran's eta loop): each E_t' rewrites
+// component prow[t] with a dot product over the nonzeros of u, ascending
+template <int K>
+__device__ __forceinline__ double btran_etas(double u, const double (&eta)[K], int prow, int k,
+                                             int lane) {
+#pragma unroll
+  for (int t = K - 1; t >= 0; --t) {
+    if (t < k) {
+      uint64_t mask = __ballot(u != 0.0);
+      const double pr = u * eta[t];  // the oracle's products, lane-parallel
+      double acc = 0.0;
+      while (mask) {
+        const int i = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        acc += rld(pr, i);
+      }
+      if (lane == rl(prow, t)) u = acc;
+    }
+  }
+  return u;
+}
+
+// (u' B0^{-1})_lane over the nonzero rows of u, ascending (four loads in
+// flight, adds in order)
+__device__ __forceinline__ double u_b0(const Prob &P, double u, int lane) {
+  uint64_t mask = __ballot(u != 0.0);
+  double rk = 0.0;
+  const size_t lk = (size_t)(lane < P.m ? lane : 0) * P.ld;
+  while (mask) {
+    int ii[4];
+    int c = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      ii[t] = mask ? __builtin_ctzll(mask) : 0;
+      c += mask ? 1 : 0;
+      mask &= mask - 1;
+    }
+    double bv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bv[t] = P.b0[lk + ii[t]];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < c) rk += rld(u, ii[t]) * bv[t];
+  }
+  return rk;
+}
+
 template <int S, int K>
 __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP lp, LpIO io,
                                                                        PfiIO px) {
@@ -238,11 +311,17 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         io.status[b] = kUnknownStatus;
         io.obj[b] = INFINITY;
         io.iters[b] = 0;
+        if (io.path.k_out != nullptr) io.path.k_out[b] = 0;
       }
       PSTAMP(9);
       continue;
     }
 
+    // path warm start (the batched tree's warm mode 2): k pivots from the
+    // shared basis, the node's own statuses
+    const int kpath = io.path.k != nullptr ? io.path.k[b] : 0;
+    const uint32_t *ppath = io.path.path + (size_t)b * kPathMax;
+    const int8_t *pst = io.path.st + (size_t)b * N;
     // ---- working bounds; an empty box is infeasible before any pivot ----
     double tl[S], th[S];
     int sa[S];
@@ -253,7 +332,8 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       const bool valid = j < N;
       tl[s] = valid ? P.tlo(j) : 0.0;
       th[s] = valid ? P.thi(j) : 0.0;
-      sa[s] = valid ? s_wst[j] : ST_BASIC;  // slots past N act as basic: never touched
+      // slots past N act as basic: never touched
+      sa[s] = valid ? (kpath > 0 ? (int)pst[j] : s_wst[j]) : ST_BASIC;
       bad |= valid && tl[s] > th[s] + kPTol;
       if (valid) {
         lo[j] = tl[s];
@@ -265,21 +345,63 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         io.status[b] = 2;
         io.obj[b] = INFINITY;
         io.iters[b] = 0;
+        if (io.path.k_out != nullptr) io.path.k_out[b] = 0;
       }
       PSTAMP(9);
       continue;
     }
     wave_sync();
 
-    // ---- basis rows: head and bounds (basic columns carry no artificial box)
+    double eta[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) eta[t] = 0.0;
+    int prow = 0;  // lane t: pivot row of eta t
+    int pq = 0;    // lane t: entering column of eta t (path outputs)
+    int ne = 0;    // eta columns: the path's replayed pivots, then this solve's
+
+    // ---- basis rows: head, replayed path pivots, bounds (basic columns
+    // carry no artificial box)
     int h = lane < m ? s_whead[lane] : -1;
+    for (int t = 0; t < kpath; ++t) {
+      // the pivot's eta exactly as the solve that made it built it: FTRAN of
+      // the entering column through B0^{-1} and the etas so far
+      const uint32_t pv = ppath[t];
+      const int q = (int)(pv & 0xFFFFu), r = (int)(pv >> 16);
+      const double alq = apply_etas(ftran_b0(P, q, lane), eta, prow, ne, lane);
+      const double inv = 1.0 / rld(alq, r);
+      const double e = lane == r ? inv : -alq * inv;
+#pragma unroll
+      for (int u = 0; u < K; ++u)
+        if (u == ne) eta[u] = e;
+      if (lane == ne) {
+        prow = r;
+        pq = q;
+      }
+      if (lane == r) h = q;
+      ++ne;
+    }
     double lbB = 0.0, ubB = 0.0;
     if (lane < m) {
       lbB = lo[h];
       ubB = hi[h];
     }
     double d[S];
-    if (P.ocol < 0) {
+    if (kpath > 0) {
+      // reduced costs of the path's basis (oracle pfi_compute_duals): u = c_B
+      // through the etas backwards (BTRAN), rho = u' B0^{-1}, d = c - rho' A
+      double u = (lane < m && h < n) ? P.c[h] : 0.0;
+      u = btran_etas(u, eta, prow, ne, lane);
+      rho[lane] = lane < m ? u_b0(P, u, lane) : 0.0;
+      wave_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = s * 64 + lane;
+        d[s] = 0.0;
+        if (j < N && sa[s] != ST_BASIC)
+          d[s] = (j < n ? P.c[j] : 0.0) - (j >= n ? -rho[j - n] : P.col_dot(rho, j));
+      }
+      wave_sync();
+    } else if (P.ocol < 0) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int j = s * 64 + lane;
@@ -356,11 +478,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       sa[s] = st | art | (lo_j == hi_j ? kFixed : 0);
     }
 
-    double eta[K];
-#pragma unroll
-    for (int t = 0; t < K; ++t) eta[t] = 0.0;
-    int prow = 0;  // lane t: pivot row of eta t
-    int iters = 0;
+    int iters = 0;  // this solve's own pivots
 
     // oracle compute_primals (product form): z_B = -E...E B0^{-1} (N z_N)
     auto primals = [&]() -> double {
@@ -388,7 +506,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       }
       for (; k < m; ++k) sacc += P.b0[(size_t)k * ld + li] * rld(w, k);
       if (lane >= m) sacc = 0.0;
-      sacc = apply_etas(sacc, eta, prow, iters, lane);
+      sacc = apply_etas(sacc, eta, prow, ne, lane);
       return -sacc;
     };
     // oracle grow_art
@@ -457,50 +575,18 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         status = 6;
         break;
       }
-      if (iters >= kmax) {  // eta file full: the dense K3 re-solves this node
+      if (ne >= kmax) {  // eta file full: the dense K3 continues this node
         status = -1;
         break;
       }
       const double delta = rld(inf, r);
       const double sigma = delta > 0 ? 1.0 : -1.0;
 
-      // ---- BTRAN: u = e_r' E_{k-1} ... E_0 over the nonzeros of u ----
-      double u = lane == r ? 1.0 : 0.0;
-#pragma unroll
-      for (int t = K - 1; t >= 0; --t) {
-        if (t < iters) {
-          uint64_t mask = __ballot(u != 0.0);
-          const double pr = u * eta[t];  // the oracle's products, lane-parallel
-          double acc = 0.0;
-          while (mask) {
-            const int i = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            acc += rld(pr, i);
-          }
-          if (lane == rl(prow, t)) u = acc;
-        }
-      }
-      {  // rho' = u' B0^{-1} (ascending nonzero rows), published to LDS
-        uint64_t mask = __ballot(u != 0.0);
-        double rk = 0.0;
-        const size_t lk = (size_t)(lane < m ? lane : 0) * ld;
-        while (mask) {  // up to four rows per round: loads first, adds in order
-          int ii[4];
-          int c = 0;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            ii[t] = mask ? __builtin_ctzll(mask) : 0;
-            c += mask ? 1 : 0;
-            mask &= mask - 1;
-          }
-          double bv[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) bv[t] = P.b0[lk + ii[t]];
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            if (t < c) rk += rld(u, ii[t]) * bv[t];
-        }
-        rho[lane] = lane < m ? rk : 0.0;
+      // ---- BTRAN: u = e_r' E_{k-1} ... E_0 over the nonzeros of u, then
+      // rho' = u' B0^{-1}, published to LDS ----
+      {
+        const double u = btran_etas(lane == r ? 1.0 : 0.0, eta, prow, ne, lane);
+        rho[lane] = lane < m ? u_b0(P, u, lane) : 0.0;
       }
       wave_sync();
       PSTAMP(3);
@@ -575,31 +661,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       const int ql = q & 63, qs = q >> 6;
 
       // ---- FTRAN: alpha_q = E...E B0^{-1} a_q ----
-      double alq = 0.0;
-      {
-        const int li = lane < m ? lane : 0;
-        if (q < n) {  // four entries' loads in flight, adds in CSC order
-          int t = P.colptr[q];
-          const int e = P.colptr[q + 1];
-          for (; t + 4 <= e; t += 4) {
-            const int r0 = P.rowidx[t], r1 = P.rowidx[t + 1], r2 = P.rowidx[t + 2],
-                      r3 = P.rowidx[t + 3];
-            const double c0 = P.cval[t], c1 = P.cval[t + 1], c2 = P.cval[t + 2],
-                         c3 = P.cval[t + 3];
-            const double b0 = P.b0[(size_t)r0 * ld + li], b1 = P.b0[(size_t)r1 * ld + li];
-            const double b2 = P.b0[(size_t)r2 * ld + li], b3 = P.b0[(size_t)r3 * ld + li];
-            alq += b0 * c0;
-            alq += b1 * c1;
-            alq += b2 * c2;
-            alq += b3 * c3;
-          }
-          for (; t < e; ++t) alq += P.b0[(size_t)P.rowidx[t] * ld + li] * P.cval[t];
-        } else {
-          alq = -P.b0[(size_t)(q - n) * ld + li];
-        }
-        if (lane >= m) alq = 0.0;
-      }
-      alq = apply_etas(alq, eta, prow, iters, lane);
+      const double alq = apply_etas(ftran_b0(P, q, lane), eta, prow, ne, lane);
       const double arq = rld(alq, r);
       PSTAMP(6);
 
@@ -650,8 +712,12 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       const double e = lane == r ? inv : -alq * inv;
 #pragma unroll
       for (int t = 0; t < K; ++t)
-        if (t == iters) eta[t] = e;
-      if (lane == iters) prow = r;
+        if (t == ne) eta[t] = e;
+      if (lane == ne) {
+        prow = r;
+        pq = q;
+      }
+      ++ne;
       ++iters;
       fresh = false;
       PSTAMP(7);
@@ -665,8 +731,12 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       int slot = 0;
       if (lane == 0) slot = atomicAdd(px.ovf_count, 1);
       slot = rl(slot, 0);
-      if (lane == 0) px.ovf_list[slot] = b;
+      if (lane == 0) {
+        px.ovf_list[slot] = b;
+        if (io.path.k_out != nullptr) io.path.k_out[b] = 0;   // children: from the root
+      }
       if (slot < px.ovf_cap) {
+        if (lane == 0) px.c_iters[slot] = iters;
         if (lane < m) px.c_head[(size_t)slot * m + lane] = h;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -680,7 +750,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         const int li = lane < m ? lane : 0;
         for (int c = 0; c < m; ++c) {
           double v = lane < m ? P.b0[(size_t)c * ld + li] : 0.0;
-          v = apply_etas(v, eta, prow, iters, lane);
+          v = apply_etas(v, eta, prow, ne, lane);
           if (lane < m) cb[(size_t)c * m + lane] = v;  // column-major (ABI layout)
         }
       }
@@ -708,6 +778,20 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     if (lane == 0) {
       io.status[b] = status;
       io.iters[b] = iters;
+    }
+    if (io.path.k_out != nullptr) {
+      // the node's final path for its children: optimal in the product form
+      // with at most `inherit` etas, else the root (k_out 0)
+      const int ko = (status == 0 && ne > 0 && ne <= io.path.inherit) ? ne : 0;
+      if (lane == 0) io.path.k_out[b] = ko;
+      if (lane < ko) io.path.path_out[(size_t)b * kPathMax + lane] = (uint32_t)pq | ((uint32_t)prow << 16);
+      if (ko > 0) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int j = s * 64 + lane;
+          if (j < N) io.path.st_out[(size_t)b * N + j] = (int8_t)(sa[s] & 3);
+        }
+      }
     }
     wave_sync();
     PSTAMP(8);

@@ -128,8 +128,28 @@ struct LpIO {
   const int32_t *node_list;
   const int32_t *node_count;
   int list_lo, list_hi, list_ws, iter_base;
+  // per list position: the pivots already made (K3P's continuation slots;
+  // null = iter_base); the iteration limit and the Bland switch count them
+  const int32_t *iter_base_list;
   int32_t *next;                // K3L: zeroed device node counter (dynamic schedule) or null
+  // Path warm starts (K3P only; path.k == null: none).  Node b starts from
+  // the shared warm start (the root basis) after its k[b] pivots path[b]
+  // (entering column | row << 16, stride kPathMax) with column statuses
+  // st[b][n+m]; k[b] <= 0 = the shared warm start itself.  Out (optional):
+  // the node's final path for its children, k_out 0 = restart from the root
+  // (not optimal in the product form, or longer than `inherit` pivots).
+  struct {
+    const int32_t *k;
+    const uint32_t *path;
+    const int8_t *st;
+    int32_t *k_out;
+    uint32_t *path_out;
+    int8_t *st_out;
+    int inherit;
+  } path;
 };
+constexpr int kPathMax = 32;    // pivots per path warm start (MGPU_PATH_MAX)
+constexpr int kPathInherit = 24; // longest path the batched tree hands to children
 
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
@@ -155,6 +175,7 @@ struct PfiIO {
   // basis head [m], column status [n+m], reduced costs [n+m], explicit
   // B^-1 = E...E B0^-1 [m][m] column-major
   int ovf_cap;
+  int32_t *c_iters;             // [slot] the node's own pivots at the overflow
   int32_t *c_head;
   int8_t *c_st;
   double *c_d, *c_binv;

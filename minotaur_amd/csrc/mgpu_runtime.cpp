@@ -260,6 +260,7 @@ int mgpu_set_lp_pfi_wide(mgpu_ctx *c, int kmax) {
 }
 
 static_assert(MGPU_LP_PFI_MAX == kPfiMax, "ABI eta-file cap = kernel's");
+static_assert(MGPU_PATH_MAX == kPathMax, "ABI path cap = kernel's");
 static_assert(MGPU_LP_PFI_WIDE_MAX == kPfiWideMax, "ABI eta-file cap = kernel's");
 
 int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
@@ -522,9 +523,16 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     const size_t max_slots = kPfiOvfBytes / slot_bytes;
     const int cap = (size_t)io.batch < max_slots ? io.batch : (int)max_slots;
     HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 4) * sizeof(int32_t)));
+    if (io.path.k != nullptr && (wide || kcap > kPathMax))
+      return fail(c, MGPU_ERR_ARG, "%s: path warm starts run on K3P (m <= 64) with an eta cap "
+                  "<= %d", who, kPathMax);
+    if (io.path.k != nullptr && cap < io.batch)
+      return fail(c, MGPU_ERR_NOMEM, "%s: path warm starts need a continuation slot per LP "
+                  "(%d LPs, %d slots)", who, io.batch, cap);
     const size_t sb_head = al16h((size_t)cap * m * 4), sb_st = al16h((size_t)cap * N),
-                 sb_d = al16h((size_t)cap * N * 8), sb_binv = (size_t)cap * m * m * 8;
-    HIPCHK(c, c->pfi_cont.ensure(sb_head + sb_st + sb_d + sb_binv));
+                 sb_d = al16h((size_t)cap * N * 8), sb_binv = al16h((size_t)cap * m * m * 8),
+                 sb_it = (size_t)cap * 4;
+    HIPCHK(c, c->pfi_cont.ensure(sb_head + sb_st + sb_d + sb_binv + sb_it));
     // [0] overflow count, [1] K3P's next node, [2]/[3] the K3 follow-ups'
     int32_t *cnt = c->pfi_ovf.as<int32_t>();
     HIPCHK(c, hipMemsetAsync(cnt, 0, 4 * sizeof(int32_t), c->stream));
@@ -539,6 +547,7 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     px.c_st = (int8_t *)(cp + sb_head);
     px.c_d = (double *)(cp + sb_head + sb_st);
     px.c_binv = (double *)(cp + sb_head + sb_st + sb_d);
+    px.c_iters = (int32_t *)(cp + sb_head + sb_st + sb_d + sb_binv);
     if (wide) {
       HIPCHK(c, launch_lp_pfiw(c->lp, io, px, c->num_cus, c->stream));
     } else {
@@ -563,8 +572,11 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     io2.list_lo = 0;
     io2.list_hi = cap;
     io2.list_ws = 1;
+    // the pivots each node already made: kmax for K3PW; K3P's own pivots per
+    // slot (a path warm start's replayed pivots fill part of the eta file)
     io2.iter_base = px.kmax;
-    io2.iter_limit = io.iter_limit - px.kmax;  // K3P only overflows below the limit
+    io2.iter_base_list = wide ? nullptr : px.c_iters;
+    io2.iter_limit = io.iter_limit;
     io2.ws = LpWarm{px.c_head, px.c_st, px.c_d, px.c_binv, m, N, N, (long)m * m};
     io2.next = cnt + 2;
     HIPCHK(c, dense(io2));
@@ -809,6 +821,118 @@ int mgpu_lp_solve(mgpu_ctx *c, int batch, const double *lb, const double *ub,
     HIPCHK(c, hipMemcpyAsync(wo_st, c->lp_ost.p, B * N, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(wo_d, c->lp_od.p, B * N * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(wo_binv, c->lp_ob.p, B * m * m * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(c, hipStreamSynchronize(s));
+  return MGPU_OK;
+}
+
+int mgpu_lp_solve_path_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                           const int32_t *skip, const int32_t *ws_head, const int8_t *ws_st,
+                           const double *ws_d, const double *ws_binv, const int32_t *k_in,
+                           const uint32_t *path_in, const int8_t *st_in, int inherit,
+                           int iter_limit, int32_t *status, double *obj, int32_t *iters,
+                           double *x, int32_t *k_out, uint32_t *path_out, int8_t *st_out) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_path: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb || !ub || !status || !obj || !iters || !ws_head ||
+                                  !ws_st || !ws_d || !ws_binv || !k_in || !path_in ||
+                                  !st_in)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_path: bad argument");
+  if (k_out && (!path_out || !st_out))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_path: path output needs k, path and st");
+  if (inherit < 0 || inherit > MGPU_PATH_MAX)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_path: inherit must be in 0..%d", MGPU_PATH_MAX);
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  LpIO io{};
+  io.batch = batch;
+  io.lb = lb;
+  io.ub = ub;
+  io.box_stride = c->lp.n;
+  io.skip = skip;
+  io.ws.head = ws_head;
+  io.ws.st = ws_st;
+  io.ws.d = ws_d;
+  io.ws.binv = ws_binv;
+  io.iter_limit = lp_iter_limit(iter_limit);
+  io.status = status;
+  io.obj = obj;
+  io.iters = iters;
+  io.x = x;
+  io.path.k = k_in;
+  io.path.path = path_in;
+  io.path.st = st_in;
+  io.path.k_out = k_out;
+  io.path.path_out = path_out;
+  io.path.st_out = st_out;
+  io.path.inherit = inherit;
+  if (!use_pfi(c, io))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_path: path warm starts need K3P (m <= 64, "
+                "n + m <= %d, eta cap > 0)", 64 * kPfiSlots);
+  HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+  const int rc = launch_lp(c, io, "mgpu_lp_solve_path");
+  if (rc != MGPU_OK) return rc;
+  HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+  return MGPU_OK;
+}
+
+int mgpu_lp_solve_path(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                       const int32_t *ws_head, const int8_t *ws_st, const double *ws_d,
+                       const double *ws_binv, const int32_t *k_in, const uint32_t *path_in,
+                       const int8_t *st_in, int inherit, int iter_limit, int32_t *status,
+                       double *obj, int32_t *iters, double *x, int32_t *k_out,
+                       uint32_t *path_out, int8_t *st_out) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_path: no problem loaded");
+  if (batch < 0 || (batch > 0 && (!lb || !ub || !status || !obj || !iters || !ws_head ||
+                                  !ws_st || !ws_d || !ws_binv || !k_in || !path_in || !st_in)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_path: bad argument");
+  if (batch == 0) return MGPU_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = c->lp.n, m = c->lp.m, N = n + m;
+  const size_t B = (size_t)batch, P = MGPU_PATH_MAX;
+  hipStream_t s = c->stream;
+  DevBuf buf;  // per-call workspace
+  const size_t o_lb = 0, o_ub = o_lb + B * n * 8, o_wh = o_ub + B * n * 8,
+               o_wst = o_wh + al16h((size_t)m * 4), o_wd = o_wst + al16h((size_t)N),
+               o_wb = o_wd + (size_t)N * 8, o_k = o_wb + (size_t)m * m * 8,
+               o_p = o_k + al16h(B * 4), o_st = o_p + B * P * 4, o_ost = o_st + al16h(B * N),
+               o_ok = o_ost + al16h(B * N), o_op = o_ok + al16h(B * 4),
+               o_stt = o_op + B * P * 4, o_obj = o_stt + al16h(B * 4),
+               o_it = o_obj + B * 8, o_x = o_it + al16h(B * 4), total = o_x + B * n * 8;
+  HIPCHK(c, buf.ensure(total));
+  char *d = buf.as<char>();
+  auto h2d = [&](size_t off, const void *src, size_t bytes) {
+    return hipMemcpyAsync(d + off, src, bytes, hipMemcpyHostToDevice, s);
+  };
+  HIPCHK(c, h2d(o_lb, lb, B * n * 8));
+  HIPCHK(c, h2d(o_ub, ub, B * n * 8));
+  HIPCHK(c, h2d(o_wh, ws_head, (size_t)m * 4));
+  HIPCHK(c, h2d(o_wst, ws_st, (size_t)N));
+  HIPCHK(c, h2d(o_wd, ws_d, (size_t)N * 8));
+  HIPCHK(c, h2d(o_wb, ws_binv, (size_t)m * m * 8));
+  HIPCHK(c, h2d(o_k, k_in, B * 4));
+  HIPCHK(c, h2d(o_p, path_in, B * P * 4));
+  HIPCHK(c, h2d(o_st, st_in, B * N));
+  int rc = mgpu_lp_solve_path_dev(
+      c, batch, (double *)(d + o_lb), (double *)(d + o_ub), nullptr, (int32_t *)(d + o_wh),
+      (int8_t *)(d + o_wst), (double *)(d + o_wd), (double *)(d + o_wb), (int32_t *)(d + o_k),
+      (uint32_t *)(d + o_p), (int8_t *)(d + o_st), inherit, iter_limit, (int32_t *)(d + o_stt),
+      (double *)(d + o_obj), (int32_t *)(d + o_it), x ? (double *)(d + o_x) : nullptr,
+      k_out ? (int32_t *)(d + o_ok) : nullptr, k_out ? (uint32_t *)(d + o_op) : nullptr,
+      k_out ? (int8_t *)(d + o_ost) : nullptr);
+  if (rc != MGPU_OK) return rc;
+  auto d2h = [&](void *dst, size_t off, size_t bytes) {
+    return hipMemcpyAsync(dst, d + off, bytes, hipMemcpyDeviceToHost, s);
+  };
+  HIPCHK(c, d2h(status, o_stt, B * 4));
+  HIPCHK(c, d2h(obj, o_obj, B * 8));
+  HIPCHK(c, d2h(iters, o_it, B * 4));
+  if (x) HIPCHK(c, d2h(x, o_x, B * n * 8));
+  if (k_out) {
+    HIPCHK(c, d2h(k_out, o_ok, B * 4));
+    if (path_out) HIPCHK(c, d2h(path_out, o_op, B * P * 4));
+    if (st_out) HIPCHK(c, d2h(st_out, o_ost, B * N));
   }
   HIPCHK(c, hipStreamSynchronize(s));
   return MGPU_OK;

@@ -21,6 +21,8 @@ _D = ctypes.c_double
 
 LP_PFI_MAX = 32  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
 LP_PFI_WIDE_MAX = 32  # MGPU_LP_PFI_WIDE_MAX: K3PW eta-file cap
+PATH_MAX = 32  # MGPU_PATH_MAX: pivots per path warm start
+PATH_INHERIT = 24  # the batched tree's longest path handed to children (warm mode 2)
 
 # Every entry point declared in include/mgpu.h (checked by the CPU tests).
 EXPORTS = [
@@ -34,7 +36,8 @@ EXPORTS = [
     'mgpu_bnb_import', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
     'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
-    'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap',
+    'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
+    'mgpu_lp_solve_path_dev',
 ]
 
 
@@ -115,6 +118,8 @@ def load_library():
     lib.mgpu_lp_refactor.argtypes = [_P] + [_P] * 7
     lib.mgpu_lp_solve_rows.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
     lib.mgpu_lp_solve_rows_dev.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
+    lib.mgpu_lp_solve_path.argtypes = [_P, _I] + [_P] * 9 + [_I, _I] + [_P] * 7
+    lib.mgpu_lp_solve_path_dev.argtypes = [_P, _I] + [_P] * 10 + [_I, _I] + [_P] * 7
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -398,6 +403,32 @@ class Context:
             _hp(wo.head) if wo else None, _hp(wo.st) if wo else None,
             _hp(wo.d) if wo else None, _hp(wo.binv) if wo else None), 'mgpu_lp_solve')
         return LpOut(st, obj, it, x, wo)
+
+    def lp_solve_path(self, lb, ub, ws, k_in, path_in, st_in, inherit=PATH_INHERIT,
+                      iter_limit=0, want_x=True):
+        """Path warm starts (mgpu_lp_solve_path): node b starts from the shared
+        root basis ``ws`` after its k_in[b] pivots path_in[b] with statuses
+        st_in[b].  Returns (LpOut, k_out, path_out, st_out)."""
+        p = self.problem
+        lb = _np(lb, np.float64)
+        ub = _np(ub, np.float64)
+        B, N = lb.shape[0], p.n + p.m
+        st = np.zeros(B, dtype=np.int32)
+        obj = np.zeros(B)
+        it = np.zeros(B, dtype=np.int32)
+        x = np.zeros((B, p.n)) if want_x else None
+        k_out = np.zeros(B, dtype=np.int32)
+        path_out = np.zeros((B, PATH_MAX), dtype=np.uint32)
+        st_out = np.zeros((B, N), dtype=np.int8)
+        k_in = _np(k_in, np.int32)
+        path_in = _np(path_in, np.uint32).reshape(B, PATH_MAX)
+        st_in = _np(st_in, np.int8).reshape(B, N)
+        self._chk(self.lib.mgpu_lp_solve_path(
+            self.h, B, _hp(lb), _hp(ub), _hp(_np(ws.head, np.int32)), _hp(_np(ws.st, np.int8)),
+            _hp(_np(ws.d, np.float64)), _hp(_np(ws.binv, np.float64)), _hp(k_in), _hp(path_in),
+            _hp(st_in), int(inherit), int(iter_limit), _hp(st), _hp(obj), _hp(it), _hp(x),
+            _hp(k_out), _hp(path_out), _hp(st_out)), 'mgpu_lp_solve_path')
+        return LpOut(st, obj, it, x, None), k_out, path_out, st_out
 
     def lp_solve_dev(self, lb, ub, status, obj, iters, ws=None, skip=None, iter_limit=0,
                      x=None, wo=None):

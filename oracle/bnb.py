@@ -13,7 +13,10 @@ children), same pool order:
   to the free slots in the engine's order (the slots just taken, the older
   holes ascending, then new slots);
 * warm 0: node LPs from the root optimum (shared); warm 1: from the parent's
-  optimal basis, whose own optimum is handed to both children;
+  optimal basis, whose own optimum is handed to both children; warm 2: from
+  the parent's optimal basis kept as its pivot path from the root basis
+  (oracle.dual_simplex_path, K3P's product form), paths of at most
+  min(24, pfi) pivots handed on, else the children restart from the root;
 * brancher 0: MaxVioBrancher; brancher 1: the batched ReliabilityBrancher of
   bnb_rel.hip (pseudocosts frozen at the round's start plus each node's own
   updateAfterSolve observation, strong-branching LPs from each node's optimal
@@ -56,16 +59,18 @@ def _order_key(v):
 
 
 class _Node:
-    __slots__ = ('lb', 'ub', 'nlb', 'depth', 'ws', 'pvar', 'pval')
+    __slots__ = ('lb', 'ub', 'nlb', 'depth', 'ws', 'pvar', 'pval', 'path')
 
-    def __init__(self, lb, ub, nlb, depth, ws=None, pvar=-1, pval=0.0):
+    def __init__(self, lb, ub, nlb, depth, ws=None, pvar=-1, pval=0.0, path=None):
         self.lb, self.ub, self.nlb, self.depth, self.ws = lb, ub, nlb, depth, ws
         self.pvar, self.pval = pvar, pval
+        self.path = path    # warm 2: (k, pivots, statuses) or None = the root basis
 
 
 # ReliabilityBrancher defaults (ReliabilityBrancher.cpp:43-58)
 REL_MAX_CANDS, REL_ITER, REL_THRESH, REL_MIN_DIST, REL_ETOL = 20, 25, 4, 50, 1e-6
 REL_MAX_DEPTH = 1000   # maxDepth_: no strong branching below it (:105)
+PATH_INHERIT = 24      # warm 2: longest path handed to children (bnb.cpp kPathInherit)
 
 
 def _rel_score(up, down):
@@ -170,6 +175,20 @@ class CpuBnbContext:
                 for t, i in enumerate(keep):
                     wo[i] = oracle.WarmStart(w2.head[t].copy(), w2.st[t].copy(),
                                              w2.binv[t].copy(), w2.d[t].copy())
+            elif self.warm == 2:
+                N = p.n + p.m
+                k_in = np.zeros(keep.size, np.int32)
+                path_in = np.zeros((keep.size, oracle.PATH_MAX), np.uint32)
+                st_in = np.zeros((keep.size, N), np.int8)
+                for t, i in enumerate(keep):
+                    if nodes[i].path is not None:
+                        k_in[t], path_in[t], st_in[t] = nodes[i].path
+                s2, o2, i2, x2, ko, po, so = oracle.dual_simplex_path(
+                    p, f.lb[keep], f.ub[keep], self.ws, k_in, path_in, st_in, self.pfi,
+                    min(PATH_INHERIT, self.pfi))
+                self.tot.pfi_pivots += int(np.minimum(i2, self.pfi).sum())
+                for t, i in enumerate(keep):
+                    wo[i] = (int(ko[t]), po[t].copy(), so[t].copy()) if ko[t] > 0 else None
             elif self.warm:
                 ws = oracle.WarmStart(*(np.stack([getattr(nodes[i].ws, k) for i in keep])
                                         for k in ('head', 'st', 'binv', 'd')))
@@ -203,7 +222,8 @@ class CpuBnbContext:
                 j, v, up_first = choice[i]
             else:
                 j, v, up_first = self._branch(x[i], ints)
-            w = wo[i] if self.warm else self.ws
+            w = wo[i] if self.warm == 1 else self.ws
+            path = wo[i] if self.warm == 2 else None
             if dec == 5:
                 # ModifiedByBrancher: the node again with the bound change
                 nd = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth, w)
@@ -213,9 +233,10 @@ class CpuBnbContext:
                     nd.ub[j] = math.floor(v)
                 children.append(nd)
                 continue
-            down = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w, j, v)
+            down = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w, j, v,
+                         path)
             down.ub[j] = math.floor(v)
-            up = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w, j, v)
+            up = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth + 1, w, j, v, path)
             up.lb[j] = math.ceil(v)
             if self.order == 0:
                 children += [down, up] if up_first else [up, down]   # preferred on top

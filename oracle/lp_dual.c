@@ -52,8 +52,25 @@ typedef struct {
   const double *binv0;
   double *eta;         /* pfi x m: eta column t */
   int *prow;           /* pivot row of eta t */
+  int *pq;             /* entering column of eta t (path warm starts) */
   double *u;           /* m: BTRAN work vector */
 } lpw;
+
+/* Path warm start of the batched tree's warm mode 2 (bnb.cpp): the node's
+ * basis is the shared root basis after its path of k pivots (entering column
+ * q, row r; packed q | r << 16), with its own column statuses; the etas are
+ * rebuilt by FTRAN in path order (the parent's own arithmetic), the reduced
+ * costs recomputed from the basis.  k <= 0: the root basis as is.  Out: the
+ * node's final path (k_out = 0: children restart from the root). */
+typedef struct {
+  int k;
+  const unsigned *path;
+  const signed char *st;
+  int inherit;         /* longest path handed to children */
+  int *k_out;
+  unsigned *path_out;
+  signed char *st_out;
+} orc_path;
 
 static double bnd_lo(const orc_lp *P, const double *lb, int j) {
   return j < P->n ? lb[j] : P->rlo[j - P->n];
@@ -292,11 +309,37 @@ static int invert_basis(lpw *W) {
  * status -1 (the caller re-solves it densely, as the GPU does).  No
  * warm-start or dual output in this mode.
  */
+/* y' = c_B' E_{k-1} ... E_0 B0^{-1} (pfi_btran's loops from u = c_B), then
+ * d_j = c_j - y' a_j: the reduced costs of a path warm start. */
+static void pfi_compute_duals(lpw *W) {
+  const orc_lp *P = W->P;
+  int m = P->m, N = W->N;
+  double *u = W->u, *y = W->rho;
+  for (int i = 0; i < m; ++i) u[i] = W->head[i] < P->n ? P->c[W->head[i]] : 0.0;
+  for (int t = W->neta - 1; t >= 0; --t) {
+    const double *e = W->eta + (size_t) t * m;
+    double acc = 0.0;
+    for (int i = 0; i < m; ++i)
+      if (u[i] != 0.0) acc += u[i] * e[i];
+    u[W->prow[t]] = acc;
+  }
+  for (int k = 0; k < m; ++k) y[k] = 0.0;
+  for (int i = 0; i < m; ++i) {
+    if (u[i] == 0.0) continue;
+    for (int k = 0; k < m; ++k) y[k] += u[i] * W->binv0[(size_t) i * m + k];
+  }
+  for (int j = 0; j < N; ++j) {
+    if (W->st[j] == ST_BASIC) { W->d[j] = 0.0; continue; }
+    double cj = j < P->n ? P->c[j] : 0.0;
+    W->d[j] = cj - col_dot(P, y, j);
+  }
+}
+
 static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub,
                              int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
                              int have_ws, int have_binv, int iter_limit, double *obj_out,
                              double *x_out, double *y_out, int *iters_out, int pfi,
-                             int iter_base)
+                             int iter_base, const orc_path *path)
 {
   int n = P->n, m = P->m, N = n + m;
   lpw W;
@@ -309,6 +352,7 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
     W.binv0 = ws_binv;
     W.eta = (double *) malloc(sizeof(double) * (size_t) pfi * m + 8);
     W.prow = (int *) malloc(sizeof(int) * (size_t) pfi + 4);
+    W.pq = (int *) malloc(sizeof(int) * (size_t) pfi + 4);
     W.u = (double *) malloc(sizeof(double) * (size_t) m + 8);
   }
   W.blo = (double *) malloc(sizeof(double) * N);
@@ -352,7 +396,23 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
     for (int i = 0; i < m * m; ++i) W.binv[i] = 0.0;
     for (int i = 0; i < m; ++i) W.binv[i * m + i] = -1.0;
   }
-  if (have_ws && have_binv && ws_d) {
+  if (path && path->k > 0 && W.pfi) {
+    /* path warm start: replay the path's pivots on the root basis (FTRAN of
+     * each entering column through B0^{-1} and the etas so far: the eta the
+     * pivot made), the node's statuses, reduced costs of that basis */
+    for (int t = 0; t < path->k; ++t) {
+      int q = (int) (path->path[t] & 0xFFFFu), r = (int) (path->path[t] >> 16);
+      ftran_col(&W, q, W.alpha_q);
+      double inv = 1.0 / W.alpha_q[r];
+      double *e = W.eta + (size_t) W.neta * m;
+      for (int i = 0; i < m; ++i) e[i] = i == r ? inv : -W.alpha_q[i] * inv;
+      W.pq[W.neta] = q;
+      W.prow[W.neta++] = r;
+      W.head[r] = q;
+    }
+    for (int j = 0; j < N; ++j) W.st[j] = path->st[j];
+    pfi_compute_duals(&W);
+  } else if (have_ws && have_binv && ws_d) {
     /* reduced costs depend only on the basis: reuse the parent's */
     for (int j = 0; j < N; ++j) W.d[j] = W.st[j] == ST_BASIC ? 0.0 : ws_d[j];
   } else {
@@ -414,7 +474,7 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       continue;
     }
     if (iters >= iter_limit) { status = 6; break; }   /* EngineIterationLimit */
-    if (W.pfi && iters >= W.pfi) {
+    if (W.pfi && W.neta >= W.pfi) {
       /* eta file full: the dense solve continues from this basis with its
        * explicit inverse E_{k-1}...E_0 B0^{-1}, column by column */
       for (int c = 0; c < m; ++c) {
@@ -511,6 +571,7 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       double inv = 1.0 / arq;
       double *e = W.eta + (size_t) W.neta * m;
       for (int i = 0; i < m; ++i) e[i] = i == r ? inv : -W.alpha_q[i] * inv;
+      W.pq[W.neta] = q;
       W.prow[W.neta++] = r;
     } else {
       double inv = 1.0 / arq;
@@ -557,9 +618,17 @@ done:
     *obj_out = status == 2 ? INFINITY : -INFINITY;
   }
   if (iters_out) *iters_out = iters;
+  if (path && path->k_out) {
+    /* the node's final path for its children: optimal in the product form
+     * with a path no longer than `inherit`, else the root (k_out 0) */
+    int ko = (W.pfi && status == 0 && W.neta > 0 && W.neta <= path->inherit) ? W.neta : 0;
+    *path->k_out = ko;
+    for (int t = 0; t < ko; ++t) path->path_out[t] = (unsigned) W.pq[t] | ((unsigned) W.prow[t] << 16);
+    if (ko) for (int j = 0; j < N; ++j) path->st_out[j] = W.st[j];
+  }
   free(W.blo); free(W.bhi); free(W.art); free(W.z); free(W.d); free(W.binv);
   free(W.head); free(W.st); free(W.rho); free(W.w); free(W.alpha_r); free(W.alpha_q);
-  free(W.eta); free(W.prow); free(W.u);
+  free(W.eta); free(W.prow); free(W.pq); free(W.u);
   return status;
 }
 
@@ -569,17 +638,20 @@ int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
                      double *x_out, double *y_out, int *iters_out)
 {
   return dual_simplex_impl(P, lb, ub, ws_head, ws_st, ws_binv, ws_d, have_ws, have_binv,
-                           iter_limit, obj_out, x_out, y_out, iters_out, 0, 0);
+                           iter_limit, obj_out, x_out, y_out, iters_out, 0, 0, 0);
 }
 
 /* What the GPU runs for one LP of a batch that shares its warm start: K3P
- * (product form, at most pfi pivots); an LP that fills the eta file is
- * continued by the dense K3 from K3P's basis, status and reduced costs with
- * the explicit inverse (iteration counts add up).  ws_* are read-only here. */
+ * (product form, at most pfi etas: a path warm start's replayed pivots plus
+ * the solve's own); an LP that fills the eta file is continued by the dense
+ * K3 from K3P's basis, status and reduced costs with the explicit inverse
+ * (iteration counts add up; the continuation's iteration limit and Bland
+ * switch count the pivots already made).  ws_* are read-only here. */
 static int solve_shared(const orc_lp *P, const double *lb, const double *ub, const int *ws_head,
                         const signed char *ws_st, const double *ws_binv, const double *ws_d,
                         int have_ws, int have_binv, int iter_limit, double *obj, double *x,
-                        int *iters, int pfi, int *h, signed char *s, double *bi, double *dd)
+                        int *iters, int pfi, int *h, signed char *s, double *bi, double *dd,
+                        const orc_path *path)
 {
   int n = P->n, m = P->m, st;
   if (have_ws) {
@@ -590,14 +662,14 @@ static int solve_shared(const orc_lp *P, const double *lb, const double *ub, con
   }
   if (!(pfi > 0 && have_ws && have_binv))
     return dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, have_ws, have_binv, iter_limit,
-                             obj, x, 0, iters, 0, 0);
+                             obj, x, 0, iters, 0, 0, 0);
   st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, 1, 1, iter_limit, obj, x, 0, iters,
-                         pfi, 0);
+                         pfi, 0, path);
   if (st == -1) {
-    int it2 = 0;
-    st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, 1, 1, iter_limit - pfi, obj, x, 0,
-                           &it2, 0, pfi);
-    *iters = pfi + it2;
+    int it1 = *iters, it2 = 0;
+    st = dual_simplex_impl(P, lb, ub, h, s, bi, dd, 1, 1, iter_limit - it1, obj, x, 0,
+                           &it2, 0, it1, 0);
+    *iters = it1 + it2;
   }
   return st;
 }
@@ -630,7 +702,53 @@ int orc_dual_simplex_batch(int n, int m, const int *colptr, const int *rowidx,
       status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n, ws_head, ws_st,
                                ws_binv, ws_d, have, have && ws_binv != 0 && ws_d != 0,
                                iter_limit, obj + b, x ? x + (size_t) b * n : 0, iters + b, pfi,
-                               h, s, bi, dd);
+                               h, s, bi, dd, 0);
+    }
+    free(h); free(s); free(bi); free(dd);
+  }
+  return 0;
+}
+
+/* Path warm starts (the batched tree's warm mode 2): node b starts from the
+ * shared root basis after its path of k_in[b] pivots (path_in[b][0..k),
+ * stride MGPU path cap 32) with statuses st_in[b][n+m]; k_in[b] <= 0: the
+ * root basis, statuses and reduced costs.  Out: status / objective / own
+ * pivots and the node's final path for its children (k_out[b] = 0: restart
+ * from the root). */
+int orc_dual_simplex_path_batch(int n, int m, const int *colptr, const int *rowidx,
+                                const double *cval, const double *c, const double *rlo,
+                                const double *rhi, int B, const double *lb, const double *ub,
+                                const int *ws_head, const signed char *ws_st,
+                                const double *ws_binv, const double *ws_d, const int *k_in,
+                                const unsigned *path_in, const signed char *st_in, int iter_limit,
+                                int *status, double *obj, double *x, int *iters, int *k_out,
+                                unsigned *path_out, signed char *st_out, int pfi, int inherit,
+                                int nthreads)
+{
+  orc_lp P;
+  P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cval; P.c = c;
+  P.rlo = rlo; P.rhi = rhi;
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+  {
+    int *h = (int *) malloc(sizeof(int) * (size_t) (m + 1));
+    signed char *s = (signed char *) malloc((size_t) (n + m + 1));
+    double *bi = (double *) malloc(sizeof(double) * (size_t) m * m + 8);
+    double *dd = (double *) malloc(sizeof(double) * (size_t) (n + m) + 8);
+#pragma omp for schedule(dynamic, 16)
+    for (int b = 0; b < B; ++b) {
+      orc_path pa;
+      pa.k = k_in[b];
+      pa.path = path_in + (size_t) b * ORC_PATH_MAX;
+      pa.st = st_in + (size_t) b * (n + m);
+      pa.inherit = inherit;
+      pa.k_out = k_out + b;
+      pa.path_out = path_out + (size_t) b * ORC_PATH_MAX;
+      pa.st_out = st_out + (size_t) b * (n + m);
+      k_out[b] = 0;
+      status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n, ws_head, ws_st,
+                               ws_binv, ws_d, 1, 1, iter_limit, obj + b,
+                               x ? x + (size_t) b * n : 0, iters + b, pfi, h, s, bi, dd, &pa);
     }
     free(h); free(s); free(bi); free(dd);
   }
@@ -678,7 +796,7 @@ int orc_lp_bound_batch(int n, int m, const int *colptr, const int *rowidx, const
       c[col[b]] = sign[b];
       status[b] = solve_shared(&P, lb, ub, ws_head, ws_st, ws_binv, 0, have, have, iter_limit,
                                obj + b, x ? x + (size_t) b * n : 0, iters + b, pfi, h, s, bi,
-                               dd);
+                               dd, 0);
       c[col[b]] = 0.0;
     }
     free(h); free(s); free(bi); free(c); free(dd);
@@ -710,7 +828,7 @@ int orc_dual_simplex_nodes(int n, int m, const int *colptr, const int *rowidx,
                              ws_d + (size_t) b * N, 1, 1, iter_limit, obj + b,
                              x ? x + (size_t) b * n : 0, iters + b, 0, wo_head + (size_t) b * m,
                              wo_st + (size_t) b * N, wo_binv + (size_t) b * mm,
-                             wo_d + (size_t) b * N);
+                             wo_d + (size_t) b * N, 0);
   }
   return 0;
 }
@@ -766,7 +884,7 @@ int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
       status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n,
                                have ? ws_head + wb * m : 0, have ? ws_st + wb * N : 0, 0, 0, have,
                                0, iter_limit, obj + b, x ? x + (size_t) b * n : 0, iters + b, 0, h,
-                               s, bi, 0);
+                               s, bi, 0, 0);
     }
     free(cv); free(lo); free(hi); free(h); free(s); free(bi);
   }

@@ -49,6 +49,9 @@ typedef struct {
   const double *rlo, *rhi;
 } orc_lp;
 
+/* path warm starts: at most this many pivots per path (= MGPU_PATH_MAX) */
+#define ORC_PATH_MAX 32
+
 int orc_dual_simplex(const orc_lp *P, const double *lb, const double *ub,
                      int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
                      int have_ws, int have_binv, int iter_limit, double *obj_out,

@@ -236,6 +236,48 @@ def dual_simplex_nodes(p, LB, UB, ws, iter_limit=10000, nthreads=1):
     return st, obj + p.obj_const, it, x, wo
 
 
+PATH_MAX = 32     # ORC_PATH_MAX = MGPU_PATH_MAX: pivots per path warm start
+
+
+def dual_simplex_path(p, LB, UB, ws, k_in, path_in, st_in, pfi, inherit, iter_limit=10000,
+                      nthreads=1, want_x=True):
+    """Path warm starts (the batched tree's warm mode 2; orc_dual_simplex_path_batch):
+    node b starts from the shared root basis ``ws`` after its k_in[b] pivots
+    path_in[b] (q | r << 16) with statuses st_in[b]; k_in <= 0 = the root
+    basis.  Product form with ``pfi`` etas (the GPU's K3P), dense
+    continuation past it.  Returns (status, obj incl. constant, own pivots,
+    x, k_out, path_out, st_out): the node's final path for its children
+    (k_out 0 = restart from the root)."""
+    l = lib()
+    f = l.orc_dual_simplex_path_batch
+    f.restype = _I
+    f.argtypes = [_I, _I] + [_P] * 6 + [_I, _P, _P] + [_P] * 7 + [_I] + [_P] * 7 + [_I, _I, _I]
+    LB = np.ascontiguousarray(LB, dtype=np.float64)
+    UB = np.ascontiguousarray(UB, dtype=np.float64)
+    B = LB.shape[0]
+    N = p.n + p.m
+    colptr, rowidx, cval = lp_csc(p)
+    h = np.ascontiguousarray(ws.head, dtype=np.int32)
+    s = np.ascontiguousarray(ws.st, dtype=np.int8)
+    bi = np.ascontiguousarray(ws.binv, dtype=np.float64)
+    dd = np.ascontiguousarray(ws.d, dtype=np.float64)
+    k_in = np.ascontiguousarray(k_in, dtype=np.int32)
+    path_in = np.ascontiguousarray(path_in, dtype=np.uint32).reshape(B, PATH_MAX)
+    st_in = np.ascontiguousarray(st_in, dtype=np.int8).reshape(B, N)
+    st = np.zeros(B, dtype=np.int32)
+    obj = np.zeros(B)
+    it = np.zeros(B, dtype=np.int32)
+    x = np.zeros((B, p.n)) if want_x else None
+    k_out = np.zeros(B, dtype=np.int32)
+    path_out = np.zeros((B, PATH_MAX), dtype=np.uint32)
+    st_out = np.zeros((B, N), dtype=np.int8)
+    f(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj), _ptr(p.rlo), _ptr(p.rhi),
+      B, _ptr(LB), _ptr(UB), _ptr(h), _ptr(s), _ptr(bi), _ptr(dd), _ptr(k_in), _ptr(path_in),
+      _ptr(st_in), iter_limit, _ptr(st), _ptr(obj), _ptr(x), _ptr(it), _ptr(k_out),
+      _ptr(path_out), _ptr(st_out), int(pfi), int(inherit), nthreads)
+    return st, obj + p.obj_const, it, x, k_out, path_out, st_out
+
+
 def dual_simplex_root(p, lb=None, ub=None, iter_limit=100000):
     l = lib()
     _lp_sig(l)

@@ -65,6 +65,9 @@ def test_pfi_cap_matches_header():
     hdr = open(os.path.join(ROOT, 'include', 'mgpu.h')).read()
     m = re.search(r'#define MGPU_LP_PFI_MAX (\d+)', hdr)
     assert m and int(m.group(1)) == runtime.LP_PFI_MAX
+    m = re.search(r'#define MGPU_PATH_MAX (\d+)', hdr)
+    import oracle
+    assert m and int(m.group(1)) == runtime.PATH_MAX == oracle.PATH_MAX
 
 
 def test_reference_libraries_coexist_in_one_process():

@@ -72,6 +72,48 @@ def test_bnb_shard_partitions_pool(ctx):
     assert sum(counts) == before and max(counts) - min(counts) <= 1
 
 
+@pytest.mark.parametrize('warm,brancher', [(0, 0), (1, 0), (2, 0), (0, 1), (1, 1)])
+def test_bnb_depth_first_shard_matches_cpu(ctx, warm, brancher):
+    """Depth-first shard (mgpu_bnb_shard packs the kept nodes): every
+    per-slot array moves with its node — parent bases (warm 1), paths
+    (warm 2), parent branching data (reliability) — so each rank's search
+    after the shard is the CPU restatement's (which shards node objects),
+    round for round, and together they prove the HiGHS optimum."""
+    from bnb import CpuBnbContext
+    from minotaur_amd.runtime import Context
+    p = random_mkp(5, 22, 3)
+    hs, hobj = oracle.highs_milp(p)
+    other = Context(0)
+    try:
+        gpu = [ctx, other]
+        cpu = [CpuBnbContext(p, ctx.oracle_pfi() if warm != 1 and not brancher else 0)
+               for _ in range(2)]
+        for c in gpu + cpu:
+            if c in gpu:
+                c.load(p)
+            c.bnb_config(0, warm)
+            c.bnb_brancher(brancher)
+            c.bnb_init(1 << 15)
+        for _ in range(3):
+            sg = [c.bnb_round(16) for c in gpu]
+            sc = [c.bnb_round(16) for c in cpu]
+        for r in range(2):
+            assert gpu[r].bnb_shard(r, 2) == cpu[r].bnb_shard(r, 2)
+        inc = min(s.incumbent for s in sg)
+        while True:
+            sg = [c.bnb_round(16, inc) for c in gpu]
+            sc = [c.bnb_round(16, inc) for c in cpu]
+            for a, b in zip(sg, sc):
+                assert (a.rounds, a.nodes, list(a.ndec), a.lps, a.pivots, a.sb_lps) == \
+                    (b.rounds, b.nodes, list(b.ndec), b.lps, b.pivots, b.sb_lps)
+            inc = min(s.incumbent for s in sg)
+            if max(s.open for s in sg) == 0:
+                break
+        assert abs(inc - hobj) <= 1e-6 * max(1.0, abs(hobj))
+    finally:
+        other.close()
+
+
 def test_bnb_two_shards_interleaved(ctx):
     """Two ranks simulated in one process (two contexts, incumbent MIN after
     every round): the sharded search proves the HiGHS optimum."""
@@ -138,13 +180,14 @@ def test_bnb_k3l_tree_matches_cpu_and_highs(ctx):
     _check_solution(p, xg, og)
 
 
-@pytest.mark.parametrize('order,warm', [(1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize('order,warm', [(1, 0), (0, 1), (1, 1), (0, 2), (1, 2)])
 @pytest.mark.parametrize('k', range(4))
 def test_bnb_search_modes_match_cpu_and_highs(ctx, k, order, warm):
     """Best-first selection (TreeManager bfs: lowest bound first, open nodes
     pruned by the incumbent before evaluation) and parent warm starts
     (NodeIncRelaxer.cpp:146-150: each node LP from its parent's optimal
-    basis, K3 / K3L per-node warm starts): the GPU tree is the CPU
+    basis, K3 / K3L per-node warm starts; warm 2: the same basis kept as its
+    pivot path from the root, K3P): the GPU tree is the CPU
     restatement's tree (rounds, nodes, decisions, pruned-open counts) and
     proves the HiGHS MILP optimum."""
     import os
@@ -207,7 +250,7 @@ def test_bnb_tls4_lin_tree(ctx):
         _check_solution(p, xg, og)
 
 
-@pytest.mark.parametrize('order,warm', [(0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize('order,warm', [(0, 0), (1, 0), (1, 1), (0, 2), (1, 2)])
 def test_bnb_export_import_between_contexts(ctx, order, warm):
     """Node migration (mgpu_bnb_export / mgpu_bnb_import, the node send /
     receive of MpiBranchAndBound::LoadBalance_) between two engine contexts

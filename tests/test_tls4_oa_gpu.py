@@ -74,8 +74,8 @@ def _sig(st):
 
 # (order, warm, brancher, batch): MaxVio trees of 10^5 nodes, reliability
 # trees of 10^3 (the restatement's run time bounds the batch sizes)
-TREES = [(0, 0, 0, 4096), (1, 0, 0, 4096), (1, 1, 0, 8192), (1, 0, 1, 256), (0, 0, 1, 1024),
-         (1, 1, 1, 64)]
+TREES = [(0, 0, 0, 4096), (1, 0, 0, 4096), (1, 1, 0, 8192), (0, 2, 0, 4096), (1, 2, 0, 4096),
+         (1, 0, 1, 256), (0, 0, 1, 1024), (1, 1, 1, 64)]
 
 
 @pytest.mark.parametrize('order,warm,brancher,batch', TREES)
@@ -91,7 +91,7 @@ def test_tls4_oa_tree_proves_highs_optimum(ctx, order, warm, brancher, batch):
     assert abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
     ints = np.isin(p.vtype, (0, 1))
     assert np.all(np.abs(xg[ints] - np.round(xg[ints])) <= 1e-6)
-    pfi = ctx.oracle_pfi() if (warm == 0 and brancher == 0) else 0
+    pfi = ctx.oracle_pfi() if (warm != 1 and brancher == 0) else 0
     oc, _, sc, _ = bnb.solve(CpuBnbContext(p, pfi), batch=batch, capacity=1 << 20, order=order,
                              warm=warm, brancher=brancher)
     assert _sig(sg) == _sig(sc)
