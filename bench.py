@@ -222,8 +222,10 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0):
 # (name, kind, order, warm, optimum, brancher): brancher 1 = the reference's
 # default ReliabilityBrancher (strong-branching LPs count as relaxations).
 TREES = [("tls4_oa", "instance", 0, 0, 3.2, 0),
+         ("tls4_oa", "instance", 0, 2, 3.2, 0),
          ("tls4_oa", "instance", 1, 0, 3.2, 0),
          ("tls4_oa", "instance", 1, 1, 3.2, 0),
+         ("tls4_oa", "instance", 1, 2, 3.2, 0),
          ("tls4_oa", "instance", 1, 0, 3.2, 1),
          ("tls4_lin", "instance", 1, 0, 0.0, 1),
          ("nvs08_oa", "instance", 1, 0, None, 0),
@@ -257,7 +259,8 @@ def tree_search(ctx, dev, rank, world, B, args):
                        f"{nodes:.0f} nodes in {el:.2f}s")
         out.append({"instance": p.name, "vars": p.n, "rows": p.m,
                     "search": ("best-first" if order else "depth-first over batches") +
-                              (", parent-basis warm starts" if warm else
+                              (", parent-basis warm starts as pivot paths" if warm == 2 else
+                               ", parent-basis warm starts" if warm else
                                ", root-basis warm start") +
                               (", reliability branching (strong branching + pseudocosts)"
                                if br else ", MaxVio branching"),
@@ -567,7 +570,7 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
     B = LB.shape[0]
     ctx.load(p)
     cap = B * (max(1, args.warmup) + args.steps + 2) + 2
-    ctx.bnb_config(0, 0)
+    ctx.bnb_config(0, args.warm)
     ctx.bnb_brancher(0)
     ctx.bnb_init(cap)
     ctx.bnb_import(LB, UB, np.full(B, -math.inf), np.zeros(B, dtype=np.int32))
@@ -626,8 +629,9 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
                              acc["pivots"] / S, acc["pfi_pivots"] / S)
     summary = {"nodes": nodes, "lp_solves": lps, "pivots_per_lp": pivots / max(lps, 1.0),
                "nodes_per_round_per_gpu": nb, "open_after_rank0": acc["open"],
-               "search": "depth-first over batches (HBM stack), MaxVio branching, root-basis "
-                         "warm start (K3P)",
+               "search": "depth-first over batches (HBM stack), MaxVio branching, " +
+                         ("parent-basis warm starts kept as pivot paths from the root basis "
+                          "(K3P)" if args.warm == 2 else "root-basis warm start (K3P)"),
                "incumbent": state["inc"]}
     return {"elapsed": float(tot.item()), "nodes": nodes, "lps": lps, "kernels": kernels,
             "summary": summary, "incumbent": state["inc"],
@@ -706,6 +710,9 @@ def main():
     ap.add_argument('--tree-batch', type=int, default=131072,
                     help='open nodes per GPU per round of the complete trees (tree_search, '
                          'convex_batch)')
+    ap.add_argument('--warm', type=int, default=2,
+                    help='headline tree warm starts: 2 parent basis as a pivot path (default; '
+                         'NodeIncRelaxer semantics), 0 the root basis')
     ap.add_argument('--cpu-seconds', type=float, default=16.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-bnb', action='store_true',
@@ -805,11 +812,15 @@ def main():
                 "workload": ("branch-and-bound tree rounds on config 2 (tls4.nl as a MINLP: its "
                              "outer-approximation LP): every step is one mgpu_bnb_round per GPU "
                              "- pop the top B open nodes of the HBM node stack, K1 FBBT with the "
-                             "incumbent, K3P dual-simplex LP from the root basis (FBBT-"
-                             "infeasible nodes skipped), prune/integrality decision with the "
-                             "MaxVio branching choice, children written back to the stack - "
-                             "then one packed all-reduce (incumbent MIN, open counts); the pool "
-                             "starts as the root plus B seeded random-branching boxes"),
+                             "incumbent, K3P dual-simplex LP from the parent's optimal basis "
+                             "(kept as its pivot path from the root basis; NodeIncRelaxer "
+                             "semantics) with FBBT-infeasible nodes skipped, prune/integrality "
+                             "decision with the MaxVio branching choice, children (box, bound, "
+                             "path) written back to the stack - then one packed all-reduce "
+                             "(incumbent MIN, open counts); the pool starts as the root plus B "
+                             "seeded random-branching boxes" if args.warm == 2 else
+                             "branch-and-bound tree rounds on config 2 (tls4 OA-LP), root-basis "
+                             "warm starts (K3P), MaxVio branching"),
                 "instance": f"tls4-oa ({p.m} rows, {p.n} cols, {p.nnz} nnz)",
                 "nodes_per_gpu": B,
                 "global_batch": B * world,

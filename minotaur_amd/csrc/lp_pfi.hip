@@ -189,21 +189,15 @@ __device__ __forceinline__ double ftran_b0(const Prob &P, int q, int lane) {
 }
 
 // u <- u' E_{k-1} ... E_0 (oracle pfi_btran's eta loop): each E_t' rewrites
-// component prow[t] with a dot product over the nonzeros of u, ascending
+// component prow[t] with u' eta_t, the lane products summed by the
+// symmetric DPP butterfly (oracle eta_dot)
 template <int K>
 __device__ __forceinline__ double btran_etas(double u, const double (&eta)[K], int prow, int k,
                                              int lane) {
 #pragma unroll
   for (int t = K - 1; t >= 0; --t) {
     if (t < k) {
-      uint64_t mask = __ballot(u != 0.0);
-      const double pr = u * eta[t];  // the oracle's products, lane-parallel
-      double acc = 0.0;
-      while (mask) {
-        const int i = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        acc += rld(pr, i);
-      }
+      const double acc = wave_sum_sym(u * eta[t]);
       if (lane == rl(prow, t)) u = acc;
     }
   }

@@ -478,17 +478,9 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
 #pragma unroll
       for (int t = kKE - 1; t >= 0; --t) {
         if (t < iters) {
-          double acc = 0.0;
-#pragma unroll
-          for (int rs = 0; rs < kR; ++rs) {
-            uint64_t mask = __ballot(u[rs] != 0.0);
-            const double pr = u[rs] * eta[t][rs];  // the oracle's products, lane-parallel
-            while (mask) {
-              const int i = __builtin_ctzll(mask);
-              mask &= mask - 1;
-              acc += rld(pr, i);
-            }
-          }
+          // u' eta_t: lane products (row lane + row 64 + lane), summed by the
+          // symmetric DPP butterfly (oracle eta_dot)
+          const double acc = wave_sum_sym(u[0] * eta[t][0] + u[1] * eta[t][1]);
           const int pt = rl(prow, t);
 #pragma unroll
           for (int rs = 0; rs < kR; ++rs)

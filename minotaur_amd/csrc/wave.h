@@ -137,6 +137,22 @@ __device__ __forceinline__ void wave_argmax_idx(double &v, int &idx) {
   v = mx;
 }
 
+constexpr int kDppHalfMirror = 0x141;  // row_half_mirror: lane i <-> i ^ 7 in 8 lanes
+constexpr int kDppMirror = 0x140;      // row_mirror: lane i <-> i ^ 15 in 16 lanes
+
+// Deterministic wave sum with symmetric exchanges only: pairs (i, i^1),
+// (i, i^2), the half-row mirror, the row mirror, then the four rows as
+// (r0 + r1) + (r2 + r3).  Each step adds a lane and its partner (the same
+// two values in both), so the association is fixed: oracle/lp_dual.c
+// eta_dot restates it.  Wave uniform result.
+__device__ __forceinline__ double wave_sum_sym(double v) {
+  v = v + dpp_f64<kDppXor1>(v);
+  v = v + dpp_f64<kDppXor2>(v);
+  v = v + dpp_f64<kDppHalfMirror>(v);
+  v = v + dpp_f64<kDppMirror>(v);
+  return (rld(v, 0) + rld(v, 16)) + (rld(v, 32) + rld(v, 48));
+}
+
 __device__ __forceinline__ double wave_min_dpp(double v) {
   v = fmin(v, dpp_f64<kDppXor1>(v));
   v = fmin(v, dpp_f64<kDppXor2>(v));

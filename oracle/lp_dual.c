@@ -102,21 +102,35 @@ static void pfi_apply_etas(const lpw *W, double *out) {
   }
 }
 
+/* u' e_t as the product-form kernels sum it (wave.h wave_sum_sym): lane i
+ * holds u_i e_i (K3PW: plus row i + 64's product); the 64 lanes are summed
+ * by the symmetric DPP butterfly — pairs (i, i^1), (i, i^2), the half-row
+ * mirror (i, i^7), the row mirror (i, i^15) — and the four 16-lane rows as
+ * (r0 + r1) + (r2 + r3).  Every step adds a lane to its partner, so the
+ * association is fixed and the same in every lane. */
+static double eta_dot(int m, const double *u, const double *e) {
+  double a[64], b[64];
+  for (int i = 0; i < 64; ++i) {
+    a[i] = i < m ? u[i] * e[i] : 0.0;
+    if (m > 64) a[i] = a[i] + (i + 64 < m ? u[i + 64] * e[i + 64] : 0.0);
+  }
+  for (int i = 0; i < 64; ++i) b[i] = a[i] + a[i ^ 1];
+  for (int i = 0; i < 64; ++i) a[i] = b[i] + b[i ^ 2];
+  for (int i = 0; i < 64; ++i) b[i] = a[i] + a[i ^ 7];
+  for (int i = 0; i < 64; ++i) a[i] = b[i] + b[i ^ 15];
+  return (a[0] + a[16]) + (a[32] + a[48]);
+}
+
 /* rho = e_r' B^{-1}: u = e_r' E_{k-1} ... E_0 (each E_t' only rewrites
- * component prow[t], a dot product over the nonzeros of u in ascending row
- * order), then rho = u' B0^{-1} over the same nonzeros. */
+ * component prow[t] with u' e_t, eta_dot's order), then rho = u' B0^{-1}
+ * over the nonzeros of u in ascending row order. */
 static void pfi_btran(const lpw *W, int r, double *rho) {
   int m = W->P->m;
   double *u = W->u;
   for (int i = 0; i < m; ++i) u[i] = 0.0;
   u[r] = 1.0;
-  for (int t = W->neta - 1; t >= 0; --t) {
-    const double *e = W->eta + (size_t) t * m;
-    double acc = 0.0;
-    for (int i = 0; i < m; ++i)
-      if (u[i] != 0.0) acc += u[i] * e[i];
-    u[W->prow[t]] = acc;
-  }
+  for (int t = W->neta - 1; t >= 0; --t)
+    u[W->prow[t]] = eta_dot(m, u, W->eta + (size_t) t * m);
   for (int k = 0; k < m; ++k) rho[k] = 0.0;
   for (int i = 0; i < m; ++i) {
     if (u[i] == 0.0) continue;
@@ -316,13 +330,8 @@ static void pfi_compute_duals(lpw *W) {
   int m = P->m, N = W->N;
   double *u = W->u, *y = W->rho;
   for (int i = 0; i < m; ++i) u[i] = W->head[i] < P->n ? P->c[W->head[i]] : 0.0;
-  for (int t = W->neta - 1; t >= 0; --t) {
-    const double *e = W->eta + (size_t) t * m;
-    double acc = 0.0;
-    for (int i = 0; i < m; ++i)
-      if (u[i] != 0.0) acc += u[i] * e[i];
-    u[W->prow[t]] = acc;
-  }
+  for (int t = W->neta - 1; t >= 0; --t)
+    u[W->prow[t]] = eta_dot(m, u, W->eta + (size_t) t * m);
   for (int k = 0; k < m; ++k) y[k] = 0.0;
   for (int i = 0; i < m; ++i) {
     if (u[i] == 0.0) continue;
@@ -667,8 +676,8 @@ static int solve_shared(const orc_lp *P, const double *lb, const double *ub, con
                          pfi, 0, path);
   if (st == -1) {
     int it1 = *iters, it2 = 0;
-    st = dual_simplex_impl(P, lb, ub, h, s, bi, dd, 1, 1, iter_limit - it1, obj, x, 0,
-                           &it2, 0, it1, 0);
+    st = dual_simplex_impl(P, lb, ub, h, s, bi, ws_d ? dd : 0, 1, 1, iter_limit - it1, obj, x,
+                           0, &it2, 0, it1, 0);
     *iters = it1 + it2;
   }
   return st;

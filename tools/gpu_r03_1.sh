@@ -1,5 +1,6 @@
 set -o pipefail
-O=gpurun_out/r03_g9
+O=gpurun_out/r03_g11
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_bnb_gpu.py tests/test_tls4_oa_gpu.py tests/test_bnb_rel_gpu.py tests/test_lp_path_gpu.py -x -v --timeout 240 --timeout-method thread > $O/tests.txt 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest tests/test_lp_pfi_gpu.py tests/test_lp_pfi_wide_gpu.py tests/test_lp_path_gpu.py tests/test_tls4_oa_gpu.py tests/test_bnb_gpu.py tests/test_obbt_gpu.py -x -q --timeout 240 --timeout-method thread > $O/tests.txt 2>&1 || exit $?
+timeout -k 10 600 python -u bench.py --steps 10 --no-cpu-baseline --no-bnb --no-convex --no-qp --no-knapsack --no-glob > $O/bench.json 2> $O/bench.err || exit $?
 echo done
