@@ -15,6 +15,7 @@
 // runs shard the tree after the first rounds (minotaur_amd/bnb.py) and
 // exchange the incumbent with an RCCL all-reduce MIN between rounds.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -273,7 +274,12 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
     if (s->rel || m > kLpMaxM || kcap <= 0 || kcap > kPathMax)
       return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: path warm starts (warm 2) need MaxVio "
                   "branching and K3P (m <= 64, eta cap 1..%d)", kPathMax);
-    s->inherit = kcap < kPathInherit ? kcap : kPathInherit;
+    // MGPU_PATH_INHERIT (tuning experiments only; the CPU restatement
+    // assumes the default) overrides the longest inherited path
+    int inh = kPathInherit;
+    if (const char *e = std::getenv("MGPU_PATH_INHERIT")) inh = std::atoi(e);
+    if (inh < 0) inh = 0;
+    s->inherit = kcap < inh ? kcap : inh;
   }
   if (s->rel) {
     if (m > kLpMaxM && !(lp_large_lds_bytes(n, m) <= (size_t)kLargeLdsMax))

@@ -43,7 +43,7 @@ namespace mgpu {
 // Diagnostic build only (-DMGPU_STAMPS, tools/lp_stamps.py --pfi): s_memtime
 // cycles per section summed over all waves; never compiled into the product.
 __device__ unsigned long long g_pfi_stamps[16];
-#define PSTAMP_DECL unsigned long long st_acc[10] = {0}, st_t = __builtin_amdgcn_s_memtime();
+#define PSTAMP_DECL unsigned long long st_acc[12] = {0}, st_t = __builtin_amdgcn_s_memtime();
 #define PSTAMP(i)                                             \
   do {                                                        \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -52,7 +52,7 @@ __device__ unsigned long long g_pfi_stamps[16];
   } while (0)
 #define PSTAMP_FLUSH                                           \
   if ((threadIdx.x & 63) == 0)                                \
-    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_pfi_stamps[i_], st_acc[i_]);
+    for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_pfi_stamps[i_], st_acc[i_]);
 #else
 #define PSTAMP_DECL
 #define PSTAMP(i) \
@@ -95,7 +95,7 @@ __host__ __device__ inline size_t pfi_shared_bytes(int n, int m, int nnz) {
   return al16((size_t)(n + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
          al16((size_t)(m + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
          al16((size_t)m * (m + 1) * 8) + al16((size_t)N * 8) + al16((size_t)N * 4) +
-         al16((size_t)m * 4);
+         al16((size_t)m * 4) + al16((size_t)n * 4) + al16((size_t)n * 8) + 16;
 }
 // per wave: rho [64] + column values, lower and upper working bounds [N]
 __host__ __device__ inline size_t pfi_wave_bytes(int N) { return 64 * 8 + 3 * al16((size_t)N * 8); }
@@ -154,9 +154,11 @@ __device__ __forceinline__ double apply_etas(double v, const double (&eta)[K], i
 #pragma unroll
   for (int t = 0; t < K; ++t) {
     if (t < k) {
+      // select, not a (wave-uniform) branch: consecutive etas overlap
       const int p = rl(prow, t);
       const double vp = rld(v, p);
-      if (vp != 0.0) v = lane == p ? eta[t] * vp : v + eta[t] * vp;
+      const double nv = lane == p ? eta[t] * vp : v + eta[t] * vp;
+      v = vp != 0.0 ? nv : v;
     }
   }
   return v;
@@ -250,6 +252,9 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
   double *s_wd = (double *)p;    p += al16((size_t)N * 8);
   int *s_wst = (int *)p;         p += al16((size_t)N * 4);
   int *s_whead = (int *)p;       p += al16((size_t)m * 4);
+  int *s_oidx = (int *)p;        p += al16((size_t)n * 4);    // nonzero objective columns
+  double *s_oval = (double *)p;  p += al16((size_t)n * 8);
+  int *s_onnz = (int *)p;        p += 16;
   constexpr int T = 64 * kWaves;
   for (int t = threadIdx.x; t <= n; t += T) s_colptr[t] = lp.colptr[t];
   for (int t = threadIdx.x; t <= m; t += T) s_rowptr[t] = lp.rowptr[t];
@@ -267,6 +272,24 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     s_wst[t] = s == ST_BASIC ? ST_LB : s;
   }
   for (int t = threadIdx.x; t < m; t += T) s_whead[t] = io.ws.head[t];
+  if (wave == 0) {
+    // the objective's nonzero columns in column order: the objective sum
+    // skips the zero terms (adding +-0 to a sum that starts at +0 never
+    // changes its bits, so the value is the oracle's full sum)
+    int cnt = 0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane0;
+      const double cv = j < n ? lp.objd[j] : 0.0;
+      const uint64_t mask = __ballot(cv != 0.0);
+      if (cv != 0.0) {
+        const int pos = cnt + __popcll(mask & ((1ull << lane0) - 1ull));
+        s_oidx[pos] = j;
+        s_oval[pos] = cv;
+      }
+      cnt += __popcll(mask);
+    }
+    if (lane0 == 0) *s_onnz = cnt;
+  }
   __syncthreads();
   for (int t = threadIdx.x; t < m; t += T) s_wst[s_whead[t]] = ST_BASIC;  // basic = in head
   __syncthreads();
@@ -356,24 +379,40 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     // ---- basis rows: head, replayed path pivots, bounds (basic columns
     // carry no artificial box)
     int h = lane < m ? s_whead[lane] : -1;
-    for (int t = 0; t < kpath; ++t) {
-      // the pivot's eta exactly as the solve that made it built it: FTRAN of
-      // the entering column through B0^{-1} and the etas so far
-      const uint32_t pv = ppath[t];
-      const int q = (int)(pv & 0xFFFFu), r = (int)(pv >> 16);
-      const double alq = apply_etas(ftran_b0(P, q, lane), eta, prow, ne, lane);
-      const double inv = 1.0 / rld(alq, r);
-      const double e = lane == r ? inv : -alq * inv;
+    if (kpath > 0) {
+      // each pivot's eta exactly as the solve that made it built it: FTRAN
+      // of its entering column through B0^{-1} and the etas before it.  All
+      // columns B0^{-1} a_q are gathered first (independent LDS walks), then
+      // eliminated in path order: column t sees E_0 .. E_{t-1} in that order
+      // (apply_etas' operations), the columns after s take E_s together.
 #pragma unroll
-      for (int u = 0; u < K; ++u)
-        if (u == ne) eta[u] = e;
-      if (lane == ne) {
-        prow = r;
-        pq = q;
+      for (int t = 0; t < K; ++t)
+        if (t < kpath) eta[t] = ftran_b0(P, (int)(ppath[t] & 0xFFFFu), lane);
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        if (s < kpath) {
+          const uint32_t pv = ppath[s];
+          const int q = (int)(pv & 0xFFFFu), r = (int)(pv >> 16);
+          const double inv = 1.0 / rld(eta[s], r);
+          eta[s] = lane == r ? inv : -eta[s] * inv;
+          if (lane == s) {
+            prow = r;
+            pq = q;
+          }
+          if (lane == r) h = q;
+#pragma unroll
+          for (int t = s + 1; t < K; ++t) {
+            if (t < kpath) {
+              const double vp = rld(eta[t], r);
+              const double nv = lane == r ? eta[s] * vp : eta[t] + eta[s] * vp;
+              eta[t] = vp != 0.0 ? nv : eta[t];
+            }
+          }
+        }
       }
-      if (lane == r) h = q;
-      ++ne;
+      ne = kpath;
     }
+    PSTAMP(10);
     double lbB = 0.0, ubB = 0.0;
     if (lane < m) {
       lbB = lo[h];
@@ -395,6 +434,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
           d[s] = (j < n ? P.c[j] : 0.0) - (j >= n ? -rho[j - n] : P.col_dot(rho, j));
       }
       wave_sync();
+      PSTAMP(11);
     } else if (P.ocol < 0) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -477,13 +517,26 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     // oracle compute_primals (product form): z_B = -E...E B0^{-1} (N z_N)
     auto primals = [&]() -> double {
       wave_sync();
+      // row sums of N z_N in CSR (= ascending column) order.  Zero values
+      // are not skipped: a product a*0 = +-0 added to a sum that starts at
+      // +0 never changes its bits (cancellation gives +0), so the value is
+      // the oracle's; four columns' loads in flight (the tangent rows of an
+      // OA-LP hold 40+ terms).
       double w = 0.0;
       if (lane < m) {
-        for (int t = P.rowptr[lane]; t < P.rowptr[lane + 1]; ++t) {
-          const double zj = zc[P.ccol[t]];
-          if (zj == 0.0) continue;
-          w += P.rval[t] * zj;
+        int t = P.rowptr[lane];
+        const int e = P.rowptr[lane + 1];
+        for (; t + 4 <= e; t += 4) {
+          const int c0 = P.ccol[t], c1 = P.ccol[t + 1], c2 = P.ccol[t + 2], c3 = P.ccol[t + 3];
+          const double a0 = P.rval[t], a1 = P.rval[t + 1], a2 = P.rval[t + 2],
+                       a3 = P.rval[t + 3];
+          const double z0 = zc[c0], z1 = zc[c1], z2 = zc[c2], z3 = zc[c3];
+          w += a0 * z0;
+          w += a1 * z1;
+          w += a2 * z2;
+          w += a3 * z3;
         }
+        for (; t < e; ++t) w += P.rval[t] * zc[P.ccol[t]];
         const double zl = zc[n + lane];
         if (zl != 0.0) w -= zl;
       }
@@ -759,11 +812,21 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       // objective as the oracle sums it: sequentially over the columns, so
       // the value is the oracle's bit for bit (best-first search orders nodes
       // by these bounds; a last-bit difference reorders ties)
-      if (lane == 0) {
-        double sum = 0.0;
-        for (int j = 0; j < n; ++j) sum += P.cj(j) * zc[j];
-        io.obj[b] = P.ocol < 0 ? sum + lp.objoff : sum;
+      // the products lane-parallel (64 nonzero columns per pass), the sum
+      // sequential in column order through readlanes
+      double sum = 0.0;
+      if (P.ocol >= 0) {
+        sum += P.osign * zc[P.ocol];
+      } else {
+        const int no = *s_onnz;
+        for (int k0 = 0; k0 < no; k0 += 64) {
+          const int k = k0 + lane;
+          const double pr = k < no ? s_oval[k] * zc[s_oidx[k]] : 0.0;
+          const int cnt = no - k0 < 64 ? no - k0 : 64;
+          for (int i = 0; i < cnt; ++i) sum += rld(pr, i);
+        }
       }
+      if (lane == 0) io.obj[b] = P.ocol < 0 ? sum + lp.objoff : sum;
       if (io.x != nullptr)
         for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = zc[j];
     } else if (lane == 0) {

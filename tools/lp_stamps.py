@@ -14,7 +14,7 @@ NAMES = ['setup:primals', 'pricing', 'rho_write', 'pass1+min', 'pass2+argmax', '
          'steps/updates', 'binv_update', 'tail', 'outputs', 'setup:skip',
          'setup:bounds', 'setup:basis', 'setup:place']
 PFI_NAMES = ['setup', 'primals', 'pricing', 'btran+rho', 'pass1+min', 'pass2+argmax', 'ftran',
-             'steps+eta', 'outputs', 'skip/empty']
+             'steps+eta', 'outputs', 'skip/empty', 'path replay', 'path duals']
 
 
 def build():
@@ -25,7 +25,45 @@ def build():
     subprocess.run(cmd, check=True)
 
 
+def tree():
+    """--tree: K3P's sections inside the headline's tree rounds (tls4-oa, path
+    warm starts, batch PROBE_BATCH): stamps of round 4's LP call."""
+    if not os.path.exists(OUT):
+        build()
+    os.environ['MGPU_LIB'] = OUT
+    import math
+    import numpy as np
+    from minotaur_amd.problem import LinProblem, random_boxes
+    from minotaur_amd.runtime import Context, load_library
+    lib = load_library()
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
+    B = int(os.environ.get('PROBE_BATCH', '262144'))
+    LB, UB = random_boxes(p, B, 20261017)
+    ctx = Context(0)
+    ctx.load(p)
+    ctx.bnb_config(0, int(os.environ.get('PROBE_WARM', '2')))
+    ctx.bnb_init(B * 8 + 2)
+    ctx.bnb_import(LB, UB, np.full(B, -math.inf), np.zeros(B, dtype=np.int32))
+    buf = (ctypes.c_ulonglong * 16)()
+    st = None
+    for r in range(5):
+        if r == 4:
+            lib.mgpu_debug_pfi_stamps(buf, 1)
+            prev = st.pivots
+        st = ctx.bnb_round(B)
+    lib.mgpu_debug_pfi_stamps(buf, 1)
+    names = PFI_NAMES
+    tot = sum(buf[i] for i in range(len(names)))
+    piv = st.pivots - prev
+    print(f"round 4: pivots {piv}  total wave-cycles {tot:.3e}  per pivot {tot / max(piv, 1):.0f}")
+    for i, nme in enumerate(names):
+        print(f"  {nme:14s} {100.0 * buf[i] / tot:6.2f} %   {buf[i] / max(piv, 1):9.0f} cyc/pivot")
+
+
 def main():
+    if '--tree' in sys.argv:
+        tree()
+        return
     pfi = '--pfi' in sys.argv
     if not os.path.exists(OUT):
         build()
