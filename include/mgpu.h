@@ -348,6 +348,23 @@ typedef struct {
  *            146-150); the basis lives with the node in HBM, m*4 + (n+m)*9 +
  *            m*m*8 bytes per pool slot (K3 / K3L per-node warm starts). */
 int mgpu_bnb_config(mgpu_ctx *ctx, int order, int warm);
+/* order 2: the reference's own node order — TreeManager's "bfs" NodeHeap
+ *          (NodeHeap.cpp:24-47: lowest bound within 1e-6, then shallower,
+ *          then the larger node id) kept on the host with std::push_heap /
+ *          std::pop_heap, node ids as TreeManager assigns them (children in
+ *          IntVarHandler::getBranches order, guided dive included), open
+ *          nodes pruned lazily at the heap top (TreeManager::getCandidate);
+ *          with warm 1 the root LP runs from the slack basis after the
+ *          root's presolve (BranchAndBound::processRoot_).  At batch 1 this
+ *          is BranchAndBound::solve's sequence (tests/test_ref_tree_gpu.py);
+ *          larger batches pop `batch` nodes per round.  Not shardable.
+ * warm 2:  every node LP starts from its parent's optimal basis kept as a
+ *          pivot path from the root basis (mgpu_lp_solve_path; K3P, MaxVio). */
+/* Guided dive (IntVarHandler option guided_dive, default on,
+ * Environment.cpp:160-163): with an incumbent, the child whose bound moves
+ * the variable toward the incumbent's value comes first.  Order 2 only (the
+ * other orders place children by slot). */
+int mgpu_bnb_guided_dive(mgpu_ctx *ctx, int on);
 
 /* Brancher of the next mgpu_bnb_init: 0 MaxVioBrancher (default), 1
  * ReliabilityBrancher (the reference's default, ReliabilityBrancher.cpp) with

@@ -26,6 +26,7 @@
 #include "IntVarHandler.h"
 #include "LinearFunction.h"
 #include "LinearHandler.h"
+#include "MaxVioBrancher.h"
 #include "NodeIncRelaxer.h"
 #include "Objective.h"
 #include "Option.h"
@@ -176,6 +177,87 @@ int integ_bnb(int device, int hip_fbbt, int n, int m, const int *rowptr, const i
   cnt[2] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuCalls() : 0;
   cnt[3] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuLoads() : 0;
   cnt[4] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuErrors() : 0;
+  delete v_hand;
+  delete l_hand;
+  delete e;
+  delete p;
+  delete nproc;
+  delete nr;
+  delete bab;
+  delete env;
+  return 0;
+}
+
+// BranchAndBound keeps its node count in a protected member.
+class ProbeBranchAndBound : public BranchAndBound {
+ public:
+  ProbeBranchAndBound(EnvPtr env, ProblemPtr p) : BranchAndBound(env, p) {}
+  long long nodesProcessed() const { return stats_ ? (long long)stats_->nodesProc : 0; }
+};
+
+// The reference's own tree search with the MI355X engine plugged in, set up
+// for a node-for-node comparison with the batched tree at batch 1:
+// tree_search "bfs" (TreeManager's NodeHeap), pres_freq 1 (LinearHandler::
+// presolveNode at every node, PCBProcessor.cpp:143), brancher 0 MaxVio / 1
+// reliability, guided_dive as given (reference default on).  Every other
+// option keeps its default.  HipLPEngine solves the LPs; the linear handler
+// is the reference's LinearHandler (hip_fbbt 0) or HipLinearHandler.
+// res[0] UB, res[1] LB, res[2] seconds; cnt[0] nodes processed, cnt[1]
+// nodes created, cnt[2] LP solves (strong branching included), cnt[3]
+// strong-branching LPs, cnt[4] LP iterations, cnt[5] strong-branching
+// iterations.
+int integ_bnb_tree(int device, int hip_fbbt, int brancher, int guided, int n, int m,
+                   const int *rowptr, const int *colidx, const double *val, const double *rlo,
+                   const double *rhi, const int *vtype, const double *vlb, const double *vub,
+                   const double *obj, double objc, double *res, long long *cnt) {
+  EnvPtr env = (EnvPtr) new Environment();
+  int err = 0;
+  env->startTimer(err);
+  env->getOptions()->findString("tree_search")->setValue("bfs");
+  env->getOptions()->findInt("pres_freq")->setValue(1);
+  env->getOptions()->findBool("guided_dive")->setValue(guided != 0);
+  ProblemPtr p = build(env, n, m, rowptr, colidx, val, rlo, rhi, vtype, vlb, vub, obj, objc, 0);
+  ProbeBranchAndBound *bab = new ProbeBranchAndBound(env, p);
+  HandlerVector handlers;
+  IntVarHandlerPtr v_hand = (IntVarHandlerPtr) new IntVarHandler(env, p);
+  LinearHandlerPtr l_hand = hip_fbbt ? (LinearHandlerPtr) new HipLinearHandler(env, p, device)
+                                     : (LinearHandlerPtr) new LinearHandler(env, p);
+  handlers.push_back(v_hand);
+  handlers.push_back(l_hand);
+  v_hand->setModFlags(false, true);
+  l_hand->setModFlags(false, true);
+  HipLPEngine *e = new HipLPEngine(env, device);
+  PCBProcessorPtr nproc = (PCBProcessorPtr) new PCBProcessor(env, e, handlers);
+  BrancherPtr br;
+  if (brancher == 1) {
+    ReliabilityBrancherPtr rb = (ReliabilityBrancherPtr) new ReliabilityBrancher(env, handlers);
+    rb->setEngine(e);
+    br = rb;
+  } else {
+    br = (BrancherPtr) new MaxVioBrancher(env, handlers);
+  }
+  nproc->setBrancher(br);
+  bab->setNodeProcessor(nproc);
+  NodeIncRelaxerPtr nr = (NodeIncRelaxerPtr) new NodeIncRelaxer(env, handlers);
+  bab->setNodeRelaxer(nr);
+  nr->setEngine(e);
+  nr->setModFlag(false);
+  p->setNativeDer();
+  bab->shouldCreateRoot(true);
+  bab->setLogLevel(LogNone);
+  const auto t0 = std::chrono::steady_clock::now();
+  bab->solve();
+  res[2] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  res[0] = bab->getUb();
+  res[1] = bab->getLb();
+  cnt[0] = bab->nodesProcessed();
+  cnt[1] = (long long)bab->getTreeManager()->getSize();
+  std::vector<double> lps(6, 0.0);
+  e->fillStats(lps);
+  cnt[2] = (long long)lps[0];
+  cnt[3] = (long long)lps[1];
+  cnt[4] = (long long)lps[4];
+  cnt[5] = (long long)lps[5];
   delete v_hand;
   delete l_hand;
   delete e;

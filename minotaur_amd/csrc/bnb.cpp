@@ -14,6 +14,7 @@
 // (solAbs_tol / solRel_tol 1e-6, Environment.cpp:486,509-528).  Multi-GPU
 // runs shard the tree after the first rounds (minotaur_amd/bnb.py) and
 // exchange the incumbent with an RCCL all-reduce MIN between rounds.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +23,27 @@
 
 #include "bnb_internal.h"
 #include "ctx.h"
+
+// Reference node order (mgpu_bnb_config order 2): TreeManager's "bfs"
+// NodeHeap with the reference's comparator valueGreaterThan (NodeHeap.cpp:
+// 24-47: bound within 1e-6, tie-break score (0 in BranchAndBound), shallower
+// first, then the larger node id), kept on the host with the same
+// std::push_heap / std::pop_heap, node ids assigned as TreeManager does
+// (root 0, children in branch order, TreeManager.cpp:97-136, 232-249), open
+// nodes pruned lazily at the top (TreeManager::getCandidate, :162-186).
+struct HeapNode {
+  double lb;
+  int depth;
+  long long id;
+  int slot;
+};
+static bool heap_greater(const HeapNode &a, const HeapNode &b) {
+  if (a.lb > b.lb + 1e-6) return true;
+  if (a.lb < b.lb - 1e-6) return false;
+  if (a.depth < b.depth) return false;
+  if (a.depth > b.depth) return true;
+  return a.id < b.id;
+}
 
 struct BnbState {
   int n = 0, cap = 0, count = 0, maxb = 0;
@@ -52,6 +74,12 @@ struct BnbState {
   // path warm starts (warm 2): per pool slot, per batch (gathered in) and out
   DevBuf ppk, ppath, ppst, bpk, bppath, bpst, opk, oppath, opst;
   int inherit = 0;             // longest path handed to children (<= the eta cap)
+  // order 2: the host heap, free pool slots, next node id
+  std::vector<HeapNode> heap;
+  std::vector<int> free_slots;
+  long long next_id = 0;
+  bool guided = true;          // IntVarHandler guided_dive (Environment.cpp:160-163)
+  DevBuf cslots;               // [2 nb] child slots
   void release() {
     for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
                       &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
@@ -62,7 +90,8 @@ struct BnbState {
                       &cnt_dn, &last, &last_new, &ppvar, &ppval, &bnlb, &bpvar, &bpval, &rflag, &rrank,
                       &nsb, &sb_off, &sb_var, &sb_val, &dec2, &nev, &ev_var, &ev_side, &ev_cost,
                       &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit, &ev_off, &cv_var, &cv_side,
-                      &cv_cost, &ppk, &ppath, &ppst, &bpk, &bppath, &bpst, &opk, &oppath, &opst})
+                      &cv_cost, &ppk, &ppath, &ppst, &bpk, &bppath, &bpst, &opk, &oppath, &opst,
+                      &cslots})
       b->release();
   }
 };
@@ -228,16 +257,88 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
   return MGPU_OK;
 }
 
+// Reference-heap mode, after the round's scans: the host reads each node's
+// decision, bound, depth and branching choice, assigns pool slots to the
+// children (the round's own slots first, then older free slots, then new
+// ones), launches the children writer and pushes the children onto the heap
+// in the reference's branch order with the next node ids: the preferred
+// direction first, or — guided dive, with an incumbent — down first when the
+// incumbent's value of the variable is below the node's (IntVarHandler::
+// getBranches, IntVarHandler.cpp:125-175).
+int heap_children(mgpu_ctx *c, BnbState &s, BnbIO &io, int nb, const std::vector<uint32_t> &sel) {
+  std::vector<int32_t> dec(nb), bvar(nb), dep(nb);
+  std::vector<double> obj(nb), bval(nb);
+  std::vector<int8_t> bup(nb);
+  HIPCHK(c, hipMemcpyAsync(dec.data(), io.decision, (size_t)nb * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(bvar.data(), io.bvar, (size_t)nb * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dep.data(), io.depth_in, (size_t)nb * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(obj.data(), io.obj, (size_t)nb * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(bval.data(), io.bval, (size_t)nb * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(bup.data(), io.bup, (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // free slots in the order children take them
+  std::vector<int> pool(sel.begin(), sel.end());
+  for (auto it = s.free_slots.rbegin(); it != s.free_slots.rend(); ++it) pool.push_back(*it);
+  s.free_slots.clear();
+  size_t next = 0;
+  auto take = [&]() -> int { return next < pool.size() ? pool[next++] : s.hw++; };
+  std::vector<int32_t> cs;
+  struct Kid {
+    double lb;
+    int depth, slot, down;
+  };
+  std::vector<Kid> kids;
+  for (int i = 0; i < nb; ++i) {
+    if (dec[i] != 0 && dec[i] != 5) continue;
+    if (dec[i] == 5) {  // reliability's modified node: one child (not in heap mode)
+      const int sl = take();
+      cs.push_back(sl);
+      kids.push_back({obj[i], dep[i], sl, 0});
+      continue;
+    }
+    const int s_pref = take(), s_other = take();   // child index p (preferred), p + 1
+    cs.push_back(s_pref);
+    cs.push_back(s_other);
+    const bool pref_up = bup[i] != 0;
+    bool down_first = !pref_up;
+    if (s.guided && std::isfinite(s.inc) && !std::isnan(s.best_x[bvar[i]]))
+      down_first = s.best_x[bvar[i]] < bval[i];
+    const int s_down = pref_up ? s_other : s_pref, s_up = pref_up ? s_pref : s_other;
+    kids.push_back({obj[i], dep[i] + 1, down_first ? s_down : s_up, 0});
+    kids.push_back({obj[i], dep[i] + 1, down_first ? s_up : s_down, 0});
+  }
+  for (size_t k = next; k < pool.size(); ++k) s.free_slots.push_back(pool[k]);
+  if (!cs.empty()) {
+    HIPCHK(c, s.cslots.ensure(cs.size() * 4));
+    HIPCHK(c, hipMemcpyAsync(s.cslots.p, cs.data(), cs.size() * 4, hipMemcpyHostToDevice,
+                             c->stream));
+    io.child_slots = s.cslots.as<int32_t>();
+    HIPCHK(c, launch_bnb_children(io, s.n, c->stream));
+  }
+  for (const Kid &k : kids) {
+    s.heap.push_back(HeapNode{k.lb, k.depth, s.next_id++, k.slot});
+    std::push_heap(s.heap.begin(), s.heap.end(), heap_greater);
+  }
+  s.count = (int)s.heap.size();
+  return MGPU_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int mgpu_bnb_config(mgpu_ctx *c, int order, int warm) {
   if (!c) return MGPU_ERR_ARG;
-  if (order < 0 || order > 1 || warm < 0 || warm > 2)
-    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_config: order 0/1, warm 0/1/2");
+  if (order < 0 || order > 2 || warm < 0 || warm > 2)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_config: order 0/1/2, warm 0/1/2");
   c->bnb_order = order;
   c->bnb_warm = warm;
+  return MGPU_OK;
+}
+
+int mgpu_bnb_guided_dive(mgpu_ctx *c, int on) {
+  if (!c) return MGPU_ERR_ARG;
+  c->bnb_guided = on ? 1 : 0;
   return MGPU_OK;
 }
 
@@ -332,6 +433,17 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   s->root_ok = rst == 0;
   s->count = 1;
   s->best_x.assign(n, NAN);
+  if (s->order == 2) {
+    // reference heap: the root is node 0 in slot 0; slots and live flags
+    // as in best-first (the gather clears a taken slot's flag)
+    HIPCHK(c, s->plive.ensure((size_t)capacity));
+    HIPCHK(c, hipMemsetAsync(s->plive.p, 0, (size_t)capacity, c->stream));
+    HIPCHK(c, s->vals2.ensure((size_t)capacity * 4));
+    s->heap.push_back(HeapNode{-INFINITY, 0, 0, 0});
+    s->next_id = 1;
+    s->hw = 1;
+    s->guided = c->bnb_guided;
+  }
   if (s->order == 1) {
     // best-first pool: slot array with live flags, sort keys and scratch
     HIPCHK(c, s->plive.ensure((size_t)capacity));
@@ -388,9 +500,39 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   HIPCHK(c, hipSetDevice(c->device));
   if (incumbent < s.inc) s.inc = incumbent;
   const int n = s.n, m = c->lp.m, N = n + m;
-  const bool bfs = s.order == 1;
+  const bool bfs = s.order >= 1;      // the round's nodes are gathered from pool slots
+  const bool heap = s.order == 2;
+  const bool root_round = heap && s.tot.rounds == 0;
   int nb, base = 0, live = 0, holes = 0;
-  if (!bfs) {
+  std::vector<uint32_t> sel;
+  if (heap) {
+    // TreeManager::getCandidate: the heap top, pruned lazily by the
+    // incumbent (TreeManager::shouldPrune_, :403-413), then removed
+    while ((int)sel.size() < batch && !s.heap.empty()) {
+      const HeapNode top = s.heap.front();
+      std::pop_heap(s.heap.begin(), s.heap.end(), heap_greater);
+      s.heap.pop_back();
+      if (top.lb > s.inc - 1e-6 || std::fabs(s.inc - top.lb) / (std::fabs(s.inc) + 1e-6) * 100.0 < 1e-6) {
+        s.free_slots.push_back(top.slot);
+        s.tot.pruned += 1;
+        continue;
+      }
+      sel.push_back((uint32_t)top.slot);
+    }
+    nb = (int)sel.size();
+    live = (int)s.heap.size() + nb;
+    s.count = live;
+    if (nb <= 0) {
+      s.tot.open = 0;
+      if (stats) *stats = s.tot;
+      return MGPU_OK;
+    }
+    const long need = 2L * nb - nb - (long)s.free_slots.size();
+    if (s.hw + (need > 0 ? need : 0) > s.cap)
+      return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_round: node pool full (%d slots)", s.cap);
+    HIPCHK(c, hipMemcpyAsync(s.vals2.p, sel.data(), (size_t)nb * 4, hipMemcpyHostToDevice,
+                             c->stream));
+  } else if (!bfs) {
     nb = batch < s.count ? batch : s.count;
     if (s.count + nb > s.cap) nb = s.cap - s.count;  // children must fit: base + 2 nb <= cap
     if (nb <= 0) {
@@ -440,8 +582,9 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     }
   } else {
     size_t tb = s.sort_bytes;
-    HIPCHK(c, bnb_sort_pairs(s.sort_tmp.p, tb, s.keys.as<uint64_t>(), s.keys2.as<uint64_t>(),
-                             s.vals.as<uint32_t>(), s.vals2.as<uint32_t>(), s.hw, c->stream));
+    if (!heap)
+      HIPCHK(c, bnb_sort_pairs(s.sort_tmp.p, tb, s.keys.as<uint64_t>(), s.keys2.as<uint64_t>(),
+                               s.vals.as<uint32_t>(), s.vals2.as<uint32_t>(), s.hw, c->stream));
     BnbSelIO g{};
     g.nb = nb;
     g.n = n;
@@ -501,9 +644,13 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
                                 s.opst.as<int8_t>());
   } else if (s.warm) {
     // each node from its parent's optimal basis (NodeIncRelaxer.cpp:146-150);
-    // its own optimal basis comes back for its children
+    // its own optimal basis comes back for its children.  The reference's
+    // root has no warm start: its LP runs from the slack basis after the
+    // root's presolve (BranchAndBound::processRoot_), as in heap mode here.
     rc = mgpu_lp_solve_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(),
-                           w_head, w_st, w_d, w_binv, 0, 0, s.st.as<int32_t>(),
+                           root_round ? nullptr : w_head, root_round ? nullptr : w_st,
+                           root_round ? nullptr : w_d, root_round ? nullptr : w_binv, 0, 0,
+                           s.st.as<int32_t>(),
                            s.obj.as<double>(), s.it.as<int32_t>(), s.x.as<double>(),
                            s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), s.wo_d.as<double>(),
                            s.wo_binv.as<double>());
@@ -606,15 +753,19 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     io.ws_binv = s.pws_binv.as<double>();
   }
   HIPCHK(c, hipMemsetAsync(s.out.p, 0, sizeof(BnbOut), c->stream));
+  io.defer_children = heap ? 1 : 0;
   HIPCHK(c, launch_bnb_tail(io, n, c->stream));
   BnbOut o;
   HIPCHK(c, hipMemcpyAsync(&o, s.out.p, sizeof o, hipMemcpyDeviceToHost, c->stream));
   if (s.rel)
     HIPCHK(c, hipMemcpyAsync(rcnt, s.rcnt.p, sizeof rcnt, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (!bfs) {
+  if (heap) {
+    rc = heap_children(c, s, io, nb, sel);
+    if (rc != MGPU_OK) return rc;
+  } else if (!bfs) {
     s.count = base + o.nchild;
-  } else {
+  } else if (!heap) {
     s.count = live - nb + o.nchild;
     const long grow = (long)o.nchild - nb - holes;
     if (grow > 0) s.hw += (int)grow;
@@ -650,6 +801,8 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
 int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_shard: mgpu_bnb_init first");
+  if (c->bnb->order == 2)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_shard: not in the reference-heap order (order 2)");
   if (world < 1 || rank < 0 || rank >= world)
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_shard: bad rank/world");
   BnbState &s = *c->bnb;
@@ -806,6 +959,8 @@ int mgpu_bnb_export(mgpu_ctx *c, int k, double *lb, double *ub, double *nlb, int
                     int *got) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_export: mgpu_bnb_init first");
+  if (c->bnb->order == 2)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_export: not in the reference-heap order (order 2)");
   if (k < 0 || (k > 0 && (!lb || !ub || !nlb || !depth)) || !got)
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_export: bad argument");
   BnbState &s = *c->bnb;
@@ -874,6 +1029,8 @@ int mgpu_bnb_import(mgpu_ctx *c, int k, const double *lb, const double *ub, cons
                     const int32_t *depth) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_import: mgpu_bnb_init first");
+  if (c->bnb->order == 2)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_import: not in the reference-heap order (order 2)");
   if (k < 0 || (k > 0 && (!lb || !ub || !nlb || !depth)))
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_import: bad argument");
   if (k == 0) return MGPU_OK;

@@ -163,6 +163,7 @@ __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
   const bool up_first = io.bup[i] != 0;
   // free list F of best-first mode
   auto slot_of = [&](long c) -> size_t {
+    if (io.child_slots != nullptr) return (size_t)io.child_slots[c];
     if (c < io.nb) return io.slots[c];
     const long h = c - io.nb, holes = io.hw - io.live;
     if (h < holes) return io.slots[io.live + h];
@@ -288,6 +289,13 @@ hipError_t launch_bnb_tail(const BnbIO &io, int n, hipStream_t stream) {
   const int nblk = (io.nb + kScanBlock - 1) / kScanBlock;
   hipLaunchKernelGGL(bnb_scan_block, dim3(nblk), dim3(kScanBlock), 0, stream, io);
   hipLaunchKernelGGL(bnb_scan_top, dim3(1), dim3(1024), 0, stream, io, nblk);
+  if (!io.defer_children)
+    hipLaunchKernelGGL(bnb_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_bnb_children(const BnbIO &io, int n, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(bnb_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io, n);
   return hipGetLastError();
 }

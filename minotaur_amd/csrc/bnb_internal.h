@@ -23,6 +23,11 @@ struct BnbIO {
   // (slots[live, hw) of the sorted array: ascending), then new slots hw, ...
   const uint32_t *slots;        // [hw] slot ids sorted by (bound, slot)
   int live, hw;                 // live nodes before the selection, high-water mark
+  // reference-heap mode: the slot of child c is child_slots[c] (assigned on
+  // the host); defer_children: the tail runs the scans only, the children
+  // writer follows once the host has assigned the slots
+  const int32_t *child_slots;
+  int defer_children;
   uint8_t *plive;               // [cap] slot holds an open node
   // parent warm starts (ws_head != null): the node's optimal basis (the LP's
   // warm start out, batch-indexed) is copied to both children's slots
@@ -148,6 +153,7 @@ hipError_t launch_rel_gather(int nb, int base, const uint32_t *slots, const doub
                              int32_t *bpvar, double *bpval, hipStream_t stream);
 
 hipError_t launch_bnb_tail(const BnbIO &io, int n, hipStream_t stream);
+hipError_t launch_bnb_children(const BnbIO &io, int n, hipStream_t stream);
 hipError_t launch_bnb_keys(const double *pnlb, uint8_t *plive, int hw, double cutoff, double ub,
                            uint64_t *keys, uint32_t *vals, int32_t *counts, hipStream_t stream);
 hipError_t bnb_sort_pairs(void *tmp, size_t &tmp_bytes, const uint64_t *keys_in,

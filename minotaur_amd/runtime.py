@@ -37,7 +37,7 @@ EXPORTS = [
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
     'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
     'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
-    'mgpu_lp_solve_path_dev',
+    'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive',
 ]
 
 
@@ -104,6 +104,7 @@ def load_library():
     lib.mgpu_bnb_init.argtypes = [_P, _I, _P, _P, _D]
     lib.mgpu_bnb_config.argtypes = [_P, _I, _I]
     lib.mgpu_bnb_brancher.argtypes = [_P, _I]
+    lib.mgpu_bnb_guided_dive.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
     lib.mgpu_bnb_import.argtypes = [_P, _I, _P, _P, _P, _P]
     lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
@@ -544,6 +545,10 @@ class Context:
         """Next tree: order 0 depth-first / 1 best-first; warm 0 root basis /
         1 parent basis (mgpu_bnb_config)."""
         self._chk(self.lib.mgpu_bnb_config(self.h, int(order), int(warm)), 'mgpu_bnb_config')
+
+    def bnb_guided_dive(self, on):
+        """Order 2: guided dive child order (IntVarHandler guided_dive)."""
+        self._chk(self.lib.mgpu_bnb_guided_dive(self.h, int(on)), 'mgpu_bnb_guided_dive')
 
     def bnb_brancher(self, kind):
         """Next tree's brancher: 0 MaxVio, 1 reliability (mgpu_bnb_brancher)."""
