@@ -115,7 +115,11 @@ int mgpu_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in,
  *                 inverse [m][m] COLUMN-major, i.e. binv[k*m+i] = (B^-1)_ik,
  *                 so lane i's row loads coalesce); ws_shared=1: one basis for
  *                 all nodes (e.g. the root optimum), else [batch] of each.
- *                 ws_head == NULL: slack basis.  Replaces
+ *                 ws_head == NULL: slack basis.  ws_d == NULL with a
+ *                 warm basis: the reduced costs are rebuilt in the kernel for
+ *                 the loaded objective (y = c_B' B^-1, d = c - A'y; a basis
+ *                 saved under another objective, e.g. the OBBT loop; runs on
+ *                 K3 / K3L).  Replaces
  *                 getWarmStartCopy/loadFromWarmStart (:375-384, :500-505).
  *   iter_limit  : pivots per LP; 0 = the reference default 10000
  *                 (OsiLPEngine maxIterLimit_, OsiLPEngine.cpp:99), < 0 = no

@@ -47,6 +47,7 @@ HipLPEngine::HipLPEngine(EnvPtr env, int device)
       consChanged_(true),
       objChanged_(true),
       needUpload_(true),
+      dStale_(false),
       wsValid_(false),
       sol_(0),
       maxIterLimit_(10000),
@@ -217,6 +218,7 @@ void HipLPEngine::refactor_() {
 }
 
 void HipLPEngine::recomputeDuals_() {
+  dStale_ = false;
   const int m = m_, n = n_, N = n_ + m_;
   std::vector<double> y(m, 0.0);
   for (int i = 0; i < m; ++i) {
@@ -250,7 +252,8 @@ EngineStatus HipLPEngine::solve() {
     }
     needUpload_ = false;
     if (wsValid_ && consChanged_) refactor_();
-    else if (wsValid_ && objChanged_) recomputeDuals_();
+    // new objective, same basis: the kernel rebuilds the reduced costs (d = NULL)
+    else if (wsValid_ && objChanged_) dStale_ = true;
   }
   // current column bounds (edits since the last solve)
   const int n = n_, m = m_, N = n_ + m_;
@@ -264,7 +267,8 @@ EngineStatus HipLPEngine::solve() {
   out.binv.resize((size_t)m * m);
   int rc = mgpu_lp_solve(ctx_, 1, clo_.data(), chi_.data(), 0,
                          wsValid_ ? ws_.head.data() : 0, wsValid_ ? ws_.st.data() : 0,
-                         wsValid_ ? ws_.d.data() : 0, wsValid_ ? ws_.binv.data() : 0, 1,
+                         wsValid_ && !dStale_ ? ws_.d.data() : 0,
+                         wsValid_ ? ws_.binv.data() : 0, 1,
                          iterLimit_, &st, &obj, &it, x_.data(), out.head.data(),
                          out.st.data(), out.d.data(), out.binv.data());
   if (rc != MGPU_OK) {
@@ -276,6 +280,7 @@ EngineStatus HipLPEngine::solve() {
     if (status_ == ProvenOptimal || status_ == EngineIterationLimit) {
       ws_ = out;
       wsValid_ = true;
+      dStale_ = false;
       // duals from the final basis: y = c_B B^-1, reduced costs d
       y_.assign(m, 0.0);
       for (int i = 0; i < m; ++i) {

@@ -127,6 +127,7 @@ class HipLPEngine : public LPEngine {
   std::vector<int32_t> rowptr_, colidx_, ctype_;
   std::vector<double> val_, rlo_, rhi_, clo_, chi_, obj_;
   bool bndChanged_, consChanged_, objChanged_, needUpload_;
+  bool dStale_;  // ws_.d is for an older objective: solve passes d = NULL
   HipLPWarmStart ws_;
   bool wsValid_;
   SolutionPtr sol_;

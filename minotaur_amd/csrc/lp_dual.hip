@@ -384,20 +384,31 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   #pragma unroll
       for (int k = 0; k < kLpMaxM; ++k)
         binv[k] = (lane < m && k < m) ? wb[(size_t)k * m + lane] : 0.0;  // column-major: coalesced
-      if (C.ocol < 0) {
+      if (C.ocol < 0 && io.ws.d != nullptr) {
         for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
       } else {
-        // bound LP: reduced costs of the warm basis for objective osign*x[ocol]
-        // (oracle compute_duals): y = c_B' B^-1 is osign * (row r of B^-1)
-        // when ocol is basic in row r, else 0; d_j = c_j - y' a_j.
-        const uint64_t on = __ballot(lane < m && h == C.ocol);
-        C.rho[lane] = 0.0;
-        wave_sync();
-        if (on != 0ull && lane == __builtin_ctzll(on)) {
+        // reduced costs of the warm basis for the loaded objective (oracle
+        // compute_duals): y = c_B' B^-1 accumulated over the basic rows in
+        // order -- for a bound LP c_B is osign at ocol's row --, then
+        // d_j = c_j - y' a_j.  A solve handed no d (the objective changed
+        // since the basis was saved, HipLPEngine's OBBT loop) lands here too.
+        const double cb = (lane < m && h < n) ? C.cj(h) : 0.0;
+        double yk = 0.0;
+        uint64_t rows = __ballot(cb != 0.0);
+        while (rows != 0ull) {
+          const int i = __builtin_ctzll(rows);
+          rows &= rows - 1;
+          if (lane == i) {  // publish row i of B^-1
   #pragma unroll
-          for (int k = 0; k < kLpMaxM; ++k)
-            if (k < m) C.rho[k] = 0.0 + C.osign * binv[k];
+            for (int k = 0; k < kLpMaxM; ++k)
+              if (k < m) C.aq[k] = binv[k];
+          }
+          wave_sync();
+          const double bik = lane < m ? C.aq[lane] : 0.0;
+          yk += rld(cb, i) * bik;
+          wave_sync();
         }
+        C.rho[lane] = lane < m ? yk : 0.0;
         wave_sync();
         for (int j = lane; j < N; j += 64) {
           if (C.st[j] == ST_BASIC) {
@@ -411,7 +422,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
             dot = 0.0;
             for (int t = C.colptr[j]; t < C.colptr[j + 1]; ++t) dot += C.cval[t] * C.rho[C.rowidx[t]];
           }
-          C.d[j] = C.cj(j) - dot;
+          C.d[j] = (j < n ? C.cj(j) : 0.0) - dot;
         }
       }
     } else {

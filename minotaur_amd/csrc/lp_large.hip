@@ -318,9 +318,25 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
       __syncthreads();
       for (int i = tid; i < m; i += kT) s.st[s.head[i]] = ST_BASIC;
       __syncthreads();
-      if (s.ocol < 0) {
+      if (s.ocol < 0 && io.ws.d != nullptr) {
         const double *wd = io.ws.d + bw * io.ws.s_d;
         for (int j = tid; j < N; j += kT) s.d[j] = s.st[j] == ST_BASIC ? 0.0 : wd[j];
+      } else if (s.ocol < 0) {
+        // no d with the warm start (objective changed since the basis was
+        // saved): oracle compute_duals, y = c_B' B^-1 over the basic rows in
+        // order (thread k owns y_k), d_j = c_j - y' a_j
+        for (int k = tid; k < m; k += kT) {
+          double y = 0.0;
+          for (int i = 0; i < m; ++i) {
+            const int hi = s.head[i];
+            const double cb = hi < n ? s.c[hi] : 0.0;
+            if (cb != 0.0) y += cb * s.Bi[(size_t)k * m + i];
+          }
+          s.rho[k] = y;
+        }
+        __syncthreads();
+        for (int j = tid; j < N; j += kT)
+          s.d[j] = s.st[j] == ST_BASIC ? 0.0 : (j < n ? s.c[j] : 0.0) - col_dot(s, s.rho, j);
       } else {
         // bound LP (oracle compute_duals): y = c_B' B^-1 = osign * row r of
         // B^-1 when ocol is basic in row r, else 0; d_j = c_j - y' a_j

@@ -507,7 +507,10 @@ bool use_pfi(const mgpu_ctx *c, const LpIO &io) {
   const bool shared = io.ws.head != nullptr && io.ws.s_head == 0 && io.ws.s_st == 0 &&
                       io.ws.s_d == 0 && io.ws.s_binv == 0 && io.ws_index == nullptr;
   bool wide;
-  return shared && io.wo_head == nullptr && pfi_cap(c, &wide) > 0;
+  // K3P/K3PW take d from the warm start (bound LPs rebuild it from ocol); a
+  // warm start without d for the loaded objective goes to K3 / K3L
+  const bool has_d = io.ws.d != nullptr || io.obj_col != nullptr;
+  return shared && has_d && io.wo_head == nullptr && pfi_cap(c, &wide) > 0;
 }
 
 int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
@@ -640,8 +643,10 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve: no problem loaded");
   if (batch < 0 || (batch > 0 && (!lb || !ub || !status || !obj || !iters)))
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: bad argument");
-  if (ws_head && (!ws_st || !ws_d || !ws_binv))
-    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: warm start needs head, st, d and binv");
+  // ws_d may be null: the kernel then rebuilds the reduced costs of the warm
+  // basis for the loaded objective (a basis saved under another objective)
+  if (ws_head && (!ws_st || !ws_binv))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: warm start needs head, st and binv");
   if (wo_head && (!wo_st || !wo_d || !wo_binv))
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve: warm-start output needs all four arrays");
   if (batch == 0) return MGPU_OK;
@@ -790,7 +795,7 @@ int mgpu_lp_solve(mgpu_ctx *c, int batch, const double *lb, const double *ub,
   if (ws_head) {
     HIPCHK(c, h2d(c->lp_wh, ws_head, wsB * m * 4));
     HIPCHK(c, h2d(c->lp_wst, ws_st, wsB * N));
-    HIPCHK(c, h2d(c->lp_wd, ws_d, wsB * N * 8));
+    if (ws_d) HIPCHK(c, h2d(c->lp_wd, ws_d, wsB * N * 8));
     HIPCHK(c, h2d(c->lp_wb, ws_binv, wsB * m * m * 8));
   }
   HIPCHK(c, c->lp_st.ensure(B * 4));
@@ -806,7 +811,7 @@ int mgpu_lp_solve(mgpu_ctx *c, int batch, const double *lb, const double *ub,
   int rc = mgpu_lp_solve_dev(
       c, batch, c->lp_lb.as<double>(), c->lp_ub.as<double>(),
       skip ? c->lp_skip.as<int32_t>() : nullptr, ws_head ? c->lp_wh.as<int32_t>() : nullptr,
-      ws_head ? c->lp_wst.as<int8_t>() : nullptr, ws_head ? c->lp_wd.as<double>() : nullptr,
+      ws_head ? c->lp_wst.as<int8_t>() : nullptr, ws_d ? c->lp_wd.as<double>() : nullptr,
       ws_head ? c->lp_wb.as<double>() : nullptr, ws_shared, iter_limit, c->lp_st.as<int32_t>(),
       c->lp_obj.as<double>(), c->lp_it.as<int32_t>(), x ? c->lp_x.as<double>() : nullptr,
       wo_head ? c->lp_oh.as<int32_t>() : nullptr, wo_head ? c->lp_ost.as<int8_t>() : nullptr,

@@ -22,8 +22,19 @@ previous one; the batch warm-starts all from the root basis.  Optimal values
 agree to LP tolerance (1e-6, the north-star bar); at degenerate optima the
 primal vertex fed to setItmpFromSol_ can differ, which the tests check
 against the same replay over the CPU oracle's LPs.
+
+* ``obbt_chained`` — the exact mode: tightenLP_'s loop as the reference runs
+  it with HipLPEngine as bte_, one bound LP at a time on the GPU, each from
+  the previous LP's optimal basis (bte_->load drops the warm start, so the
+  first LP starts from the slack basis; a basis survives only ProvenOptimal /
+  EngineIterationLimit, HipLPEngine::solve), the reduced costs of that basis
+  rebuilt in the kernel for the new objective (mgpu_lp_solve with ws_d =
+  NULL).  Same LPs, same vertices, so the same setItmpFromSol_ decisions and
+  the same final bounds as the reference's postSolveRootNode.
 """
 from __future__ import annotations
+
+import dataclasses
 
 import math
 
@@ -229,3 +240,78 @@ def obbt(ctx, qp, rows, x_root, ws, lb=None, ub=None, incumbent=math.inf, iter_l
            for i, (c, s) in enumerate(zip(cols, signs))}
     inf, nlb, nub, mods, used = replay(qp, itmp, lb, ub, res)
     return inf, nlb, nub, mods, int(cols.size), used
+
+
+def _bound_objective(p, v, sign):
+    """lp->changeObj(x_v or -x_v, 0.0) (QuadHandler.cpp:2258-2278)."""
+    c = np.zeros(p.n)
+    c[v] = sign
+    return dataclasses.replace(p, name=f'{p.name}-obj{v}{"+" if sign > 0 else "-"}', obj=c,
+                               obj_const=0.0)
+
+
+class GpuChain:
+    """One bound LP on the GPU the way HipLPEngine::solve runs it: the loaded
+    problem's objective, warm basis (head, st, binv) without reduced costs
+    (rebuilt in K3 / K3L for this objective), x and the final basis back."""
+
+    def __init__(self, ctx, iter_limit=0):
+        self.ctx, self.iter_limit = ctx, iter_limit
+
+    def __call__(self, p, ws):
+        from .runtime import WarmStart
+        self.ctx.load(p)
+        o = self.ctx.lp_solve(p.vlb[None], p.vub[None], ws=ws, iter_limit=self.iter_limit,
+                              want_x=True, want_ws=True)
+        st = int(o.status[0])
+        wo = None
+        if st in (0, 6):
+            wo = WarmStart(o.ws.head[0], o.ws.st[0], None, o.ws.binv[0])
+        return st, float(o.obj[0]), o.x[0], wo
+
+
+def obbt_chained(solve, qp, rows, x_root, lb=None, ub=None, incumbent=math.inf):
+    """tightenLP_ (QuadHandler.cpp:2218-2297) one bound LP at a time, each
+    warm-started from the last optimal basis.  ``solve(p, ws) -> (status,
+    obj, x, ws_out)`` solves LinProblem p (ws None: slack basis; ws_out None
+    unless optimal / iteration limit): ``GpuChain(ctx)`` on the device, or a
+    CPU restatement in tests.  Returns (infeasible, lb, ub, mods, log) with
+    log[k] = (col, sign, status, value) of every LP solved, in order."""
+    lb = np.array(qp.vlb if lb is None else lb, dtype=np.float64)
+    ub = np.array(qp.vub if ub is None else ub, dtype=np.float64)
+    itmp = select_vars(qp, x_root, lb, ub)
+    # the clone: bounds frozen at load, cutoff row when an incumbent is known
+    rel = relaxation_lp(qp, rows, lb.copy(), ub.copy(), incumbent)
+    mods, log = [], []
+    ws = None
+
+    def bnd(v, sign):
+        nonlocal ws
+        st, ob, xs, wo = solve(_bound_objective(rel, v, sign), ws)
+        if wo is not None:
+            ws = wo
+        log.append((v, sign, st, ob))
+        if st in (0, 6, 4):            # getBndByLP_ (:2080-2109)
+            return ob, False, xs
+        return math.inf, True, xs
+
+    for v in range(qp.nv):
+        t = itmp[v]
+        if t == 0:
+            continue
+        nlb, nub = -math.inf, math.inf
+        if t in (1, 3):
+            b, inf, xs = bnd(v, 1.0)
+            if inf:
+                continue
+            nlb = b
+            _set_itmp_from_sol(itmp, xs, lb, ub)
+        if t == 2:
+            b, inf, xs = bnd(v, -1.0)
+            if inf:
+                continue
+            nub = -b
+            _set_itmp_from_sol(itmp, xs, lb, ub)
+        if _update_pbounds(v, nlb, nub, qp.vtype, lb, ub, mods) < 0:
+            return True, lb, ub, mods, log
+    return False, lb, ub, mods, log

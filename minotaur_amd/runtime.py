@@ -394,7 +394,7 @@ class Context:
         if ws is not None:
             wh = _np(ws.head, np.int32)
             wst = _np(ws.st, np.int8)
-            wd = _np(ws.d, np.float64)
+            wd = None if ws.d is None else _np(ws.d, np.float64)  # None: rebuilt
             wb = _np(ws.binv, np.float64)
             shared = 1 if wh.ndim == 1 else 0
         sk = None if skip is None else _np(skip, np.int32)

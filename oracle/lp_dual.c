@@ -709,7 +709,7 @@ int orc_dual_simplex_batch(int n, int m, const int *colptr, const int *rowidx,
     for (int b = 0; b < B; ++b) {
       int have = ws_head != 0;
       status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n, ws_head, ws_st,
-                               ws_binv, ws_d, have, have && ws_binv != 0 && ws_d != 0,
+                               ws_binv, ws_d, have, have && ws_binv != 0,
                                iter_limit, obj + b, x ? x + (size_t) b * n : 0, iters + b, pfi,
                                h, s, bi, dd, 0);
     }
@@ -832,9 +832,14 @@ int orc_dual_simplex_nodes(int n, int m, const int *colptr, const int *rowidx,
   const size_t N = (size_t) (n + m), mm = (size_t) m * m;
 #pragma omp parallel for num_threads(nthreads) schedule(dynamic, 8)
   for (int b = 0; b < B; ++b) {
-    status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n, ws_head + (size_t) b * m,
-                             ws_st + (size_t) b * N, ws_binv + (size_t) b * mm,
-                             ws_d + (size_t) b * N, 1, 1, iter_limit, obj + b,
+    /* ws_head NULL: slack basis; ws_d NULL: reduced costs rebuilt for c */
+    int have = ws_head != 0;
+    status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n,
+                             have ? ws_head + (size_t) b * m : 0,
+                             have ? ws_st + (size_t) b * N : 0,
+                             have ? ws_binv + (size_t) b * mm : 0,
+                             have && ws_d ? ws_d + (size_t) b * N : 0, have, have, iter_limit,
+                             obj + b,
                              x ? x + (size_t) b * n : 0, iters + b, 0, wo_head + (size_t) b * m,
                              wo_st + (size_t) b * N, wo_binv + (size_t) b * mm,
                              wo_d + (size_t) b * N, 0);

@@ -198,7 +198,10 @@ def dual_simplex(p, LB, UB, ws=None, iter_limit=10000, nthreads=1, want_x=False,
         h = np.ascontiguousarray(ws.head, dtype=np.int32)
         s = np.ascontiguousarray(ws.st, dtype=np.int8)
         bi = np.ascontiguousarray(ws.binv, dtype=np.float64)
-        dd = np.ascontiguousarray(ws.d, dtype=np.float64)
+        if ws.d is not None:
+            dd = np.ascontiguousarray(ws.d, dtype=np.float64)
+        else:
+            pfi = 0  # no d: reduced costs rebuilt for this objective, dense K3 on the GPU
     l.orc_dual_simplex_batch(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj),
                              _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(h),
                              _ptr(s), _ptr(bi), _ptr(dd), iter_limit, _ptr(st), _ptr(obj), _ptr(x),
@@ -209,7 +212,8 @@ def dual_simplex(p, LB, UB, ws=None, iter_limit=10000, nthreads=1, want_x=False,
 
 def dual_simplex_nodes(p, LB, UB, ws, iter_limit=10000, nthreads=1):
     """Per-node warm starts in and out (dense arithmetic, K3/K3L): ws is a
-    WarmStart whose arrays carry a leading batch axis (binv row-major);
+    WarmStart whose arrays carry a leading batch axis (binv row-major), or
+    None (slack basis); ws.d None rebuilds the reduced costs for p.obj;
     returns (status, obj incl. constant, iters, x, WarmStart out)."""
     l = lib()
     l.orc_dual_simplex_nodes.restype = _I
@@ -219,21 +223,39 @@ def dual_simplex_nodes(p, LB, UB, ws, iter_limit=10000, nthreads=1):
     UB = np.ascontiguousarray(UB, dtype=np.float64)
     B = LB.shape[0]
     colptr, rowidx, cval = lp_csc(p)
-    h = np.ascontiguousarray(ws.head, dtype=np.int32)
-    s = np.ascontiguousarray(ws.st, dtype=np.int8)
-    bi = np.ascontiguousarray(ws.binv, dtype=np.float64)
-    dd = np.ascontiguousarray(ws.d, dtype=np.float64)
+    N = p.n + p.m
+    h = s = bi = dd = None
+    if ws is not None:    # None: slack basis
+        h = np.ascontiguousarray(ws.head, dtype=np.int32)
+        s = np.ascontiguousarray(ws.st, dtype=np.int8)
+        bi = np.ascontiguousarray(ws.binv, dtype=np.float64)
+        if ws.d is not None:  # None: reduced costs rebuilt for p's objective
+            dd = np.ascontiguousarray(ws.d, dtype=np.float64)
     st = np.zeros(B, dtype=np.int32)
     obj = np.zeros(B)
     it = np.zeros(B, dtype=np.int32)
     x = np.zeros((B, p.n))
-    wo = WarmStart(np.zeros_like(h), np.zeros_like(s), np.zeros_like(bi), np.zeros_like(dd))
+    wo = WarmStart(np.zeros((B, p.m), np.int32), np.zeros((B, N), np.int8),
+                   np.zeros((B, p.m, p.m)), np.zeros((B, N)))
     l.orc_dual_simplex_nodes(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj),
                              _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(h), _ptr(s),
                              _ptr(bi), _ptr(dd), iter_limit, _ptr(st), _ptr(obj), _ptr(x),
                              _ptr(it), _ptr(wo.head), _ptr(wo.st), _ptr(wo.binv), _ptr(wo.d),
                              nthreads)
     return st, obj + p.obj_const, it, x, wo
+
+
+def chain_solve(p, ws, iter_limit=10000):
+    """One LP of p from the single warm start ws (None: slack basis; ws.d
+    None: reduced costs rebuilt for p.obj) with its final basis back when
+    optimal / at the iteration limit: minotaur_amd.obbt.obbt_chained's solve
+    step restated on the CPU (K3's dense arithmetic)."""
+    W = None if ws is None else WarmStart(ws.head[None], ws.st[None], ws.binv[None], None)
+    st, obj, it, x, wo = dual_simplex_nodes(p, p.vlb[None], p.vub[None], W, iter_limit)
+    out = None
+    if st[0] in (0, 6):
+        out = WarmStart(wo.head[0], wo.st[0], wo.binv[0], None)
+    return int(st[0]), float(obj[0]), x[0], out
 
 
 PATH_MAX = 32     # ORC_PATH_MAX = MGPU_PATH_MAX: pivots per path warm start

@@ -260,3 +260,31 @@ def test_default_iteration_limit_is_osilp_default():
         assert np.any(g.status == 6) and np.all(g.iters[g.status == 6] == cap)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize('variant', [0, 2])
+@pytest.mark.parametrize('name', ['tls4', 'knapsack', 'random3'])
+def test_warm_basis_without_reduced_costs(ctx, name, variant):
+    """ws_d = NULL: a basis saved under one objective, solved under another
+    (HipLPEngine after changeObj, the chained OBBT): K3 (variant 0 routes a
+    d-less warm start to it) and K3L rebuild y = c_B' B^-1 and d = c - A'y
+    as the oracle's compute_duals does -- statuses, pivots and objective
+    bits equal the oracle's."""
+    import dataclasses
+    from minotaur_amd.runtime import WarmStart
+    p, g = load_lp(name)
+    ctx.load(p)
+    root, ws = ctx.root_solve()
+    rng = np.random.default_rng(7)
+    q = dataclasses.replace(p, obj=np.round(rng.normal(size=p.n), 3))
+    ctx.load(q)
+    lb, ub = g['lb'][:64], g['ub'][:64]
+    ctx.set_lp_variant(variant)
+    try:
+        r = ctx.lp_solve(lb, ub, WarmStart(ws.head, ws.st, None, ws.binv), want_x=True)
+    finally:
+        ctx.set_lp_variant(0)
+    ows = oracle.WarmStart(ws.head, ws.st, ws.binv_rows(), None)
+    st, obj, it, _ = oracle.dual_simplex(q, lb, ub, ows)
+    assert np.array_equal(r.status, st) and np.array_equal(r.iters, it)
+    assert np.array_equal(r.obj, obj)

@@ -63,3 +63,51 @@ def test_select_vars_marks():
     assert set(np.unique(itmp)) <= {0, 1, 2, 3}
     narrow = (qp.vub - qp.vlb) < 2
     assert np.all(itmp[narrow] == 0)
+
+
+@pytest.mark.parametrize('seed', [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize('cut', [False, True])
+def test_chained_obbt_restatement(seed, cut):
+    """obbt_chained over the C oracle (one bound LP at a time, each from the
+    previous optimal basis with rebuilt reduced costs): every LP's value is
+    HiGHS's, the flagged LPs are a subset of the batch, the feasible point
+    survives.  (The GPU test pins it to the reference's own tightenLP_.)"""
+    qp = random_qcqp(seed, nv0=8, ncon=4)
+    rows = oracle.quad_root_rows(qp)
+    p0 = obbt.relaxation_lp(qp, rows)
+    st, ob, x, y, it, ws = oracle.dual_simplex_root(p0)
+    assert st == 0
+    inc = ob + 1.0 + abs(ob) if cut else math.inf
+    inf, lb, ub, mods, log = obbt.obbt_chained(oracle.chain_solve, qp, rows, x, incumbent=inc)
+    assert not inf and log
+    p = obbt.relaxation_lp(qp, rows, cutoff=inc)
+    itmp = obbt.select_vars(qp, x, qp.vlb, qp.vub)
+    cols, signs = obbt.bound_lp_batch(itmp)
+    flagged = set(zip(cols.tolist(), signs.tolist()))
+    for v, s, st_k, val in log:
+        assert (v, s) in flagged
+        c = np.zeros(p.n)
+        c[v] = s
+        hs, ho = oracle.highs_obj(p, c)
+        assert hs == st_k
+        if st_k == 0:
+            assert abs(ho - val) <= 1e-6 * max(1.0, abs(ho))
+    assert np.all(lb >= qp.vlb) and np.all(ub <= qp.vub)
+    if not cut:   # (a cutoff may legitimately remove the known feasible point)
+        tol = 1e-6 * (1 + np.abs(qp.xstar))
+        assert np.all(lb <= qp.xstar + tol) and np.all(qp.xstar <= ub + tol)
+
+
+def test_chain_solve_rebuilds_reduced_costs():
+    """A warm basis handed over without reduced costs is re-priced for the
+    new objective: the same optimum as from the slack basis."""
+    qp = random_qcqp(2, nv0=8, ncon=4)
+    rows = oracle.quad_root_rows(qp)
+    p = obbt.relaxation_lp(qp, rows)
+    st, ob, x, ws = oracle.chain_solve(p, None)
+    assert st == 0 and ws is not None and ws.d is None
+    q = obbt._bound_objective(p, int(qp.sq_x[0]), -1.0)
+    a = oracle.chain_solve(q, ws)
+    b = oracle.chain_solve(q, None)
+    assert a[0] == b[0] == 0
+    assert abs(a[1] - b[1]) <= 1e-9 * max(1.0, abs(b[1]))
