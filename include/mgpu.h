@@ -279,6 +279,38 @@ int mgpu_set_lp_pfi_wide(mgpu_ctx *ctx, int kmax);
  * pfi=k)); 0 when such a batch runs a dense kernel (K3 / K3L). */
 int mgpu_lp_pfi_cap(mgpu_ctx *ctx);
 
+/* ---- the single-LP route (an LPEngine solving one LP at a time) ----
+ * Replaces the per-solve traffic of OsiLPEngine::solve / getWarmStartCopy /
+ * loadFromWarmStart (src/interfaces/OsiLPEngine.cpp:571-652, :375-384,
+ * :500-505) for HipLPEngine: warm starts stay in DEVICE slots (basic column
+ * per row, column status, reduced costs, basis inverse of the loaded
+ * problem's n, m), the host only passes slot ids, and one call is one K3 /
+ * K3L launch that reads the box from and writes its results to a pinned host
+ * block (no copy-engine transfers).
+ *   mgpu_ws_alloc : a free slot sized for the loaded problem (slots of other
+ *                   sizes stay valid for their problem);
+ *   mgpu_ws_free  : return it (no device work);
+ *   mgpu_ws_read / mgpu_ws_write : host copies (head [m], st [n+m], d [n+m],
+ *                   binv [m][m] column-major; NULL skips an array on read, d
+ *                   may be NULL on write) -- synchronous, for rare host edits
+ *                   (rows added / removed, refactor);
+ *   mgpu_lp_solve1: one LP on box lb/ub [n] from slot ws_in (-1: slack
+ *                   basis; ws_d = 0: the slot's reduced costs are for another
+ *                   objective and are rebuilt), final basis into slot ws_out
+ *                   (-1: none; written when status is 0 or 6), status / obj
+ *                   (incl. the objective constant) / iters as mgpu_lp_solve,
+ *                   x [n] and rc [n+m] (reduced costs of the structurals,
+ *                   then of the logicals = the row duals y; 0 for basic
+ *                   columns) when status is 0 or 6.  Synchronous. */
+int mgpu_ws_alloc(mgpu_ctx *ctx, int *slot);
+int mgpu_ws_free(mgpu_ctx *ctx, int slot);
+int mgpu_ws_read(mgpu_ctx *ctx, int slot, int32_t *head, int8_t *st, double *d, double *binv);
+int mgpu_ws_write(mgpu_ctx *ctx, int slot, const int32_t *head, const int8_t *st,
+                  const double *d, const double *binv);
+int mgpu_lp_solve1(mgpu_ctx *ctx, const double *lb, const double *ub, int ws_in, int ws_d,
+                   int ws_out, int iter_limit, int32_t *status, double *obj, int32_t *iters,
+                   double *x, double *rc);
+
 /* Batched bound LPs: LP b minimises obj_sign[b] * x[obj_col[b]] over the
  * loaded relaxation on ONE box lb/ub [n] (the relaxation's), warm-started
  * from one shared basis (head [m], st [n+m], binv [m][m] column-major, as

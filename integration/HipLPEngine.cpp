@@ -33,7 +33,32 @@ using namespace Minotaur;
 const std::string HipLPEngine::me_ = "HipLPEngine: ";
 
 void HipLPWarmStart::write(std::ostream &out) const {
-  out << "HipLPWarmStart: " << head.size() << " basic columns" << std::endl;
+  out << "HipLPWarmStart: " << (dev ? dev->m : (int)head.size()) << " basic columns"
+      << (dev ? " (device)" : "") << std::endl;
+}
+
+HipLPCtx::~HipLPCtx() {
+  if (ctx) mgpu_destroy(ctx);
+}
+
+HipLPSlot::~HipLPSlot() {
+  if (owner && owner->ctx && id >= 0) mgpu_ws_free(owner->ctx, id);
+}
+
+bool HipLPWarmStart::fetch() {
+  if (!head.empty()) return true;
+  if (!dev || !dev->owner || !dev->owner->ctx) return false;
+  const int n = dev->n, m = dev->m;
+  head.resize(m);
+  st.resize(n + m);
+  d.resize(n + m);
+  binv.resize((size_t)m * m);
+  if (mgpu_ws_read(dev->owner->ctx, dev->id, head.data(), st.data(), d.data(), binv.data()) !=
+      MGPU_OK) {
+    head.clear();
+    return false;
+  }
+  return true;
 }
 
 HipLPEngine::HipLPEngine(EnvPtr env, int device)
@@ -59,14 +84,17 @@ HipLPEngine::HipLPEngine(EnvPtr env, int device)
   std::memset(stats_, 0, sizeof(HipLPStats));
   timer_ = env_->getNewTimer();
   status_ = EngineUnknownStatus;
-  if (mgpu_create(device_, &ctx_) != MGPU_OK) {
-    ctx_ = 0;
+  own_ = std::make_shared<HipLPCtx>();
+  if (mgpu_create(device_, &own_->ctx) != MGPU_OK) {
+    own_->ctx = 0;
     logger_->errStream() << me_ << "no HIP device " << device_ << std::endl;
   }
+  ctx_ = own_->ctx;
 }
 
 HipLPEngine::~HipLPEngine() {
-  if (ctx_) mgpu_destroy(ctx_);
+  ws_ = HipLPWarmStart();
+  own_.reset();  // the context goes with the last warm start still holding a slot
   delete stats_;
   delete timer_;
   if (problem_) {
@@ -128,6 +156,7 @@ void HipLPEngine::load(ProblemPtr problem) {
   delete sol_;
   sol_ = new Solution(1E20, 0, problem_);
   wsValid_ = false;
+  ws_ = HipLPWarmStart();
   objChanged_ = bndChanged_ = consChanged_ = needUpload_ = true;
   problem->setEngine(this);
 }
@@ -147,6 +176,8 @@ int HipLPEngine::upload_() {
 // singular basis is dropped for the slack basis.
 void HipLPEngine::refactor_() {
   const int m = m_, n = n_;
+  ws_.fetch();
+  ws_.dev.reset();  // the host vectors are edited below
   if ((int)ws_.head.size() != m) {
     wsValid_ = false;
     return;
@@ -255,42 +286,37 @@ EngineStatus HipLPEngine::solve() {
     // new objective, same basis: the kernel rebuilds the reduced costs (d = NULL)
     else if (wsValid_ && objChanged_) dStale_ = true;
   }
-  // current column bounds (edits since the last solve)
+  // current column bounds (edits since the last solve); the LP starts from
+  // the kept basis in its device slot and leaves its basis in a fresh slot
   const int n = n_, m = m_, N = n_ + m_;
   int32_t st = 0, it = 0;
   double obj = 0.0;
-  x_.assign(n, 0.0);
-  HipLPWarmStart out;
-  out.head.resize(m);
-  out.st.resize(N);
-  out.d.resize(N);
-  out.binv.resize((size_t)m * m);
-  int rc = mgpu_lp_solve(ctx_, 1, clo_.data(), chi_.data(), 0,
-                         wsValid_ ? ws_.head.data() : 0, wsValid_ ? ws_.st.data() : 0,
-                         wsValid_ && !dStale_ ? ws_.d.data() : 0,
-                         wsValid_ ? ws_.binv.data() : 0, 1,
-                         iterLimit_, &st, &obj, &it, x_.data(), out.head.data(),
-                         out.st.data(), out.d.data(), out.binv.data());
+  x_.resize(n);
+  rcAll_.resize(N);
+  int in = -1;
+  if (wsValid_) {
+    in = devWs_();
+    if (in < 0) wsValid_ = false;
+  }
+  std::shared_ptr<HipLPSlot> out = newSlot_();
+  int rc = out ? mgpu_lp_solve1(ctx_, clo_.data(), chi_.data(), in, dStale_ ? 0 : 1, out->id,
+                                iterLimit_, &st, &obj, &it, x_.data(), rcAll_.data())
+               : MGPU_ERR_NOMEM;
   if (rc != MGPU_OK) {
-    logger_->errStream() << me_ << mgpu_last_error(ctx_) << std::endl;
+    logger_->errStream() << me_ << (ctx_ ? mgpu_last_error(ctx_) : "no context") << std::endl;
     status_ = EngineError;
     sol_->setObjValue(INFINITY);
   } else {
     status_ = (EngineStatus)st;
     if (status_ == ProvenOptimal || status_ == EngineIterationLimit) {
-      ws_ = out;
+      ws_ = HipLPWarmStart();
+      ws_.dev = out;
       wsValid_ = true;
       dStale_ = false;
-      // duals from the final basis: y = c_B B^-1, reduced costs d
-      y_.assign(m, 0.0);
-      for (int i = 0; i < m; ++i) {
-        const int h = ws_.head[i];
-        const double cb = h < n ? obj_[h] : 0.0;
-        if (cb != 0.0)
-          for (int k = 0; k < m; ++k) y_[k] += cb * ws_.binv[(size_t)k * m + i];
-      }
-      rc_.assign(n, 0.0);
-      for (int j = 0; j < n; ++j) rc_[j] = ws_.st[j] == 3 ? 0.0 : ws_.d[j];
+      // duals from the final basis, computed in the kernel: reduced costs of
+      // the structurals, and of the logicals (d_{n+r} = y_r for the row -e_r)
+      rc_.assign(rcAll_.begin(), rcAll_.begin() + n);
+      y_.assign(rcAll_.begin() + n, rcAll_.end());
       sol_->setPrimal(x_.data());
       sol_->setObjValue(obj + off);
       sol_->setDualOfCons(y_.data());
@@ -330,6 +356,8 @@ EngineStatus HipLPEngine::solve() {
 
 void HipLPEngine::addConstraint(ConstraintPtr) {
   // the new row's logical joins the basis (refactor_ on the next solve)
+  if (wsValid_ && !ws_.fetch()) wsValid_ = false;
+  ws_.dev.reset();
   if (wsValid_) {
     const int N = n_ + m_;
     ws_.head.push_back(N);
@@ -341,6 +369,8 @@ void HipLPEngine::addConstraint(ConstraintPtr) {
 
 void HipLPEngine::removeCons(std::vector<ConstraintPtr> &delcons) {
   // basis kept only if every removed row's logical is basic
+  if (wsValid_ && !ws_.fetch()) wsValid_ = false;
+  ws_.dev.reset();
   if (wsValid_) {
     std::vector<char> del(m_, 0);
     for (ConstraintPtr c : delcons) del[c->getIndex()] = 1;
@@ -419,6 +449,7 @@ void HipLPEngine::negateObj() {
 
 void HipLPEngine::clear() {
   wsValid_ = false;
+  ws_ = HipLPWarmStart();
   needUpload_ = true;
   if (problem_) {
     problem_->unsetEngine();
@@ -445,16 +476,52 @@ WarmStartPtr HipLPEngine::getWarmStartCopy() {
 }
 
 void HipLPEngine::loadFromWarmStart(const WarmStartPtr ws) {
-  const HipLPWarmStart *w = dynamic_cast<const HipLPWarmStart *>(ws);
+  HipLPWarmStart *w = dynamic_cast<HipLPWarmStart *>(ws);
   assert(w);
-  if (w && !w->head.empty() && (int)w->head.size() == m_ &&
-      (int)w->st.size() == n_ + m_) {
-    ws_ = *w;
+  if (!w) return;
+  if (w->dev && w->dev->owner == own_ && w->dev->n == n_ && w->dev->m == m_) {
+    ws_ = *w;  // shares the device slot: no device work
+    wsValid_ = true;
+    return;
+  }
+  // another engine's warm start (testOsiWarmStart): through the host
+  HipLPWarmStart h = *w;
+  if (!h.fetch()) return;
+  h.dev.reset();
+  if ((int)h.head.size() == m_ && (int)h.st.size() == n_ + m_) {
+    ws_ = h;
     wsValid_ = true;
   }
 }
 
+std::shared_ptr<HipLPSlot> HipLPEngine::newSlot_() {
+  int id = -1;
+  if (!ctx_ || mgpu_ws_alloc(ctx_, &id) != MGPU_OK) return nullptr;
+  std::shared_ptr<HipLPSlot> s = std::make_shared<HipLPSlot>();
+  s->owner = own_;
+  s->id = id;
+  s->n = n_;
+  s->m = m_;
+  return s;
+}
+
+int HipLPEngine::devWs_() {
+  if (ws_.dev && ws_.dev->owner == own_ && ws_.dev->n == n_ && ws_.dev->m == m_)
+    return ws_.dev->id;
+  if (!ws_.fetch() || (int)ws_.head.size() != m_ || (int)ws_.st.size() != n_ + m_ ||
+      ws_.binv.size() != (size_t)m_ * m_)
+    return -1;
+  std::shared_ptr<HipLPSlot> s = newSlot_();
+  if (!s ||
+      mgpu_ws_write(ctx_, s->id, ws_.head.data(), ws_.st.data(),
+                    (int)ws_.d.size() == n_ + m_ ? ws_.d.data() : 0, ws_.binv.data()) != MGPU_OK)
+    return -1;
+  ws_.dev = s;
+  return s->id;
+}
+
 void HipLPEngine::getBasics(int *index) {
+  if (wsValid_ && !ws_.fetch()) return;
   for (int i = 0; i < m_ && wsValid_; ++i) index[i] = ws_.head[i];
 }
 

@@ -16,6 +16,7 @@
 #define MINOTAURHIPLPENGINE_H
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -44,20 +45,42 @@ struct HipLPStats {
   UInt strIters;
 };
 
+// The engine's mgpu context.  Shared by the engine and every device warm
+// start it handed out, so a tree node's warm start outliving the engine still
+// frees its slot into a live context.
+struct HipLPCtx {
+  mgpu_ctx *ctx = nullptr;
+  ~HipLPCtx();
+};
+
+// One device warm-start slot (mgpu_ws_alloc) of an n x m problem; freed when
+// the last warm start holding it dies.
+struct HipLPSlot {
+  std::shared_ptr<HipLPCtx> owner;
+  int id = -1, n = 0, m = 0;
+  ~HipLPSlot();
+};
+
 // Warm start = the engine's basis: basic column per row, column status,
 // reduced costs and the dense basis inverse (column-major).  The reference
-// keeps Clp's CoinWarmStartBasis (OsiLPEngine.cpp:375-384, 500-505).
+// keeps Clp's CoinWarmStartBasis (OsiLPEngine.cpp:375-384, 500-505).  Here
+// the basis normally lives in a device slot (dev), written by the solve that
+// produced it and read by the next solve that starts from it; copies share
+// the slot (it is never written again).  The host vectors are filled only
+// when a host edit needs them (fetch), or hold a basis not yet uploaded.
 class HipLPWarmStart : public WarmStart {
  public:
   HipLPWarmStart() {}
   ~HipLPWarmStart() {}
-  bool hasInfo() { return !head.empty(); }
+  bool hasInfo() { return dev != nullptr || !head.empty(); }
   void write(std::ostream &out) const;
+  bool fetch();  // host vectors from the device slot (if empty); false if none
 
   std::vector<int32_t> head;
   std::vector<int8_t> st;
   std::vector<double> d;
   std::vector<double> binv;
+  std::shared_ptr<HipLPSlot> dev;
 };
 typedef HipLPWarmStart *HipLPWarmStartPtr;
 
@@ -118,9 +141,12 @@ class HipLPEngine : public LPEngine {
   void refactor_();            // host Gauss-Jordan of the kept basis
   void recomputeDuals_();      // d = c - A'y, y = c_B B^-1
   int upload_();
+  std::shared_ptr<HipLPSlot> newSlot_();  // a free device slot for this problem
+  int devWs_();                // slot id of ws_ in this context (uploads a host basis)
 
   EnvPtr env_;
   ProblemPtr problem_;
+  std::shared_ptr<HipLPCtx> own_;
   mgpu_ctx *ctx_;
   int device_;
   int n_, m_;
@@ -135,7 +161,7 @@ class HipLPEngine : public LPEngine {
   bool strBr_;
   HipLPStats *stats_;
   Timer *timer_;
-  std::vector<double> x_, y_, rc_;
+  std::vector<double> x_, y_, rc_, rcAll_;
   std::vector<SolveRec> log_;
   static const std::string me_;
 };

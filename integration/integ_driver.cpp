@@ -129,6 +129,16 @@ int integ_lp_eg0(int device) {
   return s;
 }
 
+// HipLPEngine::fillStats of the engine of the last integ_bnb / integ_bnb_tree
+// run: calls, strong-branching calls, seconds in solve, strong-branching
+// seconds, pivots, strong-branching pivots (integ_last_lp_stats).
+static std::vector<double> g_last_lp_stats(6, 0.0);
+
+int integ_last_lp_stats(double *out) {
+  for (int k = 0; k < 6; ++k) out[k] = g_last_lp_stats[k];
+  return 0;
+}
+
 // AMPLOsiUT::testOsiBnB generalised: the reference BranchAndBound with
 // IntVarHandler + (reference LinearHandler | HipLinearHandler), PCBProcessor,
 // ReliabilityBrancher and NodeIncRelaxer, all on a HipLPEngine.
@@ -174,6 +184,7 @@ int integ_bnb(int device, int hip_fbbt, int n, int m, const int *rowptr, const i
   std::vector<double> lps(6, 0.0);
   e->fillStats(lps);
   cnt[1] = (int)lps[0];
+  g_last_lp_stats = lps;
   cnt[2] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuCalls() : 0;
   cnt[3] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuLoads() : 0;
   cnt[4] = hip_fbbt ? (int)((HipLinearHandler *)l_hand)->gpuErrors() : 0;
@@ -258,6 +269,7 @@ int integ_bnb_tree(int device, int hip_fbbt, int brancher, int guided, int n, in
   cnt[3] = (long long)lps[1];
   cnt[4] = (long long)lps[4];
   cnt[5] = (long long)lps[5];
+  g_last_lp_stats = lps;
   delete v_hand;
   delete l_hand;
   delete e;

@@ -85,6 +85,20 @@ struct mgpu_ctx {
   DevBuf nr_map, nr_ws, nr_vals;
   hipEvent_t ev9 = nullptr, ev10 = nullptr;  // around K3R
   double last_refac_ms = 0.0;
+  // device warm-start slots (mgpu_ws_*): chunks of equal-size slots per (n, m)
+  struct WsChunk {
+    char *base = nullptr;
+    int n = 0, m = 0, cap = 0;
+    size_t bytes = 0;          // one slot
+    std::vector<int> free;
+  };
+  std::vector<WsChunk> ws_chunks;
+  // single-LP route (mgpu_lp_solve1): pinned host block the kernel reads the
+  // box from and writes its results to (zero copy)
+  char *lp1_pin = nullptr;
+  size_t lp1_pin_bytes = 0;
+  char *fb1_pin = nullptr;     // the same for mgpu_fbbt at batch 1
+  size_t fb1_pin_bytes = 0;
   QuadState *quad = nullptr;   // K2 problem (mgpu_load_quad)
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
   QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)

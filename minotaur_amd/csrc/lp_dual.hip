@@ -32,7 +32,9 @@ namespace mgpu {
 // Diagnostic build only (-DMGPU_STAMPS, tools/lp_stamps.py): s_memtime
 // cycles per section summed over all waves; never compiled into the product.
 __device__ unsigned long long g_lp_stamps[16];
-#define STAMP_DECL unsigned long long st_acc[10] = {0}, st_t = __builtin_amdgcn_s_memtime();
+#define STAMP_KSTART const unsigned long long st_k0 = __builtin_amdgcn_s_memtime();
+#define STAMP_DECL unsigned long long st_acc[10] = {0}, st_t = __builtin_amdgcn_s_memtime(); \
+  const unsigned long long st_pro = st_t - st_k0;
 #define STAMP(i)                                              \
   do {                                                        \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -41,8 +43,13 @@ __device__ unsigned long long g_lp_stamps[16];
   } while (0)
 #define STAMP_FLUSH                                            \
   if ((threadIdx.x & 63) == 0)                                \
-    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_lp_stamps[i_], st_acc[i_]);
+    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_lp_stamps[i_], st_acc[i_]); \
+  if ((threadIdx.x & 63) == 0) {                               \
+    atomicAdd(&g_lp_stamps[10], __builtin_amdgcn_s_memtime() - st_k0); \
+    atomicAdd(&g_lp_stamps[11], st_pro);                       \
+  }
 #else
+#define STAMP_KSTART
 #define STAMP_DECL
 #define STAMP(i) \
   do {           \
@@ -66,7 +73,8 @@ __host__ __device__ constexpr size_t al16(size_t b) { return (b + 15) & ~(size_t
 
 __host__ __device__ inline size_t shared_a_bytes(int n, int m, int nnz) {
   return al16((size_t)(n + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
-         al16((size_t)(m + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8);
+         al16((size_t)(m + 1) * 4) + al16((size_t)nnz * 4) + al16((size_t)nnz * 8) +
+         3 * al16((size_t)n * 8) + 2 * al16((size_t)m * 8);  // c, box (batch 1), row bounds
 }
 // Shared warm start (one basis for every node, e.g. the root optimum)
 // staged once per workgroup: B^-1 (column-major), reduced costs, status,
@@ -187,7 +195,8 @@ __device__ __forceinline__ void grow_art(const Ctx &C, double ab) {
 
 // oracle compute_primals: z_B = -B^{-1} (N z_N); lane k forms w_k from CSR
 // row k in column order, then lane i takes row i of B^{-1} times w.
-__device__ __forceinline__ double compute_primals(const Ctx &C, const double (&binv)[kLpMaxM]) {
+template <int M>
+__device__ __forceinline__ double compute_primals(const Ctx &C, const double (&binv)[M]) {
   wave_sync();
   double w = 0.0;
   const int k = C.lane;
@@ -207,12 +216,15 @@ __device__ __forceinline__ double compute_primals(const Ctx &C, const double (&b
   }
   double s = 0.0;
 #pragma unroll
-  for (int q = 0; q < kLpMaxM; ++q) s += binv[q] * rld(w, q);
+  for (int q = 0; q < M; ++q) s += binv[q] * rld(w, q);
   return -s;
 }
 
-template <int W, bool kSharedWs>
+// M: basis rows held per lane (m <= M; 8, 16, 32 or 64): the B^-1 row
+// registers and every unrolled row loop are sized to the problem's bucket.
+template <int W, bool kSharedWs, int M>
 __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
+  STAMP_KSTART
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = lp.n, m = lp.m, N = n + m, nnz = lp.nnz;
   const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -241,6 +253,27 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     s_cval[t] = lp.cval[t];
     s_ccol[t] = lp.ccol[t];
     s_rval[t] = lp.rval[t];
+  }
+  // objective and row bounds beside the matrix (the objective sum and the
+  // rebuilt reduced costs read them column by column); a single-LP launch
+  // (HipLPEngine's route) also stages its box here, so its loads overlap
+  // the matrix's instead of following them
+  double *s_c = (double *)p;    p += al16((size_t)n * 8);
+  double *s_rlo = (double *)p;  p += al16((size_t)m * 8);
+  double *s_rhi = (double *)p;  p += al16((size_t)m * 8);
+  double *s_blb = (double *)p;  p += al16((size_t)n * 8);
+  double *s_bub = (double *)p;  p += al16((size_t)n * 8);
+  const bool box1 = io.batch == 1 && io.node_list == nullptr;
+  for (int t = threadIdx.x; t < n; t += 64 * W) {
+    s_c[t] = lp.objd[t];
+    if (box1) {
+      s_blb[t] = io.lb[t];
+      s_bub[t] = io.ub[t];
+    }
+  }
+  for (int t = threadIdx.x; t < m; t += 64 * W) {
+    s_rlo[t] = lp.rlo[t];
+    s_rhi[t] = lp.rhi[t];
   }
   double *s_wbinv = nullptr, *s_wd = nullptr;
   int8_t *s_wst = nullptr;
@@ -297,9 +330,9 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     C.rho = (double *)wp; wp += 64 * 8;
     C.aq = (double *)wp;  wp += 64 * 8;
     C.n = n; C.m = m; C.N = N;
-    C.nlb = io.lb + (size_t)b * io.box_stride;
-    C.nub = io.ub + (size_t)b * io.box_stride;
-    C.rlo = lp.rlo; C.rhi = lp.rhi; C.c = lp.objd;
+    C.nlb = box1 ? s_blb : io.lb + (size_t)b * io.box_stride;
+    C.nub = box1 ? s_bub : io.ub + (size_t)b * io.box_stride;
+    C.rlo = s_rlo; C.rhi = s_rhi; C.c = s_c;
     C.ocol = io.obj_col != nullptr ? io.obj_col[b] : -1;
     C.osign = io.obj_col != nullptr ? io.obj_sign[b] : 0.0;
     C.lane = lane;
@@ -324,8 +357,8 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         wr[t] = s_rval[t];
       }
       for (int i = lane; i < m; i += 64) {
-        wlo[i] = lp.rlo[i];
-        whi[i] = lp.rhi[i];
+        wlo[i] = s_rlo[i];
+        whi[i] = s_rhi[i];
       }
       wave_sync();
       const double *rec = io.nr.vals + (size_t)b * io.nr.stride;
@@ -366,7 +399,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
 
     // ---- basis: warm start (parent / root optimum) or slack basis ----
     const bool warm = io.ws.head != nullptr;
-    double binv[kLpMaxM];
+    double binv[M];
     int h = -1;
     if (warm) {
       const int32_t *wh = kSharedWs ? s_whead : io.ws.head + (size_t)bw * io.ws.s_head;
@@ -382,7 +415,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       if (lane < m) C.st[h] = ST_BASIC;
       wave_sync();
   #pragma unroll
-      for (int k = 0; k < kLpMaxM; ++k)
+      for (int k = 0; k < M; ++k)
         binv[k] = (lane < m && k < m) ? wb[(size_t)k * m + lane] : 0.0;  // column-major: coalesced
       if (C.ocol < 0 && io.ws.d != nullptr) {
         for (int j = lane; j < N; j += 64) C.d[j] = C.st[j] == ST_BASIC ? 0.0 : wd[j];
@@ -400,7 +433,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
           rows &= rows - 1;
           if (lane == i) {  // publish row i of B^-1
   #pragma unroll
-            for (int k = 0; k < kLpMaxM; ++k)
+            for (int k = 0; k < M; ++k)
               if (k < m) C.aq[k] = binv[k];
           }
           wave_sync();
@@ -432,7 +465,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         C.d[j] = j < n ? C.cj(j) : 0.0;  // y = 0 for the slack basis
       }
   #pragma unroll
-      for (int k = 0; k < kLpMaxM; ++k) binv[k] = (k == lane && lane < m) ? -1.0 : 0.0;
+      for (int k = 0; k < M; ++k) binv[k] = (k == lane && lane < m) ? -1.0 : 0.0;
     }
     wave_sync();
     double art_bound = kArt0;
@@ -525,7 +558,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       // ---- row r of B^{-1} to LDS (read back as a broadcast) ----
       if (lane == r) {
   #pragma unroll
-        for (int k = 0; k < kLpMaxM; k += 2) {
+        for (int k = 0; k < M; k += 2) {
           double2 v;
           v.x = binv[k];
           v.y = binv[k + 1];
@@ -628,7 +661,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       }
       double alq = 0.0;
   #pragma unroll
-      for (int k = 0; k < kLpMaxM; ++k) alq += binv[k] * rld(aqk, k);
+      for (int k = 0; k < M; ++k) alq += binv[k] * rld(aqk, k);
       const double arq = rld(alq, r);
 
       STAMP(5);
@@ -670,7 +703,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       // ---- rank-1 update of B^{-1} ----
       const double inv = 1.0 / arq;
   #pragma unroll
-      for (int k = 0; k < kLpMaxM; ++k) {
+      for (int k = 0; k < M; ++k) {
         const double nr = C.rho[k] * inv;
         binv[k] = lane == r ? nr : binv[k] - alq * nr;
       }
@@ -699,6 +732,9 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       }
       if (io.x != nullptr)
         for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = C.z[j];
+      if (io.rc != nullptr)
+        for (int j = lane; j < N; j += 64)
+          io.rc[(size_t)b * N + j] = C.st[j] == ST_BASIC ? 0.0 : C.d[j];
       if (io.wo_head != nullptr) {
         if (lane < m) io.wo_head[(size_t)b * m + lane] = h;
         for (int j = lane; j < N; j += 64) {
@@ -708,7 +744,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         if (lane < m) {
           double *dst = io.wo_binv + (size_t)b * m * m + lane;
   #pragma unroll
-          for (int k = 0; k < kLpMaxM; ++k)
+          for (int k = 0; k < M; ++k)
             if (k < m) dst[(size_t)k * m] = binv[k];   // column-major: coalesced
         }
       }
@@ -764,24 +800,34 @@ hipError_t launch_lp_dual(const DevLP &lp, const LpIO &io, int num_cus, hipStrea
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)lp_dual_kernel<kLpWaves, false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)lp_dual_kernel<kLpWaves, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
+    const void *fns[] = {
+        (const void *)lp_dual_kernel<kLpWaves, false, 8>, (const void *)lp_dual_kernel<kLpWaves, true, 8>,
+        (const void *)lp_dual_kernel<kLpWaves, false, 16>, (const void *)lp_dual_kernel<kLpWaves, true, 16>,
+        (const void *)lp_dual_kernel<kLpWaves, false, 32>, (const void *)lp_dual_kernel<kLpWaves, true, 32>,
+        (const void *)lp_dual_kernel<kLpWaves, false, 64>, (const void *)lp_dual_kernel<kLpWaves, true, 64>};
+    for (const void *f : fns) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
   // persistent grid: two workgroups (8 waves) per CU is the residency the
-  // 214-VGPR / 74-KB LDS budget admits; more nodes loop inside the waves
+  // 214-VGPR / 74-KB LDS budget admits at M = 64; more nodes loop inside the waves
   const int want = (io.batch + kLpWaves - 1) / kLpWaves;
   const int blocks = want < 2 * num_cus ? want : 2 * num_cus;
-  if (shared)
-    hipLaunchKernelGGL((lp_dual_kernel<kLpWaves, true>), dim3(blocks), dim3(64 * kLpWaves), lds,
-                       stream, lp, io);
-  else
-    hipLaunchKernelGGL((lp_dual_kernel<kLpWaves, false>), dim3(blocks), dim3(64 * kLpWaves), lds,
-                       stream, lp, io);
+  auto go = [&](auto mtag) {
+    constexpr int Mb = decltype(mtag)::value;
+    if (shared)
+      hipLaunchKernelGGL((lp_dual_kernel<kLpWaves, true, Mb>), dim3(blocks), dim3(64 * kLpWaves),
+                         lds, stream, lp, io);
+    else
+      hipLaunchKernelGGL((lp_dual_kernel<kLpWaves, false, Mb>), dim3(blocks), dim3(64 * kLpWaves),
+                         lds, stream, lp, io);
+  };
+  if (lp.m <= 8) go(std::integral_constant<int, 8>{});
+  else if (lp.m <= 16) go(std::integral_constant<int, 16>{});
+  else if (lp.m <= 32) go(std::integral_constant<int, 32>{});
+  else go(std::integral_constant<int, 64>{});
   return hipGetLastError();
 }
 

@@ -608,6 +608,9 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
       }
       if (io.x != nullptr)
         for (int j = tid; j < n; j += kT) io.x[(size_t)b * n + j] = s.z[j];
+      if (io.rc != nullptr)
+        for (int j = tid; j < N; j += kT)
+          io.rc[(size_t)b * N + j] = s.st[j] == ST_BASIC ? 0.0 : s.d[j];
       if (io.wo_head != nullptr) {
         for (int i = tid; i < m; i += kT) io.wo_head[(size_t)b * m + i] = s.head[i];
         for (int j = tid; j < N; j += kT) {

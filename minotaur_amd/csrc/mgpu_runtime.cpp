@@ -64,6 +64,13 @@ int mgpu_destroy(mgpu_ctx *c) {
                     &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch,
                     &c->fbbt_next, &c->nr_map, &c->nr_ws, &c->nr_vals})
     b->release();
+  for (auto &ch : c->ws_chunks)
+    if (ch.base) (void)hipFree(ch.base);
+  c->ws_chunks.clear();
+  if (c->lp1_pin) (void)hipHostFree(c->lp1_pin);
+  c->lp1_pin = nullptr;
+  if (c->fb1_pin) (void)hipHostFree(c->fb1_pin);
+  c->fb1_pin = nullptr;
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -430,6 +437,42 @@ int mgpu_fbbt(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
   HIPCHK(c, hipSetDevice(c->device));
   const size_t nb = (size_t)batch * c->lp.n * sizeof(double);
   const int cap = mod_cap > 0 ? mod_cap : 0;
+  if (batch == 1) {
+    // one node (HipLinearHandler::presolveNode): the kernel reads the box
+    // from and writes its results to a pinned host block, no copy-engine
+    // transfers (as mgpu_lp_solve1)
+    const size_t o_ub = nb, o_lo = 2 * nb, o_uo = 3 * nb, o_i = 4 * nb, o_mv = o_i + 16,
+                 o_ml = o_mv + al16h((size_t)cap * 4), o_mval = o_ml + al16h((size_t)cap * 4),
+                 bytes = o_mval + (size_t)cap * 8 + 16;
+    if (c->fb1_pin_bytes < bytes) {
+      if (c->fb1_pin) (void)hipHostFree(c->fb1_pin);
+      c->fb1_pin = nullptr;
+      c->fb1_pin_bytes = 0;
+      HIPCHK(c, hipHostMalloc((void **)&c->fb1_pin, bytes, hipHostMallocDefault));
+      c->fb1_pin_bytes = bytes;
+    }
+    char *hp = c->fb1_pin, *dp = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer((void **)&dp, hp, 0));
+    std::memcpy(hp, lb_in, nb);
+    std::memcpy(hp + o_ub, ub_in, nb);
+    int rc = mgpu_fbbt_dev(c, 1, (const double *)dp, (const double *)(dp + o_ub), incumbent,
+                           (double *)(dp + o_lo), (double *)(dp + o_uo), (int32_t *)(dp + o_i),
+                           (int32_t *)(dp + o_i + 4), cap, (int32_t *)(dp + o_mv),
+                           (int32_t *)(dp + o_ml), (double *)(dp + o_mval));
+    if (rc != MGPU_OK) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memcpy(lb_out, hp + o_lo, nb);
+    std::memcpy(ub_out, hp + o_uo, nb);
+    *infeas = *(const int32_t *)(hp + o_i);
+    *nmods = *(const int32_t *)(hp + o_i + 4);
+    const int k = *nmods < cap ? *nmods : cap;
+    if (k > 0 && mod_var && mod_lu && mod_val) {
+      std::memcpy(mod_var, hp + o_mv, (size_t)k * 4);
+      std::memcpy(mod_lu, hp + o_ml, (size_t)k * 4);
+      std::memcpy(mod_val, hp + o_mval, (size_t)k * 8);
+    }
+    return MGPU_OK;
+  }
   HIPCHK(c, c->io_lb_in.ensure(nb));
   HIPCHK(c, c->io_ub_in.ensure(nb));
   HIPCHK(c, c->io_lb_out.ensure(nb));
@@ -679,6 +722,189 @@ int mgpu_lp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   const int rc = launch_lp(c, io, "mgpu_lp_solve");
   if (rc != MGPU_OK) return rc;
   HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+  return MGPU_OK;
+}
+
+// ---- device warm-start slots and the single-LP route ----------------------
+// An LPEngine solves one LP at a time and keeps one warm start per tree node
+// (HipLPEngine: getWarmStartCopy / loadFromWarmStart).  The warm starts live
+// in device slots [head m | st n+m | d n+m | binv m*m] that K3 / K3L read and
+// write in place; the host only moves slot ids.  The box goes in and the
+// results come out through one pinned host block the kernel reads and writes
+// directly (no copy engine round trips).
+namespace {
+constexpr int kWsChunkSlots = 256;
+struct WsLayout {
+  size_t st, d, binv, bytes;
+};
+WsLayout ws_layout(int n, int m) {
+  const size_t N = (size_t)n + m;
+  WsLayout L;
+  L.st = al16h((size_t)m * 4);
+  L.d = L.st + al16h(N);
+  L.binv = L.d + al16h(N * 8);
+  L.bytes = (L.binv + (size_t)m * m * 8 + 255) & ~(size_t)255;
+  return L;
+}
+char *ws_slot(mgpu_ctx *c, int slot, int *n, int *m) {
+  if (slot < 0) return nullptr;
+  const size_t k = (size_t)slot / kWsChunkSlots, i = (size_t)slot % kWsChunkSlots;
+  if (k >= c->ws_chunks.size() || !c->ws_chunks[k].base) return nullptr;
+  const auto &ch = c->ws_chunks[k];
+  *n = ch.n;
+  *m = ch.m;
+  return ch.base + i * ch.bytes;
+}
+}  // namespace
+
+int mgpu_ws_alloc(mgpu_ctx *c, int *slot) {
+  if (!c || !slot) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_ws_alloc: no problem loaded");
+  const int n = c->lp.n, m = c->lp.m;
+  for (size_t k = 0; k < c->ws_chunks.size(); ++k) {
+    auto &ch = c->ws_chunks[k];
+    if (ch.n == n && ch.m == m && !ch.free.empty()) {
+      *slot = (int)k * kWsChunkSlots + ch.free.back();
+      ch.free.pop_back();
+      return MGPU_OK;
+    }
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  mgpu_ctx::WsChunk ch;
+  ch.n = n;
+  ch.m = m;
+  ch.cap = kWsChunkSlots;
+  ch.bytes = ws_layout(n, m).bytes;
+  HIPCHK(c, hipMalloc((void **)&ch.base, ch.bytes * ch.cap));
+  ch.free.reserve(ch.cap);
+  for (int i = ch.cap - 1; i >= 1; --i) ch.free.push_back(i);
+  size_t k = c->ws_chunks.size();
+  for (size_t t = 0; t < c->ws_chunks.size(); ++t)  // reuse a released chunk index
+    if (!c->ws_chunks[t].base) { k = t; break; }
+  if (k == c->ws_chunks.size()) c->ws_chunks.emplace_back();
+  c->ws_chunks[k] = std::move(ch);
+  *slot = (int)k * kWsChunkSlots;
+  return MGPU_OK;
+}
+
+int mgpu_ws_free(mgpu_ctx *c, int slot) {
+  if (!c || slot < 0) return MGPU_ERR_ARG;
+  const size_t k = (size_t)slot / kWsChunkSlots;
+  if (k >= c->ws_chunks.size() || !c->ws_chunks[k].base)
+    return fail(c, MGPU_ERR_ARG, "mgpu_ws_free: bad slot %d", slot);
+  c->ws_chunks[k].free.push_back(slot % kWsChunkSlots);
+  return MGPU_OK;
+}
+
+int mgpu_ws_read(mgpu_ctx *c, int slot, int32_t *head, int8_t *st, double *d, double *binv) {
+  if (!c) return MGPU_ERR_ARG;
+  int n = 0, m = 0;
+  char *p = ws_slot(c, slot, &n, &m);
+  if (!p) return fail(c, MGPU_ERR_ARG, "mgpu_ws_read: bad slot %d", slot);
+  const WsLayout L = ws_layout(n, m);
+  const size_t N = (size_t)n + m;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (head) HIPCHK(c, hipMemcpy(head, p, (size_t)m * 4, hipMemcpyDeviceToHost));
+  if (st) HIPCHK(c, hipMemcpy(st, p + L.st, N, hipMemcpyDeviceToHost));
+  if (d) HIPCHK(c, hipMemcpy(d, p + L.d, N * 8, hipMemcpyDeviceToHost));
+  if (binv) HIPCHK(c, hipMemcpy(binv, p + L.binv, (size_t)m * m * 8, hipMemcpyDeviceToHost));
+  return MGPU_OK;
+}
+
+int mgpu_ws_write(mgpu_ctx *c, int slot, const int32_t *head, const int8_t *st,
+                  const double *d, const double *binv) {
+  if (!c || !head || !st || !binv) return MGPU_ERR_ARG;
+  int n = 0, m = 0;
+  char *p = ws_slot(c, slot, &n, &m);
+  if (!p) return fail(c, MGPU_ERR_ARG, "mgpu_ws_write: bad slot %d", slot);
+  const WsLayout L = ws_layout(n, m);
+  const size_t N = (size_t)n + m;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(p, head, (size_t)m * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(p + L.st, st, N, hipMemcpyHostToDevice));
+  if (d) HIPCHK(c, hipMemcpy(p + L.d, d, N * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(p + L.binv, binv, (size_t)m * m * 8, hipMemcpyHostToDevice));
+  return MGPU_OK;
+}
+
+int mgpu_lp_solve1(mgpu_ctx *c, const double *lb, const double *ub, int ws_in, int ws_d,
+                   int ws_out, int iter_limit, int32_t *status, double *obj, int32_t *iters,
+                   double *x, double *rc) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve1: no problem loaded");
+  if (!lb || !ub || !status || !obj || !iters)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve1: bad argument");
+  const int n = c->lp.n, m = c->lp.m, N = n + m;
+  int sn = 0, sm = 0;
+  char *pin_ws = ws_in >= 0 ? ws_slot(c, ws_in, &sn, &sm) : nullptr;
+  if (ws_in >= 0 && (!pin_ws || sn != n || sm != m))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve1: warm-start slot %d is not for this problem",
+                ws_in);
+  char *pout_ws = ws_out >= 0 ? ws_slot(c, ws_out, &sn, &sm) : nullptr;
+  if (ws_out >= 0 && (!pout_ws || sn != n || sm != m))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve1: output slot %d is not for this problem",
+                ws_out);
+  if (ws_in >= 0 && ws_in == ws_out)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve1: input and output slot are the same");
+  HIPCHK(c, hipSetDevice(c->device));
+  // pinned block: [lb n][ub n][x n][rc N][obj][status, iters]
+  const size_t o_ub = (size_t)n * 8, o_x = 2 * o_ub, o_rc = 3 * o_ub, o_obj = o_rc + (size_t)N * 8,
+               o_st = o_obj + 8, bytes = o_st + 8;
+  if (c->lp1_pin_bytes < bytes) {
+    if (c->lp1_pin) (void)hipHostFree(c->lp1_pin);
+    c->lp1_pin = nullptr;
+    c->lp1_pin_bytes = 0;
+    HIPCHK(c, hipHostMalloc((void **)&c->lp1_pin, bytes, hipHostMallocDefault));
+    c->lp1_pin_bytes = bytes;
+  }
+  // (a staged variant, one H2D of the box and one D2H of the results, measured
+  // 46 vs 44 us per LP through Python: the copy commands cost more than the
+  // kernel's reads over the link)
+  char *hp = c->lp1_pin, *dp = nullptr;
+  HIPCHK(c, hipHostGetDevicePointer((void **)&dp, hp, 0));
+  std::memcpy(hp, lb, (size_t)n * 8);
+  std::memcpy(hp + o_ub, ub, (size_t)n * 8);
+  LpIO io{};
+  io.batch = 1;
+  io.lb = (const double *)dp;
+  io.ub = (const double *)(dp + o_ub);
+  io.box_stride = n;
+  if (pin_ws) {
+    const WsLayout L = ws_layout(n, m);
+    io.ws.head = (const int32_t *)pin_ws;
+    io.ws.st = (const int8_t *)(pin_ws + L.st);
+    io.ws.d = ws_d ? (const double *)(pin_ws + L.d) : nullptr;
+    io.ws.binv = (const double *)(pin_ws + L.binv);
+  }
+  if (pout_ws) {
+    const WsLayout L = ws_layout(n, m);
+    io.wo_head = (int32_t *)pout_ws;
+    io.wo_st = (int8_t *)(pout_ws + L.st);
+    io.wo_d = (double *)(pout_ws + L.d);
+    io.wo_binv = (double *)(pout_ws + L.binv);
+  }
+  io.iter_limit = lp_iter_limit(iter_limit);
+  io.status = (int32_t *)(dp + o_st);
+  io.iters = (int32_t *)(dp + o_st + 4);
+  io.obj = (double *)(dp + o_obj);
+  io.x = (double *)(dp + o_x);
+  io.rc = (double *)(dp + o_rc);
+  if (!use_large_lp(c)) {  // one workgroup, static schedule: nothing to reset
+    if (c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
+      return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve1: problem too large for K3 (m=%d)", m);
+    HIPCHK(c, launch_lp_dual(c->lp, io, c->num_cus, c->stream));
+  } else {
+    const int rc2 = launch_lp(c, io, "mgpu_lp_solve1");
+    if (rc2 != MGPU_OK) return rc2;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *status = *(const int32_t *)(hp + o_st);
+  *iters = *(const int32_t *)(hp + o_st + 4);
+  *obj = *(const double *)(hp + o_obj);
+  if (x) std::memcpy(x, hp + o_x, (size_t)n * 8);
+  if (rc) std::memcpy(rc, hp + o_rc, (size_t)N * 8);
   return MGPU_OK;
 }
 

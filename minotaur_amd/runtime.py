@@ -37,7 +37,8 @@ EXPORTS = [
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
     'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
     'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
-    'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive',
+    'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive', 'mgpu_ws_alloc', 'mgpu_ws_free',
+    'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1',
 ]
 
 
@@ -121,6 +122,11 @@ def load_library():
     lib.mgpu_lp_solve_rows_dev.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
     lib.mgpu_lp_solve_path.argtypes = [_P, _I] + [_P] * 9 + [_I, _I] + [_P] * 7
     lib.mgpu_lp_solve_path_dev.argtypes = [_P, _I] + [_P] * 10 + [_I, _I] + [_P] * 7
+    lib.mgpu_ws_alloc.argtypes = [_P, ctypes.POINTER(_I)]
+    lib.mgpu_ws_free.argtypes = [_P, _I]
+    lib.mgpu_ws_read.argtypes = [_P, _I, _P, _P, _P, _P]
+    lib.mgpu_ws_write.argtypes = [_P, _I, _P, _P, _P, _P]
+    lib.mgpu_lp_solve1.argtypes = [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -404,6 +410,44 @@ class Context:
             _hp(wo.head) if wo else None, _hp(wo.st) if wo else None,
             _hp(wo.d) if wo else None, _hp(wo.binv) if wo else None), 'mgpu_lp_solve')
         return LpOut(st, obj, it, x, wo)
+
+    # -- the single-LP route: device warm-start slots ------------------------
+    def ws_alloc(self) -> int:
+        s = _I(0)
+        self._chk(self.lib.mgpu_ws_alloc(self.h, ctypes.byref(s)), 'mgpu_ws_alloc')
+        return s.value
+
+    def ws_free(self, slot):
+        self._chk(self.lib.mgpu_ws_free(self.h, int(slot)), 'mgpu_ws_free')
+
+    def ws_read(self, slot) -> WarmStart:
+        p = self.problem
+        n, m = p.n, p.m
+        w = WarmStart(np.zeros(m, np.int32), np.zeros(n + m, np.int8), np.zeros(n + m),
+                      np.zeros((m, m)))
+        self._chk(self.lib.mgpu_ws_read(self.h, int(slot), _hp(w.head), _hp(w.st), _hp(w.d),
+                                        _hp(w.binv)), 'mgpu_ws_read')
+        return w
+
+    def ws_write(self, slot, ws):
+        d = None if ws.d is None else _np(ws.d, np.float64)
+        self._chk(self.lib.mgpu_ws_write(self.h, int(slot), _hp(_np(ws.head, np.int32)),
+                                         _hp(_np(ws.st, np.int8)), _hp(d),
+                                         _hp(_np(ws.binv, np.float64))), 'mgpu_ws_write')
+
+    def lp_solve1(self, lb, ub, ws_in=-1, ws_d=True, ws_out=-1, iter_limit=0):
+        """mgpu_lp_solve1: one LP from device slot ws_in (-1 slack), final
+        basis into slot ws_out; returns (status, obj, iters, x, rc)."""
+        p = self.problem
+        st, it = _I(0), _I(0)
+        obj = ctypes.c_double(0.0)
+        x = np.zeros(p.n)
+        rc = np.zeros(p.n + p.m)
+        self._chk(self.lib.mgpu_lp_solve1(
+            self.h, _hp(_np(lb, np.float64)), _hp(_np(ub, np.float64)), int(ws_in),
+            1 if ws_d else 0, int(ws_out), int(iter_limit), ctypes.byref(st), ctypes.byref(obj),
+            ctypes.byref(it), _hp(x), _hp(rc)), 'mgpu_lp_solve1')
+        return st.value, obj.value, it.value, x, rc
 
     def lp_solve_path(self, lb, ub, ws, k_in, path_in, st_in, inherit=PATH_INHERIT,
                       iter_limit=0, want_x=True):

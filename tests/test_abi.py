@@ -12,7 +12,7 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
 def declared_symbols():
     hdr = open(os.path.join(ROOT, 'include', 'mgpu.h')).read()
     hdr = re.sub(r'/\*.*?\*/', '', hdr, flags=re.S)
-    return sorted(set(re.findall(r'\b(mgpu_[a-z_]+)\s*\(', hdr)))
+    return sorted(set(re.findall(r'\b(mgpu_[a-z0-9_]+)\s*\(', hdr)))
 
 
 def test_header_declares_entry_points():
@@ -48,7 +48,7 @@ def _header_arity():
     hdr = open(os.path.join(ROOT, 'include', 'mgpu.h')).read()
     hdr = re.sub(r'/\*.*?\*/', '', hdr, flags=re.S)
     out = {}
-    for name, args in re.findall(r'\b(mgpu_[a-z_]+)\s*\(([^)]*)\)\s*;', hdr):
+    for name, args in re.findall(r'\b(mgpu_[a-z0-9_]+)\s*\(([^)]*)\)\s*;', hdr):
         args = args.strip()
         out[name] = 0 if args in ('', 'void') else len(args.split(','))
     return out

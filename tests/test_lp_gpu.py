@@ -288,3 +288,57 @@ def test_warm_basis_without_reduced_costs(ctx, name, variant):
     st, obj, it, _ = oracle.dual_simplex(q, lb, ub, ows)
     assert np.array_equal(r.status, st) and np.array_equal(r.iters, it)
     assert np.array_equal(r.obj, obj)
+
+
+@pytest.mark.parametrize('variant', [0, 2])
+@pytest.mark.parametrize('name', ['tls4', 'knapsack', 'random3'])
+def test_single_lp_route_device_slots(ctx, name, variant):
+    """mgpu_lp_solve1 (HipLPEngine's route): warm starts in device slots,
+    box in / results out through the pinned block.  A chain of LPs, each
+    from the previous one's slot, equals mgpu_lp_solve with the same warm
+    starts through the host bit for bit (status, pivots, objective, x), the
+    slot holds the same basis, rc is d with basic columns zeroed; ws_d = 0
+    rebuilds d as a d-less host warm start does."""
+    from golden_io import bits_equal
+    from minotaur_amd.runtime import WarmStart
+    p, g = load_lp(name)
+    ctx.load(p)
+    ctx.set_lp_variant(variant)
+    slots = []
+    try:
+        prev, hws = -1, None
+        for b in range(12):
+            lb, ub = g['lb'][b], g['ub'][b]
+            out = ctx.ws_alloc()
+            slots.append(out)
+            st, obj, it, x, rc = ctx.lp_solve1(lb, ub, prev, True, out)
+            r = ctx.lp_solve(lb[None], ub[None], hws, want_x=True, want_ws=True)
+            assert (st, it) == (int(r.status[0]), int(r.iters[0]))
+            assert bits_equal(np.array([obj]), r.obj)
+            if st in (0, 6):
+                assert bits_equal(x, r.x[0])
+                w = ctx.ws_read(out)
+                assert np.array_equal(w.head, r.ws.head[0]) and np.array_equal(w.st, r.ws.st[0])
+                assert bits_equal(w.d, r.ws.d[0]) and bits_equal(w.binv, r.ws.binv[0])
+                assert bits_equal(rc, np.where(w.st == 3, 0.0, w.d))
+                prev = out
+                hws = WarmStart(r.ws.head[0], r.ws.st[0], r.ws.d[0], r.ws.binv[0])
+        # a basis under a new objective: rebuilt reduced costs both ways
+        q = p.__class__(**{**p.__dict__, 'obj': -p.obj})
+        ctx.load(q)
+        st, obj, it, x, rc = ctx.lp_solve1(p.vlb, p.vub, prev, False, -1)
+        r = ctx.lp_solve(p.vlb[None], p.vub[None],
+                         WarmStart(hws.head, hws.st, None, hws.binv), want_x=True)
+        assert (st, it) == (int(r.status[0]), int(r.iters[0]))
+        assert bits_equal(np.array([obj]), r.obj)
+        # a slot written from the host reads back
+        ctx.load(p)
+        s2 = ctx.ws_alloc()
+        slots.append(s2)
+        ctx.ws_write(s2, hws)
+        w = ctx.ws_read(s2)
+        assert np.array_equal(w.head, hws.head) and bits_equal(w.binv, hws.binv)
+    finally:
+        ctx.set_lp_variant(0)
+        for s in slots:
+            ctx.ws_free(s)

@@ -1,7 +1,8 @@
 set -o pipefail
-O=gpurun_out/r03_g19
+O=gpurun_out/r03_g30
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_lp_gpu.py tests/test_integration_gpu.py -v --timeout 120 --timeout-method thread > $O/tests.txt 2>&1
+
+timeout -k 10 300 python -u tools/b1_timing.py > $O/b1t.txt 2>&1
 rc=$?
-tail -3 $O/tests.txt
+tail -c 300 $O/b1t.txt
 exit $rc

@@ -60,9 +60,49 @@ def tree():
         print(f"  {nme:14s} {100.0 * buf[i] / tot:6.2f} %   {buf[i] / max(piv, 1):9.0f} cyc/pivot")
 
 
+def b1():
+    """--b1: K3's sections for single LPs through mgpu_lp_solve1 (HipLPEngine's
+    route; mkp-24-4, each LP from the previous LP's slot): wave-cycles per LP
+    per section, the kernel's total and its prologue (matrix / warm-start
+    staging before the node loop)."""
+    if not os.path.exists(OUT):
+        build()
+    os.environ['MGPU_LIB'] = OUT
+    import numpy as np
+    from minotaur_amd.problem import random_mkp
+    from minotaur_amd.runtime import Context, load_library
+    lib = load_library()
+    p = random_mkp(3, 24, 4)
+    ctx = Context(0)
+    ctx.load(p)
+    rng = np.random.default_rng(1)
+    s0, s1 = ctx.ws_alloc(), ctx.ws_alloc()
+    ctx.lp_solve1(p.vlb, p.vub, -1, True, s0)
+    buf = (ctypes.c_ulonglong * 16)()
+    lib.mgpu_debug_lp_stamps(buf, 1)
+    piv = 0
+    L = 400
+    for k in range(L):
+        lb, ub = p.vlb.copy(), p.vub.copy()
+        j = rng.integers(p.n)
+        if k & 1:
+            ub[j] = p.vlb[j]
+        else:
+            lb[j] = p.vub[j]
+        piv += ctx.lp_solve1(lb, ub, s0, True, s1)[2]
+    lib.mgpu_debug_lp_stamps(buf, 1)
+    print(f"{L} LPs, {piv / L:.2f} pivots each; wave-cycles per LP:")
+    for i, nme in enumerate(NAMES[:10]):
+        print(f"  {nme:14s} {buf[i] / L:9.0f}")
+    print(f"  {'kernel total':14s} {buf[10] / L:9.0f}   (prologue {buf[11] / L:.0f}; 4 waves summed)")
+
+
 def main():
     if '--tree' in sys.argv:
         tree()
+        return
+    if '--b1' in sys.argv:
+        b1()
         return
     pfi = '--pfi' in sys.argv
     if not os.path.exists(OUT):
