@@ -179,6 +179,44 @@ def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
     }
 
 
+def tree_cpu_baseline(p, brancher, seconds):
+    """The tree on the CPU at one core: the reference's
+    own BranchAndBound (bfs NodeHeap, PCBProcessor, NodeIncRelaxer,
+    LinearHandler node FBBT, MaxVio or ReliabilityBrancher, guided dive) with
+    CpuLPEngine -- an LPEngine over the C restatement of the dual simplex
+    (oracle/ref/CpuLPEngine.cpp; Clp is absent) -- from the prebuilt
+    oracle/_ref/libminotaur_hip_integ.so, bounded by the reference's
+    time_limit option.  None when that library is absent."""
+    import ctypes
+    path = os.path.join(ROOT, 'oracle', '_ref', 'libminotaur_hip_integ.so')
+    if not os.path.exists(path):
+        return None
+    from minotaur_amd import runtime
+    runtime.load_library()
+    lib = ctypes.CDLL(path, mode=os.RTLD_LAZY | os.RTLD_GLOBAL)
+    P = ctypes.c_void_p
+    lib.integ_bnb_tree_cpu.argtypes = [ctypes.c_int] * 4 + [P] * 9 + [ctypes.c_double] * 2 + \
+        [P, P]
+
+    def _p(a):
+        return a.ctypes.data_as(P)
+    res = np.zeros(3)
+    cnt = np.zeros(6, dtype=np.int64)
+    lib.integ_bnb_tree_cpu(int(brancher), 1, p.n, p.m, _p(p.rowptr), _p(p.colidx), _p(p.val),
+                           _p(p.rlo), _p(p.rhi), _p(p.vtype), _p(p.vlb), _p(p.vub), _p(p.obj),
+                           float(p.obj_const), float(seconds), _p(res), _p(cnt))
+    done = bool(res[2] < 0.98 * seconds)
+    return {"value": float(cnt[0]) / max(res[2], 1e-9), "unit": "nodes/s", "cores": 1,
+            "kind": "reference",
+            "sample": (f"{p.name}: the reference BranchAndBound (bfs, LinearHandler FBBT, "
+                       f"{'ReliabilityBrancher' if brancher else 'MaxVioBrancher'}) with the "
+                       f"dual-simplex restatement as its LP engine (Clp absent), one core, "
+                       + (f"solved in {res[2]:.3f}s" if done else
+                          f"stopped by time_limit {seconds:g}s")),
+            "nodes": int(cnt[0]), "lp_solves": int(cnt[2]), "seconds": float(res[2]),
+            "solved": done, "ub": float(res[0])}
+
+
 def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0):
     """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
     across ranks after the shared first rounds: one packed all-reduce per
@@ -239,8 +277,9 @@ def tree_search(ctx, dev, rank, world, B, args):
     """Supplementary: complete branch-and-bound trees (every node popped from
     the HBM pool, children pushed, incumbent pruning) with their proven
     optima checked against HiGHS' MILP value."""
-    from minotaur_amd.problem import LinProblem, random_boxes, random_mkp
+    from minotaur_amd.problem import LinProblem, random_mkp
     out = []
+    cpu_trees = {}
     for name, kind, order, warm, opt, br in TREES:
         if kind == "mkp":
             p = random_mkp(1, 60, 8)
@@ -271,10 +310,13 @@ def tree_search(ctx, dev, rank, world, B, args):
                     "nodes_per_s": nodes / el, "relaxations_per_s": (lps + sbl) / el,
                     "batch_per_gpu": B, "optimum": inc, "optimum_highs": opt,
                     "optimum_matches_highs": bool(abs(inc - opt) <= 1e-6 * max(1.0, abs(opt)))})
-        if kind == "mkp" and order == 0 and rank == 0 and world == 1 \
-                and not args.no_cpu_baseline:
-            LB, UB = random_boxes(p, 4096, 7)
-            out[-1]["cpu_baseline"] = cpu_baseline(p, LB, UB, 6.0, "mkp random-branching boxes")
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            key = (p.name, br)
+            if key not in cpu_trees:
+                cpu_trees[key] = tree_cpu_baseline(p, br, args.tree_cpu_seconds)
+                progress(rank, f"cpu tree {p.name} brancher {br}: {cpu_trees[key]}")
+            if cpu_trees[key] is not None:
+                out[-1]["cpu_baseline"] = cpu_trees[key]
     return out
 
 
@@ -714,6 +756,8 @@ def main():
                     help='headline tree warm starts: 2 parent basis as a pivot path (default; '
                          'NodeIncRelaxer semantics), 0 the root basis')
     ap.add_argument('--cpu-seconds', type=float, default=16.0)
+    ap.add_argument('--tree-cpu-seconds', type=float, default=3.0,
+                    help="time_limit of each tree_search entry's one-core reference tree")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-bnb', action='store_true',
                     help='skip the supplementary full tree search (mkp MILP)')
@@ -795,6 +839,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(p, LB, UB, args.cpu_seconds, "tls4-oa")
+            # the same instance's tree on one core by the reference's own
+            # BranchAndBound (nodes/s like value; not the same node boxes)
+            cpu["reference_tree_one_core"] = tree_cpu_baseline(p, 0, 2 * args.tree_cpu_seconds)
         line = {
             "metric": "B&B nodes/sec + relaxations solved/sec at 1/2/4/8 MI355X",
             "value": nodes / elapsed,

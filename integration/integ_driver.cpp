@@ -14,6 +14,7 @@
 #include "TreeManager.h"
 #include "Environment.h"
 #include "Function.h"
+#include "CpuLPEngine.h"
 #include "HipLPEngine.h"
 #include "HipLinearHandler.h"
 #include "HipQuadHandler.h"
@@ -217,27 +218,33 @@ class ProbeBranchAndBound : public BranchAndBound {
 // nodes created, cnt[2] LP solves (strong branching included), cnt[3]
 // strong-branching LPs, cnt[4] LP iterations, cnt[5] strong-branching
 // iterations.
-int integ_bnb_tree(int device, int hip_fbbt, int brancher, int guided, int n, int m,
-                   const int *rowptr, const int *colidx, const double *val, const double *rlo,
-                   const double *rhi, const int *vtype, const double *vlb, const double *vub,
-                   const double *obj, double objc, double *res, long long *cnt) {
+static int bnb_tree(int device, int hip_fbbt, int brancher, int guided, int n, int m,
+                    const int *rowptr, const int *colidx, const double *val, const double *rlo,
+                    const double *rhi, const int *vtype, const double *vlb, const double *vub,
+                    const double *obj, double objc, double *res, long long *cnt,
+                    double time_limit) {
   EnvPtr env = (EnvPtr) new Environment();
   int err = 0;
   env->startTimer(err);
   env->getOptions()->findString("tree_search")->setValue("bfs");
   env->getOptions()->findInt("pres_freq")->setValue(1);
   env->getOptions()->findBool("guided_dive")->setValue(guided != 0);
+  // (BabOptions reads the option in the BranchAndBound constructor)
+  if (time_limit > 0) env->getOptions()->findDouble("time_limit")->setValue(time_limit);
   ProblemPtr p = build(env, n, m, rowptr, colidx, val, rlo, rhi, vtype, vlb, vub, obj, objc, 0);
   ProbeBranchAndBound *bab = new ProbeBranchAndBound(env, p);
   HandlerVector handlers;
   IntVarHandlerPtr v_hand = (IntVarHandlerPtr) new IntVarHandler(env, p);
-  LinearHandlerPtr l_hand = hip_fbbt ? (LinearHandlerPtr) new HipLinearHandler(env, p, device)
-                                     : (LinearHandlerPtr) new LinearHandler(env, p);
+  const bool cpu = device < 0;  // the tree-level CPU baseline: CpuLPEngine + LinearHandler
+  LinearHandlerPtr l_hand = hip_fbbt && !cpu
+                                ? (LinearHandlerPtr) new HipLinearHandler(env, p, device)
+                                : (LinearHandlerPtr) new LinearHandler(env, p);
   handlers.push_back(v_hand);
   handlers.push_back(l_hand);
   v_hand->setModFlags(false, true);
   l_hand->setModFlags(false, true);
-  HipLPEngine *e = new HipLPEngine(env, device);
+  LPEnginePtr e = cpu ? (LPEnginePtr) new CpuLPEngine(env)
+                      : (LPEnginePtr) new HipLPEngine(env, device);
   PCBProcessorPtr nproc = (PCBProcessorPtr) new PCBProcessor(env, e, handlers);
   BrancherPtr br;
   if (brancher == 1) {
@@ -279,6 +286,29 @@ int integ_bnb_tree(int device, int hip_fbbt, int brancher, int guided, int n, in
   delete bab;
   delete env;
   return 0;
+}
+
+int integ_bnb_tree(int device, int hip_fbbt, int brancher, int guided, int n, int m,
+                   const int *rowptr, const int *colidx, const double *val, const double *rlo,
+                   const double *rhi, const int *vtype, const double *vlb, const double *vub,
+                   const double *obj, double objc, double *res, long long *cnt) {
+  if (device < 0) return -1;
+  return bnb_tree(device, hip_fbbt, brancher, guided, n, m, rowptr, colidx, val, rlo, rhi,
+                  vtype, vlb, vub, obj, objc, res, cnt, 0.0);
+}
+
+// The same tree search on the CPU at one core -- CpuLPEngine (the C
+// restatement of the dual simplex) + the reference's LinearHandler -- for
+// bench.py's tree-level cpu_baseline; time_limit > 0 bounds it (the
+// reference's "time_limit" option, BranchAndBound.cpp:582), res / cnt as
+// integ_bnb_tree (res[2] = seconds actually spent).
+int integ_bnb_tree_cpu(int brancher, int guided, int n, int m, const int *rowptr,
+                       const int *colidx, const double *val, const double *rlo,
+                       const double *rhi, const int *vtype, const double *vlb, const double *vub,
+                       const double *obj, double objc, double time_limit, double *res,
+                       long long *cnt) {
+  return bnb_tree(-1, 0, brancher, guided, n, m, rowptr, colidx, val, rlo, rhi, vtype, vlb, vub,
+                  obj, objc, res, cnt, time_limit);
 }
 
 // ---- quadratic handler: reference QuadHandler vs HipQuadHandler ----------

@@ -421,8 +421,10 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
     }
     for (int j = 0; j < N; ++j) W.st[j] = path->st[j];
     pfi_compute_duals(&W);
-  } else if (have_ws && have_binv && ws_d) {
-    /* reduced costs depend only on the basis: reuse the parent's */
+  } else if (have_ws && have_binv == 1 && ws_d) {
+    /* reduced costs depend only on the basis: reuse the parent's
+     * (have_binv == 2: the inverse is given but ws_d, an output only, is for
+     * another objective -- rebuilt below, as mgpu_lp_solve1 with ws_d = 0) */
     for (int j = 0; j < N; ++j) W.d[j] = W.st[j] == ST_BASIC ? 0.0 : ws_d[j];
   } else {
     compute_duals(&W);

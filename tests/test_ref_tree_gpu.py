@@ -120,3 +120,21 @@ def test_gpu_fbbt_handler_same_reference_tree(integ):
     b = reference_tree(integ, p, hip_fbbt=1)
     assert (a["processed"], a["created"], a["lps"], a["ub"]) == \
         (b["processed"], b["created"], b["lps"], b["ub"])
+
+
+@pytest.mark.parametrize('brancher', [0, 1])
+@pytest.mark.parametrize('name', ['nvs08_oa', 'knapsack_oa', 'mkp-18-3', 'mkp-24-4'])
+def test_cpu_baseline_tree_is_the_gpu_engine_tree(integ, name, brancher):
+    """bench.py's tree-level CPU baseline runs the same tree as the reference
+    with HipLPEngine: CpuLPEngine (the C restatement) and K3 agree LP for LP,
+    so BranchAndBound processes and creates the same nodes, solves the same
+    LPs (strong branching included) and returns the same incumbent."""
+    from test_ref_tree_cpu import cpu_tree
+    integ.integ_bnb_tree_cpu.argtypes = [ctypes.c_int] * 4 + [P] * 9 + \
+        [ctypes.c_double] * 2 + [P, P]
+    p = _cases()[name]
+    a = reference_tree(integ, p, brancher=brancher)
+    b = cpu_tree(integ, p, brancher)
+    assert (a["processed"], a["created"], a["lps"], a["sb_lps"]) == \
+        (b["processed"], b["created"], b["lps"], b["sb_lps"]), (a, b)
+    assert a["ub"] == b["ub"]
