@@ -624,7 +624,7 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
     def step(acc):
         st = ctx.bnb_round(B, state["inc"])
         ev[0].record()
-        inc, most, _ = comm.round_reduce(st.incumbent, st.open)
+        inc, most, _, _ = comm.round_reduce(st.incumbent, st.open)
         ev[1].record()
         ev[1].synchronize()
         state["inc"] = min(state["inc"], inc)

@@ -451,11 +451,37 @@ int mgpu_bnb_shard(mgpu_ctx *ctx, int rank, int world, int *kept);
  *                    best-first order the first k live pool slots) and
  *                    returns their boxes, bounds and depths; *got = count.
  *   mgpu_bnb_import: adds k open nodes (with parent warm starts they start
- *                    from the root basis). */
+ *                    from the root basis; best-first: the lowest free slots
+ *                    first, as mgpu_bnb_import_dev). */
 int mgpu_bnb_export(mgpu_ctx *ctx, int k, double *lb, double *ub, double *nlb, int32_t *depth,
                     int *got);
 int mgpu_bnb_import(mgpu_ctx *ctx, int k, const double *lb, const double *ub, const double *nlb,
                     const int32_t *depth);
+
+/* Bound-aware load balancing on device rows (MpiBranchAndBound::LoadBalance_,
+ * src/base/MpiBranchAndBound.cpp:78-195).  LoadBalance_ pops each rank's
+ * next 50 P candidates (TreeManager::getCandidate, :93-105), all-gathers
+ * their lower bounds (:107), sorts them (:111-135) and deals the i-th best to
+ * rank i mod P (:142-188), one MPI_Send of a serialised node per move.
+ *   mgpu_bnb_pick:       this rank's next S candidates in its search order
+ *                        (depth-first: the stack top, topmost first;
+ *                        best-first: pruned by the incumbent, then ascending
+ *                        (bound, slot)); their bounds into lbs[0, *got) (host).
+ *                        The nodes stay in the pool.
+ *   mgpu_bnb_export_dev: removes the picked nodes idx[0, k) (indices into the
+ *                        last pick, host array) and packs them, in that
+ *                        order, into device rows buf[k][2n + 2] =
+ *                        [lb | ub | bound | depth] (Serializer.cpp:26-112's
+ *                        content); the depth-first stack closes its gaps.
+ *   mgpu_bnb_import_dev: adds k nodes from device rows buf (best-first: the
+ *                        lowest free pool slots, then past the high-water
+ *                        mark; depth-first: on top), in row order; they
+ *                        start from the root basis.
+ *   mgpu_bnb_count:      open nodes and pool slots left for imports. */
+int mgpu_bnb_pick(mgpu_ctx *ctx, int S, double *lbs, int *got);
+int mgpu_bnb_export_dev(mgpu_ctx *ctx, int k, const int32_t *idx, double *d_rows);
+int mgpu_bnb_import_dev(mgpu_ctx *ctx, int k, const double *d_rows);
+int mgpu_bnb_count(mgpu_ctx *ctx, int *open, int *spare);
 
 /* ---- QP relaxation with an MFMA KKT block (K5) ---------------
  * Replaces BqpdEngine::solve (src/interfaces/BqpdEngine.cpp:449-534) on the

@@ -46,10 +46,12 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
     without it the two callables allreduce_min / allreduce_max(float) ->
     float are used.  With ``comm`` and lb_every > 0, every lb_every rounds
     (and whenever some rank ran out of nodes while others hold more than a
-    batch) the open nodes are rebalanced across ranks (dist.rebalance:
-    MpiBranchAndBound::LoadBalance_).  Returns (incumbent, x or None, stats,
-    rounds, mine) where mine = {nodes, lps, pivots, pruned, sb_lps, sb_pivots,
-    moved} evaluated
+    batch) the open nodes are rebalanced across ranks by their bounds
+    (dist.rebalance: MpiBranchAndBound::LoadBalance_).  A rank whose round
+    fails makes every rank raise in the same round (the error rides the
+    round's all-reduce).  Returns (incumbent, x or None, stats, rounds, mine)
+    where mine = {nodes, lps, pivots, pruned, sb_lps, sb_pivots, moved,
+    lb_log: per rebalance the bounds picked and received} evaluated
     by this rank, the shared first rounds counted on rank 0 only (so sums
     over ranks are exact)."""
     from . import dist as mdist
@@ -64,25 +66,36 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
     rounds = 0
     moved = 0
     shared = (0, 0, 0, 0, 0, 0)
-    n = ctx.problem.n
+    lb_log = []
     while rounds < max_rounds:
-        st = ctx.bnb_round(batch, inc)
+        err, exc = 0, None
+        try:
+            st = ctx.bnb_round(batch, inc)
+        except Exception as e:              # reported to every rank below
+            if comm is None or world == 1:
+                raise
+            err, exc = 1, e
         rounds += 1
-        open_now = st.open
-        if not sharded and (open_now >= shard_at or open_now == 0):
+        open_now = st.open if not err else 0
+        if not err and not sharded and (open_now >= shard_at or open_now == 0):
             shared = (st.nodes, st.lps, st.pivots, st.pruned, st.sb_lps,
                       st.sb_pivots)                           # identical on every rank
             open_now = ctx.bnb_shard(rank, world)
             sharded = True
         if comm is not None:
-            inc, most, least = comm.round_reduce(st.incumbent, open_now)
+            inc_r = st.incumbent if st is not None and not err else math.inf
+            inc, most, least, failed = comm.round_reduce(inc_r, open_now, err)
+            if failed:
+                raise exc if exc is not None else RuntimeError(
+                    'solve_distributed: a peer rank failed in round %d' % rounds)
             if most == 0.0:
                 break
             # the trigger uses only all-reduced values: every rank agrees
             if sharded and world > 1 and lb_every > 0 and (
                     rounds % lb_every == 0 or (least == 0 and most > batch)):
-                open_now, k = mdist.rebalance(ctx, comm, open_now, n)
+                open_now, k, picked, got = mdist.rebalance(ctx, comm, batch)
                 moved += k
+                lb_log.append((picked.tolist(), got.tolist()))
         else:
             inc = allreduce_min(st.incumbent)
             if allreduce_max(float(open_now)) == 0.0:
@@ -94,4 +107,5 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
                                         (st.nodes, st.lps, st.pivots, st.pruned, st.sb_lps,
                                          st.sb_pivots), sub)}
     mine['moved'] = moved
+    mine['lb_log'] = lb_log
     return inc, (x if obj == inc else None), st, rounds, mine

@@ -80,6 +80,7 @@ struct BnbState {
   long long next_id = 0;
   bool guided = true;          // IntVarHandler guided_dive (Environment.cpp:160-163)
   DevBuf cslots;               // [2 nb] child slots
+  std::vector<int> pick;       // mgpu_bnb_pick: pool slots of the picked nodes, in pick order
   void release() {
     for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
                       &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
@@ -953,14 +954,282 @@ int mgpu_strong_branch(mgpu_ctx *c, const double *lb, const double *ub, int ncan
 }
 
 // Node migration for load balancing across ranks (MpiBranchAndBound::
-// LoadBalance_, MpiBranchAndBound.cpp:78-195: node boxes, bounds and depths
-// move between processes).  Host buffers; boxes [k][n].
+// LoadBalance_, MpiBranchAndBound.cpp:78-195).  LoadBalance_ pops each rank's
+// next 50 P candidates (:93-105), all-gathers their lower bounds (:107),
+// sorts them globally and deals the i-th best to rank i mod P (:111-188).
+// mgpu_bnb_pick is the pop (the nodes stay in the pool, only their bounds
+// leave), mgpu_bnb_export_dev packs the chosen ones into device rows and
+// removes them, mgpu_bnb_import_dev places received rows.  Rows are
+// [lb n | ub n | bound | depth] f64 (bnb_migrate.hip).
+}  // extern "C"
+
+namespace {
+
+// every per-slot array of the pool (a node's box, bound, depth and the state
+// that travels with it inside one pool)
+std::vector<std::pair<DevBuf *, size_t>> slot_rows(BnbState &s, int m) {
+  const size_t n = (size_t)s.n, N = n + (size_t)m;
+  std::vector<std::pair<DevBuf *, size_t>> r = {
+      {&s.plb, n * 8}, {&s.pub, n * 8}, {&s.pnlb, 8}, {&s.pdepth, 4}};
+  if (s.warm == 1) {
+    r.push_back({&s.pws_head, (size_t)m * 4});
+    r.push_back({&s.pws_st, N});
+    r.push_back({&s.pws_d, N * 8});
+    r.push_back({&s.pws_binv, (size_t)m * m * 8});
+  }
+  if (s.warm == 2) {
+    r.push_back({&s.ppk, 4});
+    r.push_back({&s.ppath, (size_t)kPathMax * 4});
+    r.push_back({&s.ppst, N});
+  }
+  if (s.rel) {
+    r.push_back({&s.ppvar, 4});
+    r.push_back({&s.ppval, 8});
+  }
+  return r;
+}
+
+inline double key_to_double(uint64_t k) {
+  const uint64_t b = (k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  double v;
+  std::memcpy(&v, &b, 8);
+  return v;
+}
+
+// removes the nodes at pool slots `slots` after packing them into `buf`
+// (device rows); depth-first: the slots must lie in the stack's top `region`
+// slots, the others of that region keep their order and close the gaps
+int take_nodes(mgpu_ctx *c, BnbState &s, const std::vector<int32_t> &slots, int region,
+               double *buf) {
+  const int k = (int)slots.size();
+  if (k == 0) return MGPU_OK;
+  DevBuf dsl;
+  HIPCHK(c, dsl.ensure((size_t)k * 4));
+  HIPCHK(c, hipMemcpyAsync(dsl.p, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, launch_bnb_pack(dsl.as<int32_t>(), k, s.n, s.plb.as<double>(), s.pub.as<double>(),
+                            s.pnlb.as<double>(), s.pdepth.as<int32_t>(),
+                            s.order == 1 ? s.plive.as<uint8_t>() : nullptr, buf, c->stream));
+  if (s.order == 0) {
+    const int base = s.count - region;
+    std::vector<uint8_t> gone((size_t)region, 0);
+    for (int32_t v : slots) gone[(size_t)(v - base)] = 1;
+    // the kept nodes of the region close up in order; only rows that change
+    // place move
+    std::vector<int32_t> f2, t2;
+    int w = 0;
+    for (int t = 0; t < region; ++t) {
+      if (gone[(size_t)t]) continue;
+      if (t != w) {
+        f2.push_back(base + t);
+        t2.push_back(base + w);
+      }
+      ++w;
+    }
+    if (!f2.empty()) {
+      const int km = (int)f2.size();
+      DevBuf ft, tmp;
+      HIPCHK(c, ft.ensure((size_t)km * 8));
+      HIPCHK(c, hipMemcpyAsync(ft.p, f2.data(), (size_t)km * 4, hipMemcpyHostToDevice,
+                               c->stream));
+      HIPCHK(c, hipMemcpyAsync(ft.as<int32_t>() + km, t2.data(), (size_t)km * 4,
+                               hipMemcpyHostToDevice, c->stream));
+      auto rows = slot_rows(s, c->lp.m);
+      size_t most = 0;
+      for (auto &r : rows) most = r.second > most ? r.second : most;
+      HIPCHK(c, tmp.ensure((size_t)km * most));
+      for (auto &r : rows)
+        HIPCHK(c, launch_bnb_move_rows(r.first->as<unsigned char>(), tmp.as<unsigned char>(),
+                                       r.second, ft.as<int32_t>(), ft.as<int32_t>() + km, km,
+                                       c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s.count -= k;
+  s.tot.open = s.count;
+  return MGPU_OK;
+}
+
+// places k device rows: on top of the stack, or (best-first) into the
+// lowest free pool slots first and past the high-water mark for the rest
+int place_nodes(mgpu_ctx *c, BnbState &s, int k, const double *buf) {
+  if (k == 0) return MGPU_OK;
+  const int m = c->lp.m, N = s.n + m;
+  std::vector<int32_t> slots;
+  slots.reserve((size_t)k);
+  if (s.order == 0) {
+    if (s.count + k > s.cap) return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_import: node pool full");
+    for (int t = 0; t < k; ++t) slots.push_back(s.count + t);
+  } else {
+    std::vector<uint8_t> live((size_t)(s.hw > 0 ? s.hw : 1), 0);
+    if (s.hw > 0) {
+      HIPCHK(c, hipMemcpyAsync(live.data(), s.plive.p, (size_t)s.hw, hipMemcpyDeviceToHost,
+                               c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    for (int i = 0; i < s.hw && (int)slots.size() < k; ++i)
+      if (!live[(size_t)i]) slots.push_back(i);
+    const int extra = k - (int)slots.size();
+    if (s.hw + extra > s.cap) return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_import: node pool full");
+    for (int t = 0; t < extra; ++t) slots.push_back(s.hw + t);
+    s.hw += extra;
+  }
+  DevBuf dsl;
+  HIPCHK(c, dsl.ensure((size_t)k * 4));
+  HIPCHK(c, hipMemcpyAsync(dsl.p, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice,
+                           c->stream));
+  MigrateIO io{};
+  io.k = k;
+  io.n = s.n;
+  io.m = m;
+  io.N = N;
+  io.slots = dsl.as<int32_t>();
+  io.buf = buf;
+  io.plb = s.plb.as<double>();
+  io.pub = s.pub.as<double>();
+  io.pnlb = s.pnlb.as<double>();
+  io.pdepth = s.pdepth.as<int32_t>();
+  io.plive = s.order == 1 ? s.plive.as<uint8_t>() : nullptr;
+  io.ppvar = s.rel ? s.ppvar.as<int32_t>() : nullptr;
+  io.ppk = s.warm == 2 ? s.ppk.as<int32_t>() : nullptr;
+  if (s.warm == 1) {  // a migrated node starts from the root basis
+    io.ws_head = s.pws_head.as<int32_t>();
+    io.ws_st = s.pws_st.as<int8_t>();
+    io.ws_d = s.pws_d.as<double>();
+    io.ws_binv = s.pws_binv.as<double>();
+    io.r_head = s.ws_head.as<int32_t>();
+    io.r_st = s.ws_st.as<int8_t>();
+    io.r_d = s.ws_d.as<double>();
+    io.r_binv = s.ws_binv.as<double>();
+  }
+  HIPCHK(c, launch_bnb_unpack(io, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s.count += k;
+  s.tot.open = s.count;
+  return MGPU_OK;
+}
+
+int check_migrate(mgpu_ctx *c, const char *what) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "%s: mgpu_bnb_init first", what);
+  if (c->bnb->order == 2)
+    return fail(c, MGPU_ERR_ARG, "%s: not in the reference-heap order (order 2)", what);
+  return MGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgpu_bnb_pick(mgpu_ctx *c, int S, double *lbs, int *got) {
+  int rc = check_migrate(c, "mgpu_bnb_pick");
+  if (rc != MGPU_OK) return rc;
+  if (S < 0 || (S > 0 && !lbs) || !got) return fail(c, MGPU_ERR_ARG, "mgpu_bnb_pick: bad argument");
+  BnbState &s = *c->bnb;
+  HIPCHK(c, hipSetDevice(c->device));
+  s.pick.clear();
+  *got = 0;
+  if (s.order == 0) {
+    // the stack's next candidates: its top, topmost first
+    const int k = S < s.count ? S : s.count;
+    if (k > 0) {
+      std::vector<double> v((size_t)k);
+      HIPCHK(c, hipMemcpyAsync(v.data(), s.pnlb.as<double>() + (s.count - k), (size_t)k * 8,
+                               hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (int t = 0; t < k; ++t) {
+        lbs[t] = v[(size_t)(k - 1 - t)];
+        s.pick.push_back(s.count - 1 - t);
+      }
+    }
+    *got = k;
+    return MGPU_OK;
+  }
+  // best-first: TreeManager::getCandidate's pruning by the incumbent, then
+  // the live nodes in (bound, slot) order, as a round selects them
+  if (s.hw <= 0) {
+    s.count = 0;
+    s.tot.open = 0;
+    return MGPU_OK;
+  }
+  HIPCHK(c, hipMemsetAsync(s.counts.p, 0, 8, c->stream));
+  HIPCHK(c, launch_bnb_keys(s.pnlb.as<double>(), s.plive.as<uint8_t>(), s.hw, s.inc, s.inc,
+                            s.keys.as<uint64_t>(), s.vals.as<uint32_t>(), s.counts.as<int32_t>(),
+                            c->stream));
+  size_t tb = s.sort_bytes;
+  HIPCHK(c, bnb_sort_pairs(s.sort_tmp.p, tb, s.keys.as<uint64_t>(), s.keys2.as<uint64_t>(),
+                           s.vals.as<uint32_t>(), s.vals2.as<uint32_t>(), s.hw, c->stream));
+  int32_t cnt[2] = {0, 0};
+  HIPCHK(c, hipMemcpyAsync(cnt, s.counts.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s.count = cnt[0];
+  s.tot.pruned += cnt[1];
+  s.tot.open = s.count;
+  const int k = S < s.count ? S : s.count;
+  if (k > 0) {
+    std::vector<uint64_t> keys((size_t)k);
+    std::vector<uint32_t> sl((size_t)k);
+    HIPCHK(c, hipMemcpyAsync(keys.data(), s.keys2.p, (size_t)k * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(sl.data(), s.vals2.p, (size_t)k * 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int t = 0; t < k; ++t) {
+      lbs[t] = key_to_double(keys[(size_t)t]);
+      s.pick.push_back((int)sl[(size_t)t]);
+    }
+  }
+  *got = k;
+  return MGPU_OK;
+}
+
+int mgpu_bnb_export_dev(mgpu_ctx *c, int k, const int32_t *idx, double *buf) {
+  int rc = check_migrate(c, "mgpu_bnb_export_dev");
+  if (rc != MGPU_OK) return rc;
+  BnbState &s = *c->bnb;
+  if (k < 0 || (k > 0 && (!idx || !buf)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_export_dev: bad argument");
+  const int np = (int)s.pick.size();
+  std::vector<uint8_t> seen((size_t)(np > 0 ? np : 1), 0);
+  std::vector<int32_t> slots;
+  for (int t = 0; t < k; ++t) {
+    if (idx[t] < 0 || idx[t] >= np || seen[(size_t)idx[t]])
+      return fail(c, MGPU_ERR_ARG, "mgpu_bnb_export_dev: index %d is not a distinct entry of "
+                  "the last mgpu_bnb_pick (%d nodes)", idx[t], np);
+    seen[(size_t)idx[t]] = 1;
+    slots.push_back(s.pick[(size_t)idx[t]]);
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  rc = take_nodes(c, s, slots, np, buf);
+  s.pick.clear();
+  return rc;
+}
+
+int mgpu_bnb_import_dev(mgpu_ctx *c, int k, const double *buf) {
+  int rc = check_migrate(c, "mgpu_bnb_import_dev");
+  if (rc != MGPU_OK) return rc;
+  if (k < 0 || (k > 0 && !buf)) return fail(c, MGPU_ERR_ARG, "mgpu_bnb_import_dev: bad argument");
+  BnbState &s = *c->bnb;
+  HIPCHK(c, hipSetDevice(c->device));
+  s.pick.clear();
+  return place_nodes(c, s, k, buf);
+}
+
+int mgpu_bnb_count(mgpu_ctx *c, int *open, int *spare) {
+  int rc = check_migrate(c, "mgpu_bnb_count");
+  if (rc != MGPU_OK) return rc;
+  if (open) *open = c->bnb->count;
+  if (spare) *spare = c->bnb->cap - c->bnb->count;
+  return MGPU_OK;
+}
+
+// Host-buffer forms (boxes [k][n]): the stack's top k / the first k live
+// slots leave; imports go through the same placement as the device rows.
 int mgpu_bnb_export(mgpu_ctx *c, int k, double *lb, double *ub, double *nlb, int32_t *depth,
                     int *got) {
-  if (!c) return MGPU_ERR_ARG;
-  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_export: mgpu_bnb_init first");
-  if (c->bnb->order == 2)
-    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_export: not in the reference-heap order (order 2)");
+  int rc = check_migrate(c, "mgpu_bnb_export");
+  if (rc != MGPU_OK) return rc;
   if (k < 0 || (k > 0 && (!lb || !ub || !nlb || !depth)) || !got)
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_export: bad argument");
   BnbState &s = *c->bnb;
@@ -968,113 +1237,62 @@ int mgpu_bnb_export(mgpu_ctx *c, int k, double *lb, double *ub, double *nlb, int
   const int n = s.n;
   if (k > s.count) k = s.count;
   *got = 0;
+  s.pick.clear();
   if (k == 0) return MGPU_OK;
+  std::vector<int32_t> slots;
   if (s.order == 0) {
-    // the top k of the stack (contiguous): no compaction needed
-    const size_t o = (size_t)(s.count - k);
-    HIPCHK(c, hipMemcpyAsync(lb, s.plb.as<double>() + o * n, (size_t)k * n * 8,
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ub, s.pub.as<double>() + o * n, (size_t)k * n * 8,
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(nlb, s.pnlb.as<double>() + o, (size_t)k * 8, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(depth, s.pdepth.as<int32_t>() + o, (size_t)k * 4,
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int t = 0; t < k; ++t) slots.push_back(s.count - k + t);
   } else {
-    // best-first pool: the first k live slots
     std::vector<uint8_t> live((size_t)s.hw);
     HIPCHK(c, hipMemcpyAsync(live.data(), s.plive.p, (size_t)s.hw, hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    std::vector<uint32_t> slots;
     for (int i = 0; i < s.hw && (int)slots.size() < k; ++i)
-      if (live[i]) slots.push_back((uint32_t)i);
+      if (live[(size_t)i]) slots.push_back(i);
     k = (int)slots.size();
-    DevBuf dsl, tlb, tub, tdep;
-    HIPCHK(c, dsl.ensure((size_t)k * 4));
-    HIPCHK(c, tlb.ensure((size_t)k * n * 8));
-    HIPCHK(c, tub.ensure((size_t)k * n * 8));
-    HIPCHK(c, tdep.ensure((size_t)k * 4));
-    HIPCHK(c, hipMemcpyAsync(dsl.p, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice,
-                             c->stream));
-    BnbSelIO g{};
-    g.nb = k;
-    g.n = n;
-    g.slots = dsl.as<uint32_t>();
-    g.plb = s.plb.as<double>();
-    g.pub = s.pub.as<double>();
-    g.pdepth = s.pdepth.as<int32_t>();
-    g.plive = s.plive.as<uint8_t>();
-    g.wlb = tlb.as<double>();
-    g.wub = tub.as<double>();
-    g.depth_in = tdep.as<int32_t>();
-    HIPCHK(c, launch_bnb_gather(g, c->stream));
-    HIPCHK(c, hipMemcpyAsync(lb, tlb.p, (size_t)k * n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ub, tub.p, (size_t)k * n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(depth, tdep.p, (size_t)k * 4, hipMemcpyDeviceToHost, c->stream));
-    std::vector<double> all((size_t)s.hw);
-    HIPCHK(c, hipMemcpyAsync(all.data(), s.pnlb.p, (size_t)s.hw * 8, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (int t = 0; t < k; ++t) nlb[t] = all[slots[t]];
   }
-  s.count -= k;
-  s.tot.open = s.count;
+  const size_t W = 2 * (size_t)n + 2;
+  DevBuf rows;
+  HIPCHK(c, rows.ensure((size_t)k * W * 8));
+  rc = take_nodes(c, s, slots, k, rows.as<double>());
+  if (rc != MGPU_OK) return rc;
+  std::vector<double> h((size_t)k * W);
+  HIPCHK(c, hipMemcpy(h.data(), rows.p, h.size() * 8, hipMemcpyDeviceToHost));
+  for (int t = 0; t < k; ++t) {
+    const double *r = h.data() + (size_t)t * W;
+    std::memcpy(lb + (size_t)t * n, r, (size_t)n * 8);
+    std::memcpy(ub + (size_t)t * n, r + n, (size_t)n * 8);
+    nlb[t] = r[2 * n];
+    depth[t] = (int32_t)r[2 * n + 1];
+  }
   *got = k;
   return MGPU_OK;
 }
 
 int mgpu_bnb_import(mgpu_ctx *c, int k, const double *lb, const double *ub, const double *nlb,
                     const int32_t *depth) {
-  if (!c) return MGPU_ERR_ARG;
-  if (!c->bnb) return fail(c, MGPU_ERR_STATE, "mgpu_bnb_import: mgpu_bnb_init first");
-  if (c->bnb->order == 2)
-    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_import: not in the reference-heap order (order 2)");
+  int rc = check_migrate(c, "mgpu_bnb_import");
+  if (rc != MGPU_OK) return rc;
   if (k < 0 || (k > 0 && (!lb || !ub || !nlb || !depth)))
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_import: bad argument");
   if (k == 0) return MGPU_OK;
   BnbState &s = *c->bnb;
   HIPCHK(c, hipSetDevice(c->device));
-  const int n = s.n, m = c->lp.m, N = n + m;
-  // stack: on top; best-first: appended past the high-water mark
-  const int at = s.order == 0 ? s.count : s.hw;
-  if (at + k > s.cap) return fail(c, MGPU_ERR_NOMEM, "mgpu_bnb_import: node pool full");
-  HIPCHK(c, hipMemcpyAsync(s.plb.as<double>() + (size_t)at * n, lb, (size_t)k * n * 8,
-                           hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(s.pub.as<double>() + (size_t)at * n, ub, (size_t)k * n * 8,
-                           hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(s.pnlb.as<double>() + at, nlb, (size_t)k * 8, hipMemcpyHostToDevice,
-                           c->stream));
-  HIPCHK(c, hipMemcpyAsync(s.pdepth.as<int32_t>() + at, depth, (size_t)k * 4,
-                           hipMemcpyHostToDevice, c->stream));
-  if (s.order == 1) {
-    HIPCHK(c, hipMemsetAsync(s.plive.as<uint8_t>() + at, 1, (size_t)k, c->stream));
-    s.hw += k;
+  s.pick.clear();
+  const int n = s.n;
+  const size_t W = 2 * (size_t)n + 2;
+  std::vector<double> h((size_t)k * W);
+  for (int t = 0; t < k; ++t) {
+    double *r = h.data() + (size_t)t * W;
+    std::memcpy(r, lb + (size_t)t * n, (size_t)n * 8);
+    std::memcpy(r + n, ub + (size_t)t * n, (size_t)n * 8);
+    r[2 * n] = nlb[t];
+    r[2 * n + 1] = (double)depth[t];
   }
-  if (s.rel)  // migrated nodes carry no parent branching data
-    HIPCHK(c, hipMemsetAsync(s.ppvar.as<int32_t>() + at, 0xFF, (size_t)k * 4, c->stream));
-  if (s.warm == 2)  // a migrated node starts from the root basis
-    HIPCHK(c, hipMemsetAsync(s.ppk.as<int32_t>() + at, 0, (size_t)k * 4, c->stream));
-  if (s.warm == 1) {
-    // a migrated node starts from the root basis (its parent's stays with
-    // the rank that branched it)
-    for (int t = 0; t < k; ++t) {
-      const size_t o = (size_t)(at + t);
-      HIPCHK(c, hipMemcpyAsync(s.pws_head.as<int32_t>() + o * m, s.ws_head.p, (size_t)m * 4,
-                               hipMemcpyDeviceToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(s.pws_st.as<int8_t>() + o * N, s.ws_st.p, (size_t)N,
-                               hipMemcpyDeviceToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(s.pws_d.as<double>() + o * N, s.ws_d.p, (size_t)N * 8,
-                               hipMemcpyDeviceToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(s.pws_binv.as<double>() + o * m * m, s.ws_binv.p,
-                               (size_t)m * m * 8, hipMemcpyDeviceToDevice, c->stream));
-    }
-  }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  s.count += k;
-  s.tot.open = s.count;
-  return MGPU_OK;
+  DevBuf rows;
+  HIPCHK(c, rows.ensure(h.size() * 8));
+  HIPCHK(c, hipMemcpyAsync(rows.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream));
+  return place_nodes(c, s, k, rows.as<double>());
 }
 
 int mgpu_bnb_best(mgpu_ctx *c, double *obj, double *x) {

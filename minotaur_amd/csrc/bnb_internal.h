@@ -169,4 +169,30 @@ hipError_t launch_bnb_shard(double *plb, double *pub, double *pnlb, int32_t *pde
                             double *tub, double *tnlb, int32_t *tdep, int count, int n,
                             int rank, int world, int *kept, hipStream_t stream);
 
+// Node migration (bnb_migrate.hip): packed rows [lb n | ub n | bound | depth]
+// into pool slots, per-node state reset for a migrated node.
+struct MigrateIO {
+  int k, n, m, N;
+  const int32_t *slots;         // [k] destination pool slots
+  const double *buf;            // [k][2n + 2]
+  double *plb, *pub, *pnlb;
+  int32_t *pdepth;
+  uint8_t *plive;               // best-first pool flags (null: stack)
+  int32_t *ppvar;               // reliability: parent branching variable (null: none)
+  int32_t *ppk;                 // path warm starts: path length (null: none)
+  int32_t *ws_head;             // parent warm starts (null: none) <- the root basis r_*
+  int8_t *ws_st;
+  double *ws_d, *ws_binv;
+  const int32_t *r_head;
+  const int8_t *r_st;
+  const double *r_d, *r_binv;
+};
+hipError_t launch_bnb_pack(const int32_t *slots, int k, int n, const double *plb,
+                           const double *pub, const double *pnlb, const int32_t *pdepth,
+                           uint8_t *plive, double *buf, hipStream_t stream);
+hipError_t launch_bnb_unpack(const MigrateIO &io, hipStream_t stream);
+hipError_t launch_bnb_move_rows(unsigned char *rows, unsigned char *tmp, size_t row_bytes,
+                                const int32_t *from, const int32_t *to, int k,
+                                hipStream_t stream);
+
 }  // namespace mgpu

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -68,97 +69,127 @@ def allreduce_max(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def balance_plan(counts, world):
-    """MpiBranchAndBound::LoadBalance_ (:78-195) made deterministic: from the
-    all-gathered open-node counts, the (src, dst, k) transfers that leave
-    every rank with floor(T/P) or ceil(T/P) nodes (the first T mod P ranks get
-    the extra one), donors and receivers matched in rank order.  Every rank
-    computes the same list."""
-    total = int(sum(counts))
-    target = [total // world + (1 if r < total % world else 0) for r in range(world)]
-    give = [(r, int(counts[r]) - target[r]) for r in range(world) if counts[r] > target[r]]
-    need = [(r, target[r] - int(counts[r])) for r in range(world) if counts[r] < target[r]]
-    plan, i, j = [], 0, 0
-    while i < len(give) and j < len(need):
-        src, g = give[i]
-        dst, d = need[j]
-        k = min(g, d)
-        plan.append((src, dst, k))
-        give[i] = (src, g - k)
-        need[j] = (dst, d - k)
-        if give[i][1] == 0:
-            i += 1
-        if need[j][1] == 0:
-            j += 1
-    return plan
+MIN_NODES_PER_RANK = 50   # MpiBranchAndBound.cpp:80
+
+
+def lb_deal(world_lbs, world, per_rank):
+    """MpiBranchAndBound::LoadBalance_'s deal (:111-188) on a tensor of the
+    all-gathered bounds [world * per_rank] (rank-major, +inf padding): the
+    picked nodes in ascending (bound, owner, local index) order -- a stable
+    sort of the rank-major vector; the reference's std::sort leaves ties
+    unordered -- the i-th one dealt to rank i mod world, stopping at the
+    first +inf (:137-148).  Returns (owner, local, receiver) tensors in that
+    order (on world_lbs' device)."""
+    import math as _m
+    order = torch.sort(world_lbs, stable=True).indices
+    nfin = int((world_lbs != _m.inf).sum().item())
+    order = order[:nfin]
+    i = torch.arange(nfin, device=world_lbs.device)
+    return order // per_rank, order % per_rank, i % world
 
 
 class Comm:
     """The per-round exchange of the node-sharded tree on torch.distributed
     (RCCL over xGMI with device tensors, gloo with CPU tensors):
 
-    * ``round_reduce(inc, open)``: ONE all-reduce MIN of the packed triple
-      [incumbent, -open, open] -> (global incumbent, max and min open count
-      over ranks): the incumbent MIN of :387-389 / :197-208, the stop test of
-      :85 and the idle-rank test of the load balancer in one collective per
-      round;
-    * ``allgather_counts``: the open-node counts of every rank (the
-      Allgather of :107, node counts instead of 50·P lower bounds);
-    * ``send_nodes`` / ``recv_nodes``: node boxes, bounds and depths packed
-      in one f64 tensor per transfer (Serializer.cpp:26-112 content)."""
+    * ``round_reduce(inc, open, err)``: ONE all-reduce MIN of the packed
+      [incumbent, -open, open, -err] -> (global incumbent, max and min open
+      count over ranks, any rank failed): the incumbent MIN of :387-389 /
+      :197-208, the stop test of :85 and the idle-rank test of the load
+      balancer in one collective per round; a rank whose round failed makes
+      every rank stop together instead of leaving its peers blocked;
+    * ``allgather_vec``: one f64 vector per rank (the Allgather of :107);
+    * ``all_to_all_rows``: node rows between all ranks in one collective
+      (the per-node MPI_Send / MPI_Recv of :159-185)."""
 
     def __init__(self, rank, world, device=None):
         self.rank, self.world = rank, world
         self.device = device if device is not None else torch.device('cpu')
 
-    def round_reduce(self, inc, n_open):
-        t = torch.tensor([float(inc), -float(n_open), float(n_open)], dtype=torch.float64,
-                         device=self.device)
+    def round_reduce(self, inc, n_open, err=0):
+        t = torch.tensor([float(inc), -float(n_open), float(n_open), -float(err)],
+                         dtype=torch.float64, device=self.device)
         if active():
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
         v = t.tolist()
-        return v[0], -v[1], v[2]
+        return v[0], -v[1], v[2], -v[3]
 
-    def allgather_counts(self, n_open):
-        t = torch.tensor([float(n_open)], dtype=torch.float64, device=self.device)
+    def allgather_vec(self, vec):
+        t = torch.as_tensor(vec, dtype=torch.float64).to(self.device)
         if not active():
-            return [int(n_open)]
-        out = [torch.zeros_like(t) for _ in range(self.world)]
-        dist.all_gather(out, t)
-        return [int(o.item()) for o in out]
+            return t.view(1, -1)
+        out = torch.empty((self.world, t.numel()), dtype=torch.float64, device=self.device)
+        if self.device.type == 'cpu':   # gloo
+            dist.all_gather(list(out.unbind(0)), t)
+        else:
+            dist.all_gather_into_tensor(out, t)
+        return out
 
-    def send_nodes(self, dst, lb, ub, nlb, depth):
-        k, n = lb.shape
-        buf = torch.empty(k * (2 * n + 2), dtype=torch.float64)
-        v = buf.view(k, 2 * n + 2)
-        v[:, :n] = torch.from_numpy(lb)
-        v[:, n:2 * n] = torch.from_numpy(ub)
-        v[:, 2 * n] = torch.from_numpy(nlb)
-        v[:, 2 * n + 1] = torch.from_numpy(depth.astype('float64'))
-        dist.send(buf.to(self.device), dst)
-
-    def recv_nodes(self, src, k, n):
-        buf = torch.empty(k * (2 * n + 2), dtype=torch.float64, device=self.device)
-        dist.recv(buf, src)
-        v = buf.cpu().view(k, 2 * n + 2).numpy()
-        return (v[:, :n].copy(), v[:, n:2 * n].copy(), v[:, 2 * n].copy(),
-                v[:, 2 * n + 1].astype('int32'))
+    def all_to_all_rows(self, rows, send_counts, recv_counts, width):
+        inp = rows.to(self.device).contiguous()
+        out = torch.empty((int(sum(recv_counts)), width), dtype=torch.float64,
+                          device=self.device)
+        if active():
+            dist.all_to_all_single(out, inp, [int(c) for c in recv_counts],
+                                   [int(c) for c in send_counts])
+        else:
+            out.copy_(inp)
+        return out
 
 
-def rebalance(ctx, comm, n_open, n):
-    """One load-balancing step on the tree pool of ``ctx``: all-gather the
-    counts, run the common plan, export / send, receive / import.  Returns
-    (this rank's open count afterwards, nodes moved globally)."""
-    counts = comm.allgather_counts(n_open)
-    plan = balance_plan(counts, comm.world)
-    for src, dst, k in plan:
-        if comm.rank == src:
-            lb, ub, nlb, dep = ctx.bnb_export(k)
-            assert len(nlb) == k
-            comm.send_nodes(dst, lb, ub, nlb, dep)
-            n_open -= k
-        elif comm.rank == dst:
-            lb, ub, nlb, dep = comm.recv_nodes(src, k, n)
-            ctx.bnb_import(lb, ub, nlb, dep)
-            n_open += k
-    return n_open, sum(k for _, _, k in plan)
+def rebalance(ctx, comm, batch=0):
+    """One bound-aware load-balancing step (MpiBranchAndBound::LoadBalance_,
+    :78-195) on the tree pool of ``ctx``:
+
+    1. every rank picks its next S candidates (mgpu_bnb_pick) -- the
+       reference pops 50 P per rank; a round of the batched tree takes
+       ``batch`` nodes, so S = max(50 P, batch): the globally best P x batch
+       nodes are what the ranks evaluate next;
+    2. one all-gather of the S bounds (+inf padded) and the pool room of
+       every rank;
+    3. every rank computes the same deal (lb_deal): the i-th best goes to
+       rank i mod P; nodes whose owner is their receiver stay in place;
+    4. a plan that would overflow some receiver's pool fails on EVERY rank
+       (same data, same check), so no rank is left blocked in a collective;
+    5. the moving nodes leave as device rows (mgpu_bnb_export_dev), cross in
+       ONE all-to-all (RCCL over xGMI on MI355X) and are imported in deal
+       order (mgpu_bnb_import_dev).
+
+    Returns (this rank's open count afterwards, nodes moved globally, the
+    bounds this rank picked, the bounds of the nodes it received in deal
+    order)."""
+    P, r = comm.world, comm.rank
+    S = max(MIN_NODES_PER_RANK * P, int(batch))
+    lbs = ctx.bnb_pick(S)
+    n_open, spare = ctx.bnb_count()
+    vec = torch.full((S + 1,), float('inf'), dtype=torch.float64)
+    vec[:len(lbs)] = torch.from_numpy(lbs)
+    vec[S] = float(spare)
+    g = comm.allgather_vec(vec)
+    owner, local, recv = lb_deal(g[:, :S].reshape(-1), P, S)
+    moved = owner != recv
+    gain = (torch.bincount(recv[moved], minlength=P) -
+            torch.bincount(owner[moved], minlength=P)).to(torch.float64)
+    if bool((gain > g[:, S]).any().item()):
+        raise RuntimeError('rebalance: the deal would overflow a node pool '
+                           f'(gain {gain.tolist()}, room {g[:, S].tolist()})')
+    send = moved & (owner == r)
+    dst = recv[send]
+    perm = torch.sort(dst, stable=True).indices            # grouped by receiver, deal order
+    idx = local[send][perm].to(torch.int32).cpu().numpy()
+    send_counts = torch.bincount(dst, minlength=P).tolist()
+    got = moved & (recv == r)
+    src = owner[got]
+    recv_counts = torch.bincount(src, minlength=P).tolist()
+    rows = ctx.bnb_export_rows(idx)
+    width = 2 * ctx.problem.n + 2
+    out = comm.all_to_all_rows(rows, send_counts, recv_counts, width)
+    # the all-to-all delivers rows grouped by sender; import them in deal order
+    a2a = torch.sort(src, stable=True).indices               # a2a row -> deal position
+    inv = torch.empty_like(a2a)
+    inv[a2a] = torch.arange(a2a.numel(), device=a2a.device)
+    ordered = out[inv.to(out.device)] if out.shape[0] else out
+    ctx.bnb_import_rows(ordered)
+    n_open = n_open - len(idx) + int(ordered.shape[0])
+    got_lbs = ordered[:, width - 2].cpu().numpy() if ordered.shape[0] else np.empty(0)
+    return n_open, int(moved.sum().item()), lbs, got_lbs

@@ -38,7 +38,8 @@ EXPORTS = [
     'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
     'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
     'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive', 'mgpu_ws_alloc', 'mgpu_ws_free',
-    'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1',
+    'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1', 'mgpu_bnb_pick', 'mgpu_bnb_export_dev',
+    'mgpu_bnb_import_dev', 'mgpu_bnb_count',
 ]
 
 
@@ -108,6 +109,10 @@ def load_library():
     lib.mgpu_bnb_guided_dive.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
     lib.mgpu_bnb_import.argtypes = [_P, _I, _P, _P, _P, _P]
+    lib.mgpu_bnb_pick.argtypes = [_P, _I, _P, _P]
+    lib.mgpu_bnb_export_dev.argtypes = [_P, _I, _P, _P]
+    lib.mgpu_bnb_import_dev.argtypes = [_P, _I, _P]
+    lib.mgpu_bnb_count.argtypes = [_P, _P, _P]
     lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
     lib.mgpu_bnb_best.argtypes = [_P, _P, _P]
     lib.mgpu_bnb_shard.argtypes = [_P, _I, _I, _P]
@@ -679,6 +684,43 @@ class Context:
         self._chk(self.lib.mgpu_bnb_import(self.h, int(k), _hp(_np(lb, np.float64)),
                                            _hp(_np(ub, np.float64)), _hp(_np(nlb, np.float64)),
                                            _hp(_np(depth, np.int32))), 'mgpu_bnb_import')
+
+    def bnb_pick(self, S):
+        """mgpu_bnb_pick: bounds of this rank's next S candidates (np [got])."""
+        lbs = np.empty(max(int(S), 1))
+        got = ctypes.c_int(0)
+        self._chk(self.lib.mgpu_bnb_pick(self.h, int(S), _hp(lbs), ctypes.byref(got)),
+                  'mgpu_bnb_pick')
+        return lbs[:got.value].copy()
+
+    def bnb_export_rows(self, idx):
+        """mgpu_bnb_export_dev: the picked nodes idx leave the pool as device
+        rows [k, 2n + 2] (a torch tensor on this context's device)."""
+        import torch
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        k, n = len(idx), self.problem.n
+        buf = torch.empty((k, 2 * n + 2), dtype=torch.float64,
+                          device=torch.device('cuda', self.device))
+        self._chk(self.lib.mgpu_bnb_export_dev(self.h, k, _hp(idx) if k else None,
+                                               buf.data_ptr() if k else None),
+                  'mgpu_bnb_export_dev')
+        return buf
+
+    def bnb_import_rows(self, rows):
+        """mgpu_bnb_import_dev: rows [k, 2n + 2] (torch; moved to this device)."""
+        import torch
+        k = int(rows.shape[0])
+        if k == 0:
+            return
+        buf = rows.to(device=torch.device('cuda', self.device), dtype=torch.float64).contiguous()
+        self._chk(self.lib.mgpu_bnb_import_dev(self.h, k, buf.data_ptr()), 'mgpu_bnb_import_dev')
+
+    def bnb_count(self):
+        """mgpu_bnb_count: (open nodes, pool slots left for imports)."""
+        o, v = ctypes.c_int(0), ctypes.c_int(0)
+        self._chk(self.lib.mgpu_bnb_count(self.h, ctypes.byref(o), ctypes.byref(v)),
+                  'mgpu_bnb_count')
+        return o.value, v.value
 
     def bnb_best(self):
         x = np.empty(self.problem.n)

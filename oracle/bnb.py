@@ -463,6 +463,7 @@ class CpuBnbContext:
 
     def bnb_export(self, k):
         """mgpu_bnb_export: the stack's top k, or the first k live slots."""
+        self.pick = []
         n = self.problem.n
         if self.order == 0:
             k = min(k, len(self.pool))
@@ -480,13 +481,84 @@ class CpuBnbContext:
                 np.array([nd.nlb for nd in nodes]), np.array([nd.depth for nd in nodes],
                                                              dtype=np.int32))
 
-    def bnb_import(self, lb, ub, nlb, depth):
-        """mgpu_bnb_import: on top of the stack / past the high-water mark;
-        with parent warm starts a migrated node starts from the root basis."""
-        for t in range(len(nlb)):
-            self.pool.append(_Node(np.array(lb[t]), np.array(ub[t]), float(nlb[t]),
-                                   int(depth[t]), self.ws))
+    def _place(self, nodes):
+        """mgpu_bnb_import[_dev]'s placement: on top of the stack, or the
+        lowest free slots first, then past the high-water mark."""
+        if self.order == 0:
+            self.pool.extend(nodes)
+        else:
+            free = [i for i, nd in enumerate(self.pool) if nd is None]
+            for t, nd in enumerate(nodes):
+                if t < len(free):
+                    self.pool[free[t]] = nd
+                else:
+                    self.pool.append(nd)
         self.tot.open = sum(nd is not None for nd in self.pool)
+
+    def _migrant(self, lb, ub, nlb, depth):
+        # a migrated node starts from the root basis, without parent
+        # branching data
+        return _Node(np.array(lb, dtype=np.float64), np.array(ub, dtype=np.float64),
+                     float(nlb), int(depth), self.ws)
+
+    def bnb_import(self, lb, ub, nlb, depth):
+        """mgpu_bnb_import."""
+        self._place([self._migrant(lb[t], ub[t], nlb[t], depth[t]) for t in range(len(nlb))])
+
+    # -- mgpu_bnb_pick / export_dev / import_dev (LoadBalance_) ----------------
+    def bnb_pick(self, S):
+        """The next S candidates: the stack's top (topmost first), or the
+        live nodes pruned by the incumbent and sorted by (bound, slot)."""
+        if self.order == 0:
+            k = min(int(S), len(self.pool))
+            self.pick = [len(self.pool) - 1 - t for t in range(k)]
+        else:
+            inc = float(self.inc)
+            for i, nd in enumerate(self.pool):
+                if nd is None:
+                    continue
+                lb = float(nd.nlb)
+                if lb > inc - 1e-6 or abs(inc - lb) / (abs(inc) + 1e-6) * 100.0 < 1e-6:
+                    self.pool[i] = None
+                    self.tot.pruned += 1
+            live = sorted((i for i, nd in enumerate(self.pool) if nd is not None),
+                          key=lambda i: (_order_key(self.pool[i].nlb), i))
+            self.tot.open = len(live)
+            self.pick = live[:int(S)]
+        return np.array([self.pool[i].nlb for i in self.pick], dtype=np.float64)
+
+    def bnb_export_rows(self, idx):
+        """Rows [k, 2n + 2] = [lb | ub | bound | depth] of picked nodes idx,
+        removed from the pool (the stack keeps the others' order)."""
+        import torch
+        n = self.problem.n
+        slots = [self.pick[int(i)] for i in idx]
+        assert len(set(slots)) == len(slots)
+        rows = torch.empty((len(slots), 2 * n + 2), dtype=torch.float64)
+        for t, sl in enumerate(slots):
+            nd = self.pool[sl]
+            rows[t, :n] = torch.from_numpy(np.asarray(nd.lb, dtype=np.float64))
+            rows[t, n:2 * n] = torch.from_numpy(np.asarray(nd.ub, dtype=np.float64))
+            rows[t, 2 * n] = float(nd.nlb)
+            rows[t, 2 * n + 1] = float(nd.depth)
+        if self.order == 0:
+            gone = set(slots)
+            self.pool = [nd for i, nd in enumerate(self.pool) if i not in gone]
+        else:
+            for sl in slots:
+                self.pool[sl] = None
+        self.pick = []
+        self.tot.open = sum(nd is not None for nd in self.pool)
+        return rows
+
+    def bnb_import_rows(self, rows):
+        n = self.problem.n
+        v = rows.detach().cpu().numpy()
+        self._place([self._migrant(r[:n], r[n:2 * n], r[2 * n], int(r[2 * n + 1])) for r in v])
+
+    def bnb_count(self):
+        live = sum(nd is not None for nd in self.pool)
+        return live, self.cap - live
 
     def bnb_best(self):
         return self.inc, self.best_x.copy()

@@ -284,3 +284,67 @@ def test_bnb_export_import_between_contexts(ctx, order, warm):
         assert sts[1].nodes > 0
     finally:
         other.close()
+
+
+@pytest.mark.parametrize('order,warm', [(0, 0), (1, 0), (1, 1), (0, 2), (1, 2)])
+def test_bnb_pick_rows_match_cpu_restatement(ctx, order, warm):
+    """The bound-aware migration entry points (mgpu_bnb_pick / export_dev /
+    import_dev, LoadBalance_'s pop, send and receive) equal the CPU
+    restatement's: the same picked bounds, the same device rows, and after
+    the rows went out and came back (into the lowest free slots / on top of
+    the stack) the tree still runs round for round like the restatement's
+    and proves the HiGHS optimum."""
+    from bnb import CpuBnbContext
+    p = random_mkp(5, 22, 3)
+    hs, hobj = oracle.highs_milp(p)
+    ctx.load(p)
+    cpu = CpuBnbContext(p, ctx.oracle_pfi())
+    for c in (ctx, cpu):
+        c.bnb_config(order, warm)
+        c.bnb_brancher(0)
+        c.bnb_init(1 << 14)
+    for _ in range(5):
+        sg, sc = ctx.bnb_round(16), cpu.bnb_round(16)
+    assert ctx.bnb_count() == cpu.bnb_count()
+    lg, lc = ctx.bnb_pick(40), cpu.bnb_pick(40)
+    assert len(lg) > 8 and np.array_equal(lg, lc)
+    idx = [1, 4, 5, 7, 2]
+    rg, rc = ctx.bnb_export_rows(idx), cpu.bnb_export_rows(idx)
+    assert np.array_equal(rg.cpu().numpy(), rc.numpy())
+    assert ctx.bnb_count() == cpu.bnb_count()
+    ctx.bnb_import_rows(rg)
+    cpu.bnb_import_rows(rc)
+    assert ctx.bnb_count() == cpu.bnb_count()
+    while True:
+        sg, sc = ctx.bnb_round(16), cpu.bnb_round(16)
+        assert (sg.rounds, sg.nodes, list(sg.ndec), sg.open) == \
+            (sc.rounds, sc.nodes, list(sc.ndec), sc.open)
+        if sg.open == 0:
+            break
+    assert abs(sg.incumbent - hobj) <= 1e-6 * max(1.0, abs(hobj))
+
+
+def test_bnb_repeated_migration_near_capacity(ctx):
+    """best-first imports reuse free slots below the high-water
+    mark, so many export / import cycles on a nearly full pool never run out
+    of slots, and the tree still proves the optimum afterwards."""
+    p = random_mkp(5, 22, 3)
+    hs, hobj = oracle.highs_milp(p)
+    ctx.load(p)
+    ctx.bnb_config(1, 0)
+    ctx.bnb_brancher(0)
+    cap = 256
+    ctx.bnb_init(cap)
+    st = None
+    for _ in range(6):
+        st = ctx.bnb_round(16)
+    for cycle in range(200):
+        lbs = ctx.bnb_pick(64)              # (prunes by the incumbent first)
+        n_open, spare = ctx.bnb_count()
+        k = len(lbs)
+        rows = ctx.bnb_export_rows(list(range(k)))
+        ctx.bnb_import_rows(rows)
+        assert ctx.bnb_count() == (n_open, spare)
+    while st.open:
+        st = ctx.bnb_round(16)
+    assert abs(st.incumbent - hobj) <= 1e-6 * max(1.0, abs(hobj))

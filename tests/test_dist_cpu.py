@@ -154,17 +154,36 @@ def _lb_worker(rank, world, port, out, order):
     inc, x, st, rounds, mine = bnb.solve_distributed(ctx, 8, rank, world, capacity=1 << 14,
                                                      order=order, comm=Comm(rank, world),
                                                      lb_every=3)
-    out[rank] = (inc, rounds, mine['nodes'], mine['moved'])
+    out[rank] = (inc, rounds, mine['nodes'], mine['moved'], mine['lb_log'])
     dist.destroy_process_group()
+
+
+def _expected_receipts(picks, world):
+    """LoadBalance_'s deal restated in plain Python (MpiBranchAndBound.cpp:
+    111-188): all picked bounds in (bound, owner, local) order, the i-th to
+    rank i mod world; per rank the bounds it receives from other ranks, in
+    deal order."""
+    infos = sorted((lb, r, t) for r in range(world) for t, lb in enumerate(picks[r]))
+    got = [[] for _ in range(world)]
+    for i, (lb, r, t) in enumerate(infos):
+        if lb == math.inf:
+            break
+        if i % world != r:
+            got[i % world].append(lb)
+    return got
 
 
 @pytest.mark.parametrize('order', [0, 1])
 def test_rebalanced_sharded_tree_search(order):
     """MpiBranchAndBound::LoadBalance_ semantics over gloo: the split after
-    the shared rounds leaves rank 1 without nodes; the periodic rebalance
-    (all-gather of open counts, common plan, nodes exported, sent, imported)
-    gives it work, both ranks evaluate nodes, and the run still proves the
-    HiGHS optimum with one packed all-reduce per round."""
+    the shared rounds leaves rank 1 without nodes; the periodic bound-aware
+    rebalance (pick, all-gather of bounds and pool room, common deal, one
+    all-to-all of node rows, import in deal order) gives it work, both ranks
+    evaluate nodes, and the run still proves the HiGHS optimum with one
+    packed all-reduce per round.  Every rebalance moved exactly the nodes the
+    reference's deal names: the bounds each rank received are those of the
+    deal positions i with i mod 2 = rank owned by the other rank -- at the
+    first one (rank 1 empty) the odd-positioned best bounds of rank 0."""
     import oracle
     from minotaur_amd.problem import random_mkp
     hs, hobj = oracle.highs_milp(random_mkp(2, 18, 3))
@@ -172,20 +191,67 @@ def test_rebalanced_sharded_tree_search(order):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_lb_worker, args=(world, _free_port(), out, order), nprocs=world, join=True)
-    (i0, r0, m0, mv0), (i1, r1, m1, mv1) = out[0], out[1]
+    (i0, r0, m0, mv0, log0), (i1, r1, m1, mv1, log1) = out[0], out[1]
     assert i0 == i1 and abs(i0 - hobj) <= 1e-6 * max(1.0, abs(hobj))
     assert r0 == r1
     assert mv0 == mv1 > 0            # the plan is global: same count on every rank
     assert m0 > 0 and m1 > 0         # rank 1 got work only through migration
+    assert len(log0) == len(log1) > 0
+    assert len(log1[0][0]) == 0 and len(log1[0][1]) > 0
+    assert log1[0][1] == sorted(log0[0][0])[1::2]
+    for (p0, g0), (p1, g1) in zip(log0, log1):
+        e0, e1 = _expected_receipts([p0, p1], world)
+        assert g0 == e0 and g1 == e1
 
 
-def test_balance_plan():
-    from minotaur_amd.dist import balance_plan
-    assert balance_plan([10, 0], 2) == [(0, 1, 5)]
-    plan = balance_plan([7, 0, 3, 10], 4)
-    after = [7, 0, 3, 10]
-    for s, d, k in plan:
-        after[s] -= k
-        after[d] += k
-    assert sorted(after) == [5, 5, 5, 5] and sum(k for _, _, k in plan) == 7
-    assert balance_plan([4, 4, 4], 3) == []
+def test_lb_deal():
+    """lb_deal on a hand-made gather: stable (bound, owner, local) order,
+    round-robin receivers, +inf padding dropped."""
+    from minotaur_amd.dist import lb_deal
+    inf = math.inf
+    g = torch.tensor([3.0, 1.0, inf,      # rank 0 picks
+                      1.0, 2.0, 0.5])     # rank 1 picks
+    owner, local, recv = lb_deal(g, 2, 3)
+    assert owner.tolist() == [1, 0, 1, 1, 0]
+    assert local.tolist() == [2, 1, 0, 1, 0]
+    assert recv.tolist() == [0, 1, 0, 1, 0]
+
+
+def test_cpu_pick_export_import_roundtrip():
+    """The CPU restatement's pick / export_rows / import_rows: best-first
+    picks ascend by bound, exported rows leave the pool and come back into
+    the lowest free slots (imports reuse holes before growing the
+    high-water mark); depth-first keeps the order of the nodes left."""
+    import oracle
+    from bnb import CpuBnbContext
+    from minotaur_amd.problem import random_mkp
+    p = random_mkp(2, 18, 3)
+    hs, hobj = oracle.highs_milp(p)
+    for order in (0, 1):
+        ctx = CpuBnbContext(p)
+        ctx.bnb_config(order, 0)
+        ctx.bnb_brancher(0)
+        ctx.bnb_init(1 << 12)
+        for _ in range(4):
+            st = ctx.bnb_round(8)
+        n_open, spare = ctx.bnb_count()
+        assert n_open == st.open and spare == (1 << 12) - n_open
+        hw = len(ctx.pool)
+        lbs = ctx.bnb_pick(6)
+        if order == 1:
+            assert list(lbs) == sorted(lbs)
+        before = [nd for nd in ctx.pool if nd is not None]
+        rows = ctx.bnb_export_rows([1, 3, 4])
+        assert rows.shape == (3, 2 * p.n + 2)
+        assert [float(v) for v in rows[:, 2 * p.n]] == [lbs[1], lbs[3], lbs[4]]
+        assert ctx.bnb_count()[0] == n_open - 3
+        gone = {id(before_nd) for before_nd in before} - {id(nd) for nd in ctx.pool}
+        assert len(gone) == 3
+        if order == 0:   # the others keep their order
+            assert [id(nd) for nd in ctx.pool] == [id(nd) for nd in before if id(nd) not in gone]
+        ctx.bnb_import_rows(rows)
+        assert ctx.bnb_count()[0] == n_open
+        assert len(ctx.pool) == hw          # best-first: the holes were reused
+        while st.open:                      # the tree still proves the optimum
+            st = ctx.bnb_round(8)
+        assert abs(ctx.inc - hobj) <= 1e-6 * max(1.0, abs(hobj))
