@@ -483,6 +483,46 @@ int mgpu_bnb_export_dev(mgpu_ctx *ctx, int k, const int32_t *idx, double *d_rows
 int mgpu_bnb_import_dev(mgpu_ctx *ctx, int k, const double *d_rows);
 int mgpu_bnb_count(mgpu_ctx *ctx, int *open, int *spare);
 
+/* ---- Batched spatial branch-and-bound (the glob path) --------------------
+ * The node loop of the reference's glob solver (Glob::createBab_,
+ * src/solvers/Glob.cpp:134-220: BranchAndBound + NodeIncRelaxer +
+ * PCBProcessor, handlers IntVarHandler / LinearHandler / QuadHandler,
+ * brancher=maxvio) for a QCQP after SimpleTransformer.  Prerequisites: the
+ * relaxation LP loaded (mgpu_load_lp: the original rows with products
+ * replaced, then QuadHandler::relax_'s secant / McCormick rows at the root
+ * box; columns = the quadratic problem's variables), the quadratic problem
+ * (mgpu_load_quad) and the node-rows map of the rewritten entries
+ * (mgpu_set_node_rows, record stride = its row-state length R).
+ *   mgpu_glob_init:  the root (the loaded column bounds, its rows from
+ *                    mgpu_quad_rows) on an HBM stack of `capacity` nodes; the
+ *                    root LP from the slack basis gives the basis every node
+ *                    LP starts from (refactored for the node's rows).
+ *   mgpu_glob_round: pops the top `batch` nodes: K2 (QuadHandler::
+ *                    presolveNode from the parent's rows, tightenQuad_ on),
+ *                    K3R + K3 on each node's own rows, then shouldPrune_,
+ *                    IntVarHandler / QuadHandler isFeasible and MaxVio
+ *                    branching over both handlers' candidates (spatial
+ *                    branching at the LP value on a continuous variable,
+ *                    floor / ceil on an integer one), two children per
+ *                    branched node (the preferred one on top).
+ *   mgpu_glob_best:  the incumbent value and point (NaN: none).
+ * Decision codes of ndec: 0 branched, 1 infeasible (K2 or LP), 2 pruned by
+ * bound, 3 feasible (incumbent candidate), 4 engine problem (the round
+ * returns MGPU_ERR_ENGINE), 5 not feasible without a branching candidate
+ * (the reference hands such a node to an NLP engine, PCBProcessor.cpp:
+ * 311-330; here it is closed and counted). */
+typedef struct {
+  long long rounds, nodes;
+  long long ndec[6];
+  long long lps, pivots;       /* LPs solved (nodes not K2-infeasible), their pivots */
+  long long br_int, br_cont;   /* branchings at floor / ceil, at the LP value */
+  int open, last_batch;
+  double incumbent;
+} mgpu_glob_stats;
+int mgpu_glob_init(mgpu_ctx *ctx, int capacity, double incumbent);
+int mgpu_glob_round(mgpu_ctx *ctx, int batch, double incumbent, mgpu_glob_stats *stats);
+int mgpu_glob_best(mgpu_ctx *ctx, double *obj, double *x);
+
 /* ---- QP relaxation with an MFMA KKT block (K5) ---------------
  * Replaces BqpdEngine::solve (src/interfaces/BqpdEngine.cpp:449-534) on the
  * QP relaxation QPDRelaxer builds (examples/QPDRelaxer.cpp:56-126):

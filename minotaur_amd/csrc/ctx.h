@@ -16,6 +16,7 @@ using namespace mgpu;
 struct QuadState;  // quad_runtime.cpp
 struct BnbState;   // bnb.cpp
 struct QpState;    // qp_runtime.cpp
+struct GlobState;  // glob_runtime.cpp
 
 struct DevBuf {
   void *p = nullptr;
@@ -102,6 +103,7 @@ struct mgpu_ctx {
   QuadState *quad = nullptr;   // K2 problem (mgpu_load_quad)
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
   QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)
+  GlobState *glob = nullptr;   // batched spatial B&B (mgpu_glob_init)
 };
 
 namespace {
@@ -141,6 +143,7 @@ hipError_t upload(DevBuf &b, const T *src, size_t count) {
 void quad_state_free(mgpu_ctx *c);  // quad_runtime.cpp
 void bnb_state_free(mgpu_ctx *c);   // bnb.cpp
 void qp_state_free(mgpu_ctx *c);    // qp_runtime.cpp
+void glob_state_free(mgpu_ctx *c);  // glob_runtime.cpp
 // an LP batch with per-node warm starts through the K3 / K3L selection of
 // mgpu_lp_solve (mgpu_runtime.cpp); io.next is set here
 int launch_lp_nodes(mgpu_ctx *c, const LpIO &io);

@@ -1,0 +1,279 @@
+// Batched spatial branch-and-bound over the McCormick relaxation: the node
+// loop of the reference's glob solver (Glob::createBab_, src/solvers/
+// Glob.cpp:134-220: BranchAndBound + NodeIncRelaxer + PCBProcessor with
+// IntVarHandler, LinearHandler, QuadHandler and, brancher=maxvio,
+// MaxVioBrancher; BranchAndBound.cpp:424-514) for a QCQP after
+// SimpleTransformer: one round pops the top B open nodes of an HBM stack and
+// runs, all on the device,
+//   K2   QuadHandler::presolveNode (QuadHandler.cpp:1204-1269): bound
+//        propagation over the products and tightenQuad_, then the rewrite of
+//        the node's secant / McCormick rows (upSqCon_ / upBilCon_,
+//        :3322-3419) from its PARENT's row state (the incremental
+//        relaxation: NodeIncRelaxer keeps the parent's rows, :94-175);
+//   K3R + K3   the node's own LP with those rows (OsiLPEngine::
+//        changeConstraint then solve, OsiLPEngine.cpp:206-243, 571-652),
+//        warm-started from the root basis refactored for the node's matrix;
+//   decide     shouldPrune_, IntVarHandler + QuadHandler isFeasible, and
+//        MaxVioBrancher over both handlers' candidates (glob_tree.hip),
+//        spatial branching at the LP value on a continuous variable;
+//   children   two per branched node, each with the node's tightened box,
+//        the branching bound and the node's rows.
+// One small record comes back per round (counts, best feasible node).
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "ctx.h"
+#include "glob_internal.h"
+#include "quad_state.h"
+
+struct GlobState {
+  int nv = 0, R = 0, cap = 0, count = 0, maxb = 0;
+  double inc = INFINITY;
+  bool root_ws = false;
+  std::vector<double> best_x;
+  mgpu_glob_stats tot{};
+  DevBuf plb, pub, prows, pnlb, pdepth;
+  DevBuf wlb, wub, wrows, kinf, knm, st, obj, it, x, cand, dec, bvar, bval, bup, bint, pos,
+      depth_in, out;
+  DevBuf ws_head, ws_st, ws_d, ws_binv, r_st, r_obj, r_it;
+  DevBuf fvtype, fsq, fbil, flptr, flvar, flval, fqptr, fqv1, fqv2, fqval, fclb, fcub;
+  void release() {
+    for (DevBuf *b : {&plb, &pub, &prows, &pnlb, &pdepth, &wlb, &wub, &wrows, &kinf, &knm, &st,
+                      &obj, &it, &x, &cand, &dec, &bvar, &bval, &bup, &bint, &pos, &depth_in,
+                      &out, &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj, &r_it, &fvtype,
+                      &fsq, &fbil, &flptr, &flvar, &flval, &fqptr, &fqv1, &fqv2, &fqval, &fclb,
+                      &fcub})
+      b->release();
+  }
+};
+
+void glob_state_free(mgpu_ctx *c) {
+  if (c && c->glob) {
+    c->glob->release();
+    delete c->glob;
+    c->glob = nullptr;
+  }
+}
+
+namespace {
+
+int ensure_glob_batch(mgpu_ctx *c, GlobState &s, int B) {
+  if (B <= s.maxb) return MGPU_OK;
+  const size_t nv = (size_t)s.nv, R = (size_t)(s.R > 0 ? s.R : 1);
+  HIPCHK(c, s.wlb.ensure((size_t)B * nv * 8));
+  HIPCHK(c, s.wub.ensure((size_t)B * nv * 8));
+  HIPCHK(c, s.wrows.ensure((size_t)B * R * 8));
+  HIPCHK(c, s.x.ensure((size_t)B * nv * 8));
+  HIPCHK(c, s.cand.ensure((size_t)B * nv * 4 * 8));
+  for (DevBuf *b : {&s.kinf, &s.knm, &s.st, &s.it, &s.dec, &s.bvar, &s.pos, &s.depth_in})
+    HIPCHK(c, b->ensure((size_t)B * 4));
+  for (DevBuf *b : {&s.obj, &s.bval}) HIPCHK(c, b->ensure((size_t)B * 8));
+  for (DevBuf *b : {&s.bup, &s.bint}) HIPCHK(c, b->ensure((size_t)B));
+  HIPCHK(c, s.out.ensure(sizeof(GlobOut)));
+  s.maxb = B;
+  return MGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgpu_glob_init(mgpu_ctx *c, int capacity, double incumbent) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->loaded || !c->quad || !c->nr_set)
+    return fail(c, MGPU_ERR_STATE, "mgpu_glob_init: load the relaxation LP (mgpu_load_lp), the "
+                "quadratic problem (mgpu_load_quad) and the node-rows map first");
+  const QuadState &q = *c->quad;
+  if (c->lp.n != q.nv || c->nr_stride != q.R)
+    return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: LP columns (%d) / row-record stride (%d) do "
+                "not match the quadratic problem (%d vars, %d row values)", c->lp.n,
+                c->nr_stride, q.nv, q.R);
+  if (c->lp.m > kLpMaxM)
+    return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: node rows need m <= %d (m = %d)", kLpMaxM,
+                c->lp.m);
+  if (capacity < 1) return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: capacity < 1");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  glob_state_free(c);
+  GlobState *s = new GlobState();
+  c->glob = s;
+  const int nv = q.nv, R = q.R, m = c->lp.m, N = nv + m;
+  s->nv = nv;
+  s->R = R;
+  s->cap = capacity;
+  s->inc = incumbent;
+  s->best_x.assign((size_t)nv, NAN);
+  s->tot.incumbent = incumbent;
+  HIPCHK(c, s->plb.ensure((size_t)capacity * nv * 8));
+  HIPCHK(c, s->pub.ensure((size_t)capacity * nv * 8));
+  HIPCHK(c, s->prows.ensure((size_t)capacity * (R > 0 ? R : 1) * 8));
+  HIPCHK(c, s->pnlb.ensure((size_t)capacity * 8));
+  HIPCHK(c, s->pdepth.ensure((size_t)capacity * 4));
+  // the problem data of the decision kernel
+  std::vector<uint8_t> vt((size_t)nv);
+  for (int j = 0; j < nv; ++j) vt[(size_t)j] = (uint8_t)q.h_vtype[(size_t)j];
+  HIPCHK(c, upload(s->fvtype, vt.data(), vt.size()));
+  HIPCHK(c, upload(s->flptr, q.h_lptr.data(), q.h_lptr.size()));
+  HIPCHK(c, upload(s->flvar, q.h_lvar.data(), q.h_lvar.size()));
+  HIPCHK(c, upload(s->flval, q.h_lval.data(), q.h_lval.size()));
+  HIPCHK(c, upload(s->fqptr, q.h_qptr.data(), q.h_qptr.size()));
+  HIPCHK(c, upload(s->fqv1, q.h_qv1.data(), q.h_qv1.size()));
+  HIPCHK(c, upload(s->fqv2, q.h_qv2.data(), q.h_qv2.size()));
+  HIPCHK(c, upload(s->fqval, q.h_qval.data(), q.h_qval.size()));
+  HIPCHK(c, upload(s->fclb, q.h_clb.data(), q.h_clb.size()));
+  HIPCHK(c, upload(s->fcub, q.h_cub.data(), q.h_cub.size()));
+  // the root: the loaded column bounds, QuadHandler::relax_'s rows there
+  std::vector<double> lb((size_t)nv), ub((size_t)nv), rows((size_t)(R > 0 ? R : 1));
+  HIPCHK(c, hipMemcpy(lb.data(), c->collb.p, (size_t)nv * 8, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(ub.data(), c->colub.p, (size_t)nv * 8, hipMemcpyDeviceToHost));
+  int rc = mgpu_quad_rows(c, lb.data(), ub.data(), rows.data(), nullptr);
+  if (rc != MGPU_OK) return rc;
+  const double ninf = -INFINITY;
+  const int32_t zero = 0;
+  HIPCHK(c, hipMemcpy(s->plb.p, lb.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(s->pub.p, ub.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+  if (R > 0) HIPCHK(c, hipMemcpy(s->prows.p, rows.data(), (size_t)R * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(s->pnlb.p, &ninf, 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(s->pdepth.p, &zero, 4, hipMemcpyHostToDevice));
+  s->count = 1;
+  // the root basis every node LP refactors for its own rows: the loaded LP
+  // (the root's rows) from the slack basis
+  HIPCHK(c, s->ws_head.ensure((size_t)m * 4 + 4));
+  HIPCHK(c, s->ws_st.ensure((size_t)N));
+  HIPCHK(c, s->ws_d.ensure((size_t)N * 8));
+  HIPCHK(c, s->ws_binv.ensure((size_t)m * m * 8 + 8));
+  for (DevBuf *b : {&s->r_st, &s->r_it}) HIPCHK(c, b->ensure(4));
+  HIPCHK(c, s->r_obj.ensure(8));
+  rc = mgpu_lp_solve_dev(c, 1, c->collb.as<double>(), c->colub.as<double>(), nullptr, nullptr,
+                         nullptr, nullptr, nullptr, 1, 0, s->r_st.as<int32_t>(),
+                         s->r_obj.as<double>(), s->r_it.as<int32_t>(), nullptr,
+                         s->ws_head.as<int32_t>(), s->ws_st.as<int8_t>(), s->ws_d.as<double>(),
+                         s->ws_binv.as<double>());
+  if (rc != MGPU_OK) return rc;
+  int32_t rst = 0;
+  HIPCHK(c, hipMemcpyAsync(&rst, s->r_st.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s->root_ws = rst == 0;
+  s->tot.open = 1;
+  return MGPU_OK;
+}
+
+int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *stats) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->glob) return fail(c, MGPU_ERR_STATE, "mgpu_glob_round: mgpu_glob_init first");
+  if (batch < 1) return fail(c, MGPU_ERR_ARG, "mgpu_glob_round: batch < 1");
+  GlobState &s = *c->glob;
+  const QuadState &q = *c->quad;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (incumbent < s.inc) s.inc = incumbent;
+  int nb = batch < s.count ? batch : s.count;
+  if (s.count + nb > s.cap) nb = s.cap - s.count;  // children must fit: base + 2 nb <= cap
+  if (nb <= 0) {
+    if (s.count > 0) return fail(c, MGPU_ERR_NOMEM, "mgpu_glob_round: node pool full");
+    s.tot.open = 0;
+    if (stats) *stats = s.tot;
+    return MGPU_OK;
+  }
+  const int base = s.count - nb, nv = s.nv, R = s.R;
+  int rc = ensure_glob_batch(c, s, nb);
+  if (rc != MGPU_OK) return rc;
+  // K2 from the parents' rows
+  rc = mgpu_quad_fbbt_dev(c, nb, s.plb.as<double>() + (size_t)base * nv,
+                          s.pub.as<double>() + (size_t)base * nv, s.inc, 1,
+                          s.prows.as<double>() + (size_t)base * R, 0, s.wlb.as<double>(),
+                          s.wub.as<double>(), s.wrows.as<double>(), s.kinf.as<int32_t>(),
+                          s.knm.as<int32_t>(), 0, nullptr, nullptr, nullptr, nullptr);
+  if (rc != MGPU_OK) return rc;
+  // the node LPs with their own rows (K3R + K3), K2-infeasible nodes skipped
+  rc = mgpu_lp_solve_rows_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(),
+                              s.kinf.as<int32_t>(), s.wrows.as<double>(),
+                              s.root_ws ? s.ws_head.as<int32_t>() : nullptr,
+                              s.root_ws ? s.ws_st.as<int8_t>() : nullptr, 1, 0,
+                              s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
+                              s.x.as<double>());
+  if (rc != MGPU_OK) return rc;
+  GlobIO io{};
+  io.nb = nb;
+  io.base = base;
+  io.nv = nv;
+  io.R = R;
+  io.vtype = s.fvtype.as<uint8_t>();
+  io.nsq = (int)q.sq_x.size();
+  io.nbil = (int)q.bil_x0.size();
+  io.ncon = q.ncon;
+  io.nfun = q.ncon + (q.has_obj ? 1 : 0);
+  io.sq = q.dq.sq;
+  io.bil = q.dq.bil;
+  io.lptr = s.flptr.as<int32_t>();
+  io.lvar = s.flvar.as<int32_t>();
+  io.lval = s.flval.as<double>();
+  io.qptr = s.fqptr.as<int32_t>();
+  io.qv1 = s.fqv1.as<int32_t>();
+  io.qv2 = s.fqv2.as<int32_t>();
+  io.qval = s.fqval.as<double>();
+  io.clb = s.fclb.as<double>();
+  io.cub = s.fcub.as<double>();
+  io.obj_const = q.obj_const;
+  io.inc = s.inc;
+  io.abs_tol = 1e-6;   // solAbs_tol / solRel_tol (Environment.cpp:486, 509-528)
+  io.rel_tol = 1e-6;
+  io.kinf = s.kinf.as<int32_t>();
+  io.wlb = s.wlb.as<double>();
+  io.wub = s.wub.as<double>();
+  io.wrows = s.wrows.as<double>();
+  io.status = s.st.as<int32_t>();
+  io.iters = s.it.as<int32_t>();
+  io.obj = s.obj.as<double>();
+  io.x = s.x.as<double>();
+  io.cand = s.cand.as<double>();
+  io.dec = s.dec.as<int32_t>();
+  io.bvar = s.bvar.as<int32_t>();
+  io.pos = s.pos.as<int32_t>();
+  io.depth_in = s.depth_in.as<int32_t>();
+  io.bval = s.bval.as<double>();
+  io.bup = s.bup.as<int8_t>();
+  io.bint = s.bint.as<int8_t>();
+  io.out = s.out.as<GlobOut>();
+  io.plb = s.plb.as<double>();
+  io.pub = s.pub.as<double>();
+  io.prows = s.prows.as<double>();
+  io.pnlb = s.pnlb.as<double>();
+  io.pdepth = s.pdepth.as<int32_t>();
+  HIPCHK(c, launch_glob_round_tail(io, c->stream));
+  GlobOut o;
+  HIPCHK(c, hipMemcpyAsync(&o, s.out.p, sizeof o, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s.count = base + o.nchild;
+  if (o.best_idx >= 0 && o.best < s.inc) {
+    s.inc = o.best;
+    HIPCHK(c, hipMemcpy(s.best_x.data(), s.x.as<double>() + (size_t)o.best_idx * nv,
+                        (size_t)nv * 8, hipMemcpyDeviceToHost));
+  }
+  s.tot.rounds += 1;
+  s.tot.nodes += nb;
+  for (int k = 0; k < 6; ++k) s.tot.ndec[k] += o.ndec[k];
+  s.tot.lps += o.lps;
+  s.tot.pivots += o.pivots;
+  s.tot.br_int += o.br_int;
+  s.tot.br_cont += o.ndec[0] - o.br_int;
+  s.tot.open = s.count;
+  s.tot.last_batch = nb;
+  s.tot.incumbent = s.inc;
+  if (stats) *stats = s.tot;
+  if (o.ndec[4] > 0)
+    return fail(c, MGPU_ERR_ENGINE, "mgpu_glob_round: %lld nodes ended with an engine problem "
+                "(K2 propagation cap / default bound, or an unbounded / unknown LP status)",
+                (long long)o.ndec[4]);
+  return MGPU_OK;
+}
+
+int mgpu_glob_best(mgpu_ctx *c, double *obj, double *x) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->glob) return fail(c, MGPU_ERR_STATE, "mgpu_glob_best: mgpu_glob_init first");
+  if (obj) *obj = c->glob->inc;
+  if (x) std::memcpy(x, c->glob->best_x.data(), (size_t)c->glob->nv * 8);
+  return MGPU_OK;
+}
+
+}  // extern "C"

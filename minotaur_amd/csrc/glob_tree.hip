@@ -1,0 +1,319 @@
+// Batched spatial branch-and-bound over the McCormick relaxation (the glob
+// path), gfx950: the node decision, summary and child
+// writer of one round of mgpu_glob_round (glob_runtime.cpp).
+//
+// The reference's mglob runs BranchAndBound with the handlers IntVarHandler,
+// LinearHandler, QuadHandler (SimpleTransformer.cpp:940-963) and, with the
+// option brancher=maxvio, MaxVioBrancher (Glob.cpp:134-192).  After a node's
+// presolve (K2, QuadHandler::presolveNode) and LP (K3R + K3 with the node's
+// rewritten McCormick / secant rows), PCBProcessor decides:
+//   * shouldPrune_ (PCBProcessor.cpp:400-523): the engine-status switch and
+//     the bound test against the incumbent (solAbs_tol / solRel_tol 1e-6);
+//   * isFeasible: IntVarHandler::isFeasible (IntVarHandler.cpp:54-84) and
+//     QuadHandler::isFeasible (QuadHandler.cpp:904-953: every original
+//     quadratic constraint's activity within aTol_ 1e-6 / rTol_ 1e-7, and a
+//     quadratic objective's value against the relaxation's);
+//   * otherwise MaxVioBrancher::findBranches (MaxVioBrancher.cpp): candidates
+//     from IntVarHandler (IntVarHandler.cpp:86-110: dd = x - floor x,
+//     ud = ceil x - x) then QuadHandler (QuadHandler.cpp:473-614: y = x^2
+//     violated from above, y = x0 x1 violated per LinBil::isViolated, a
+//     variable at its bounds is not a candidate), merged per variable by
+//     adding the distances (the later handler takes over when its distance
+//     sum is >= the earlier one's), score 0.8 min + 0.2 max (x 0.1 for the
+//     original variables: every candidate here), the first maximum in
+//     variable order; up branch first when dd > ud.  IntVarHandler branches
+//     at floor / ceil (IntVarHandler.cpp:133-175), QuadHandler at the value
+//     itself (QuadHandler.cpp:422-471).
+// One thread per node: the decision is a few hundred flops of sequential,
+// order-dependent sums (the CPU restatement, oracle/glob.py, adds in the
+// same order, so decisions and scores are bit-identical); the per-variable
+// candidate sums live in a [node][var] scratch.
+#include "glob_internal.h"
+
+namespace mgpu {
+namespace {
+
+constexpr double kQATol = 1e-6;    // QuadHandler aTol_ (QuadHandler.cpp:61)
+constexpr double kQRTol = 1e-7;    // QuadHandler rTol_ (:67)
+constexpr double kQBTol = 1e-8;    // QuadHandler bTol_ (:62), isAtBnds_
+constexpr double kBilATol = 1e-5;  // LinBil aTol_ (LinBil.cpp:28)
+constexpr double kBilRTol = 1e-4;  // LinBil rTol_
+constexpr double kIntTol = 1e-6;   // IntVarHandler intTol_
+
+__device__ __forceinline__ bool at_bnds(double v, double l, double u) {
+  return fabs(v - l) < kQBTol || fabs(v - u) < kQBTol;
+}
+
+__global__ __launch_bounds__(256) void glob_decide(GlobIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb) return;
+  const int nv = io.nv;
+  const double *x = io.x + (size_t)b * nv;
+  const double *lb = io.wlb + (size_t)b * nv;
+  const double *ub = io.wub + (size_t)b * nv;
+  io.depth_in[b] = io.pdepth[io.base + b];
+  const int st = io.status[b];
+  const double val = io.obj[b];
+  int dec = 0;
+  int bvar = -1, bup = 0, bint = 0;
+  double bval = 0.0;
+  if (io.kinf[b] != 0) {
+    dec = io.kinf[b] == 1 ? 1 : 4;   // presolveNode infeasible / K2 failure
+  } else if (st == 2 || st == 3 || st == 8 || st == 10 || st == 11) {
+    dec = 1;
+  } else if (st == 5) {
+    dec = 2;
+  } else if (!(st == 0 || st == 1 || st == 6)) {
+    dec = 4;
+  } else if (val >= io.inc - io.abs_tol || val >= io.inc - fabs(io.inc) * io.rel_tol) {
+    dec = 2;
+  } else {
+    // isFeasible: integrality, then the original quadratic constraints and
+    // a quadratic objective (QuadHandler::isFeasible)
+    bool feas = true;
+    for (int j = 0; j < nv && feas; ++j) {
+      const uint8_t t = io.vtype[j];
+      if ((t == kBinary || t == kInteger) && fabs(x[j] - floor(x[j] + 0.5)) > kIntTol)
+        feas = false;
+    }
+    for (int c = 0; c < io.nfun && feas; ++c) {
+      const int q0 = io.qptr[c], q1 = io.qptr[c + 1];
+      if (q0 == q1) continue;          // linear: LinearHandler's
+      double act = 0.0;
+      for (int t = io.lptr[c]; t < io.lptr[c + 1]; ++t) act += io.lval[t] * x[io.lvar[t]];
+      for (int t = q0; t < q1; ++t) act += io.qval[t] * x[io.qv1[t]] * x[io.qv2[t]];
+      if (c == io.ncon) {              // the objective
+        act += io.obj_const;
+        const double vio = fabs(val - act);
+        if (vio > fabs(act) * kQRTol && vio > kQATol) feas = false;
+        continue;
+      }
+      const double cub = io.cub[c], clb = io.clb[c];
+      if (act > cub + kQATol && (cub == 0.0 || act > cub + fabs(cub) * kQRTol)) feas = false;
+      if (act < clb - kQATol && (clb == 0.0 || act < clb - fabs(clb) * kQRTol)) feas = false;
+    }
+    if (feas) {
+      dec = 3;
+    } else {
+      // candidates per variable: IntVarHandler's, then QuadHandler's
+      double *id = io.cand + (size_t)b * nv * 4, *iu = id + nv, *qd = iu + nv, *qu = qd + nv;
+      for (int j = 0; j < nv; ++j) id[j] = iu[j] = qd[j] = qu[j] = -1.0;  // -1: none
+      for (int j = 0; j < nv; ++j) {
+        const uint8_t t = io.vtype[j];
+        const double v = x[j];
+        if ((t == kBinary || t == kInteger) && fabs(floor(v + 0.5) - v) > kIntTol) {
+          id[j] = v - floor(v);
+          iu[j] = ceil(v) - v;
+        }
+      }
+      // distances are >= 0; a later candidate of the same variable adds its
+      // distances to the earlier ones (new + existing, :507-512)
+      auto add_q = [&](int j, double d, double u) {
+        if (qd[j] < 0.0) {
+          qd[j] = d;
+          qu[j] = u;
+        } else {
+          qd[j] = d + qd[j];
+          qu[j] = u + qu[j];
+        }
+      };
+      for (int k = 0; k < io.nsq; ++k) {
+        const int j = io.sq[2 * k], y = io.sq[2 * k + 1];
+        const double x0 = x[j], yv = x[y];
+        if (yv - x0 * x0 > fabs(yv) * kQRTol && yv - x0 * x0 > kQATol) {
+          const double dd = (yv - x0 * x0) / sqrt(1.0 + (lb[j] + x0) * (lb[j] + x0));
+          const double ud = (yv - x0 * x0) / sqrt(1.0 + (ub[j] + x0) * (ub[j] + x0));
+          add_q(j, dd, ud);
+        }
+      }
+      for (int k = 0; k < io.nbil; ++k) {
+        const int j0 = io.bil[3 * k], j1 = io.bil[3 * k + 1], y = io.bil[3 * k + 2];
+        const double v0 = x[j0], v1 = x[j1], yv = x[y];
+        const double pr = v1 * v0;
+        if (!(fabs(pr - yv) > kBilATol && fabs(pr - yv) > fabs(yv) * kBilRTol)) continue;
+        if (!at_bnds(v0, lb[j0], ub[j0])) {
+          double dd, ud;
+          if (v0 * v1 > yv) {
+            dd = (-yv + v0 * v1) / sqrt(1.0 + v0 * v0 + ub[j1] * ub[j1]);
+            ud = (-yv + v0 * v1) / sqrt(1.0 + v0 * v0 + lb[j1] * lb[j1]);
+          } else {
+            dd = (yv - v0 * v1) / sqrt(1.0 + v0 * v0 + lb[j1] * lb[j1]);
+            ud = (yv - v0 * v1) / sqrt(1.0 + v0 * v0 + ub[j1] * ub[j1]);
+          }
+          add_q(j0, dd, ud);
+        }
+        if (!at_bnds(v1, lb[j1], ub[j1])) {
+          double dd, ud;
+          if (v0 * v1 > yv) {
+            dd = (-yv + v1 * v0) / sqrt(1.0 + v1 * v1 + ub[j0] * ub[j0]);
+            ud = (-yv + v1 * v0) / sqrt(1.0 + v1 * v1 + lb[j0] * lb[j0]);
+          } else {
+            dd = (yv - v1 * v0) / sqrt(1.0 + v1 * v1 + lb[j0] * lb[j0]);
+            ud = (yv - v1 * v0) / sqrt(1.0 + v1 * v1 + ub[j0] * ub[j0]);
+          }
+          add_q(j1, dd, ud);
+        }
+      }
+      // MaxVioBrancher::findCandidates_ merge + findBestCandidate_
+      double best = -INFINITY;
+      for (int j = 0; j < nv; ++j) {
+        const bool hi = id[j] >= 0.0, hq = qd[j] >= 0.0;
+        if (!hi && !hq) continue;
+        double d, u;
+        int isint;
+        if (hi && hq) {
+          // the later handler (QuadHandler) takes the candidate when its
+          // distance sum is >= IntVarHandler's (MaxVioBrancher.cpp:109-113)
+          isint = (id[j] + iu[j] <= qd[j] + qu[j]) ? 0 : 1;
+          d = id[j] + qd[j];
+          u = iu[j] + qu[j];
+        } else if (hi) {
+          isint = 1;
+          d = id[j];
+          u = iu[j];
+        } else {
+          isint = 0;
+          d = qd[j];
+          u = qu[j];
+        }
+        const double lo = d < u ? d : u, hv = d < u ? u : d;
+        const double sc = 0.1 * (0.8 * lo + 0.2 * hv);
+        if (sc > best) {
+          best = sc;
+          bvar = j;
+          bint = isint;
+          bup = d > u ? 1 : 0;
+        }
+      }
+      if (bvar < 0) {
+        dec = 5;   // no candidate (the reference hands the node to an NLP engine)
+      } else {
+        dec = 0;
+        bval = x[bvar];
+      }
+    }
+  }
+  io.dec[b] = dec;
+  io.bvar[b] = bvar;
+  io.bval[b] = bval;
+  io.bup[b] = (int8_t)bup;
+  io.bint[b] = (int8_t)bint;
+}
+
+// One block: decision counts, the children's exclusive prefix (2 per
+// branched node), LP count and pivots, the best feasible node (lowest
+// objective, lowest index on ties).  Chunked: thread t owns nodes
+// [t*C, (t+1)*C).
+__global__ __launch_bounds__(1024) void glob_summary(GlobIO io) {
+  __shared__ int s_cnt[1024];
+  __shared__ double s_best[1024];
+  __shared__ int s_bidx[1024];
+  __shared__ long long s_piv[1024];
+  __shared__ int s_lps[1024];
+  __shared__ int s_dec[1024][6];
+  __shared__ int s_bi[1024];
+  const int t = threadIdx.x, nb = io.nb;
+  const int C = (nb + 1023) / 1024;
+  const int b0 = t * C, b1 = b0 + C < nb ? b0 + C : nb;
+  int cnt = 0, lps = 0, bi = 0;
+  long long piv = 0;
+  int dc[6] = {0, 0, 0, 0, 0, 0};
+  double best = INFINITY;
+  int bidx = -1;
+  for (int b = b0; b < b1; ++b) {
+    const int d = io.dec[b];
+    dc[d] += 1;
+    if (d == 0) {
+      cnt += 2;
+      bi += io.bint[b];
+    }
+    if (io.kinf[b] == 0) {
+      lps += 1;
+      piv += io.iters[b];
+    }
+    if (d == 3 && io.obj[b] < best) {
+      best = io.obj[b];
+      bidx = b;
+    }
+  }
+  s_cnt[t] = cnt;
+  s_best[t] = best;
+  s_bidx[t] = bidx;
+  s_piv[t] = piv;
+  s_lps[t] = lps;
+  s_bi[t] = bi;
+  for (int k = 0; k < 6; ++k) s_dec[t][k] = dc[k];
+  __syncthreads();
+  if (t == 0) {
+    GlobOut o{};
+    int run = 0;
+    o.best = INFINITY;
+    o.best_idx = -1;
+    for (int u = 0; u < 1024; ++u) {
+      const int c = s_cnt[u];
+      s_cnt[u] = run;
+      run += c;
+      for (int k = 0; k < 6; ++k) o.ndec[k] += s_dec[u][k];
+      o.lps += s_lps[u];
+      o.pivots += s_piv[u];
+      o.br_int += s_bi[u];
+      if (s_bidx[u] >= 0 && s_best[u] < o.best) {
+        o.best = s_best[u];
+        o.best_idx = s_bidx[u];
+      }
+    }
+    o.nchild = run;
+    *io.out = o;
+  }
+  __syncthreads();
+  int run = s_cnt[t];
+  for (int b = b0; b < b1; ++b) {
+    io.pos[b] = run;
+    if (io.dec[b] == 0) run += 2;
+  }
+}
+
+// One wave per branched node: two children at base + pos[b], the preferred
+// one last (the top of the stack is processed first), each the node's
+// tightened box with the branching bound, its rewritten rows, its LP value
+// as the bound and depth + 1.
+__global__ __launch_bounds__(256) void glob_children(GlobIO io) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= io.nb || io.dec[b] != 0) return;
+  const int nv = io.nv, R = io.R, j = io.bvar[b];
+  const double v = io.bval[b];
+  const bool isint = io.bint[b] != 0;
+  const double dn = isint ? floor(v) : v, up = isint ? ceil(v) : v;
+  for (int c = 0; c < 2; ++c) {
+    // c = 0: the other branch, c = 1: the preferred one (on top)
+    const bool upc = (c == 1) == (io.bup[b] != 0);
+    const size_t s = (size_t)io.base + io.pos[b] + c;
+    for (int k = lane; k < nv; k += 64) {
+      double l = io.wlb[(size_t)b * nv + k], u = io.wub[(size_t)b * nv + k];
+      if (k == j) {
+        if (upc) l = up;
+        else u = dn;
+      }
+      io.plb[s * nv + k] = l;
+      io.pub[s * nv + k] = u;
+    }
+    for (int k = lane; k < R; k += 64) io.prows[s * R + k] = io.wrows[(size_t)b * R + k];
+    if (lane == 0) {
+      io.pnlb[s] = io.obj[b];
+      io.pdepth[s] = io.depth_in[b] + 1;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_glob_round_tail(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_decide, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  hipLaunchKernelGGL(glob_summary, dim3(1), dim3(1024), 0, stream, io);
+  hipLaunchKernelGGL(glob_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+}  // namespace mgpu

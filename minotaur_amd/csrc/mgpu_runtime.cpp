@@ -82,6 +82,7 @@ int mgpu_destroy(mgpu_ctx *c) {
   if (c->ev8) (void)hipEventDestroy(c->ev8);
   if (c->ev9) (void)hipEventDestroy(c->ev9);
   if (c->ev10) (void)hipEventDestroy(c->ev10);
+  glob_state_free(c);
   quad_state_free(c);
   bnb_state_free(c);
   qp_state_free(c);
@@ -137,6 +138,7 @@ int mgpu_load_lp(mgpu_ctx *c, int n, int m, const int32_t *rowptr, const int32_t
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   bnb_state_free(c);  // a tree belongs to the problem it was started on
+  glob_state_free(c);
   c->nr_set = false;  // so do per-node rows (positions in its CSR)
   c->lp = DevLP{};
   // CSR terms, packed

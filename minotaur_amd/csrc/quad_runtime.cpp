@@ -17,23 +17,7 @@
 #include <cstring>
 
 #include "ctx.h"
-
-struct QuadState {
-  DevQuad dq{};
-  int nv0 = 0, nv = 0, R = 0;
-  std::vector<int32_t> sq_x, bil_x0, bil_x1;
-  bool obj_in_prog1 = false;
-  double obj_const = 0.0;
-  DevBuf vtype, sq, bil, fun[2], term[2];
-  DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_rin, io_rout, io_inf, io_nm, io_kind,
-      io_idx, io_v1, io_v2, scratch;
-  void release() {
-    for (DevBuf *b : {&vtype, &sq, &bil, &fun[0], &fun[1], &term[0], &term[1], &io_lb_in,
-                      &io_ub_in, &io_lb_out, &io_ub_out, &io_rin, &io_rout, &io_inf, &io_nm,
-                      &io_kind, &io_idx, &io_v1, &io_v2, &scratch})
-      b->release();
-  }
-};
+#include "quad_state.h"
 
 void quad_state_free(mgpu_ctx *c) {
   if (c && c->quad) {
@@ -169,6 +153,7 @@ int mgpu_load_quad(mgpu_ctx *c, int nv0, int nv, const int32_t *vtype, int nsq,
   }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  glob_state_free(c);  // a glob tree belongs to the problem it was started on
   quad_state_free(c);
   QuadState *q = new QuadState();
   c->quad = q;
@@ -179,6 +164,19 @@ int mgpu_load_quad(mgpu_ctx *c, int nv0, int nv, const int32_t *vtype, int nsq,
   q->bil_x0.assign(bil_x0, bil_x0 + nbil);
   q->bil_x1.assign(bil_x1, bil_x1 + nbil);
   q->obj_const = obj_const;
+  // the original functions as given (the glob tree's QuadHandler::isFeasible)
+  q->ncon = ncon;
+  q->has_obj = has_obj != 0;
+  q->h_lptr.assign(lptr, lptr + nfun + 1);
+  q->h_qptr.assign(qptr, qptr + nfun + 1);
+  q->h_lvar.assign(lvar, lvar + lptr[nfun]);
+  q->h_lval.assign(lval, lval + lptr[nfun]);
+  q->h_qv1.assign(qv1, qv1 + qptr[nfun]);
+  q->h_qv2.assign(qv2, qv2 + qptr[nfun]);
+  q->h_qval.assign(qval, qval + qptr[nfun]);
+  q->h_clb.assign(clb, clb + ncon);
+  q->h_cub.assign(cub, cub + ncon);
+  q->h_vtype.assign(vtype, vtype + nv);
 
   std::vector<uint8_t> vt(nv);
   for (int j = 0; j < nv; ++j) vt[j] = (uint8_t)vtype[j];

@@ -1,0 +1,47 @@
+"""Batched spatial branch-and-bound over a QCQP's McCormick relaxation (the
+glob path; mgpu_glob_*, minotaur_amd/csrc/glob_runtime.cpp).
+
+The reference's glob solver (src/solvers/Glob.cpp:134-220) runs
+BranchAndBound with NodeIncRelaxer, PCBProcessor, the handlers IntVarHandler
+/ LinearHandler / QuadHandler of SimpleTransformer and (option
+brancher=maxvio) MaxVioBrancher.  Here one round evaluates the top ``batch``
+nodes of an HBM stack at once: K2 (QuadHandler::presolveNode, rows rewritten
+from the parent's), K3R + K3 (each node's LP with its own rows), the decision
+and MaxVio branching, children pushed.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+from .quad import relaxation_lp
+
+
+def setup(ctx, qp):
+    """Load a QuadProblem for the glob tree: the quadratic problem, the LP
+    relaxation at the root box (QuadHandler::relax_'s rows) and the map of
+    the per-node rewritten entries.  Returns (LinProblem, NodeRows)."""
+    ctx.load_quad(qp)
+    rows0 = ctx.quad_rows()
+    p, nr = relaxation_lp(qp, rows0)
+    ctx.load(p)
+    ctx.set_node_rows(nr)
+    return p, nr
+
+
+def solve(ctx, qp, batch=1024, capacity=None, max_rounds=10**9, incumbent=math.inf,
+          loaded=False):
+    """Runs the tree until the stack is empty (or max_rounds): returns
+    (incumbent, x or None, stats, seconds)."""
+    if not loaded:
+        setup(ctx, qp)
+    cap = capacity or 64 * batch
+    t0 = time.perf_counter()
+    ctx.glob_init(cap, incumbent)
+    st = None
+    for _ in range(max_rounds):
+        st = ctx.glob_round(batch)
+        if st.open == 0:
+            break
+    obj, x = ctx.glob_best()
+    return obj, (x if math.isfinite(obj) else None), st, time.perf_counter() - t0

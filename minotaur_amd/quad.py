@@ -175,13 +175,15 @@ def _eval(lin, quad, x):
 
 
 def random_qcqp(seed: int, nv0: int = 12, ncon: int = 8, with_obj: bool = True,
-                aux_bounds: str = 'product'):
+                aux_bounds: str = 'product', squares: bool = True):
     """Seeded synthetic QCQP exercising every branch of QuadHandler's node
     FBBT: univariate terms a x^2 + b x (x also linear), pure squares,
     bilinears, sign-definite and sign-changing boxes, integer and binary
     variables, one- and two-sided rows, equalities, rows without a linear
     part (skipped by tightenQuad_) and purely bilinear rows (type Bilinear,
-    also skipped)."""
+    also skipped).  squares=False turns every square x_a^2 into the product
+    x_a x_(a+1) (same random stream): a bilinear-only QCQP, whose McCormick
+    relaxation needs no cut loop (the glob tree's instances)."""
     rng = np.random.default_rng(seed)
     vtype, vlb, vub = [], [], []
     for j in range(nv0):
@@ -218,7 +220,8 @@ def random_qcqp(seed: int, nv0: int = 12, ncon: int = 8, with_obj: bool = True,
                     b = (a + 1) % nv0
                 quad[(min(a, b), max(a, b))] = coef()
             else:
-                quad[(a, a)] = coef()
+                b2 = a if squares else (a + 1) % nv0
+                quad[(min(a, b2), max(a, b2))] = coef()
                 if rng.random() < 0.6 and style != 8:
                     lin[a] = coef()
         if style != 8:
@@ -241,7 +244,8 @@ def random_qcqp(seed: int, nv0: int = 12, ncon: int = 8, with_obj: bool = True,
         lin, quad = {}, {}
         for _ in range(int(rng.integers(2, 5))):
             a = int(rng.integers(0, nv0))
-            quad[(a, a)] = float(rng.uniform(0.5, 2.0))
+            b2 = a if squares else (a + 1) % nv0
+            quad[(min(a, b2), max(a, b2))] = float(rng.uniform(0.5, 2.0))
             lin[a] = coef()
         for _ in range(int(rng.integers(0, 3))):
             a, b = rng.integers(0, nv0, size=2)

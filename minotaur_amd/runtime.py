@@ -39,7 +39,7 @@ EXPORTS = [
     'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
     'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive', 'mgpu_ws_alloc', 'mgpu_ws_free',
     'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1', 'mgpu_bnb_pick', 'mgpu_bnb_export_dev',
-    'mgpu_bnb_import_dev', 'mgpu_bnb_count',
+    'mgpu_bnb_import_dev', 'mgpu_bnb_count', 'mgpu_glob_init', 'mgpu_glob_round', 'mgpu_glob_best',
 ]
 
 
@@ -52,6 +52,15 @@ class BnbStats(ctypes.Structure):
                 ('pivots', ctypes.c_longlong), ('sb_lps', ctypes.c_longlong),
                 ('sb_pivots', ctypes.c_longlong), ('sb_pruned', ctypes.c_longlong),
                 ('sb_modified', ctypes.c_longlong), ('pfi_pivots', ctypes.c_longlong)]
+
+class GlobStats(ctypes.Structure):
+    """mgpu_glob_stats (include/mgpu.h)."""
+    _fields_ = [('rounds', ctypes.c_longlong), ('nodes', ctypes.c_longlong),
+                ('ndec', ctypes.c_longlong * 6), ('lps', ctypes.c_longlong),
+                ('pivots', ctypes.c_longlong), ('br_int', ctypes.c_longlong),
+                ('br_cont', ctypes.c_longlong), ('open', ctypes.c_int),
+                ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double)]
+
 
 _lib = None
 
@@ -113,6 +122,9 @@ def load_library():
     lib.mgpu_bnb_export_dev.argtypes = [_P, _I, _P, _P]
     lib.mgpu_bnb_import_dev.argtypes = [_P, _I, _P]
     lib.mgpu_bnb_count.argtypes = [_P, _P, _P]
+    lib.mgpu_glob_init.argtypes = [_P, _I, _D]
+    lib.mgpu_glob_round.argtypes = [_P, _I, _D, ctypes.POINTER(GlobStats)]
+    lib.mgpu_glob_best.argtypes = [_P, _P, _P]
     lib.mgpu_bnb_round.argtypes = [_P, _I, _D, ctypes.POINTER(BnbStats)]
     lib.mgpu_bnb_best.argtypes = [_P, _P, _P]
     lib.mgpu_bnb_shard.argtypes = [_P, _I, _I, _P]
@@ -721,6 +733,23 @@ class Context:
         self._chk(self.lib.mgpu_bnb_count(self.h, ctypes.byref(o), ctypes.byref(v)),
                   'mgpu_bnb_count')
         return o.value, v.value
+
+    # -- batched spatial B&B (mgpu_glob_*) ------------------------------------
+    def glob_init(self, capacity, incumbent=math.inf):
+        self._chk(self.lib.mgpu_glob_init(self.h, int(capacity), float(incumbent)),
+                  'mgpu_glob_init')
+
+    def glob_round(self, batch, incumbent=math.inf) -> GlobStats:
+        st = GlobStats()
+        self._chk(self.lib.mgpu_glob_round(self.h, int(batch), float(incumbent),
+                                           ctypes.byref(st)), 'mgpu_glob_round')
+        return st
+
+    def glob_best(self):
+        x = np.empty(self.quad.nv)
+        v = ctypes.c_double(0.0)
+        self._chk(self.lib.mgpu_glob_best(self.h, ctypes.byref(v), _hp(x)), 'mgpu_glob_best')
+        return v.value, x
 
     def bnb_best(self):
         x = np.empty(self.problem.n)

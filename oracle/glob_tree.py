@@ -1,0 +1,249 @@
+"""TEST INFRASTRUCTURE ONLY (imported by tests/ and bench.py's cpu_baseline
+leg, never by the product path): a CPU restatement of one round of the
+batched spatial branch-and-bound (mgpu_glob_round,
+minotaur_amd/csrc/glob_runtime.cpp + glob_tree.hip), built from the C
+restatements of K2 (oracle.quad_fbbt, bit-identical to the reference's
+QuadHandler::presolveNode) and of the per-node-rows LP (oracle.
+dual_simplex_rows, K3R + K3's pivots), plus the decision below in the same
+arithmetic order as the GPU kernel (sequential sums, no fused multiply-add),
+so the two trees agree round for round.
+
+Reference semantics restated (file:line under /root/reference/src/base):
+* PCBProcessor::shouldPrune_ (PCBProcessor.cpp:400-523): engine-status
+  switch, bound test with solAbs_tol / solRel_tol 1e-6;
+* IntVarHandler::isFeasible (IntVarHandler.cpp:54-84), QuadHandler::
+  isFeasible (QuadHandler.cpp:904-953; aTol_ 1e-6, rTol_ 1e-7);
+* candidates: IntVarHandler::getBranchingCandidates (IntVarHandler.cpp:
+  86-110), QuadHandler::getBranchingCandidates (QuadHandler.cpp:473-614;
+  LinBil::isViolated, LinBil.cpp:64-82, aTol 1e-5, rTol 1e-4; isAtBnds_
+  bTol_ 1e-8, :897-902);
+* MaxVioBrancher::findCandidates_ / findBestCandidate_ (MaxVioBrancher.cpp:
+  merge per variable, score 0.1 (0.8 min + 0.2 max), first maximum, up
+  first when dd > ud);
+* children: IntVarHandler::getBranches at floor / ceil, QuadHandler::
+  getBranches at the value (QuadHandler.cpp:422-471).
+Parity with the reference's own glob solver is unpinned (it needs Ipopt /
+filterSQP and its cut loop); the GPU tree is pinned against this
+restatement and its incumbents against the QCQP itself.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+import oracle
+from oracle import WarmStart
+
+BINARY, INTEGER = 0, 1
+
+
+class _GStats:
+    def __init__(self):
+        self.rounds = self.nodes = 0
+        self.ndec = [0] * 6
+        self.lps = self.pivots = 0
+        self.br_int = self.br_cont = 0
+        self.open = self.last_batch = 0
+        self.incumbent = math.inf
+
+
+def _at_bnds(v, l, u):
+    return abs(v - l) < 1e-8 or abs(v - u) < 1e-8
+
+
+def decide(qp, kinf, st, val, x, lb, ub, inc):
+    """One node: (decision, bvar, bval, bup, bint) as glob_decide."""
+    nv = qp.nv
+    if kinf != 0:
+        return (1 if kinf == 1 else 4), -1, 0.0, 0, 0
+    if st in (2, 3, 8, 10, 11):
+        return 1, -1, 0.0, 0, 0
+    if st == 5:
+        return 2, -1, 0.0, 0, 0
+    if st not in (0, 1, 6):
+        return 4, -1, 0.0, 0, 0
+    if val >= inc - 1e-6 or val >= inc - abs(inc) * 1e-6:
+        return 2, -1, 0.0, 0, 0
+    vt = qp.vtype
+    feas = True
+    for j in range(nv):
+        if vt[j] in (BINARY, INTEGER) and abs(x[j] - math.floor(x[j] + 0.5)) > 1e-6:
+            feas = False
+            break
+    nfun = qp.ncon + (1 if qp.has_obj else 0)
+    c = 0
+    while feas and c < nfun:
+        q0, q1 = int(qp.qptr[c]), int(qp.qptr[c + 1])
+        if q0 != q1:
+            act = 0.0
+            for t in range(int(qp.lptr[c]), int(qp.lptr[c + 1])):
+                act += float(qp.lval[t]) * x[qp.lvar[t]]
+            for t in range(q0, q1):
+                act += float(qp.qval[t]) * x[qp.qv1[t]] * x[qp.qv2[t]]
+            if c == qp.ncon:
+                act += float(qp.obj_const)
+                vio = abs(val - act)
+                if vio > abs(act) * 1e-7 and vio > 1e-6:
+                    feas = False
+            else:
+                cub, clb = float(qp.cub[c]), float(qp.clb[c])
+                if act > cub + 1e-6 and (cub == 0.0 or act > cub + abs(cub) * 1e-7):
+                    feas = False
+                if act < clb - 1e-6 and (clb == 0.0 or act < clb - abs(clb) * 1e-7):
+                    feas = False
+        c += 1
+    if feas:
+        return 3, -1, 0.0, 0, 0
+    idd, iud, qd, qu = {}, {}, {}, {}
+    for j in range(nv):
+        v = x[j]
+        if vt[j] in (BINARY, INTEGER) and abs(math.floor(v + 0.5) - v) > 1e-6:
+            idd[j] = v - math.floor(v)
+            iud[j] = math.ceil(v) - v
+
+    def add_q(j, d, u):
+        if j not in qd:
+            qd[j], qu[j] = d, u
+        else:
+            qd[j], qu[j] = d + qd[j], u + qu[j]
+
+    for k in range(qp.nsq):
+        j, y = int(qp.sq_x[k]), int(qp.sq_y[k])
+        x0, yv = x[j], x[y]
+        if yv - x0 * x0 > abs(yv) * 1e-7 and yv - x0 * x0 > 1e-6:
+            dd = (yv - x0 * x0) / math.sqrt(1.0 + (lb[j] + x0) * (lb[j] + x0))
+            ud = (yv - x0 * x0) / math.sqrt(1.0 + (ub[j] + x0) * (ub[j] + x0))
+            add_q(j, dd, ud)
+    for k in range(qp.nbil):
+        j0, j1, y = int(qp.bil_x0[k]), int(qp.bil_x1[k]), int(qp.bil_y[k])
+        v0, v1, yv = x[j0], x[j1], x[y]
+        pr = v1 * v0
+        if not (abs(pr - yv) > 1e-5 and abs(pr - yv) > abs(yv) * 1e-4):
+            continue
+        if not _at_bnds(v0, lb[j0], ub[j0]):
+            if v0 * v1 > yv:
+                dd = (-yv + v0 * v1) / math.sqrt(1.0 + v0 * v0 + ub[j1] * ub[j1])
+                ud = (-yv + v0 * v1) / math.sqrt(1.0 + v0 * v0 + lb[j1] * lb[j1])
+            else:
+                dd = (yv - v0 * v1) / math.sqrt(1.0 + v0 * v0 + lb[j1] * lb[j1])
+                ud = (yv - v0 * v1) / math.sqrt(1.0 + v0 * v0 + ub[j1] * ub[j1])
+            add_q(j0, dd, ud)
+        if not _at_bnds(v1, lb[j1], ub[j1]):
+            if v0 * v1 > yv:
+                dd = (-yv + v1 * v0) / math.sqrt(1.0 + v1 * v1 + ub[j0] * ub[j0])
+                ud = (-yv + v1 * v0) / math.sqrt(1.0 + v1 * v1 + lb[j0] * lb[j0])
+            else:
+                dd = (yv - v1 * v0) / math.sqrt(1.0 + v1 * v1 + lb[j0] * lb[j0])
+                ud = (yv - v1 * v0) / math.sqrt(1.0 + v1 * v1 + ub[j0] * ub[j0])
+            add_q(j1, dd, ud)
+    best, bvar, bup, bint = -math.inf, -1, 0, 0
+    for j in range(nv):
+        hi, hq = j in idd, j in qd
+        if not hi and not hq:
+            continue
+        if hi and hq:
+            isint = 0 if idd[j] + iud[j] <= qd[j] + qu[j] else 1
+            d, u = idd[j] + qd[j], iud[j] + qu[j]
+        elif hi:
+            isint, d, u = 1, idd[j], iud[j]
+        else:
+            isint, d, u = 0, qd[j], qu[j]
+        lo, hv = (d, u) if d < u else (u, d)
+        sc = 0.1 * (0.8 * lo + 0.2 * hv)
+        if sc > best:
+            best, bvar, bint, bup = sc, j, isint, (1 if d > u else 0)
+    if bvar < 0:
+        return 5, -1, 0.0, 0, 0
+    return 0, bvar, float(x[bvar]), bup, bint
+
+
+class CpuGlobContext:
+    """mgpu_glob_init / mgpu_glob_round / mgpu_glob_best on the CPU."""
+
+    def __init__(self, qp):
+        from minotaur_amd.quad import relaxation_lp
+        self.qp = qp
+        self.rows0 = oracle.quad_root_rows(qp)
+        self.p, self.nr = relaxation_lp(qp, self.rows0)
+
+    def glob_init(self, capacity, incumbent=math.inf):
+        qp = self.qp
+        self.cap = capacity
+        st, obj, x, y, it, ws = oracle.dual_simplex_root(self.p)
+        self.ws = WarmStart(ws.head, ws.st, None, None) if st == 0 else None
+        self.pool = [(qp.vlb.astype(np.float64).copy(), qp.vub.astype(np.float64).copy(),
+                      self.rows0.copy(), -math.inf, 0)]
+        self.inc = incumbent
+        self.best_x = np.full(qp.nv, np.nan)
+        self.tot = _GStats()
+        self.tot.incumbent = incumbent
+        self.tot.open = 1
+
+    def glob_round(self, batch, incumbent=math.inf):
+        qp = self.qp
+        if incumbent < self.inc:
+            self.inc = incumbent
+        nb = min(batch, len(self.pool))
+        if len(self.pool) + nb > self.cap:
+            nb = self.cap - len(self.pool)
+        if nb <= 0:
+            if self.pool:
+                raise RuntimeError('glob pool full')
+            self.tot.open = 0
+            return self.tot
+        base = len(self.pool) - nb
+        nodes = self.pool[base:]
+        del self.pool[base:]
+        LB = np.stack([nd[0] for nd in nodes])
+        UB = np.stack([nd[1] for nd in nodes])
+        RW = np.stack([nd[2] for nd in nodes])
+        o = oracle.quad_fbbt(qp, LB, UB, self.inc, 1, RW)
+        st, obj, it, x = oracle.dual_simplex_rows(self.p, o.lb, o.ub, self.nr, o.rows,
+                                                  ws=self.ws, want_x=True)
+        best, bidx = math.inf, -1
+        children = []
+        ndec = [0] * 6
+        for b in range(nb):
+            kinf = int(o.infeas[b])
+            if kinf == 0:
+                self.tot.lps += 1
+                self.tot.pivots += int(it[b])
+            dec, bv, bval, bup, bint = decide(qp, kinf, int(st[b]), float(obj[b]), x[b],
+                                              o.lb[b], o.ub[b], self.inc)
+            ndec[dec] += 1
+            if dec == 3 and obj[b] < best:
+                best, bidx = float(obj[b]), b
+            if dec == 0:
+                if bint:
+                    self.tot.br_int += 1
+                else:
+                    self.tot.br_cont += 1
+                dn = math.floor(bval) if bint else bval
+                up = math.ceil(bval) if bint else bval
+                for c in range(2):
+                    upc = (c == 1) == (bup != 0)
+                    lb, ub = o.lb[b].copy(), o.ub[b].copy()
+                    if upc:
+                        lb[bv] = up
+                    else:
+                        ub[bv] = dn
+                    children.append((lb, ub, o.rows[b].copy(), float(obj[b]),
+                                     nodes[b][4] + 1))
+        self.pool.extend(children)
+        if bidx >= 0 and best < self.inc:
+            self.inc = best
+            self.best_x = x[bidx].copy()
+        self.tot.rounds += 1
+        self.tot.nodes += nb
+        for k in range(6):
+            self.tot.ndec[k] += ndec[k]
+        self.tot.open = len(self.pool)
+        self.tot.last_batch = nb
+        self.tot.incumbent = self.inc
+        if ndec[4]:
+            raise RuntimeError('glob round: engine problem')
+        return self.tot
+
+    def glob_best(self):
+        return self.inc, self.best_x.copy()

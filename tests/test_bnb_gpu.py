@@ -333,7 +333,7 @@ def test_bnb_repeated_migration_near_capacity(ctx):
     ctx.load(p)
     ctx.bnb_config(1, 0)
     ctx.bnb_brancher(0)
-    cap = 256
+    cap = 2048        # 200 cycles x 64 rows would need 12 800 slots if imports grew the pool
     ctx.bnb_init(cap)
     st = None
     for _ in range(6):

@@ -1,0 +1,66 @@
+"""GPU: the batched spatial branch-and-bound (mgpu_glob_*: K2 from the
+parents' rows, K3R + K3 on each node's own rows, the glob decision and MaxVio
+branching over IntVarHandler and QuadHandler candidates, children on an HBM
+stack) equals its CPU restatement (oracle/glob_tree.py: the C restatements of
+K2 and of the per-node-rows LP, the same decision arithmetic) round for
+round -- nodes, decisions, branchings, LP solves and pivots, open nodes --
+and ends on the same incumbent bits and point."""
+import math
+
+import numpy as np
+import pytest
+
+from minotaur_amd import glob as mglob
+from minotaur_amd.quad import random_qcqp
+
+pytestmark = pytest.mark.gpu
+
+CASES = [(0, 5, 3), (1, 8, 5), (2, 6, 4), (2, 8, 5), (3, 8, 5), (4, 6, 4), (5, 8, 5),
+         (0, 8, 5)]
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from minotaur_amd.runtime import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize('batch', [1, 16, 256])
+@pytest.mark.parametrize('seed,nv0,ncon', CASES)
+def test_glob_tree_matches_cpu_restatement(ctx, seed, nv0, ncon, batch):
+    from glob_tree import CpuGlobContext
+    qp = random_qcqp(seed, nv0=nv0, ncon=ncon, squares=False)
+    mglob.setup(ctx, qp)
+    cpu = CpuGlobContext(qp)
+    ctx.glob_init(1 << 15)
+    cpu.glob_init(1 << 15)
+    for _ in range(60 if batch == 1 else 25):
+        sg, sc = ctx.glob_round(batch), cpu.glob_round(batch)
+        assert (sg.rounds, sg.nodes, list(sg.ndec), sg.br_int, sg.br_cont, sg.lps, sg.pivots,
+                sg.open) == (sc.rounds, sc.nodes, list(sc.ndec), sc.br_int, sc.br_cont,
+                             sc.lps, sc.pivots, sc.open)
+        assert sg.incumbent == sc.incumbent or (math.isinf(sg.incumbent) and
+                                                math.isinf(sc.incumbent))
+        if sg.open == 0:
+            break
+    og, xg = ctx.glob_best()
+    oc, xc = cpu.glob_best()
+    assert og == oc or (math.isinf(og) and math.isinf(oc))
+    if math.isfinite(og):
+        assert np.array_equal(xg, xc)
+
+
+def test_glob_tree_closes(ctx):
+    """A complete tree at batch 1024: every node decided, the stack empties,
+    the incumbent is feasible for the QCQP's original constraints."""
+    qp = random_qcqp(0, nv0=8, ncon=5, squares=False)
+    obj, x, st, secs = mglob.solve(ctx, qp, batch=1024, capacity=1 << 18)
+    assert st.open == 0 and st.nodes == sum(st.ndec) and st.ndec[4] == 0
+    assert math.isfinite(obj)
+    for c in range(qp.ncon):
+        act = sum(qp.lval[t] * x[qp.lvar[t]] for t in range(qp.lptr[c], qp.lptr[c + 1]))
+        act += sum(qp.qval[t] * x[qp.qv1[t]] * x[qp.qv2[t]]
+                   for t in range(qp.qptr[c], qp.qptr[c + 1]))
+        assert qp.clb[c] - 1e-5 <= act <= qp.cub[c] + 1e-5
