@@ -30,13 +30,9 @@
 namespace mgpu {
 namespace {
 
-// write-out order of the global variant (A/B switch for tools: build with
-// -DMGPU_FBBT_OUT_NODE_OUTER for the node-outer order)
-#ifdef MGPU_FBBT_OUT_NODE_OUTER
-constexpr bool kFbbtOutVarOuter = false;
-#else
+// write-out order of the global variant: var-outer (each store one
+// coalesced 512-B row; the node-outer order measured the same)
 constexpr bool kFbbtOutVarOuter = true;
-#endif
 
 // ---- wave-uniform broadcast ------------------------------------------------
 __device__ __forceinline__ int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
@@ -868,15 +864,8 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
 // lanes of the nodes that finished early.
 // kWG waves per workgroup share one LDS copy of the records (each wave has
 // its own scratch slot and node queue position; no barrier after staging).
-// (diagnostic builds: -DMGPU_FBBT_WPE=k asks the compiler for k waves per
-// SIMD, i.e. at most 512/k VGPRs)
-#ifdef MGPU_FBBT_WPE
-#define MGPU_K1P_ATTR __attribute__((amdgpu_waves_per_eu(MGPU_FBBT_WPE)))
-#else
-#define MGPU_K1P_ATTR
-#endif
 template <int kWG>
-__global__ MGPU_K1P_ATTR __launch_bounds__(kLanes * kWG) void fbbt_linear_persist(DevLP lp,
+__global__ __launch_bounds__(kLanes * kWG) void fbbt_linear_persist(DevLP lp,
                                                                                    FbbtIO io) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x & (kLanes - 1);
