@@ -381,34 +381,25 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     int h = lane < m ? s_whead[lane] : -1;
     if (kpath > 0) {
       // each pivot's eta exactly as the solve that made it built it: FTRAN
-      // of its entering column through B0^{-1} and the etas before it.  All
-      // columns B0^{-1} a_q are gathered first (independent LDS walks), then
-      // eliminated in path order: column t sees E_0 .. E_{t-1} in that order
-      // (apply_etas' operations), the columns after s take E_s together.
+      // of its entering column through B0^{-1} and the etas before it
+      // (apply_etas' operations in path order), one pivot after the other.
+      // A runtime loop with ONE inlined eta pass: the fully unrolled K x K
+      // elimination it replaces was most of the kernel's 159 KB of code.
+#pragma unroll 1
+      for (int s = 0; s < kpath; ++s) {
+        const uint32_t pv = ppath[s];
+        const int q = (int)(pv & 0xFFFFu), r = (int)(pv >> 16);
+        const double v = apply_etas(ftran_b0(P, q, lane), eta, prow, s, lane);
+        const double inv = 1.0 / rld(v, r);
+        const double e = lane == r ? inv : -v * inv;
 #pragma unroll
-      for (int t = 0; t < K; ++t)
-        if (t < kpath) eta[t] = ftran_b0(P, (int)(ppath[t] & 0xFFFFu), lane);
-#pragma unroll
-      for (int s = 0; s < K; ++s) {
-        if (s < kpath) {
-          const uint32_t pv = ppath[s];
-          const int q = (int)(pv & 0xFFFFu), r = (int)(pv >> 16);
-          const double inv = 1.0 / rld(eta[s], r);
-          eta[s] = lane == r ? inv : -eta[s] * inv;
-          if (lane == s) {
-            prow = r;
-            pq = q;
-          }
-          if (lane == r) h = q;
-#pragma unroll
-          for (int t = s + 1; t < K; ++t) {
-            if (t < kpath) {
-              const double vp = rld(eta[t], r);
-              const double nv = lane == r ? eta[s] * vp : eta[t] + eta[s] * vp;
-              eta[t] = vp != 0.0 ? nv : eta[t];
-            }
-          }
+        for (int t = 0; t < K; ++t)
+          if (t == s) eta[t] = e;
+        if (lane == s) {
+          prow = r;
+          pq = q;
         }
+        if (lane == r) h = q;
       }
       ne = kpath;
     }
@@ -573,11 +564,19 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     };
 
     PSTAMP(0);
-    double zB = primals();
-    PSTAMP(1);
+    // primal values are recomputed at ONE place (the top of the loop) so the
+    // eta pass inside primals() is inlined once
+    double zB = 0.0;
+    bool need = true;   // recompute before pricing
     int status = kUnknownStatus;
     bool fresh = true;
     for (;;) {
+      if (need) {
+        zB = primals();
+        PSTAMP(1);
+        fresh = true;
+        need = false;
+      }
       // ---- pricing: most infeasible basic row, lowest row on ties ----
       double inf = 0.0;
       if (lane < m) {
@@ -590,9 +589,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       PSTAMP(2);
       if (best == 0.0) {
         if (!fresh) {
-          zB = primals();
-          PSTAMP(1);
-          fresh = true;
+          need = true;
           continue;
         }
         bool g = false;
@@ -613,9 +610,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         }
         art_bound *= 1e3;
         grow(art_bound);
-        zB = primals();
-        PSTAMP(1);
-        fresh = true;
+        need = true;
         continue;
       }
       if (iters >= io.iter_limit) {
@@ -677,9 +672,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         }
         art_bound *= 1e3;
         grow(art_bound);
-        zB = primals();
-        PSTAMP(1);
-        fresh = true;
+        need = true;
         continue;
       }
       // ---- Harris pass 2: largest |alpha| among ratios <= tmax; the owner

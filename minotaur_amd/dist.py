@@ -105,6 +105,11 @@ class Comm:
     def __init__(self, rank, world, device=None):
         self.rank, self.world = rank, world
         self.device = device if device is not None else torch.device('cpu')
+        # gloo moves host tensors only (the N>1 rehearsal on one GPU box):
+        # device tensors are staged through the host there; RCCL takes them
+        # as they are
+        if active() and dist.get_backend() == 'gloo':
+            self.device = torch.device('cpu')
 
     def round_reduce(self, inc, n_open, err=0):
         t = torch.tensor([float(inc), -float(n_open), float(n_open), -float(err)],
