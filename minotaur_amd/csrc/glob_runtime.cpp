@@ -12,7 +12,8 @@
 //        relaxation: NodeIncRelaxer keeps the parent's rows, :94-175);
 //   K3R + K3   the node's own LP with those rows (OsiLPEngine::
 //        changeConstraint then solve, OsiLPEngine.cpp:206-243, 571-652),
-//        warm-started from the root basis refactored for the node's matrix;
+//        warm-started from the root basis refactored for the node's matrix
+//        (m > 64: K3L with the rows in HBM and the refactorisation inside);
 //   decide     shouldPrune_, IntVarHandler + QuadHandler isFeasible, and
 //        MaxVioBrancher over both handlers' candidates (glob_tree.hip),
 //        spatial branching at the LP value on a continuous variable;
@@ -89,9 +90,6 @@ int mgpu_glob_init(mgpu_ctx *c, int capacity, double incumbent) {
     return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: LP columns (%d) / row-record stride (%d) do "
                 "not match the quadratic problem (%d vars, %d row values)", c->lp.n,
                 c->nr_stride, q.nv, q.R);
-  if (c->lp.m > kLpMaxM)
-    return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: node rows need m <= %d (m = %d)", kLpMaxM,
-                c->lp.m);
   if (capacity < 1) return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: capacity < 1");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));

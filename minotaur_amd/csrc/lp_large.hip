@@ -218,6 +218,79 @@ __device__ __forceinline__ void compute_primals(const S<kT> &s) {
   __syncthreads();
 }
 
+// Per-node refactorisation of a warm basis for the node's own matrix (the
+// glob path with m > 64; K3R's job for m <= 64): oracle/lp_dual.c
+// invert_basis -- Gauss-Jordan on [B | I] with partial pivoting (first row
+// of largest |pivot| at or below the diagonal; |pivot| < 1e-12 = singular),
+// the same element operations -- with B in this workgroup's HBM slot and I
+// becoming B^-1 in the inverse slot, both column-major (thread r owns rows
+// r, r + kT, ...).  Returns false when singular (the caller takes the slack
+// basis, as the oracle does).
+template <int kT>
+__device__ bool refactor_basis(S<kT> &s, double *Bm) {
+  const int n = s.n, m = s.m, tid = threadIdx.x;
+  const size_t mm = (size_t)m * m;
+  for (size_t e = tid; e < mm; e += kT) {
+    Bm[e] = 0.0;
+    s.Bi[e] = (e / m) == (e % m) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int i = tid; i < m; i += kT) {   // column i of B = the column of head[i]
+    const int h = s.head[i];
+    if (h >= n) {
+      Bm[(size_t)i * m + (h - n)] = -1.0;
+    } else {
+      for (int t = s.colptr[h]; t < s.colptr[h + 1]; ++t)
+        Bm[(size_t)i * m + s.rowidx[t]] = s.cval[t];
+    }
+  }
+  __syncthreads();
+  for (int c = 0; c < m; ++c) {
+    double bv = -1.0;
+    int br = INT_MAX;
+    for (int r = c + tid; r < m; r += kT) {
+      const double a = fabs(Bm[(size_t)c * m + r]);
+      if (a > bv) {
+        bv = a;
+        br = r;
+      }
+    }
+    blk_argmax(bv, br, s);
+    if (!(bv >= 1e-12)) return false;
+    if (br != c) {
+      for (int k = tid; k < m; k += kT) {
+        const size_t o = (size_t)k * m;
+        double t = Bm[o + c];
+        Bm[o + c] = Bm[o + br];
+        Bm[o + br] = t;
+        t = s.Bi[o + c];
+        s.Bi[o + c] = s.Bi[o + br];
+        s.Bi[o + br] = t;
+      }
+      __syncthreads();
+    }
+    const double inv = 1.0 / Bm[(size_t)c * m + c];
+    __syncthreads();
+    for (int k = tid; k < m; k += kT) {
+      Bm[(size_t)k * m + c] *= inv;
+      s.Bi[(size_t)k * m + c] *= inv;
+    }
+    __syncthreads();
+    for (int r = tid; r < m; r += kT) {
+      if (r == c) continue;
+      const double f = Bm[(size_t)c * m + r];
+      if (f == 0.0) continue;
+      for (int k = 0; k < m; ++k) {
+        const size_t o = (size_t)k * m;
+        Bm[o + r] -= f * Bm[o + c];
+        s.Bi[o + r] -= f * s.Bi[o + c];
+      }
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
 template <int kT>
 __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double *binv_slots) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -284,6 +357,41 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
       }
       continue;
     }
+    const bool nrows = io.nr.vals != nullptr;
+    double *wg = nrows ? io.nr.wg + (size_t)blockIdx.x * io.nr.wg_stride : nullptr;
+    if (nrows) {
+      // the node's matrix and row bounds (K3's per-node rows): the loaded
+      // values, then its own entries (OsiLPEngine::changeConstraint of the
+      // rewritten rows), in this workgroup's HBM slot
+      const int nnz = lp.nnz;
+      double *wc = wg, *wr = wc + nnz, *wlo = wr + nnz, *whi = wlo + m;
+      for (int t = tid; t < nnz; t += kT) {
+        wc[t] = lp.cval[t];
+        wr[t] = lp.rval[t];
+      }
+      for (int i = tid; i < m; i += kT) {
+        wlo[i] = lp.rlo[i];
+        whi[i] = lp.rhi[i];
+      }
+      __syncthreads();
+      const double *rec = io.nr.vals + (size_t)b * io.nr.stride;
+      for (int q = tid; q < io.nr.ncoef; q += kT) {
+        double v = rec[io.nr.coef_src[q]];
+        if (fabs(v) <= kLfTol) v = 0.0;
+        wc[io.nr.csc_pos[q]] = v;
+        wr[io.nr.csr_pos[q]] = v;
+      }
+      for (int q = tid; q < io.nr.nrow; q += kT) {
+        const int r = io.nr.row[q];
+        if (io.nr.lo_src[q] >= 0) wlo[r] = rec[io.nr.lo_src[q]];
+        if (io.nr.hi_src[q] >= 0) whi[r] = rec[io.nr.hi_src[q]];
+      }
+      __syncthreads();
+      s.cval = wc;
+      s.rval = wr;
+      s.rlo = wlo;
+      s.rhi = whi;
+    }
     // ---- working bounds; an empty box is infeasible before any pivot ----
     bool bad = false;
     for (int j = tid; j < N; j += kT) {
@@ -302,22 +410,28 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
     }
 
     // ---- basis: warm start or slack basis (B = -I) ----
-    const bool warm = io.ws.head != nullptr;
+    bool warm = io.ws.head != nullptr;
+    const size_t bw = io.ws_index != nullptr ? (size_t)io.ws_index[b]
+                      : io.list_ws ? (size_t)bi : (size_t)b;
     if (warm) {
-      const size_t bw = io.ws_index != nullptr ? (size_t)io.ws_index[b]
-                        : io.list_ws ? (size_t)bi : (size_t)b;
       const int32_t *wh = io.ws.head + bw * io.ws.s_head;
       const int8_t *wst = io.ws.st + bw * io.ws.s_st;
-      const double *wb = io.ws.binv + bw * io.ws.s_binv;
       for (int j = tid; j < N; j += kT) {
         const int8_t v = wst[j];
         s.st[j] = v == ST_BASIC ? ST_LB : v;
       }
       for (int i = tid; i < m; i += kT) s.head[i] = wh[i];
-      for (size_t e = tid; e < mm; e += kT) s.Bi[e] = wb[e];  // column-major both
+      if (io.ws.binv != nullptr) {
+        const double *wb = io.ws.binv + bw * io.ws.s_binv;
+        for (size_t e = tid; e < mm; e += kT) s.Bi[e] = wb[e];  // column-major both
+      }
       __syncthreads();
       for (int i = tid; i < m; i += kT) s.st[s.head[i]] = ST_BASIC;
       __syncthreads();
+      if (io.ws.binv == nullptr && nrows)
+        warm = refactor_basis(s, wg + 2 * (size_t)lp.nnz + 2 * (size_t)m);
+    }
+    if (warm) {
       if (s.ocol < 0 && io.ws.d != nullptr) {
         const double *wd = io.ws.d + bw * io.ws.s_d;
         for (int j = tid; j < N; j += kT) s.d[j] = s.st[j] == ST_BASIC ? 0.0 : wd[j];

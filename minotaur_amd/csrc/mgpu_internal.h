@@ -95,6 +95,11 @@ struct NodeRowsIO {
   const int32_t *row;           // [nrow] row index
   const int32_t *lo_src;        // [nrow] offset of the row's lower bound, -1 = loaded
   const int32_t *hi_src;        // [nrow] offset of the row's upper bound, -1 = loaded
+  // K3L (m > 64): per-workgroup scratch in HBM for the node's matrix values
+  // and row bounds and, for a warm start given without an inverse, the
+  // basis matrix of the in-kernel refactorisation: wg + blockIdx.x * wg_stride
+  double *wg;
+  long wg_stride;               // doubles per workgroup: 2 nnz + 2 m + m m
 };
 // LinearFunction::addTerm keeps only |a| > 1e-9 (LinearFunction.cpp:22,
 // 89-95): a smaller node coefficient is the term's absence, i.e. 0.

@@ -102,10 +102,15 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
   if (ws_head && !ws_st)
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: warm start needs head and st");
   const int n = c->lp.n, m = c->lp.m, N = n + m, nnz = c->lp.nnz;
-  if (m > kLpMaxM || m == 0 || lp_lds_bytes_rows(n, m, nnz) > 160 * 1024 ||
-      lp_refactor_lds_bytes(n, m, nnz) > 160 * 1024)
-    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: needs 0 < m <= %d and the node matrix "
-                "in LDS (m=%d, nnz=%d)", kLpMaxM, m, nnz);
+  if (m == 0) return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: m = 0");
+  // K3R + K3 while the node matrix and the refactorisation fit one wave's
+  // LDS (m <= 64); beyond, K3L with the node rows in a per-workgroup HBM
+  // slot and the warm basis refactored inside the kernel
+  const bool large = m > kLpMaxM || lp_lds_bytes_rows(n, m, nnz) > 160 * 1024 ||
+                     lp_refactor_lds_bytes(n, m, nnz) > 160 * 1024;
+  if (large && lp_large_lds_bytes(n, m) > (size_t)kLargeLdsMax)
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: n+m=%d too large for K3L's LDS state",
+                N);
   if (batch == 0) return MGPU_OK;
   HIPCHK(c, hipSetDevice(c->device));
   const MapView mv = map_view(c);
@@ -134,6 +139,28 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
   io.iters = iters;
   io.x = x;
   HIPCHK(c, hipEventRecord(c->ev9, c->stream));
+  if (large) {
+    const int grid = lp_large_grid(batch, n, m, c->num_cus);
+    const long wgs = 2L * nnz + 2L * m + (long)m * m;
+    HIPCHK(c, c->lp_slots.ensure((size_t)grid * m * m * sizeof(double) + 8));
+    HIPCHK(c, c->nr_ws.ensure((size_t)grid * wgs * sizeof(double) + 8));
+    io.nr.wg = c->nr_ws.as<double>();
+    io.nr.wg_stride = wgs;
+    if (ws_head)  // head + statuses only: K3L refactors them for each node's matrix
+      io.ws = LpWarm{ws_head, ws_st, nullptr, nullptr, ws_shared ? 0 : m, ws_shared ? 0 : N,
+                     0, 0};
+    HIPCHK(c, hipEventRecord(c->ev10, c->stream));
+    c->last_lp_pfi = false;
+    HIPCHK(c, c->lp_next.ensure(sizeof(int32_t)));
+    HIPCHK(c, hipMemsetAsync(c->lp_next.p, 0, sizeof(int32_t), c->stream));
+    io.next = c->lp_next.as<int32_t>();
+    HIPCHK(c, lp_large_prepare());
+    (void)hipGetLastError();
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    HIPCHK(c, launch_lp_large(c->lp, io, c->lp_slots.as<double>(), grid, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+    return MGPU_OK;
+  }
   if (ws_head) {
     // K3R: every node's warm start for its own matrix
     const size_t B = (size_t)batch;

@@ -52,6 +52,28 @@ def test_glob_tree_matches_cpu_restatement(ctx, seed, nv0, ncon, batch):
         assert np.array_equal(xg, xc)
 
 
+@pytest.mark.parametrize('seed,nv0,ncon', [(2, 16, 10), (0, 16, 10)])
+def test_glob_tree_beyond_64_rows_matches_cpu(ctx, seed, nv0, ncon):
+    """A relaxation past one wave of rows (m 78..90): the node LPs run on K3L
+    with their rows in HBM and the root basis refactored inside the kernel;
+    the tree still equals the CPU restatement round for round."""
+    from glob_tree import CpuGlobContext
+    qp = random_qcqp(seed, nv0=nv0, ncon=ncon, squares=False)
+    p, nr = mglob.setup(ctx, qp)
+    assert p.m > 64
+    cpu = CpuGlobContext(qp)
+    ctx.glob_init(1 << 14)
+    cpu.glob_init(1 << 14)
+    for _ in range(8):
+        sg, sc = ctx.glob_round(64), cpu.glob_round(64)
+        assert (sg.nodes, list(sg.ndec), sg.br_int, sg.br_cont, sg.lps, sg.pivots, sg.open) == \
+            (sc.nodes, list(sc.ndec), sc.br_int, sc.br_cont, sc.lps, sc.pivots, sc.open)
+        assert sg.incumbent == sc.incumbent or (math.isinf(sg.incumbent) and
+                                                math.isinf(sc.incumbent))
+        if sg.open == 0:
+            break
+
+
 def test_glob_tree_closes(ctx):
     """A complete tree at batch 1024: every node decided, the stack empties,
     the incumbent is feasible for the QCQP's original constraints."""

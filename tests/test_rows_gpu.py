@@ -212,3 +212,35 @@ def test_lp_refactor_single_basis(ctx):
     h2[1] = h2[0]
     w2, sing2 = ctx.lp_refactor(h2, ws.st)
     assert sing2 == 1 and np.array_equal(w2.head, np.arange(q.n, q.n + q.m))
+
+
+@pytest.mark.parametrize('seed,nv0,ncon', [(1, 16, 10), (0, 18, 12), (1, 20, 14)])
+@pytest.mark.parametrize('warm', [True, False])
+def test_rows_lp_beyond_64_rows(ctx, seed, nv0, ncon, warm):
+    """Per-node rows past one wave of rows (m = 76..104): K3L takes the
+    node's matrix into its HBM slot and, for a warm basis given as head +
+    statuses, refactors it in the kernel (the oracle's invert_basis, then
+    compute_duals).  Statuses and pivots equal the oracle's node-rows mode,
+    objectives within 1e-9, HiGHS within 1e-6."""
+    from minotaur_amd.runtime import WarmStart
+    qp, rows0, p, nr, ws = _setup(ctx, seed, nv0=nv0, ncon=ncon)
+    assert p.m > 64
+    LB, UB = random_quad_boxes(qp, 300, 700 + seed)
+    q = ctx.quad_fbbt(LB, UB, rows0, qt=1)
+    w = WarmStart(ws.head, ws.st, None, None) if warm else None
+    r = ctx.lp_solve_rows(q.lb, q.ub, q.rows, ws=w, skip=q.infeasible, want_x=True)
+    so, oo, io, xo = oracle.dual_simplex_rows(p, q.lb, q.ub, nr, q.rows, ws=w, nthreads=8,
+                                              want_x=True)
+    live = q.infeasible == 0
+    assert live.sum() > 30
+    assert np.all(r.status[~live] == 12)
+    assert np.array_equal(r.status[live], so[live])
+    assert np.array_equal(r.iters[live], io[live])
+    opt = live & (so == 0)
+    assert np.allclose(r.obj[opt], oo[opt], rtol=1e-9, atol=1e-9)
+    assert np.allclose(r.x[opt], xo[opt], rtol=1e-9, atol=1e-8)
+    for b in np.nonzero(live)[0][::7]:
+        hs, hv = oracle.highs(nr.node_problem(p, q.rows[b]), q.lb[b], q.ub[b])
+        assert hs == r.status[b], b
+        if hs == 0:
+            assert _close(r.obj[b], hv, 1e-6), (b, r.obj[b], hv)
