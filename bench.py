@@ -512,14 +512,16 @@ def glob_tree(ctx, dev, rank, world, args, B=8192, max_rounds=400):
     -- every round pops B nodes, runs K2 from the parents' rows, K3R + K3 on
     each node's own rows, the glob decision with MaxVio branching over the
     IntVarHandler and QuadHandler candidates and pushes the children -- to
-    completion (or max_rounds).  Rank r runs seed s + r (weak scaling).
+    completion (or max_rounds).  Rank r runs seed s + r (weak scaling).  The
+    last instance's relaxation has 90 rows: its node LPs run on K3L with the
+    rows in HBM and the root basis refactored inside the kernel.
     A one-core CPU baseline runs the restatement (oracle/glob_tree.py) on
     the same instance for a bounded time."""
     import torch
     from minotaur_amd import glob as mglob
     from minotaur_amd.quad import random_qcqp
     out = []
-    for seed, nv0, ncon in ((17, 10, 6), (9, 12, 7), (19, 12, 7)):
+    for seed, nv0, ncon in ((17, 10, 6), (9, 12, 7), (19, 12, 7), (2, 16, 10)):
         qp = random_qcqp(seed + rank, nv0=nv0, ncon=ncon, squares=False)
         p, nr = mglob.setup(ctx, qp)
         mglob.solve(ctx, qp, batch=64, capacity=1 << 14, max_rounds=2, loaded=True)  # warm-up
