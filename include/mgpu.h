@@ -206,19 +206,23 @@ int mgpu_lp_solve_path_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const d
  * the basis is refactored for each node's matrix on the device (K3R: the
  * oracle's Gauss-Jordan with partial pivoting; singular -> slack basis) and
  * its reduced costs recomputed, then the dense dual simplex K3 runs from it
- * (m <= 64).  Outputs as mgpu_lp_solve. */
+ * (m <= 64).  Outputs as mgpu_lp_solve.  ws_binv (optional, shared warm start,
+ * m <= 64): B^-1 of the warm basis for the LOADED matrix, [m][m]
+ * column-major; K3R then replaces only the basic columns a node's rows
+ * changed (one product-form update each) instead of refactoring from
+ * scratch.  Beyond 64 rows K3L refactors inside the kernel (ws_binv unused). */
 int mgpu_set_node_rows(mgpu_ctx *ctx, int stride, int ncoef, const int32_t *coef_pos,
                        const int32_t *coef_src, int nrow, const int32_t *row_idx,
                        const int32_t *lo_src, const int32_t *hi_src);
 int mgpu_lp_solve_rows(mgpu_ctx *ctx, int batch, const double *lb, const double *ub,
                        const int32_t *skip, const double *vals, const int32_t *ws_head,
                        const int8_t *ws_st, int ws_shared, int iter_limit, int32_t *status,
-                       double *obj, int32_t *iters, double *x);
+                       double *obj, int32_t *iters, double *x, const double *ws_binv);
 int mgpu_lp_solve_rows_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double *d_ub,
                            const int32_t *d_skip, const double *d_vals,
                            const int32_t *d_ws_head, const int8_t *d_ws_st, int ws_shared,
                            int iter_limit, int32_t *d_status, double *d_obj, int32_t *d_iters,
-                           double *d_x);
+                           double *d_x, const double *d_ws_binv);
 
 /* The warm basis refactored for the LOADED matrix (host pointers, one
  * basis): what Clp does with the kept basis after OsiLPEngine::

@@ -74,9 +74,49 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
     const int8_t s = wst[j];
     st[j] = s == ST_BASIC ? ST_LB : s;
   }
-  for (int t = lane; t < m * ld; t += 64) Ls[t] = 0.0;
   wave_sync();
   for (int i = lane; i < m; i += 64) st[hd[i]] = ST_BASIC;
+  const bool row = lane < m;
+  const size_t mm = (size_t)m * m;
+  bool done = false;
+  if (io.binv0 != nullptr) {
+    // column replacement from the root inverse (oracle colrep_refactor):
+    // only the basic structural columns whose entries this node rewrote
+    // differ from the root basis; each takes its node column by one
+    // product-form update of B^-1, held row-major in Ls (stride ld)
+    for (size_t t = lane; t < mm; t += 64) Ls[(t % m) * ld + t / m] = io.binv0[t];
+    wave_sync();
+    done = true;
+    for (int i = 0; i < m; ++i) {
+      const int h = hd[i];
+      if (h >= n) continue;
+      bool ch = false;
+      for (int t = lp.colptr[h] + lane; t < lp.colptr[h + 1]; t += 64) ch |= wc[t] != lp.cval[t];
+      if (!__any(ch)) continue;
+      double al = 0.0;
+      if (row)
+        for (int t = lp.colptr[h]; t < lp.colptr[h + 1]; ++t)
+          al += Ls[(size_t)lane * ld + lp.rowidx[t]] * wc[t];
+      const double piv = rld(al, i);
+      if (fabs(piv) < kSingTol) {
+        done = false;  // refactor from scratch below
+        break;
+      }
+      const double inv = 1.0 / piv;
+      for (int k = lane; k < m; k += 64) Ls[(size_t)i * ld + k] *= inv;
+      wave_sync();
+      if (row && lane != i && al != 0.0)
+        for (int k = 0; k < m; ++k) Ls[(size_t)lane * ld + k] -= al * Ls[(size_t)i * ld + k];
+      wave_sync();
+    }
+  }
+  int32_t *oh = io.o_head + (size_t)b * m;
+  int8_t *ost = io.o_st + (size_t)b * N;
+  double *od = io.o_d + (size_t)b * N;
+  double *ob = io.o_binv + mm * b;
+  if (!done) {
+  for (int t = lane; t < m * ld; t += 64) Ls[t] = 0.0;
+  wave_sync();
   // dense basis matrix: column i of B = column head[i] of [A | -I]
   for (int i = lane; i < m; i += 64) {
     const int h = hd[i];
@@ -88,7 +128,6 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
   }
   wave_sync();
 
-  const bool row = lane < m;
   constexpr int kC = 8;          // register chunk of the skipped updates
   constexpr int NQ = M / kC;
   static_assert(M % kC == 0, "register rows are whole chunks");
@@ -170,11 +209,6 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
     wave_sync();  // prow is rewritten by the next step
   }
 
-  const size_t mm = (size_t)m * m;
-  int32_t *oh = io.o_head + (size_t)b * m;
-  int8_t *ost = io.o_st + (size_t)b * N;
-  double *od = io.o_d + (size_t)b * N;
-  double *ob = io.o_binv + mm * b;
   if (io.o_sing != nullptr && lane == 0) io.o_sing[b] = sing ? 1 : 0;
   if (sing) {
     // oracle: the warm start is dropped for the slack basis (B^-1 = -I,
@@ -196,6 +230,9 @@ __global__ __launch_bounds__(64) void lp_refactor_kernel(DevLP lp, RefacIO io) {
       if (k < m) Ls[(size_t)lpos * ld + pord[k]] = Iv[k];
   }
   wave_sync();
+  } else if (io.o_sing != nullptr && lane == 0) {
+    io.o_sing[b] = 0;
+  }
   // column-major B^-1: column k is one coalesced store over the lanes
   for (int k = 0; k < m; ++k)
     for (int i = lane; i < m; i += 64) ob[(size_t)k * m + i] = Ls[(size_t)i * ld + k];

@@ -245,6 +245,10 @@ struct RefacIO {
   double *o_d;                  // [B][n+m]
   double *o_binv;               // [B][m][m] column-major
   int32_t *o_sing;              // [B] 1: singular, slack basis (or null)
+  // the warm basis' inverse for the LOADED matrix ([m][m] column-major,
+  // shared) or null: with it, a node's basis is refactored by replacing only
+  // the basic columns its rows changed (Gauss-Jordan when a pivot is tiny)
+  const double *binv0;
 };
 size_t lp_refactor_lds_bytes(int n, int m, int nnz);
 hipError_t launch_lp_refactor(const DevLP &lp, const RefacIO &io, hipStream_t stream);

@@ -93,7 +93,7 @@ int mgpu_set_node_rows(mgpu_ctx *c, int stride, int ncoef, const int32_t *coef_p
 int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub,
                            const int32_t *skip, const double *vals, const int32_t *ws_head,
                            const int8_t *ws_st, int ws_shared, int iter_limit, int32_t *status,
-                           double *obj, int32_t *iters, double *x) {
+                           double *obj, int32_t *iters, double *x, const double *ws_binv) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_rows: no problem loaded");
   if (!c->nr_set) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_rows: no node rows set");
@@ -101,6 +101,8 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: bad argument");
   if (ws_head && !ws_st)
     return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: warm start needs head and st");
+  if (ws_binv && (!ws_head || !ws_shared))
+    return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: ws_binv needs a shared warm start");
   const int n = c->lp.n, m = c->lp.m, N = n + m, nnz = c->lp.nnz;
   if (m == 0) return fail(c, MGPU_ERR_ARG, "mgpu_lp_solve_rows: m = 0");
   // K3R + K3 while the node matrix and the refactorisation fit one wave's
@@ -180,6 +182,7 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
     rf.o_st = (int8_t *)(w + s_head);
     rf.o_d = (double *)(w + s_head + s_st);
     rf.o_binv = (double *)(w + s_head + s_st + s_d);
+    rf.binv0 = ws_binv;
     HIPCHK(c, launch_lp_refactor(c->lp, rf, c->stream));
     io.ws = LpWarm{rf.o_head, rf.o_st, rf.o_d, rf.o_binv, m, N, N, (long)m * m};
   }
@@ -197,7 +200,7 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
 int mgpu_lp_solve_rows(mgpu_ctx *c, int batch, const double *lb, const double *ub,
                        const int32_t *skip, const double *vals, const int32_t *ws_head,
                        const int8_t *ws_st, int ws_shared, int iter_limit, int32_t *status,
-                       double *obj, int32_t *iters, double *x) {
+                       double *obj, int32_t *iters, double *x, const double *ws_binv) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_rows: no problem loaded");
   if (!c->nr_set) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_rows: no node rows set");
@@ -223,6 +226,7 @@ int mgpu_lp_solve_rows(mgpu_ctx *c, int batch, const double *lb, const double *u
     HIPCHK(c, h2d(c->lp_wh, ws_head, wsB * m * 4));
     HIPCHK(c, h2d(c->lp_wst, ws_st, wsB * N));
   }
+  if (ws_binv) HIPCHK(c, h2d(c->lp_wb, ws_binv, (size_t)m * m * 8));
   HIPCHK(c, c->lp_st.ensure(B * 4));
   HIPCHK(c, c->lp_obj.ensure(B * 8));
   HIPCHK(c, c->lp_it.ensure(B * 4));
@@ -232,7 +236,8 @@ int mgpu_lp_solve_rows(mgpu_ctx *c, int batch, const double *lb, const double *u
       skip ? c->lp_skip.as<int32_t>() : nullptr, c->nr_vals.as<double>(),
       ws_head ? c->lp_wh.as<int32_t>() : nullptr, ws_head ? c->lp_wst.as<int8_t>() : nullptr,
       ws_shared, iter_limit, c->lp_st.as<int32_t>(), c->lp_obj.as<double>(),
-      c->lp_it.as<int32_t>(), x ? c->lp_x.as<double>() : nullptr);
+      c->lp_it.as<int32_t>(), x ? c->lp_x.as<double>() : nullptr,
+      ws_binv ? c->lp_wb.as<double>() : nullptr);
   if (rc != MGPU_OK) return rc;
   HIPCHK(c, hipMemcpyAsync(status, c->lp_st.p, B * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipMemcpyAsync(obj, c->lp_obj.p, B * 8, hipMemcpyDeviceToHost, s));

@@ -135,8 +135,8 @@ def load_library():
     lib.mgpu_qp_solve_dev.argtypes = [_P, _I, _P, _P, _I, _P, _P, _P, _P]
     lib.mgpu_set_node_rows.argtypes = [_P, _I, _I, _P, _P, _I, _P, _P, _P]
     lib.mgpu_lp_refactor.argtypes = [_P] + [_P] * 7
-    lib.mgpu_lp_solve_rows.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
-    lib.mgpu_lp_solve_rows_dev.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 4
+    lib.mgpu_lp_solve_rows.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 5
+    lib.mgpu_lp_solve_rows_dev.argtypes = [_P, _I] + [_P] * 6 + [_I, _I] + [_P] * 5
     lib.mgpu_lp_solve_path.argtypes = [_P, _I] + [_P] * 9 + [_I, _I] + [_P] * 7
     lib.mgpu_lp_solve_path_dev.argtypes = [_P, _I] + [_P] * 10 + [_I, _I] + [_P] * 7
     lib.mgpu_ws_alloc.argtypes = [_P, ctypes.POINTER(_I)]
@@ -538,7 +538,9 @@ class Context:
     def lp_solve_rows(self, lb, ub, vals, ws=None, skip=None, iter_limit=0, want_x=False):
         """Every node's own LP (node rows from ``vals`` [B, stride]); ``ws``:
         a WarmStart whose head/st (1-D shared or per node) are refactored for
-        each node's matrix; None = slack basis."""
+        each node's matrix -- with ws.binv (shared, column-major, the warm
+        basis' inverse for the loaded matrix) by column replacement, else
+        from scratch; None = slack basis."""
         p = self.problem
         lb = _np(lb, np.float64)
         ub = _np(ub, np.float64)
@@ -548,16 +550,18 @@ class Context:
         obj = np.zeros(B)
         it = np.zeros(B, dtype=np.int32)
         x = np.zeros((B, p.n)) if want_x else None
-        wh = wst = None
+        wh = wst = wb = None
         shared = 1
         if ws is not None:
             wh = _np(ws.head, np.int32)
             wst = _np(ws.st, np.int8)
             shared = 1 if wh.ndim == 1 else 0
+            if ws.binv is not None:
+                wb = _np(ws.binv, np.float64)
         sk = None if skip is None else _np(skip, np.int32)
         self._chk(self.lib.mgpu_lp_solve_rows(
             self.h, B, _hp(lb), _hp(ub), _hp(sk), _hp(vals), _hp(wh), _hp(wst), shared,
-            int(iter_limit), _hp(st), _hp(obj), _hp(it), _hp(x)), 'mgpu_lp_solve_rows')
+            int(iter_limit), _hp(st), _hp(obj), _hp(it), _hp(x), _hp(wb)), 'mgpu_lp_solve_rows')
         return LpOut(st, obj, it, x, None)
 
     def lp_solve_rows_dev(self, lb, ub, vals, status, obj, iters, ws=None, skip=None,
@@ -568,7 +572,9 @@ class Context:
         self._chk(self.lib.mgpu_lp_solve_rows_dev(
             self.h, B, _dp(lb), _dp(ub), _dp(skip), _dp(vals),
             _dp(ws.head) if ws else None, _dp(ws.st) if ws else None, shared, int(iter_limit),
-            _dp(status), _dp(obj), _dp(iters), _dp(x)), 'mgpu_lp_solve_rows_dev')
+            _dp(status), _dp(obj), _dp(iters), _dp(x),
+            _dp(ws.binv) if ws is not None and ws.binv is not None else None),
+            'mgpu_lp_solve_rows_dev')
 
     def lp_bound(self, cols, signs, lb=None, ub=None, ws=None, iter_limit=0, want_x=False):
         """Bound LPs min sign_b * x[col_b] on one box (host arrays); ws: the

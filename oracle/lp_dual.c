@@ -858,6 +858,45 @@ int orc_dual_simplex_nodes(int n, int m, const int *colptr, const int *rowidx,
  * loaded), from the warm basis head/st (shared when ws_shared, else per node)
  * with the inverse rebuilt for the node's matrix (invert_basis, singular ->
  * slack basis) and compute_duals; dense arithmetic (K3R + K3). */
+/* K3R's column-replacement refactor (m <= 64): the node's basis differs
+ * from the warm (root) basis only in the basic structural columns whose
+ * rewritten entries changed; starting from the root inverse binv0
+ * (row-major), each such basis position i (ascending) takes its node column
+ * a' by one product-form update: alpha = B^-1 a' (ftran_col's order), row i
+ * / alpha_i, row r -= alpha_r row i (the dual simplex's update).  Returns 0
+ * when some |alpha_i| < 1e-12 (the caller refactors from scratch). */
+static int colrep_refactor(int n, int m, const int *colptr, const int *rowidx,
+                           const double *cval0, const double *cv, const int *head,
+                           const double *binv0, double *bi, double *alpha)
+{
+  memcpy(bi, binv0, sizeof(double) * (size_t) m * m);
+  for (int i = 0; i < m; ++i) {
+    int h = head[i], changed = 0;
+    if (h >= n) continue;
+    for (int k = colptr[h]; k < colptr[h + 1]; ++k)
+      if (cv[k] != cval0[k]) { changed = 1; break; }
+    if (!changed) continue;
+    for (int r = 0; r < m; ++r) alpha[r] = 0.0;
+    for (int k = colptr[h]; k < colptr[h + 1]; ++k) {
+      int r = rowidx[k];
+      double a = cv[k];
+      for (int ii = 0; ii < m; ++ii) alpha[ii] += bi[(size_t) ii * m + r] * a;
+    }
+    if (fabs(alpha[i]) < 1e-12) return 0;
+    double inv = 1.0 / alpha[i];
+    double *br = bi + (size_t) i * m;
+    for (int k = 0; k < m; ++k) br[k] *= inv;
+    for (int ii = 0; ii < m; ++ii) {
+      if (ii == i) continue;
+      double f = alpha[ii];
+      if (f == 0.0) continue;
+      double *bj = bi + (size_t) ii * m;
+      for (int k = 0; k < m; ++k) bj[k] -= f * br[k];
+    }
+  }
+  return 1;
+}
+
 int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
                           const double *cval, const double *c, const double *rlo,
                           const double *rhi, int B, const double *lb, const double *ub,
@@ -865,7 +904,7 @@ int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
                           const int *coef_src, int nrow, const int *row, const int *lo_src,
                           const int *hi_src, const int *ws_head, const signed char *ws_st,
                           int ws_shared, int iter_limit, int *status, double *obj, double *x,
-                          int *iters, int nthreads)
+                          int *iters, int nthreads, const double *ws_binv0)
 {
   const int nnz = colptr[n];
   const size_t N = (size_t) (n + m);
@@ -878,6 +917,7 @@ int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
     int *h = (int *) malloc(sizeof(int) * (size_t) (m + 1));
     signed char *s = (signed char *) malloc(N + 1);
     double *bi = (double *) malloc(sizeof(double) * (size_t) m * m + 8);
+    double *al = (double *) malloc(sizeof(double) * (size_t) (m + 1));
     orc_lp P;
     P.n = n; P.m = m; P.colptr = colptr; P.rowidx = rowidx; P.cval = cv; P.c = c;
     P.rlo = lo; P.rhi = hi;
@@ -897,12 +937,26 @@ int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
       }
       const int have = ws_head != 0;
       const size_t wb = ws_shared ? 0 : (size_t) b;
-      status[b] = solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n,
-                               have ? ws_head + wb * m : 0, have ? ws_st + wb * N : 0, 0, 0, have,
-                               0, iter_limit, obj + b, x ? x + (size_t) b * n : 0, iters + b, 0, h,
-                               s, bi, 0, 0);
+      /* the root inverse given (shared warm start, m <= 64): the basis by
+       * column replacement, reduced costs rebuilt (have_binv 2); else the
+       * Gauss-Jordan refactor of invert_basis */
+      int hb = 0;
+      if (have && ws_binv0 && ws_shared &&
+          colrep_refactor(n, m, colptr, rowidx, cval, cv, ws_head, ws_binv0, bi, al))
+        hb = 2;
+      if (hb) {
+        memcpy(h, ws_head, sizeof(int) * (size_t) m);
+        memcpy(s, ws_st, N);
+      }
+      status[b] = hb ? dual_simplex_impl(&P, lb + (size_t) b * n, ub + (size_t) b * n, h, s, bi,
+                                         0, 1, 2, iter_limit, obj + b,
+                                         x ? x + (size_t) b * n : 0, 0, iters + b, 0, 0, 0)
+                     : solve_shared(&P, lb + (size_t) b * n, ub + (size_t) b * n,
+                                    have ? ws_head + wb * m : 0, have ? ws_st + wb * N : 0, 0, 0,
+                                    have, 0, iter_limit, obj + b, x ? x + (size_t) b * n : 0,
+                                    iters + b, 0, h, s, bi, 0, 0);
     }
-    free(cv); free(lo); free(hi); free(h); free(s); free(bi);
+    free(cv); free(lo); free(hi); free(h); free(s); free(bi); free(al);
   }
   return 0;
 }

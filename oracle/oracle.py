@@ -622,12 +622,14 @@ def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1
     """Per-node rows (mgpu_lp_solve_rows): node b solves ``p`` with the entries
     and row bounds of ``nr`` (a quad.NodeRows) taken from ``vals[b]``, from
     the warm basis ``ws`` (head/st; 1-D shared or per node) refactored for
-    its matrix.  Returns (status, obj incl. constant, iters, x)."""
+    its matrix: from ws.binv (the shared root inverse, row-major; m <= 64)
+    by column replacement, else by Gauss-Jordan.  Returns (status, obj incl.
+    constant, iters, x)."""
     l = lib()
     l.orc_dual_simplex_rows.restype = _I
     l.orc_dual_simplex_rows.argtypes = ([_I, _I] + [_P] * 6 + [_I] + [_P] * 3 + [_I, _I]
                                         + [_P] * 2 + [_I] + [_P] * 5 + [_I, _I] + [_P] * 4
-                                        + [_I])
+                                        + [_I, _P])
     LB = np.ascontiguousarray(LB, dtype=np.float64)
     UB = np.ascontiguousarray(UB, dtype=np.float64)
     vals = np.ascontiguousarray(vals, dtype=np.float64)
@@ -645,12 +647,16 @@ def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1
     row = np.ascontiguousarray(nr.row_idx, dtype=np.int32)
     lo = np.ascontiguousarray(nr.lo_src, dtype=np.int32)
     hi = np.ascontiguousarray(nr.hi_src, dtype=np.int32)
-    h = s = None
+    h = s = b0 = None
     shared = 1
     if ws is not None:
         h = np.ascontiguousarray(ws.head, dtype=np.int32)
         s = np.ascontiguousarray(ws.st, dtype=np.int8)
         shared = 1 if h.ndim == 1 else 0
+        # the root inverse (row-major) of a shared warm start: K3R's column
+        # replacement (m <= 64); without it, the Gauss-Jordan refactor
+        if ws.binv is not None and shared and p.m <= 64:
+            b0 = np.ascontiguousarray(ws.binv, dtype=np.float64)
     st = np.zeros(B, dtype=np.int32)
     obj = np.zeros(B)
     it = np.zeros(B, dtype=np.int32)
@@ -659,5 +665,5 @@ def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1
                             _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(vals),
                             int(nr.stride), int(cpos.size), _ptr(cpos), _ptr(csrc), int(row.size),
                             _ptr(row), _ptr(lo), _ptr(hi), _ptr(h), _ptr(s), shared, iter_limit,
-                            _ptr(st), _ptr(obj), _ptr(x), _ptr(it), nthreads)
+                            _ptr(st), _ptr(obj), _ptr(x), _ptr(it), nthreads, _ptr(b0))
     return st, obj + p.obj_const, it, x
