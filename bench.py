@@ -467,7 +467,10 @@ def glob_batch(ctx, dev, rank, world, args, B=65536, reps=10):
     z32 = lambda: torch.zeros(B, dtype=torch.int32, device=dev)   # noqa: E731
     inf, nm, st, it = z32(), z32(), z32(), z32()
     ob = torch.zeros(B, dtype=torch.float64, device=dev)
-    wsd = WarmStart(t(ws.head.astype(np.int32)), t(ws.st.astype(np.int8)), None, None)
+    # the root inverse (column-major) lets K3R replace only the basic columns
+    # a node's rows changed instead of refactoring from scratch
+    wsd = WarmStart(t(ws.head.astype(np.int32)), t(ws.st.astype(np.int8)), None,
+                    t(np.ascontiguousarray(ws.binv.T)))
 
     def step():
         ctx.quad_fbbt_dev(lb, ub, rows, lb2, ub2, rows2, inf, nm, qt=1)
