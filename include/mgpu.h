@@ -210,7 +210,7 @@ int mgpu_lp_solve_path_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const d
  * m <= 64): B^-1 of the warm basis for the LOADED matrix, [m][m]
  * column-major; K3R then replaces only the basic columns a node's rows
  * changed (one product-form update each) instead of refactoring from
- * scratch.  Beyond 64 rows K3L refactors inside the kernel (ws_binv unused). */
+ * scratch; beyond 64 rows K3L does the same inside the kernel. */
 int mgpu_set_node_rows(mgpu_ctx *ctx, int stride, int ncoef, const int32_t *coef_pos,
                        const int32_t *coef_src, int nrow, const int32_t *row_idx,
                        const int32_t *lo_src, const int32_t *hi_src);

@@ -190,7 +190,7 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
                               s.root_ws ? s.ws_st.as<int8_t>() : nullptr, 1, 0,
                               s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
                               s.x.as<double>(),
-                              s.root_ws && c->lp.m <= kLpMaxM ? s.ws_binv.as<double>() : nullptr);
+                              s.root_ws ? s.ws_binv.as<double>() : nullptr);
   if (rc != MGPU_OK) return rc;
   GlobIO io{};
   io.nb = nb;

@@ -291,6 +291,47 @@ __device__ bool refactor_basis(S<kT> &s, double *Bm) {
   return true;
 }
 
+// K3R's column replacement for m > 64 (oracle colrep_refactor): from the
+// root inverse, each basic structural column the node's rows changed is
+// swapped in by one product-form update (alpha = B^-1 a' in CSC order, row
+// i / alpha_i, row r -= alpha_r row i), B^-1 column-major in the inverse
+// slot.  Returns false when a pivot is below 1e-12 (the caller refactors
+// from scratch).
+template <int kT>
+__device__ bool colrep_basis(S<kT> &s, const double *cval0, const double *binv0) {
+  const int n = s.n, m = s.m, tid = threadIdx.x;
+  const size_t mm = (size_t)m * m;
+  for (size_t e = tid; e < mm; e += kT) s.Bi[e] = binv0[e];
+  __syncthreads();
+  for (int i = 0; i < m; ++i) {
+    const int h = s.head[i];
+    if (h >= n) continue;
+    bool ch = false;
+    for (int t = s.colptr[h] + tid; t < s.colptr[h + 1]; t += kT) ch |= s.cval[t] != cval0[t];
+    if (!blk_any(ch, s)) continue;
+    for (int r = tid; r < m; r += kT) {
+      double al = 0.0;
+      for (int t = s.colptr[h]; t < s.colptr[h + 1]; ++t)
+        al += s.Bi[(size_t)s.rowidx[t] * m + r] * s.cval[t];
+      s.aq[r] = al;
+    }
+    __syncthreads();
+    const double piv = s.aq[i];
+    if (fabs(piv) < 1e-12) return false;
+    const double inv = 1.0 / piv;
+    for (int k = tid; k < m; k += kT) s.Bi[(size_t)k * m + i] *= inv;
+    __syncthreads();
+    for (int r = tid; r < m; r += kT) {
+      if (r == i) continue;
+      const double f = s.aq[r];
+      if (f == 0.0) continue;
+      for (int k = 0; k < m; ++k) s.Bi[(size_t)k * m + r] -= f * s.Bi[(size_t)k * m + i];
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
 template <int kT>
 __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double *binv_slots) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -429,7 +470,8 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
       for (int i = tid; i < m; i += kT) s.st[s.head[i]] = ST_BASIC;
       __syncthreads();
       if (io.ws.binv == nullptr && nrows)
-        warm = refactor_basis(s, wg + 2 * (size_t)lp.nnz + 2 * (size_t)m);
+        warm = (io.nr.binv0 != nullptr && colrep_basis(s, lp.cval, io.nr.binv0)) ||
+               refactor_basis(s, wg + 2 * (size_t)lp.nnz + 2 * (size_t)m);
     }
     if (warm) {
       if (s.ocol < 0 && io.ws.d != nullptr) {

@@ -100,6 +100,8 @@ struct NodeRowsIO {
   // basis matrix of the in-kernel refactorisation: wg + blockIdx.x * wg_stride
   double *wg;
   long wg_stride;               // doubles per workgroup: 2 nnz + 2 m + m m
+  const double *binv0;          // K3L: the warm basis' inverse for the loaded
+                                // matrix ([m][m] column-major, shared) or null
 };
 // LinearFunction::addTerm keeps only |a| > 1e-9 (LinearFunction.cpp:22,
 // 89-95): a smaller node coefficient is the term's absence, i.e. 0.

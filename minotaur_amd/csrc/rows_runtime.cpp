@@ -148,6 +148,7 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
     HIPCHK(c, c->nr_ws.ensure((size_t)grid * wgs * sizeof(double) + 8));
     io.nr.wg = c->nr_ws.as<double>();
     io.nr.wg_stride = wgs;
+    io.nr.binv0 = ws_binv;
     if (ws_head)  // head + statuses only: K3L refactors them for each node's matrix
       io.ws = LpWarm{ws_head, ws_st, nullptr, nullptr, ws_shared ? 0 : m, ws_shared ? 0 : N,
                      0, 0};

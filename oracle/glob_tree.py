@@ -171,9 +171,8 @@ class CpuGlobContext:
         qp = self.qp
         self.cap = capacity
         st, obj, x, y, it, ws = oracle.dual_simplex_root(self.p)
-        # the root inverse lets m <= 64 refactor by column replacement (K3R)
-        self.ws = WarmStart(ws.head, ws.st, ws.binv if self.p.m <= 64 else None,
-                            None) if st == 0 else None
+        # the root inverse: nodes refactor by column replacement (K3R / K3L)
+        self.ws = WarmStart(ws.head, ws.st, ws.binv, None) if st == 0 else None
         self.pool = [(qp.vlb.astype(np.float64).copy(), qp.vub.astype(np.float64).copy(),
                       self.rows0.copy(), -math.inf, 0)]
         self.inc = incumbent

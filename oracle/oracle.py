@@ -622,8 +622,8 @@ def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1
     """Per-node rows (mgpu_lp_solve_rows): node b solves ``p`` with the entries
     and row bounds of ``nr`` (a quad.NodeRows) taken from ``vals[b]``, from
     the warm basis ``ws`` (head/st; 1-D shared or per node) refactored for
-    its matrix: from ws.binv (the shared root inverse, row-major; m <= 64)
-    by column replacement, else by Gauss-Jordan.  Returns (status, obj incl.
+    its matrix: from ws.binv (the shared root inverse, row-major) by column
+    replacement, else by Gauss-Jordan.  Returns (status, obj incl.
     constant, iters, x)."""
     l = lib()
     l.orc_dual_simplex_rows.restype = _I
@@ -653,9 +653,9 @@ def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1
         h = np.ascontiguousarray(ws.head, dtype=np.int32)
         s = np.ascontiguousarray(ws.st, dtype=np.int8)
         shared = 1 if h.ndim == 1 else 0
-        # the root inverse (row-major) of a shared warm start: K3R's column
-        # replacement (m <= 64); without it, the Gauss-Jordan refactor
-        if ws.binv is not None and shared and p.m <= 64:
+        # the root inverse (row-major) of a shared warm start: the column
+        # replacement of K3R / K3L; without it, the Gauss-Jordan refactor
+        if ws.binv is not None and shared:
             b0 = np.ascontiguousarray(ws.binv, dtype=np.float64)
     st = np.zeros(B, dtype=np.int32)
     obj = np.zeros(B)

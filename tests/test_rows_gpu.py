@@ -274,3 +274,31 @@ def test_rows_lp_column_replacement_refactor(ctx, seed):
         assert hs == r.status[b], b
         if hs == 0:
             assert _close(r.obj[b], hv, 1e-6), (b, r.obj[b], hv)
+
+
+@pytest.mark.parametrize('seed,nv0,ncon', [(1, 16, 10), (0, 18, 12)])
+def test_rows_lp_column_replacement_beyond_64_rows(ctx, seed, nv0, ncon):
+    """The column replacement inside K3L (m = 76..100): from the root inverse,
+    the changed basic columns swapped in one update each; statuses and pivots
+    equal the oracle's same mode, objectives 1e-9, HiGHS 1e-6."""
+    from minotaur_amd.runtime import WarmStart
+    qp, rows0, p, nr, ws = _setup(ctx, seed, nv0=nv0, ncon=ncon)
+    assert p.m > 64
+    LB, UB = random_quad_boxes(qp, 300, 900 + seed)
+    q = ctx.quad_fbbt(LB, UB, rows0, qt=1)
+    wg = WarmStart(ws.head, ws.st, None, np.ascontiguousarray(ws.binv.T))
+    wo = oracle.WarmStart(ws.head, ws.st, ws.binv, None)
+    r = ctx.lp_solve_rows(q.lb, q.ub, q.rows, ws=wg, skip=q.infeasible, want_x=True)
+    so, oo, io, xo = oracle.dual_simplex_rows(p, q.lb, q.ub, nr, q.rows, ws=wo, nthreads=8,
+                                              want_x=True)
+    live = q.infeasible == 0
+    assert live.sum() > 30
+    assert np.array_equal(r.status[live], so[live])
+    assert np.array_equal(r.iters[live], io[live])
+    opt = live & (so == 0)
+    assert np.allclose(r.obj[opt], oo[opt], rtol=1e-9, atol=1e-9)
+    for b in np.nonzero(live)[0][::7]:
+        hs, hv = oracle.highs(nr.node_problem(p, q.rows[b]), q.lb[b], q.ub[b])
+        assert hs == r.status[b], b
+        if hs == 0:
+            assert _close(r.obj[b], hv, 1e-6), (b, r.obj[b], hv)
