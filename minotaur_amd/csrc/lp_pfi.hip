@@ -164,6 +164,25 @@ __device__ __forceinline__ double apply_etas(double v, const double (&eta)[K], i
   return v;
 }
 
+// apply_etas on G columns at once: the same operations, in the same order,
+// on each column (bit for bit G apply_etas calls), as G independent chains
+template <int K, int G>
+__device__ __forceinline__ void apply_etas_n(double (&v)[G], const double (&eta)[K], int prow,
+                                             int k, int lane) {
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    if (t < k) {
+      const int p = rl(prow, t);
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const double vp = rld(v[i], p);
+        const double nv = lane == p ? eta[t] * vp : v[i] + eta[t] * vp;
+        v[i] = vp != 0.0 ? nv : v[i];
+      }
+    }
+  }
+}
+
 // B0^{-1} a_q (oracle ftran_col, product form, before the etas): four CSC
 // entries' loads in flight, adds in CSC order; lanes >= m give 0
 __device__ __forceinline__ double ftran_b0(const Prob &P, int q, int lane) {
@@ -199,8 +218,14 @@ __device__ __forceinline__ double btran_etas(double u, const double (&eta)[K], i
 #pragma unroll
   for (int t = K - 1; t >= 0; --t) {
     if (t < k) {
-      const double acc = wave_sum_sym(u * eta[t]);
-      if (lane == rl(prow, t)) u = acc;
+      // all products zero: u_p is 0 (eta_t's pivot entry is not), and the
+      // sum would write a zero back; skipping changes at most the sign of
+      // a zero, which no later step reads (sums, and u_b0 skips zeros)
+      const double pr = u * eta[t];
+      if (__ballot(pr != 0.0) != 0ull) {
+        const double acc = wave_sum_sym(pr);
+        if (lane == rl(prow, t)) u = acc;
+      }
     }
   }
   return u;
@@ -381,25 +406,50 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     int h = lane < m ? s_whead[lane] : -1;
     if (kpath > 0) {
       // each pivot's eta exactly as the solve that made it built it: FTRAN
-      // of its entering column through B0^{-1} and the etas before it
-      // (apply_etas' operations in path order), one pivot after the other.
-      // A runtime loop with ONE inlined eta pass: the fully unrolled K x K
-      // elimination it replaces was most of the kernel's 159 KB of code.
+      // of its entering column through B0^{-1}, then the etas before it in
+      // path order (apply_etas' operations).  kRG path columns at a time:
+      // the etas of the earlier groups go into them as kRG independent
+      // chains (apply_etas_n), and inside the group each new eta is applied
+      // to the group's later columns.  Every column sees the operations of
+      // one apply_etas call in the same order, so the etas are bit for bit
+      // those of the one-column-after-the-other replay, whose dependent
+      // readlane chain was a quarter of the kernel's wave-cycles.
+      constexpr int kRG = 4;
 #pragma unroll 1
-      for (int s = 0; s < kpath; ++s) {
-        const uint32_t pv = ppath[s];
-        const int q = (int)(pv & 0xFFFFu), r = (int)(pv >> 16);
-        const double v = apply_etas(ftran_b0(P, q, lane), eta, prow, s, lane);
-        const double inv = 1.0 / rld(v, r);
-        const double e = lane == r ? inv : -v * inv;
+      for (int g = 0; g < kpath; g += kRG) {
+        double v[kRG];
+        int qg[kRG], rg[kRG];
 #pragma unroll
-        for (int t = 0; t < K; ++t)
-          if (t == s) eta[t] = e;
-        if (lane == s) {
-          prow = r;
-          pq = q;
+        for (int i = 0; i < kRG; ++i) {
+          const bool ok = g + i < kpath;  // wave-uniform
+          const uint32_t pv = ok ? ppath[g + i] : 0u;
+          qg[i] = (int)(pv & 0xFFFFu);
+          rg[i] = (int)(pv >> 16);
+          v[i] = ok ? ftran_b0(P, qg[i], lane) : 0.0;
         }
-        if (lane == r) h = q;
+        apply_etas_n(v, eta, prow, g, lane);
+#pragma unroll
+        for (int i = 0; i < kRG; ++i) {
+          if (g + i < kpath) {
+            const int s = g + i, r = rg[i], q = qg[i];
+            const double inv = 1.0 / rld(v[i], r);
+            const double e = lane == r ? inv : -v[i] * inv;
+#pragma unroll
+            for (int t = 0; t < K; ++t)
+              if (t == s) eta[t] = e;
+            if (lane == s) {
+              prow = r;
+              pq = q;
+            }
+            if (lane == r) h = q;
+#pragma unroll
+            for (int i2 = i + 1; i2 < kRG; ++i2) {
+              const double vp = rld(v[i2], r);
+              const double nv = lane == r ? e * vp : v[i2] + e * vp;
+              v[i2] = vp != 0.0 ? nv : v[i2];
+            }
+          }
+        }
       }
       ne = kpath;
     }
