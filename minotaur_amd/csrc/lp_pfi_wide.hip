@@ -479,12 +479,17 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
       for (int t = kKE - 1; t >= 0; --t) {
         if (t < iters) {
           // u' eta_t: lane products (row lane + row 64 + lane), summed by the
-          // symmetric DPP butterfly (oracle eta_dot)
-          const double acc = wave_sum_sym(u[0] * eta[t][0] + u[1] * eta[t][1]);
-          const int pt = rl(prow, t);
+          // symmetric DPP butterfly (oracle eta_dot).  All products zero:
+          // u_pt is 0 (eta_t's pivot entry is not) and the sum would write
+          // a zero back, so the eta is skipped (K3P's btran_etas)
+          const double p0 = u[0] * eta[t][0], p1 = u[1] * eta[t][1];
+          if (__ballot(p0 != 0.0 || p1 != 0.0) != 0ull) {
+            const double acc = wave_sum_sym(p0 + p1);
+            const int pt = rl(prow, t);
 #pragma unroll
-          for (int rs = 0; rs < kR; ++rs)
-            if (rs * 64 + lane == pt) u[rs] = acc;
+            for (int rs = 0; rs < kR; ++rs)
+              if (rs * 64 + lane == pt) u[rs] = acc;
+          }
         }
       }
       {  // rho' = u' B0^{-1} (ascending nonzero rows), published to LDS
