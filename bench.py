@@ -217,13 +217,14 @@ def tree_cpu_baseline(p, brancher, seconds):
             "solved": done, "ub": float(res[0])}
 
 
-def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0):
+def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None):
     """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
     across ranks after the shared first rounds: one packed all-reduce per
     round (incumbent MIN + open counts), open nodes rebalanced every 8 rounds
     or when a rank runs dry (dist.rebalance).  Returns (incumbent, nodes, LP
     solves, pivots, pruned-open, rounds, seconds, nodes moved, strong-branching
-    LPs, their pivots) — counts summed over ranks, seconds the max."""
+    LPs, their pivots) — counts summed over ranks, seconds the max.  ``trace``
+    (a list) receives (seconds since the start, incumbent) per round."""
     import torch
     import torch.distributed as dist
     from minotaur_amd import bnb
@@ -236,10 +237,13 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    tr = []
     inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=cap,
                                                      order=order, warm=warm, comm=comm,
-                                                     lb_every=8, brancher=brancher)
+                                                     lb_every=8, brancher=brancher, trace=tr)
     torch.cuda.synchronize()
+    if trace is not None:
+        trace.extend((t - t0, v) for t, v in tr)
     if world > 1:
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
@@ -317,6 +321,39 @@ def tree_search(ctx, dev, rank, world, B, args):
                 progress(rank, f"cpu tree {p.name} brancher {br}: {cpu_trees[key]}")
             if cpu_trees[key] is not None:
                 out[-1]["cpu_baseline"] = cpu_trees[key]
+    return out
+
+
+def tls4_oa_tree(ctx, dev, rank, world, args):
+    """Config 2's complete tree: tls4-OA from the root to
+    the proven OA-MILP optimum 3.2 (= HiGHS), depth-first over batches, MaxVio
+    branching, parent-basis warm starts (warm 2), node-sharded across ranks.
+    Reported next to the headline because the headline's pool is the root
+    plus B synthetic boxes: this is the instance's own tree, its nodes/s and
+    its time to the optimum.  CPU baseline: the reference's own
+    BranchAndBound on one core (oracle/_ref, LP restatement behind
+    CpuLPEngine), bounded by --tree-cpu-seconds."""
+    from minotaur_amd.problem import LinProblem
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
+    B = args.oa_tree_batch
+    tr = []
+    inc, nodes, lps, piv, pruned, rounds, el, moved, _, _ = run_tree(
+        ctx, dev, rank, world, p, B, 0, 2, 1 << 21, 0, trace=tr)
+    tol = 1e-6 * max(1.0, abs(inc))
+    tto = next((t for t, v in tr if v <= inc + tol), el)
+    out = {"instance": f"tls4-oa ({p.m} rows, {p.n} cols)", "batch_per_gpu": B,
+           "search": "depth-first over batches, MaxVio, parent-basis warm starts",
+           "nodes": nodes, "rounds": rounds, "seconds": el, "nodes_per_s": nodes / el,
+           "relaxations_per_s": lps / el, "pivots_per_lp": piv / max(lps, 1.0),
+           "time_to_optimum_s": tto, "optimum": inc, "optimum_highs": 3.2,
+           "optimum_matches_highs": bool(abs(inc - 3.2) <= 1e-6 * 3.2)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        c1 = tree_cpu_baseline(p, 0, 4 * args.tree_cpu_seconds)
+        if c1 is not None:
+            out["cpu_reference_one_core"] = {k: c1[k] for k in ("value", "unit", "cores", "kind",
+                                                                 "nodes", "seconds", "solved",
+                                                                 "ub")}
+            out["vs_reference_one_core"] = out["nodes_per_s"] / max(c1["value"], 1e-9)
     return out
 
 
@@ -451,14 +488,13 @@ def glob_batch(ctx, dev, rank, world, args, B=65536, reps=10):
     from minotaur_amd import dist as mdist
     from minotaur_amd.quad import random_qcqp, random_quad_boxes, relaxation_lp
     from minotaur_amd.runtime import WarmStart
-    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
-    import oracle
     qp = random_qcqp(7, nv0=14, ncon=8)
     ctx.load_quad(qp)
     rows0 = ctx.quad_rows()
     p, nr = relaxation_lp(qp, rows0)
-    st0, _, _, _, _, ws = oracle.dual_simplex_root(p)
     ctx.load(p)
+    root, ws = ctx.root_solve()          # the device's own root LP and basis
+    st0 = int(root.status[0])
     ctx.set_node_rows(nr)
     LB, UB = random_quad_boxes(qp, B, mdist.shard_seed(23, rank))
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
@@ -470,7 +506,7 @@ def glob_batch(ctx, dev, rank, world, args, B=65536, reps=10):
     # the root inverse (column-major) lets K3R replace only the basic columns
     # a node's rows changed instead of refactoring from scratch
     wsd = WarmStart(t(ws.head.astype(np.int32)), t(ws.st.astype(np.int8)), None,
-                    t(np.ascontiguousarray(ws.binv.T)))
+                    t(ws.binv))       # column-major, the ABI layout
 
     def step():
         ctx.quad_fbbt_dev(lb, ub, rows, lb2, ub2, rows2, inf, nm, qt=1)
@@ -496,6 +532,8 @@ def glob_batch(ctx, dev, rank, world, args, B=65536, reps=10):
            "lp_ms": float(np.median(lp)), "pivots_per_lp": float(it.sum().item()) / max(solved, 1),
            "root_lp_status": int(st0)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+        import oracle
         S = 2048
         t0 = time.perf_counter()
         o = oracle.quad_fbbt(qp, LB[:S], UB[:S], None, 1, rows0)
@@ -798,6 +836,114 @@ def fixed_batch(ctx, dev, rank, world, args, reps=10):
             "kernels": k}
 
 
+def _r(v, k=4):
+    """Round floats for the compact line (significant digits kept)."""
+    if isinstance(v, float) and math.isfinite(v) and v != 0.0:
+        return float(f"{v:.{k}g}")
+    return v
+
+
+LINE_MAX = 6000   # the driver keeps the tail of stdout: the line must stay short
+
+
+def compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, cpu, oa_tree,
+                 supp, supp_path):
+    """The ONE stdout JSON line (< 6 KB so the driver's
+    stdout tail holds it whole): the metric, the roofline of the dominant
+    kernel, the CPU baselines, config 2's complete tree and one number per
+    supplementary object; the objects themselves go to ``supp_path``."""
+    kf, kl = kernels["fbbt"], kernels["lp_pfi"]
+    ks = {"fbbt": {"ms": _r(kf["ms"]), "achieved_gbs": _r(kf["achieved"]),
+                   "frac": _r(kf["frac"]), "bytes_per_launch": _r(kf["bytes_per_launch"])},
+          "lp_pfi": {"ms": _r(kl["ms"]), "achieved_tflops": _r(kl["achieved"]),
+                     "frac": _r(kl["frac"]), "revised_frac": _r(kl["revised_frac"]),
+                     "pivots_per_solve": _r(kl["pivots_per_solve"]),
+                     "overflow_resolve_ms": _r(kl["overflow_resolve_ms"])}}
+    rf = {k: _r(v) for k, v in roofline.items()}
+    cb = None
+    if cpu is not None:
+        cb = {"value": _r(cpu["value"]), "unit": cpu["unit"], "cores": cpu["cores"],
+              "kind": cpu["kind"], "cpu_model": cpu["cpu_model"],
+              "sample": cpu["sample"][:300],
+              "relaxations_per_s": _r(cpu["relaxations_per_s"]),
+              "one_core": {k: (_r(v) if k != "sample" else v[:200])
+                           for k, v in cpu["one_core"].items()}}
+        rt = cpu.get("reference_tree_one_core")
+        if rt:
+            cb["reference_tree_one_core"] = {"value": _r(rt["value"]), "nodes": rt["nodes"],
+                                             "seconds": _r(rt["seconds"]),
+                                             "solved": rt["solved"]}
+    oa = {k: _r(v) if isinstance(v, float) else v for k, v in oa_tree.items()
+          if not isinstance(v, dict)}
+    if "cpu_reference_one_core" in oa_tree:
+        c1 = oa_tree["cpu_reference_one_core"]
+        oa["cpu_reference_one_core"] = {"value": _r(c1["value"]), "solved": c1["solved"],
+                                        "seconds": _r(c1["seconds"])}
+
+    def rate(key, field="nodes_per_s"):
+        v = supp.get(key)
+        if v is None:
+            return None
+        if isinstance(v, list):
+            return [_r(e.get(field)) for e in v]
+        return _r(v.get(field))
+    ts = supp.get("tree_search") or []
+    line = {
+        "metric": "B&B nodes/sec + relaxations solved/sec at 1/2/4/8 MI355X",
+        "value": nodes / elapsed,
+        "unit": "nodes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": ("config 2 (tls4.nl as a MINLP: its OA-LP) branch-and-bound tree rounds: "
+                         "per step and GPU one mgpu_bnb_round = pop the top B open nodes of the "
+                         "HBM stack, K1 FBBT, K3P dual simplex from the parent's optimal basis, "
+                         "decision + MaxVio, children pushed; then one packed all-reduce "
+                         "(incumbent MIN, open counts). Pool = root + B seeded boxes (SURVEY 8d)"
+                         if args.warm == 2 else
+                         "config 2 tree rounds, root-basis warm starts (K3P), MaxVio"),
+            "instance": f"tls4-oa ({p.m} rows, {p.n} cols, {p.nnz} nnz)",
+            "nodes_per_gpu": B,
+            "global_batch": B * world,
+            "parallelism": f"node-sharded x{world}",
+        },
+        "relaxations_per_s": lps / elapsed,
+        "fbbt_node_passes_per_s": float(B) * world / (kf["ms"] * 1e-3),
+        "tree_rounds": {k: _r(v) if isinstance(v, float) else v
+                        for k, v in h["summary"].items() if k != "search"},
+        "rccl_ms_total": _r(h["rccl_ms"]),
+        "roofline": rf,
+        "kernels": ks,
+        "cpu_baseline": cb,
+        "tls4_oa_tree": oa,
+        "supplementary": {
+            "file": supp_path,
+            "fixed_batch_nodes_per_s": rate("fixed_batch"),
+            "tree_search_nodes_per_s": [_r(e["nodes_per_s"]) for e in ts] or None,
+            "tree_search_all_optima_match_highs": (all(e["optimum_matches_highs"] for e in ts)
+                                                   if ts else None),
+            "convex_batch_nodes_per_s": rate("convex_batch"),
+            "qp_per_s": rate("qp_relaxation", "qp_per_s"),
+            "knapsack_nodes_per_s": rate("knapsack_nodes"),
+            "glob_batch_nodes_per_s": rate("glob_batch"),
+            "glob_tree_nodes_per_s": rate("glob_tree"),
+        },
+    }
+    # keep the line under the driver's limit whatever the supplementary holds
+    for drop in ("supplementary", "tree_rounds", "tls4_oa_tree"):
+        if len(json.dumps(line)) <= LINE_MAX:
+            break
+        line[drop] = "see " + str(supp_path)
+    return line
+
+
 def progress(rank, msg):
     """One line per phase on stderr (the JSON line stays alone on stdout)."""
     if rank == 0:
@@ -815,6 +961,12 @@ def main():
     ap.add_argument('--tree-batch', type=int, default=131072,
                     help='open nodes per GPU per round of the complete trees (tree_search, '
                          'convex_batch)')
+    ap.add_argument('--oa-tree-batch', type=int, default=16384,
+                    help="open nodes per GPU per round of config 2's complete tree "
+                         "(tls4_oa_tree in the line)")
+    ap.add_argument('--supp-out', default=os.path.join('gpurun_out', 'bench_supplementary.json'),
+                    help='where the supplementary objects (trees, configs 3/4/5, glob) are '
+                         'written; the stdout line carries their headline numbers only')
     ap.add_argument('--warm', type=int, default=2,
                     help='headline tree warm starts: 2 parent basis as a pivot path (default; '
                          'NodeIncRelaxer semantics), 0 the root basis')
@@ -871,20 +1023,21 @@ def main():
     progress(rank, f"headline done: {1e3 * elapsed / args.steps:.2f} ms/step, "
                    f"{nodes / elapsed / 1e6:.2f} M nodes/s")
     TB = args.tree_batch
-    fixed = None if args.no_fixed else fixed_batch(ctx, dev, rank, world, args)
-    progress(rank, "fixed_batch done")
-    tree = None if args.no_bnb else tree_search(ctx, dev, rank, world, TB, args)
-    progress(rank, "tree_search done")
-    cvx = None if args.no_convex else convex_batch(ctx, dev, rank, world, TB, args)
-    progress(rank, "convex_batch done")
-    qprel = None if args.no_qp else qp_relaxation(ctx, dev, rank, world, args)
-    progress(rank, "qp_relaxation done")
-    ksn = None if args.no_knapsack else knapsack_nodes(ctx, dev, rank, world, args)
-    progress(rank, "knapsack_nodes done")
-    glob = None if args.no_glob else glob_batch(ctx, dev, rank, world, args)
-    progress(rank, "glob_batch done")
-    gtree = None if args.no_glob else glob_tree(ctx, dev, rank, world, args)
-    progress(rank, "glob_tree done")
+    oa_tree = tls4_oa_tree(ctx, dev, rank, world, args)
+    progress(rank, f"tls4_oa_tree done: {oa_tree['nodes_per_s'] / 1e6:.2f} M nodes/s")
+    supp = {}
+    for key, skip, fn in (
+            ("fixed_batch", args.no_fixed, lambda: fixed_batch(ctx, dev, rank, world, args)),
+            ("tree_search", args.no_bnb, lambda: tree_search(ctx, dev, rank, world, TB, args)),
+            ("convex_batch", args.no_convex,
+             lambda: convex_batch(ctx, dev, rank, world, TB, args)),
+            ("qp_relaxation", args.no_qp, lambda: qp_relaxation(ctx, dev, rank, world, args)),
+            ("knapsack_nodes", args.no_knapsack,
+             lambda: knapsack_nodes(ctx, dev, rank, world, args)),
+            ("glob_batch", args.no_glob, lambda: glob_batch(ctx, dev, rank, world, args)),
+            ("glob_tree", args.no_glob, lambda: glob_tree(ctx, dev, rank, world, args))):
+        supp[key] = None if skip else fn()
+        progress(rank, f"{key} done")
 
     if rank == 0:
         kernels = h["kernels"]
@@ -897,68 +1050,25 @@ def main():
         if tsrc:
             roofline["traffic_source"] = f"profiles/{tsrc} (PMC, bytes per launch)"
         if dom != "fbbt":
-            roofline["note"] = ("FP64 VALU kernel (no MFMA: per-node pivots); achieved = "
-                                "SURVEY 8(d)'s tableau flops 2m(n+m) per pivot over the pivots "
-                                "K3P ran itself / its HIP-event time; the revised-simplex count "
-                                "is kernels.lp_pfi.revised_*; peak = MI355X FP64 dense 78.6 TF/s")
+            roofline["note"] = ("FP64 VALU (no MFMA: per-node pivots); achieved = SURVEY 8(d) "
+                                "2m(n+m) flops per pivot K3P ran / its HIP-event time")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(p, LB, UB, args.cpu_seconds, "tls4-oa")
             # the same instance's tree on one core by the reference's own
             # BranchAndBound (nodes/s like value; not the same node boxes)
             cpu["reference_tree_one_core"] = tree_cpu_baseline(p, 0, 2 * args.tree_cpu_seconds)
-        line = {
-            "metric": "B&B nodes/sec + relaxations solved/sec at 1/2/4/8 MI355X",
-            "value": nodes / elapsed,
-            "unit": "nodes/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": 1e3 * elapsed / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic",
-            "config": {
-                "workload": ("branch-and-bound tree rounds on config 2 (tls4.nl as a MINLP: its "
-                             "outer-approximation LP): every step is one mgpu_bnb_round per GPU "
-                             "- pop the top B open nodes of the HBM node stack, K1 FBBT with the "
-                             "incumbent, K3P dual-simplex LP from the parent's optimal basis "
-                             "(kept as its pivot path from the root basis; NodeIncRelaxer "
-                             "semantics) with FBBT-infeasible nodes skipped, prune/integrality "
-                             "decision with the MaxVio branching choice, children (box, bound, "
-                             "path) written back to the stack - then one packed all-reduce "
-                             "(incumbent MIN, open counts); the pool starts as the root plus B "
-                             "seeded random-branching boxes" if args.warm == 2 else
-                             "branch-and-bound tree rounds on config 2 (tls4 OA-LP), root-basis "
-                             "warm starts (K3P), MaxVio branching"),
-                "instance": f"tls4-oa ({p.m} rows, {p.n} cols, {p.nnz} nnz)",
-                "nodes_per_gpu": B,
-                "global_batch": B * world,
-                "node_boxes": "seeded random branching from the root, depth 1-20 (SURVEY 8d), "
-                              "then their descendants",
-                "parallelism": f"node-sharded x{world}",
-            },
-            "relaxations_per_s": lps / elapsed,
-            "fbbt_node_passes_per_s": float(B) * world / (kernels["fbbt"]["ms"] * 1e-3),
-            "tree_rounds": h["summary"],
-            "collectives": {"incumbent_syncs": args.steps,
-                            "rccl_ms_total": h["rccl_ms"],
-                            "note": "one packed all-reduce (incumbent MIN, open max/min) per "
-                                    "round, timed with events on the engine stream"},
-            "roofline": roofline,
-            "kernels": kernels,
-            "cpu_baseline": cpu,
-            "incumbent": h["incumbent"],
-            "fixed_batch": fixed,
-            "tree_search": tree,
-            "convex_batch": cvx,
-            "qp_relaxation": qprel,
-            "knapsack_nodes": ksn,
-            "glob_batch": glob,
-            "glob_tree": gtree,
-        }
+        full = {"headline_kernels": kernels, "cpu_baseline": cpu, "tls4_oa_tree": oa_tree}
+        full.update(supp)
+        supp_path = os.path.abspath(args.supp_out)
+        try:
+            os.makedirs(os.path.dirname(supp_path), exist_ok=True)
+            with open(supp_path, 'w') as fh:
+                json.dump(full, fh, indent=1)
+        except OSError as e:
+            supp_path = f"not written ({e})"
+        line = compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, cpu,
+                            oa_tree, supp, supp_path)
         if rehearse:
             line["rehearsal"] = "all ranks on device 0 over gloo (not a scaling number)"
         print(json.dumps(line), flush=True)

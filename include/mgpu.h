@@ -148,25 +148,30 @@ int mgpu_lp_solve_dev(mgpu_ctx *ctx, int batch, const double *d_lb, const double
                       int32_t *d_wo_head, int8_t *d_wo_st, double *d_wo_d,
                       double *d_wo_binv);
 
-/* ---- path warm starts (the batched tree's warm mode 2) --------------------
+/* ---- basis warm starts (the batched tree's warm mode 2) -------------------
  * NodeIncRelaxer::createNodeRelaxation loads each child with its parent's
  * optimal basis (NodeIncRelaxer.cpp:146-150; TreeManager::branch hands both
- * children the parent's warm start, TreeManager.cpp:97-136).  A dense basis
- * inverse per open node (32 KB at m = 64) is too much to keep and move for
- * millions of nodes; a node's basis is kept instead as its PATH from the
- * shared root basis: the pivots (entering column q, row r; packed
- * q | r << 16) that led there, plus its column statuses (n+m bytes).  K3P
- * rebuilds the etas by FTRAN in path order (bit for bit the arithmetic of
- * the solves that made them), recomputes the reduced costs of that basis and
- * continues with its own pivots in the same eta file.
+ * children the parent's warm start, TreeManager.cpp:97-136; the basis itself
+ * is Clp's CoinWarmStartBasis, OsiLPEngine.cpp:375-384, 500-505).  A dense
+ * basis inverse per open node (32 KB at m = 64) is too much to keep and move
+ * for millions of nodes; a node keeps its basis as the column statuses (n+m
+ * bytes) plus the list of its basic columns that are NOT basic in the shared
+ * root basis (ascending column index, at most MGPU_PATH_MAX).  K3P rebuilds
+ * the inverse from the shared one by column replacement: each listed column
+ * takes, through FTRAN, the free row (a root basic column that is nonbasic in
+ * the node) with the largest |alpha| (lowest row on ties) and becomes an eta
+ * column; a replacement with |alpha| < 1e-9 falls back to the shared basis.
+ * Then the reduced costs of that basis are recomputed and the solve
+ * continues with its own pivots in the same eta file.  The eta count is the
+ * basis difference, not the length of the pivot history.
  *   k_in[b] <= 0      : node b starts from the shared warm start itself;
- *   path_in [batch][MGPU_PATH_MAX], st_in [batch][n+m] (0 lb, 1 ub, 2 free,
- *                       3 basic);
- *   k_out / path_out / st_out (optional): node b's final path for its
- *                       children — its replayed plus its own pivots — when
- *                       it is optimal in the product form with at most
- *                       `inherit` etas, else k_out[b] = 0 (children restart
- *                       from the shared warm start);
+ *   path_in [batch][MGPU_PATH_MAX] (the listed columns), st_in [batch][n+m]
+ *                       (0 lb, 1 ub, 2 free, 3 basic);
+ *   k_out / path_out / st_out (optional): node b's final basis for its
+ *                       children in the same form, when it is optimal in the
+ *                       product form with at most `inherit` basic columns
+ *                       outside the shared basis, else k_out[b] = 0 (children
+ *                       restart from the shared warm start);
  *   iters             : the node's own pivots.
  * Runs K3P only (m <= 64, n + m <= 256, eta cap <= MGPU_PATH_MAX; an LP that
  * fills the eta file is continued by K3).  oracle/lp_dual.c

@@ -36,7 +36,7 @@ def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
 
 def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max=None,
                       capacity=None, max_rounds=10**9, shard_at=None, order=0, warm=0,
-                      comm=None, lb_every=0, brancher=0):
+                      comm=None, lb_every=0, brancher=0, trace=None):
     """Node-sharded tree search.  Every rank runs the same deterministic
     rounds until the pool holds at least ``shard_at`` (default 4 * world)
     open nodes, then keeps nodes i = rank (mod world) (mgpu_bnb_shard) and
@@ -53,7 +53,8 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
     where mine = {nodes, lps, pivots, pruned, sb_lps, sb_pivots, moved,
     lb_log: per rebalance the bounds picked and received} evaluated
     by this rank, the shared first rounds counted on rank 0 only (so sums
-    over ranks are exact)."""
+    over ranks are exact).  ``trace`` (a list) receives (perf_counter time,
+    all-reduced incumbent) after every round."""
     from . import dist as mdist
     cap = capacity or 64 * batch
     shard_at = shard_at or 4 * world
@@ -88,6 +89,8 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
             if failed:
                 raise exc if exc is not None else RuntimeError(
                     'solve_distributed: a peer rank failed in round %d' % rounds)
+            if trace is not None:
+                trace.append((time.perf_counter(), inc))
             if most == 0.0:
                 break
             # the trigger uses only all-reduced values: every rank agrees
@@ -98,6 +101,8 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
                 lb_log.append((picked.tolist(), got.tolist()))
         else:
             inc = allreduce_min(st.incumbent)
+            if trace is not None:
+                trace.append((time.perf_counter(), inc))
             if allreduce_max(float(open_now)) == 0.0:
                 break
     obj, x = ctx.bnb_best()

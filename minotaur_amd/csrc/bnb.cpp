@@ -732,7 +732,8 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     io.hw = s.hw;
     io.plive = s.plive.as<uint8_t>();
   }
-  if (s.warm == 2) {  // children inherit the node's final path
+  if (s.warm == 2) {  // children inherit the node's final basis
+    io.kin = bfs ? s.bpk.as<int32_t>() : s.ppk.as<int32_t>() + base;
     io.N = N;
     io.opk = s.opk.as<int32_t>();
     io.oppath = s.oppath.as<uint32_t>();

@@ -49,8 +49,10 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
   s_cnt[t][5] = lp ? 1 : 0;
   s_cnt[t][6] = lp ? io.iters[i] : 0;
   // pivots the product-form kernel ran itself (an overflowing LP's first
-  // pfi_cap pivots; the rest ran in the dense continuation)
-  s_cnt[t][7] = lp ? min(io.iters[i], io.pfi_cap) : 0;
+  // pfi_cap - k pivots after its k warm-start etas; the rest ran in the
+  // dense continuation)
+  const int kin = (lp && io.kin != nullptr) ? io.kin[i] : 0;
+  s_cnt[t][7] = lp ? min(io.iters[i], max(io.pfi_cap - kin, 0)) : 0;
   __syncthreads();
   // Hillis-Steele inclusive scan of the flags
   for (int o = 1; o < kScanBlock; o <<= 1) {

@@ -66,6 +66,7 @@ namespace {
 constexpr double kPTol = 1e-7;
 constexpr double kDTol = 1e-7;
 constexpr double kPivTol = 1e-9;
+constexpr double kColrepTol = 1e-9;  // oracle COLREP_TOL
 constexpr double kArt0 = 1e7;
 constexpr double kInfB = 1e30;
 constexpr int kUnknownStatus = 12;
@@ -218,13 +219,15 @@ __device__ __forceinline__ double btran_etas(double u, const double (&eta)[K], i
 #pragma unroll
   for (int t = K - 1; t >= 0; --t) {
     if (t < k) {
-      // all products zero: u_p is 0 (eta_t's pivot entry is not), and the
-      // sum would write a zero back; skipping changes at most the sign of
-      // a zero, which no later step reads (sums, and u_b0 skips zeros)
+      // all products zero and u_p zero: the sum would write a zero back;
+      // skipping changes at most the sign of a zero, which no later step
+      // reads (sums, and u_b0 skips zeros).  A nonzero u_p whose product
+      // underflowed is still rewritten (to the sum's zero, as the oracle)
+      const int p = rl(prow, t);
       const double pr = u * eta[t];
-      if (__ballot(pr != 0.0) != 0ull) {
+      if (__ballot(pr != 0.0 || (lane == p && u != 0.0)) != 0ull) {
         const double acc = wave_sum_sym(pr);
-        if (lane == rl(prow, t)) u = acc;
+        if (lane == p) u = acc;
       }
     }
   }
@@ -359,9 +362,10 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       continue;
     }
 
-    // path warm start (the batched tree's warm mode 2): k pivots from the
-    // shared basis, the node's own statuses
-    const int kpath = io.path.k != nullptr ? io.path.k[b] : 0;
+    // basis warm start (the batched tree's warm mode 2): the parent's
+    // optimal basis as its statuses plus the kpath basic columns outside the
+    // shared basis (ascending); kpath 0 = the shared basis itself
+    int kpath = io.path.k != nullptr ? io.path.k[b] : 0;
     const uint32_t *ppath = io.path.path + (size_t)b * kPathMax;
     const int8_t *pst = io.path.st + (size_t)b * N;
     // ---- working bounds; an empty box is infeasible before any pivot ----
@@ -398,49 +402,53 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
 #pragma unroll
     for (int t = 0; t < K; ++t) eta[t] = 0.0;
     int prow = 0;  // lane t: pivot row of eta t
-    int pq = 0;    // lane t: entering column of eta t (path outputs)
-    int ne = 0;    // eta columns: the path's replayed pivots, then this solve's
+    int ne = 0;    // eta columns: the warm start's column replacements, then this solve's
 
-    // ---- basis rows: head, replayed path pivots, bounds (basic columns
-    // carry no artificial box)
+    // ---- basis rows: head, the warm start's column replacements, bounds
+    // (basic columns carry no artificial box)
     int h = lane < m ? s_whead[lane] : -1;
     if (kpath > 0) {
-      // each pivot's eta exactly as the solve that made it built it: FTRAN
-      // of its entering column through B0^{-1}, then the etas before it in
-      // path order (apply_etas' operations).  kRG path columns at a time:
-      // the etas of the earlier groups go into them as kRG independent
-      // chains (apply_etas_n), and inside the group each new eta is applied
-      // to the group's later columns.  Every column sees the operations of
-      // one apply_etas call in the same order, so the etas are bit for bit
-      // those of the one-column-after-the-other replay, whose dependent
-      // readlane chain was a quarter of the kernel's wave-cycles.
+      // Column replacement with partial pivoting (oracle colrep_basis): the
+      // root's basic columns that are nonbasic in the node free their rows;
+      // each entering column q (FTRAN through B0^{-1} and the etas so far)
+      // takes the free row with the largest |alpha| (lowest row on ties) and
+      // becomes an eta exactly as a pivot on it would.  kRG columns at a
+      // time: the etas of the earlier groups go into them as kRG independent
+      // chains (apply_etas_n); inside the group each new eta is applied to
+      // the group's later columns, so every column sees the operations of
+      // one apply_etas call in order.  No usable pivot (< kColrepTol): the
+      // shared basis instead.
+      uint64_t freem = __ballot(lane < m && pst[h] != ST_BASIC);
+      bool ok = true;
       constexpr int kRG = 4;
 #pragma unroll 1
-      for (int g = 0; g < kpath; g += kRG) {
+      for (int g = 0; g < kpath && ok; g += kRG) {
         double v[kRG];
-        int qg[kRG], rg[kRG];
+        int qg[kRG];
 #pragma unroll
         for (int i = 0; i < kRG; ++i) {
-          const bool ok = g + i < kpath;  // wave-uniform
-          const uint32_t pv = ok ? ppath[g + i] : 0u;
-          qg[i] = (int)(pv & 0xFFFFu);
-          rg[i] = (int)(pv >> 16);
-          v[i] = ok ? ftran_b0(P, qg[i], lane) : 0.0;
+          const bool in = g + i < kpath;  // wave-uniform
+          qg[i] = in ? (int)(ppath[g + i] & 0xFFFFu) : 0;
+          v[i] = in ? ftran_b0(P, qg[i], lane) : 0.0;
         }
         apply_etas_n(v, eta, prow, g, lane);
 #pragma unroll
         for (int i = 0; i < kRG; ++i) {
-          if (g + i < kpath) {
-            const int s = g + i, r = rg[i], q = qg[i];
+          if (ok && g + i < kpath) {
+            const int s = g + i, q = qg[i];
+            double best = ((freem >> lane) & 1ull) ? fabs(v[i]) : 0.0;
+            const int r = wave_argmax_lane(best);
+            if (!(best >= kColrepTol)) {
+              ok = false;
+              break;
+            }
+            freem &= ~(1ull << r);
             const double inv = 1.0 / rld(v[i], r);
             const double e = lane == r ? inv : -v[i] * inv;
 #pragma unroll
             for (int t = 0; t < K; ++t)
               if (t == s) eta[t] = e;
-            if (lane == s) {
-              prow = r;
-              pq = q;
-            }
+            if (lane == s) prow = r;
             if (lane == r) h = q;
 #pragma unroll
             for (int i2 = i + 1; i2 < kRG; ++i2) {
@@ -451,7 +459,17 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
           }
         }
       }
-      ne = kpath;
+      if (ok) {
+        ne = kpath;
+      } else {  // the shared basis, its statuses and reduced costs
+        kpath = 0;
+        h = lane < m ? s_whead[lane] : -1;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int j = s * 64 + lane;
+          if (j < N) sa[s] = s_wst[j];
+        }
+      }
     }
     PSTAMP(10);
     double lbB = 0.0, ubB = 0.0;
@@ -803,10 +821,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
 #pragma unroll
       for (int t = 0; t < K; ++t)
         if (t == ne) eta[t] = e;
-      if (lane == ne) {
-        prow = r;
-        pq = q;
-      }
+      if (lane == ne) prow = r;
       ++ne;
       ++iters;
       fresh = false;
@@ -880,15 +895,28 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       io.iters[b] = iters;
     }
     if (io.path.k_out != nullptr) {
-      // the node's final path for its children: optimal in the product form
-      // with at most `inherit` etas, else the root (k_out 0)
-      const int ko = (status == 0 && ne > 0 && ne <= io.path.inherit) ? ne : 0;
+      // the node's final basis for its children: its statuses and its basic
+      // columns outside the shared basis in ascending order (optimal, at
+      // most `inherit` of them; else k_out 0: the children start from the
+      // shared basis)
+      int ko = 0;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = s * 64 + lane;
+        ko += __popcll(__ballot(j < N && (sa[s] & 3) == ST_BASIC && s_wst[j] != ST_BASIC));
+      }
+      if (status != 0 || ko > io.path.inherit) ko = 0;
       if (lane == 0) io.path.k_out[b] = ko;
-      if (lane < ko) io.path.path_out[(size_t)b * kPathMax + lane] = (uint32_t)pq | ((uint32_t)prow << 16);
       if (ko > 0) {
+        int base = 0;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           const int j = s * 64 + lane;
+          const bool e = j < N && (sa[s] & 3) == ST_BASIC && s_wst[j] != ST_BASIC;
+          const uint64_t em = __ballot(e);
+          if (e) io.path.path_out[(size_t)b * kPathMax + base +
+                                  __popcll(em & ((1ull << lane) - 1ull))] = (uint32_t)j;
+          base += __popcll(em);
           if (j < N) io.path.st_out[(size_t)b * N + j] = (int8_t)(sa[s] & 3);
         }
       }

@@ -479,13 +479,15 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
       for (int t = kKE - 1; t >= 0; --t) {
         if (t < iters) {
           // u' eta_t: lane products (row lane + row 64 + lane), summed by the
-          // symmetric DPP butterfly (oracle eta_dot).  All products zero:
-          // u_pt is 0 (eta_t's pivot entry is not) and the sum would write
-          // a zero back, so the eta is skipped (K3P's btran_etas)
+          // symmetric DPP butterfly (oracle eta_dot).  All products zero
+          // and u_pt zero: the sum would write a zero back, so the eta is
+          // skipped (K3P's btran_etas); a nonzero u_pt whose product
+          // underflowed is still rewritten, as the oracle does
+          const int pt = rl(prow, t);
           const double p0 = u[0] * eta[t][0], p1 = u[1] * eta[t][1];
-          if (__ballot(p0 != 0.0 || p1 != 0.0) != 0ull) {
+          const bool upt = (lane == pt && u[0] != 0.0) || (64 + lane == pt && u[1] != 0.0);
+          if (__ballot(p0 != 0.0 || p1 != 0.0 || upt) != 0ull) {
             const double acc = wave_sum_sym(p0 + p1);
-            const int pt = rl(prow, t);
 #pragma unroll
             for (int rs = 0; rs < kR; ++rs)
               if (rs * 64 + lane == pt) u[rs] = acc;

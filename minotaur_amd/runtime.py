@@ -21,8 +21,8 @@ _D = ctypes.c_double
 
 LP_PFI_MAX = 32  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
 LP_PFI_WIDE_MAX = 32  # MGPU_LP_PFI_WIDE_MAX: K3PW eta-file cap
-PATH_MAX = 32  # MGPU_PATH_MAX: pivots per path warm start
-PATH_INHERIT = 24  # the batched tree's longest path handed to children (warm mode 2)
+PATH_MAX = 32  # MGPU_PATH_MAX: columns per basis warm start
+PATH_INHERIT = 24  # the batched tree's largest basis difference handed to children (warm mode 2)
 
 # Every entry point declared in include/mgpu.h (checked by the CPU tests).
 EXPORTS = [
@@ -468,9 +468,10 @@ class Context:
 
     def lp_solve_path(self, lb, ub, ws, k_in, path_in, st_in, inherit=PATH_INHERIT,
                       iter_limit=0, want_x=True):
-        """Path warm starts (mgpu_lp_solve_path): node b starts from the shared
-        root basis ``ws`` after its k_in[b] pivots path_in[b] with statuses
-        st_in[b].  Returns (LpOut, k_out, path_out, st_out)."""
+        """Basis warm starts (mgpu_lp_solve_path): node b starts from its
+        parent's basis: statuses st_in[b] and the k_in[b] basic columns
+        path_in[b] outside the shared root basis ``ws``, rebuilt by column
+        replacement.  Returns (LpOut, k_out, path_out, st_out)."""
         p = self.problem
         lb = _np(lb, np.float64)
         ub = _np(ub, np.float64)

@@ -186,7 +186,7 @@ class CpuBnbContext:
                 s2, o2, i2, x2, ko, po, so = oracle.dual_simplex_path(
                     p, f.lb[keep], f.ub[keep], self.ws, k_in, path_in, st_in, self.pfi,
                     min(PATH_INHERIT, self.pfi))
-                self.tot.pfi_pivots += int(np.minimum(i2, self.pfi).sum())
+                self.tot.pfi_pivots += int(np.minimum(i2, np.maximum(self.pfi - k_in, 0)).sum())
                 for t, i in enumerate(keep):
                     wo[i] = (int(ko[t]), po[t].copy(), so[t].copy()) if ko[t] > 0 else None
             elif self.warm:

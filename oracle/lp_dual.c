@@ -56,12 +56,21 @@ typedef struct {
   double *u;           /* m: BTRAN work vector */
 } lpw;
 
-/* Path warm start of the batched tree's warm mode 2 (bnb.cpp): the node's
- * basis is the shared root basis after its path of k pivots (entering column
- * q, row r; packed q | r << 16), with its own column statuses; the etas are
- * rebuilt by FTRAN in path order (the parent's own arithmetic), the reduced
- * costs recomputed from the basis.  k <= 0: the root basis as is.  Out: the
- * node's final path (k_out = 0: children restart from the root). */
+/* Basis warm start of the batched tree's warm mode 2 (bnb.cpp): the node's
+ * basis is its parent's optimal basis, given as the parent's column statuses
+ * st[N] and the k basic columns that are not basic in the shared root basis
+ * B0 (path[0..k), ascending column index).  They replace, one after the
+ * other, the root's basic columns that are nonbasic in st, each at the free
+ * row with the largest |alpha| (lowest row on ties): a column replacement
+ * with partial pivoting, one eta column each, exactly as a pivot makes it.
+ * The reduced costs are recomputed from the basis.  A replacement whose
+ * largest |alpha| is below COLREP_TOL falls back to the root basis.  k <= 0:
+ * the root basis as is.  Out: the node's own final basis in the same form
+ * (k_out = 0: children restart from the root).  ORC_PATH_PIVOTS (tuning A/B
+ * only): the earlier form, the node's pivot path from the root basis. */
+static int g_path_pivots = 0;
+void orc_set_path_pivots(int on) { g_path_pivots = on; }
+#define COLREP_TOL 1e-9
 typedef struct {
   int k;
   const unsigned *path;
@@ -344,6 +353,39 @@ static void pfi_compute_duals(lpw *W) {
   }
 }
 
+/* The basis warm start's column replacement (see orc_path): returns 0, with
+ * the root basis restored, when a replacement has no usable pivot. */
+static int colrep_basis(lpw *W, const orc_path *path) {
+  int m = W->P->m;
+  int *h0 = (int *) malloc(sizeof(int) * (size_t) m);
+  unsigned char *fr = (unsigned char *) malloc((size_t) m);
+  int ok = 1;
+  memcpy(h0, W->head, sizeof(int) * (size_t) m);
+  for (int i = 0; i < m; ++i) fr[i] = path->st[W->head[i]] != ST_BASIC;
+  for (int t = 0; t < path->k; ++t) {
+    int q = (int) (path->path[t] & 0xFFFFu), r = -1;
+    double best = 0.0;
+    ftran_col(W, q, W->alpha_q);
+    for (int i = 0; i < m; ++i)
+      if (fr[i] && fabs(W->alpha_q[i]) > best) { best = fabs(W->alpha_q[i]); r = i; }
+    if (r < 0 || best < COLREP_TOL) { ok = 0; break; }
+    double inv = 1.0 / W->alpha_q[r];
+    double *e = W->eta + (size_t) W->neta * m;
+    for (int i = 0; i < m; ++i) e[i] = i == r ? inv : -W->alpha_q[i] * inv;
+    W->pq[W->neta] = q;
+    W->prow[W->neta++] = r;
+    W->head[r] = q;
+    fr[r] = 0;
+  }
+  if (!ok) {
+    W->neta = 0;
+    memcpy(W->head, h0, sizeof(int) * (size_t) m);
+  }
+  free(h0);
+  free(fr);
+  return ok;
+}
+
 static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub,
                              int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
                              int have_ws, int have_binv, int iter_limit, double *obj_out,
@@ -354,6 +396,7 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
   lpw W;
   int status = 12, iters = 0, fresh = 1;
   double art_bound = ART_BOUND;
+  unsigned char *rootb = 0;   /* basis warm start output: basic in B0 */
   memset(&W, 0, sizeof W);
   W.P = P; W.N = N; W.lb = lb; W.ub = ub;
   if (pfi > 0 && have_ws && have_binv) {
@@ -405,10 +448,13 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
     for (int i = 0; i < m * m; ++i) W.binv[i] = 0.0;
     for (int i = 0; i < m; ++i) W.binv[i * m + i] = -1.0;
   }
-  if (path && path->k > 0 && W.pfi) {
-    /* path warm start: replay the path's pivots on the root basis (FTRAN of
-     * each entering column through B0^{-1} and the etas so far: the eta the
-     * pivot made), the node's statuses, reduced costs of that basis */
+  if (path && path->k_out) {
+    rootb = (unsigned char *) calloc((size_t) N, 1);
+    for (int i = 0; i < m; ++i) rootb[W.head[i]] = 1;
+  }
+  if (path && path->k > 0 && W.pfi && g_path_pivots) {
+    /* pivot path: replay each pivot on the root basis (FTRAN of its entering
+     * column through B0^{-1} and the etas so far) */
     for (int t = 0; t < path->k; ++t) {
       int q = (int) (path->path[t] & 0xFFFFu), r = (int) (path->path[t] >> 16);
       ftran_col(&W, q, W.alpha_q);
@@ -419,6 +465,9 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       W.prow[W.neta++] = r;
       W.head[r] = q;
     }
+    for (int j = 0; j < N; ++j) W.st[j] = path->st[j];
+    pfi_compute_duals(&W);
+  } else if (path && path->k > 0 && W.pfi && colrep_basis(&W, path)) {
     for (int j = 0; j < N; ++j) W.st[j] = path->st[j];
     pfi_compute_duals(&W);
   } else if (have_ws && have_binv == 1 && ws_d) {
@@ -629,14 +678,26 @@ done:
     *obj_out = status == 2 ? INFINITY : -INFINITY;
   }
   if (iters_out) *iters_out = iters;
-  if (path && path->k_out) {
+  if (path && path->k_out && g_path_pivots) {
     /* the node's final path for its children: optimal in the product form
      * with a path no longer than `inherit`, else the root (k_out 0) */
     int ko = (W.pfi && status == 0 && W.neta > 0 && W.neta <= path->inherit) ? W.neta : 0;
     *path->k_out = ko;
     for (int t = 0; t < ko; ++t) path->path_out[t] = (unsigned) W.pq[t] | ((unsigned) W.prow[t] << 16);
     if (ko) for (int j = 0; j < N; ++j) path->st_out[j] = W.st[j];
+  } else if (path && path->k_out) {
+    /* the node's final basis for its children: optimal in the product form
+     * and at most `inherit` basic columns outside B0, else the root (k_out 0) */
+    int ko = 0;
+    if (W.pfi && status == 0)
+      for (int j = 0; j < N; ++j) ko += W.st[j] == ST_BASIC && !rootb[j];
+    if (ko > path->inherit) ko = 0;
+    *path->k_out = ko;
+    for (int j = 0, t = 0; ko && j < N; ++j)
+      if (W.st[j] == ST_BASIC && !rootb[j]) path->path_out[t++] = (unsigned) j;
+    if (ko) for (int j = 0; j < N; ++j) path->st_out[j] = W.st[j];
   }
+  free(rootb);
   free(W.blo); free(W.bhi); free(W.art); free(W.z); free(W.d); free(W.binv);
   free(W.head); free(W.st); free(W.rho); free(W.w); free(W.alpha_r); free(W.alpha_q);
   free(W.eta); free(W.prow); free(W.pq); free(W.u);

@@ -263,13 +263,14 @@ PATH_MAX = 32     # ORC_PATH_MAX = MGPU_PATH_MAX: pivots per path warm start
 
 def dual_simplex_path(p, LB, UB, ws, k_in, path_in, st_in, pfi, inherit, iter_limit=10000,
                       nthreads=1, want_x=True):
-    """Path warm starts (the batched tree's warm mode 2; orc_dual_simplex_path_batch):
-    node b starts from the shared root basis ``ws`` after its k_in[b] pivots
-    path_in[b] (q | r << 16) with statuses st_in[b]; k_in <= 0 = the root
-    basis.  Product form with ``pfi`` etas (the GPU's K3P), dense
-    continuation past it.  Returns (status, obj incl. constant, own pivots,
-    x, k_out, path_out, st_out): the node's final path for its children
-    (k_out 0 = restart from the root)."""
+    """Basis warm starts (the batched tree's warm mode 2; orc_dual_simplex_path_batch):
+    node b starts from its parent's basis: statuses st_in[b] and the k_in[b]
+    basic columns outside the shared root basis ``ws`` (path_in[b], ascending),
+    rebuilt from the root inverse by column replacement with partial pivoting;
+    k_in <= 0 = the root basis.  Product form with ``pfi`` etas (the GPU's
+    K3P), dense continuation past it.  Returns (status, obj incl. constant,
+    own pivots, x, k_out, path_out, st_out): the node's final basis in the
+    same form for its children (k_out 0 = restart from the root)."""
     l = lib()
     f = l.orc_dual_simplex_path_batch
     f.restype = _I
