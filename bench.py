@@ -18,9 +18,11 @@ of the batched tree per GPU, device resident (mgpu_bnb_round):
                (MpiBranchAndBound.cpp:387-389)
 
 Nodes pruned by FBBT are not LP-solved (as in PCBProcessor::process), so
-relaxations/s <= nodes/s.  The stack starts as the root plus B synthetic
-boxes (seeded random branching from the root), a different seed
-per rank (weak scaling, node-sharded); later rounds pop their descendants.
+relaxations/s <= nodes/s.  The pool starts as the root plus B * N synthetic
+boxes (seeded random branching from the root) dealt round-robin
+over the N ranks (the root on rank 0; B per rank: weak scaling); later rounds
+pop their descendants, and every --lb-every rounds the ranks rebalance their
+open nodes by bound (dist.rebalance, inside the timed loop).
 Supplementary objects: the round-1/2 fixed batch (tls4-lin), complete trees
 from the root, configs 3/4/5, the glob batch.
 
@@ -711,6 +713,8 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
     ctx.bnb_config(0, args.warm)
     ctx.bnb_brancher(0)
     ctx.bnb_init(cap)
+    if rank > 0:
+        ctx.bnb_export(1)        # the root belongs to rank 0 (MpiBranchAndBound.cpp:246-279)
     ctx.bnb_import(LB, UB, np.full(B, -math.inf), np.zeros(B, dtype=np.int32))
     comm = mdist.Comm(rank, world, dev)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -748,8 +752,14 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    moved = 0
+    for k in range(args.steps):
         step(acc)
+        if world > 1 and args.lb_every > 0 and (k + 1) % args.lb_every == 0:
+            # one pool across the ranks: bound-aware rebalancing inside the
+            # timed loop (MpiBranchAndBound::LoadBalance_, dist.rebalance)
+            _, mv, _, _ = mdist.rebalance(ctx, comm, B)
+            moved += mv
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -771,6 +781,7 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
                          ("parent-basis warm starts kept as pivot paths from the root basis "
                           "(K3P)" if args.warm == 2 else "root-basis warm start (K3P)"),
                "incumbent": state["inc"]}
+    summary["nodes_migrated"] = moved
     return {"elapsed": float(tot.item()), "nodes": nodes, "lps": lps, "kernels": kernels,
             "summary": summary, "incumbent": state["inc"],
             "rccl_ms": float(np.sum(acc["rccl_ms"]))}
@@ -970,6 +981,9 @@ def main():
     ap.add_argument('--warm', type=int, default=2,
                     help='headline tree warm starts: 2 parent basis as a pivot path (default; '
                          'NodeIncRelaxer semantics), 0 the root basis')
+    ap.add_argument('--lb-every', type=int, default=8,
+                    help='N > 1: rebalance the open nodes across the ranks every this many '
+                         'headline rounds (dist.rebalance; 0 = never)')
     ap.add_argument('--cpu-seconds', type=float, default=16.0)
     ap.add_argument('--tree-cpu-seconds', type=float, default=3.0,
                     help="time_limit of each tree_search entry's one-core reference tree")
@@ -1017,7 +1031,10 @@ def main():
 
     p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
     B = args.batch
-    LB, UB = random_boxes(p, B, mdist.shard_seed(20261017, rank))
+    # ONE pool: the root (rank 0) plus B * world seeded boxes, dealt
+    # round-robin (MpiBranchAndBound.cpp:142-188); B per rank (weak scaling)
+    LB, UB = random_boxes(p, B * world, 20261017)
+    LB, UB = LB[rank::world].copy(), UB[rank::world].copy()
     h = tree_rounds(ctx, dev, rank, world, p, LB, UB, args)
     elapsed, nodes, lps = h["elapsed"], h["nodes"], h["lps"]
     progress(rank, f"headline done: {1e3 * elapsed / args.steps:.2f} ms/step, "

@@ -371,8 +371,10 @@ typedef struct {
   long long sb_lps, sb_pivots;  /* reliability branching: strong-branching
                                    LPs (also OsiLPStats::calls) and pivots */
   long long sb_pruned;          /* nodes PrunedByBrancher                 */
-  long long sb_modified;        /* nodes ModifiedByBrancher (re-queued
-                                   with the one-sided bound change)       */
+  long long sb_modified;        /* nodes ModifiedByBrancher (solved again
+                                   with the one-sided bound change from the
+                                   last strong-branching basis; counted in
+                                   nodes and ndec[0] once more)           */
   long long pfi_pivots;         /* node-LP pivots run by the product-form
                                    kernel itself (K3P / K3PW: at most its
                                    eta cap per LP; 0 for dense kernels)   */
@@ -403,8 +405,9 @@ int mgpu_bnb_config(mgpu_ctx *ctx, int order, int warm);
  *          root's presolve (BranchAndBound::processRoot_).  At batch 1 this
  *          is BranchAndBound::solve's sequence (tests/test_ref_tree_gpu.py);
  *          larger batches pop `batch` nodes per round.  Not shardable.
- * warm 2:  every node LP starts from its parent's optimal basis kept as a
- *          pivot path from the root basis (mgpu_lp_solve_path; K3P, MaxVio). */
+ * warm 2:  every node LP starts from its parent's optimal basis kept as its
+ *          column statuses + basic columns outside the root basis, rebuilt by
+ *          column replacement (mgpu_lp_solve_path; K3P, MaxVio). */
 /* Guided dive (IntVarHandler option guided_dive, default on,
  * Environment.cpp:160-163): with an incumbent, the child whose bound moves
  * the variable toward the incumbent's value comes first.  Order 2 only (the

@@ -71,11 +71,15 @@ struct BnbState {
   DevBuf pc_up, pc_dn, cnt_up, cnt_dn, last, last_new, ppvar, ppval, bnlb, bpvar, bpval, rflag, rrank,
       nsb, sb_off, sb_var, sb_val, dec2, nev, ev_var, ev_side, ev_cost, rcnt, clb, cub, cnode,
       cst, cobj, cit, ev_off, cv_var, cv_side, cv_cost;
+  // chained strong branching: per batch node, its chain slot, stop flag,
+  // the step's LP list and count
+  DevBuf ch_head, ch_st, ch_d, ch_binv, sbstop, sblist, sbcnt;
   // path warm starts (warm 2): per pool slot, per batch (gathered in) and out
   DevBuf ppk, ppath, ppst, bpk, bppath, bpst, opk, oppath, opst;
   int inherit = 0;             // longest path handed to children (<= the eta cap)
   // order 2: the host heap, free pool slots, next node id
   std::vector<HeapNode> heap;
+  std::vector<HeapNode> front;  // nodes modified by the brancher: solved again next
   std::vector<int> free_slots;
   long long next_id = 0;
   bool guided = true;          // IntVarHandler guided_dive (Environment.cpp:160-163)
@@ -92,7 +96,7 @@ struct BnbState {
                       &nsb, &sb_off, &sb_var, &sb_val, &dec2, &nev, &ev_var, &ev_side, &ev_cost,
                       &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit, &ev_off, &cv_var, &cv_side,
                       &cv_cost, &ppk, &ppath, &ppst, &bpk, &bppath, &bpst, &opk, &oppath, &opst,
-                      &cslots})
+                      &cslots, &ch_head, &ch_st, &ch_d, &ch_binv, &sbstop, &sblist, &sbcnt})
       b->release();
   }
 };
@@ -135,6 +139,14 @@ int ensure_batch(mgpu_ctx *c, BnbState &s, int B) {
     HIPCHK(c, s.ev_var.ensure((size_t)B * kRelEvents * 4));
     HIPCHK(c, s.ev_side.ensure((size_t)B * kRelEvents));
     HIPCHK(c, s.ev_cost.ensure((size_t)B * kRelEvents * 8));
+    const size_t N = n + m;
+    HIPCHK(c, s.ch_head.ensure((size_t)B * m * 4 + 4));
+    HIPCHK(c, s.ch_st.ensure((size_t)B * N + 4));
+    HIPCHK(c, s.ch_d.ensure((size_t)B * N * 8));
+    HIPCHK(c, s.ch_binv.ensure((size_t)B * m * m * 8 + 8));
+    HIPCHK(c, s.sbstop.ensure((size_t)B + 4));
+    HIPCHK(c, s.sblist.ensure((size_t)B * 4));
+    HIPCHK(c, s.sbcnt.ensure(16));
   }
   if (s.warm == 1 || s.rel) {  // reliability branching needs each node's optimal basis
     const size_t N = n + m;
@@ -175,7 +187,9 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
                               s.pnlb.as<double>(), s.ppvar.as<int32_t>(), s.ppval.as<double>(),
                               s.bnlb.as<double>(), s.bpvar.as<int32_t>(), s.bpval.as<double>(),
                               c->stream));
-  int32_t *tot = reinterpret_cast<int32_t *>(s.rcnt.as<char>() + 32);  // [2] after counters
+  // after the counters: [0] branching nodes, [1] strong-branching candidates,
+  // [2] observations, [3] the largest candidate count of a node
+  int32_t *tot = reinterpret_cast<int32_t *>(s.rcnt.as<char>() + 32);
   HIPCHK(c, hipMemsetAsync(s.rcnt.p, 0, 48, c->stream));
   RelIO r{};
   r.nb = nb;
@@ -217,10 +231,11 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
   r.cv_side = s.cv_side.as<int8_t>();
   r.cv_cost = s.cv_cost.as<double>();
   r.counters = s.rcnt.as<unsigned long long>();
+  r.nsb_max = tot + 3;
   HIPCHK(c, launch_rel_rank(r, s.rflag.as<int32_t>(), s.rrank.as<int32_t>(), tot, c->stream));
   HIPCHK(c, launch_rel_prepare(r, s.sb_off.as<int32_t>(), tot + 1, c->stream));
-  int32_t h_tot[2] = {0, 0};
-  HIPCHK(c, hipMemcpyAsync(h_tot, tot, 8, hipMemcpyDeviceToHost, c->stream));
+  int32_t h_tot[4] = {0, 0, 0, 0};
+  HIPCHK(c, hipMemcpyAsync(h_tot, tot, 16, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const int nchild = 2 * h_tot[1];
   if (nchild > 0) {
@@ -233,25 +248,49 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
     }
     HIPCHK(c, launch_rel_children(r, s.wlb.as<double>(), s.wub.as<double>(), s.clb.as<double>(),
                                   s.cub.as<double>(), s.cnode.as<int32_t>(), c->stream));
-    // the strong-branching LPs: child -> its node's optimal basis (strides
-    // per node, indexed through ws_index), ReliabilityBrancher's iteration cap
+    r.c_status = s.cst.as<int32_t>();
+    r.c_obj = s.cobj.as<double>();
+    r.c_iters = s.cit.as<int32_t>();
+    // the strong-branching LPs, chained per node as the reference's engine
+    // runs them: every LP from the node's chain slot (its optimal basis, then
+    // whatever basis the last optimal / iteration-limited LP left) and back
+    // into it; ReliabilityBrancher's iteration cap; after each candidate's
+    // pair the nodes with a verdict stop
+    const LpWarm node_ws{s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), s.wo_d.as<double>(),
+                         s.wo_binv.as<double>(), m, N, N, (long)m * m};
+    HIPCHK(c, launch_rel_chain_init(r, node_ws, s.ch_head.as<int32_t>(), s.ch_st.as<int8_t>(),
+                                    s.ch_d.as<double>(), s.ch_binv.as<double>(),
+                                    s.sbstop.as<uint8_t>(), m, c->stream));
     LpIO io{};
-    io.batch = nchild;
+    io.batch = nb;                    // at most one LP per node and step
     io.lb = s.clb.as<double>();
     io.ub = s.cub.as<double>();
     io.box_stride = n;
-    io.ws = LpWarm{s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), s.wo_d.as<double>(),
-                   s.wo_binv.as<double>(), m, N, N, (long)m * m};
+    io.ws = LpWarm{s.ch_head.as<int32_t>(), s.ch_st.as<int8_t>(), s.ch_d.as<double>(),
+                   s.ch_binv.as<double>(), m, N, N, (long)m * m};
     io.ws_index = s.cnode.as<int32_t>();
+    io.wo_head = s.ch_head.as<int32_t>();
+    io.wo_st = s.ch_st.as<int8_t>();
+    io.wo_d = s.ch_d.as<double>();
+    io.wo_binv = s.ch_binv.as<double>();
+    io.wo_index = s.cnode.as<int32_t>();
+    io.node_list = s.sblist.as<int32_t>();
+    io.node_count = s.sbcnt.as<int32_t>();
+    io.list_lo = 0;
+    io.list_hi = 0x7fffffff;
     io.iter_limit = kRelIterLimit;
     io.status = s.cst.as<int32_t>();
     io.obj = s.cobj.as<double>();
     io.iters = s.cit.as<int32_t>();
-    const int lrc = launch_lp_nodes(c, io);
-    if (lrc != MGPU_OK) return lrc;
-    r.c_status = s.cst.as<int32_t>();
-    r.c_obj = s.cobj.as<double>();
-    r.c_iters = s.cit.as<int32_t>();
+    for (int step = 0; step < 2 * h_tot[3]; ++step) {
+      HIPCHK(c, hipMemsetAsync(s.sbcnt.p, 0, 4, c->stream));
+      HIPCHK(c, launch_rel_chain_list(r, step, s.sbstop.as<uint8_t>(), s.sblist.as<int32_t>(),
+                                      s.sbcnt.as<int32_t>(), c->stream));
+      const int lrc = launch_lp_nodes(c, io);
+      if (lrc != MGPU_OK) return lrc;
+      if (step & 1)
+        HIPCHK(c, launch_rel_chain_stop(r, step >> 1, s.sbstop.as<uint8_t>(), c->stream));
+    }
   }
   HIPCHK(c, launch_rel_decide(r, c->stream));
   s.calls += h_tot[0];
@@ -266,7 +305,8 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
 // direction first, or — guided dive, with an incumbent — down first when the
 // incumbent's value of the variable is below the node's (IntVarHandler::
 // getBranches, IntVarHandler.cpp:125-175).
-int heap_children(mgpu_ctx *c, BnbState &s, BnbIO &io, int nb, const std::vector<uint32_t> &sel) {
+int heap_children(mgpu_ctx *c, BnbState &s, BnbIO &io, int nb, const std::vector<uint32_t> &sel,
+                  const std::vector<HeapNode> &popped) {
   std::vector<int32_t> dec(nb), bvar(nb), dep(nb);
   std::vector<double> obj(nb), bval(nb);
   std::vector<int8_t> bup(nb);
@@ -291,10 +331,13 @@ int heap_children(mgpu_ctx *c, BnbState &s, BnbIO &io, int nb, const std::vector
   std::vector<Kid> kids;
   for (int i = 0; i < nb; ++i) {
     if (dec[i] != 0 && dec[i] != 5) continue;
-    if (dec[i] == 5) {  // reliability's modified node: one child (not in heap mode)
+    if (dec[i] == 5) {
+      // ModifiedByBrancher: the same node (its id) is solved again right
+      // away with the bound change (PCBProcessor.cpp:295-310), ahead of
+      // the heap
       const int sl = take();
       cs.push_back(sl);
-      kids.push_back({obj[i], dep[i], sl, 0});
+      s.front.push_back(HeapNode{obj[i], dep[i], popped[i].id, sl});
       continue;
     }
     const int s_pref = take(), s_other = take();   // child index p (preferred), p + 1
@@ -320,7 +363,7 @@ int heap_children(mgpu_ctx *c, BnbState &s, BnbIO &io, int nb, const std::vector
     s.heap.push_back(HeapNode{k.lb, k.depth, s.next_id++, k.slot});
     std::push_heap(s.heap.begin(), s.heap.end(), heap_greater);
   }
-  s.count = (int)s.heap.size();
+  s.count = (int)(s.heap.size() + s.front.size());
   return MGPU_OK;
 }
 
@@ -506,9 +549,17 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   const bool root_round = heap && s.tot.rounds == 0;
   int nb, base = 0, live = 0, holes = 0;
   std::vector<uint32_t> sel;
+  std::vector<HeapNode> popped;
   if (heap) {
-    // TreeManager::getCandidate: the heap top, pruned lazily by the
+    // nodes modified by the brancher first (their process() call goes on),
+    // then TreeManager::getCandidate: the heap top, pruned lazily by the
     // incumbent (TreeManager::shouldPrune_, :403-413), then removed
+    size_t nf = 0;
+    for (; nf < s.front.size() && (int)sel.size() < batch; ++nf) {
+      sel.push_back((uint32_t)s.front[nf].slot);
+      popped.push_back(s.front[nf]);
+    }
+    s.front.erase(s.front.begin(), s.front.begin() + nf);
     while ((int)sel.size() < batch && !s.heap.empty()) {
       const HeapNode top = s.heap.front();
       std::pop_heap(s.heap.begin(), s.heap.end(), heap_greater);
@@ -519,9 +570,10 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
         continue;
       }
       sel.push_back((uint32_t)top.slot);
+      popped.push_back(top);
     }
     nb = (int)sel.size();
-    live = (int)s.heap.size() + nb;
+    live = (int)(s.heap.size() + s.front.size()) + nb;
     s.count = live;
     if (nb <= 0) {
       s.tot.open = 0;
@@ -753,6 +805,12 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     io.ws_st = s.pws_st.as<int8_t>();
     io.ws_d = s.pws_d.as<double>();
     io.ws_binv = s.pws_binv.as<double>();
+    if (s.rel) {  // a modified node resumes from its strong branching's basis
+      io.mo_head = s.ch_head.as<int32_t>();
+      io.mo_st = s.ch_st.as<int8_t>();
+      io.mo_d = s.ch_d.as<double>();
+      io.mo_binv = s.ch_binv.as<double>();
+    }
   }
   HIPCHK(c, hipMemsetAsync(s.out.p, 0, sizeof(BnbOut), c->stream));
   io.defer_children = heap ? 1 : 0;
@@ -763,7 +821,7 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     HIPCHK(c, hipMemcpyAsync(rcnt, s.rcnt.p, sizeof rcnt, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (heap) {
-    rc = heap_children(c, s, io, nb, sel);
+    rc = heap_children(c, s, io, nb, sel, popped);
     if (rc != MGPU_OK) return rc;
   } else if (!bfs) {
     s.count = base + o.nchild;

@@ -185,14 +185,20 @@ __global__ __launch_bounds__(256) void bnb_children(BnbIO io, int n) {
       cu[k] = (k == j && !up_first) ? floor(v) : u;
     }
     if (io.ws_head != nullptr) {
+      // the engine's basis after the node's strong branching (PCBProcessor
+      // resolves the modified node right away, PCBProcessor.cpp:295-310)
+      const bool mo = io.mo_head != nullptr;
+      const int32_t *sh = mo ? io.mo_head : io.wo_head;
+      const int8_t *ss = mo ? io.mo_st : io.wo_st;
+      const double *sd = mo ? io.mo_d : io.wo_d, *sb = mo ? io.mo_binv : io.wo_binv;
       const int m = io.m, N = io.N;
       const size_t mm = (size_t)m * m;
-      for (int k = lane; k < m; k += 64) io.ws_head[c * m + k] = io.wo_head[(size_t)i * m + k];
+      for (int k = lane; k < m; k += 64) io.ws_head[c * m + k] = sh[(size_t)i * m + k];
       for (int k = lane; k < N; k += 64) {
-        io.ws_st[c * N + k] = io.wo_st[(size_t)i * N + k];
-        io.ws_d[c * N + k] = io.wo_d[(size_t)i * N + k];
+        io.ws_st[c * N + k] = ss[(size_t)i * N + k];
+        io.ws_d[c * N + k] = sd[(size_t)i * N + k];
       }
-      for (size_t k = lane; k < mm; k += 64) io.ws_binv[c * mm + k] = io.wo_binv[(size_t)i * mm + k];
+      for (size_t k = lane; k < mm; k += 64) io.ws_binv[c * mm + k] = sb[(size_t)i * mm + k];
     }
     if (lane == 0) {
       io.pnlb[c] = io.obj[i];

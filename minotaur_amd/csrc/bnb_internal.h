@@ -35,6 +35,12 @@ struct BnbIO {
   const int32_t *wo_head;
   const int8_t *wo_st;
   const double *wo_d, *wo_binv;
+  // a node modified by the brancher (decision 5) is solved again from the
+  // basis its strong branching left (the chain slot, batch-indexed; null:
+  // wo_*)
+  const int32_t *mo_head;
+  const int8_t *mo_st;
+  const double *mo_d, *mo_binv;
   int32_t *ws_head;             // [cap][m]
   int8_t *ws_st;                // [cap][N]
   double *ws_d, *ws_binv;       // [cap][N], [cap][m][m]
@@ -141,7 +147,17 @@ struct RelIO {
   int8_t *cv_side;
   double *cv_cost;
   unsigned long long *counters; // [4] strong-branching LPs, pruned, modified, their pivots
+  int32_t *nsb_max;             // device: the round's largest nsb (rel_prepare)
 };
+// Chained strong branching: the nodes' chain slots (one warm start per node)
+// start as the node's optimal basis; step s solves the s-th strong-branching
+// LP of every node still strong-branching, from and back into its slot.
+hipError_t launch_rel_chain_init(const RelIO &io, const LpWarm &node_ws, int32_t *ch_head,
+                                 int8_t *ch_st, double *ch_d, double *ch_binv, uint8_t *stopped,
+                                 int m, hipStream_t stream);
+hipError_t launch_rel_chain_list(const RelIO &io, int s, const uint8_t *stopped, int32_t *list,
+                                 int32_t *count, hipStream_t stream);
+hipError_t launch_rel_chain_stop(const RelIO &io, int c, uint8_t *stopped, hipStream_t stream);
 hipError_t launch_rel_rank(const RelIO &io, int32_t *flag, int32_t *rank, int32_t *total,
                            hipStream_t stream);
 hipError_t launch_rel_prepare(const RelIO &io, int32_t *sb_off, int32_t *total,

@@ -22,7 +22,9 @@
 //   rel_children          : their child boxes (getBrMod: down ub = floor x,
 //                           up lb = ceil x) and warm-start index (the node's
 //                           own optimal basis);
-//   (K3: all children in one batch, iteration limit 25, :101)
+//   rel_chain_*           : the strong-branching LPs chained per node through
+//                           one warm-start slot (K3 / K3L steps, iteration
+//                           limit 25, :101), stopping at the first verdict;
 //   rel_decide            : findBestCandidate_ (:75-159) per node: reliable
 //                           pseudocost scores, the strong-branching results
 //                           (shouldPrune_, useStrongBranchInfo_: prune / one-
@@ -179,6 +181,7 @@ __global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
     }
   }
   io.nsb[b] = nsb;
+  if (nsb > 0) atomicMax(io.nsb_max, nsb);
 }
 
 // one wave per strong-branching child: the node's (FBBT-tightened) box with
@@ -230,6 +233,27 @@ __device__ __forceinline__ bool sb_prune(double chcutoff, double change, int st,
   }
 }
 
+// candidate k of node b after both strong-branching LPs: the changes
+// (max(obj - objval, 0), zeroed when a side is unreliable) and
+// useStrongBranchInfo_'s verdict: -1 a side unreliable (no observation),
+// 0 none, 1 both sides pruned, 2 the up side pruned (the down branch's bound
+// change), 3 the down side pruned (the up branch's)
+__device__ __forceinline__ int sb_outcome(const RelIO &io, size_t off, int k, double objval,
+                                          double maxchange, double &cd, double &cu) {
+  const int sd = io.c_status[off + 2 * k], su = io.c_status[off + 2 * k + 1];
+  cd = fmax(io.c_obj[off + 2 * k] - objval, 0.0);
+  cu = fmax(io.c_obj[off + 2 * k + 1] - objval, 0.0);
+  bool is_rel = true;
+  const bool pd = sb_prune(maxchange, cd, sd, is_rel);
+  const bool pu = sb_prune(maxchange, cu, su, is_rel);
+  if (!is_rel) {
+    cu = 0.0;
+    cd = 0.0;
+    return -1;
+  }
+  return (pu && pd) ? 1 : pu ? 2 : pd ? 3 : 0;
+}
+
 __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b >= io.nb) return;
@@ -272,26 +296,23 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
     const size_t off = 2 * (size_t)io.sb_off[b];
     int status = 0;   // 0 NotModified, 1 Pruned, 2 Modified
     int mvar = -1, mup = 0;
+    int ran = 0;       // candidates strong-branched (the loop stops at a verdict)
     for (int k = 0; k < nsb; ++k) {
       const int j = io.sb_var[(size_t)b * kRelMaxCands + k];
       const double v = io.sb_val[(size_t)b * kRelMaxCands + k];
       const double dd = v - floor(v), ud = ceil(v) - v;
-      const int sd = io.c_status[off + 2 * k], su = io.c_status[off + 2 * k + 1];
-      double cd = fmax(io.c_obj[off + 2 * k] - objval, 0.0);
-      double cu = fmax(io.c_obj[off + 2 * k + 1] - objval, 0.0);
-      bool is_rel = true;
-      const bool pd = sb_prune(maxchange, cd, sd, is_rel);
-      const bool pu = sb_prune(maxchange, cu, su, is_rel);
-      if (!is_rel) {
-        cu = 0.0;
-        cd = 0.0;
-      } else if (pu && pd) {
+      double cd, cu;
+      const int oc = sb_outcome(io, off, k, objval, maxchange, cd, cu);
+      ran = k + 1;
+      if (oc < 0) {
+        // an unreliable side: no verdict, no observation
+      } else if (oc == 1) {
         status = 1;
-      } else if (pu) {
+      } else if (oc == 2) {
         status = 2;       // the down branch's bound change
         mvar = j;
         mup = 0;
-      } else if (pd) {
+      } else if (oc == 3) {
         status = 2;       // the up branch's bound change
         mvar = j;
         mup = 1;
@@ -365,15 +386,58 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
       io.bup[b] = (int8_t)mup;
       atomicAdd(&io.counters[2], 1ull);
     }
-    if (nsb > 0) {
+    if (ran > 0) {  // the LPs the reference solves: up to the verdict
       unsigned long long piv = 0;
-      for (int c = 0; c < 2 * nsb; ++c) piv += (unsigned long long)io.c_iters[off + c];
-      atomicAdd(&io.counters[0], (unsigned long long)(2 * nsb));
+      for (int c = 0; c < 2 * ran; ++c) piv += (unsigned long long)io.c_iters[off + c];
+      atomicAdd(&io.counters[0], (unsigned long long)(2 * ran));
       atomicAdd(&io.counters[3], piv);
     }
   }
   io.dec_out[b] = dec;
   io.nev[b] = nev;
+}
+
+// ---- chained strong branching (ReliabilityBrancher::strongBranch_, :469-506):
+// the brancher's LPs run one after the other through the node's engine, each
+// resolving from the basis the previous one left (HipLPEngine / CpuLPEngine
+// keep a solve's basis when it ended optimal or at the iteration limit, and
+// the one it started from otherwise; the first starts from the node's optimal
+// basis), and findBestCandidate_ stops strong-branching at the first verdict
+// (:111-118).  One chain slot per node, solved in steps: step s is the s-th
+// LP of every node still strong-branching.
+
+__global__ __launch_bounds__(256) void rel_chain_init(RelIO io, LpWarm w, int32_t *ch_head,
+                                                      int8_t *ch_st, double *ch_d,
+                                                      double *ch_binv, uint8_t *stopped, int m) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= io.nb) return;
+  if (lane == 0) stopped[b] = 0;
+  if (io.nsb[b] == 0) return;
+  const int N = io.n + m;
+  const size_t mm = (size_t)m * m;
+  for (int k = lane; k < m; k += 64) ch_head[(size_t)b * m + k] = w.head[b * w.s_head + k];
+  for (int k = lane; k < N; k += 64) {
+    ch_st[(size_t)b * N + k] = w.st[b * w.s_st + k];
+    ch_d[(size_t)b * N + k] = w.d[b * w.s_d + k];
+  }
+  for (size_t k = lane; k < mm; k += 64) ch_binv[(size_t)b * mm + k] = w.binv[b * w.s_binv + k];
+}
+
+__global__ __launch_bounds__(256) void rel_chain_list(RelIO io, int s, const uint8_t *stopped,
+                                                      int32_t *list, int32_t *count) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb || stopped[b] || s >= 2 * io.nsb[b]) return;
+  list[atomicAdd(count, 1)] = 2 * io.sb_off[b] + s;
+}
+
+__global__ __launch_bounds__(256) void rel_chain_stop(RelIO io, int c, uint8_t *stopped) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb || stopped[b] || c >= io.nsb[b]) return;
+  const double objval = io.obj[b];
+  double cd, cu;
+  if (sb_outcome(io, 2 * (size_t)io.sb_off[b], c, objval, io.cutoff - objval, cd, cu) > 0)
+    stopped[b] = 1;
 }
 
 // the round's observations packed in node order (offsets: excl_scan of nev)
@@ -450,6 +514,30 @@ hipError_t launch_rel_children(const RelIO &io, const double *wlb, const double 
   if (io.nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(rel_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io, wlb, wub,
                      clb, cub, cnode);
+  return hipGetLastError();
+}
+
+hipError_t launch_rel_chain_init(const RelIO &io, const LpWarm &node_ws, int32_t *ch_head,
+                                 int8_t *ch_st, double *ch_d, double *ch_binv, uint8_t *stopped,
+                                 int m, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_chain_init, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io, node_ws,
+                     ch_head, ch_st, ch_d, ch_binv, stopped, m);
+  return hipGetLastError();
+}
+
+hipError_t launch_rel_chain_list(const RelIO &io, int s, const uint8_t *stopped, int32_t *list,
+                                 int32_t *count, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_chain_list, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io, s,
+                     stopped, list, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_rel_chain_stop(const RelIO &io, int c, uint8_t *stopped, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rel_chain_stop, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io, c,
+                     stopped);
   return hipGetLastError();
 }
 

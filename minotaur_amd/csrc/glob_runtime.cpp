@@ -20,6 +20,7 @@
 //   children   two per branched node, each with the node's tightened box,
 //        the branching bound and the node's rows.
 // One small record comes back per round (counts, best feasible node).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -164,7 +165,10 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
   GlobState &s = *c->glob;
   const QuadState &q = *c->quad;
   HIPCHK(c, hipSetDevice(c->device));
-  if (incumbent < s.inc) s.inc = incumbent;
+  if (incumbent < s.inc) {  // an outside incumbent: no point of ours matches it
+    s.inc = incumbent;
+    std::fill(s.best_x.begin(), s.best_x.end(), NAN);
+  }
   int nb = batch < s.count ? batch : s.count;
   if (s.count + nb > s.cap) nb = s.cap - s.count;  // children must fit: base + 2 nb <= cap
   if (nb <= 0) {

@@ -736,13 +736,14 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         for (int j = lane; j < N; j += 64)
           io.rc[(size_t)b * N + j] = C.st[j] == ST_BASIC ? 0.0 : C.d[j];
       if (io.wo_head != nullptr) {
-        if (lane < m) io.wo_head[(size_t)b * m + lane] = h;
+        const size_t bo = io.wo_index != nullptr ? (size_t)io.wo_index[b] : (size_t)b;
+        if (lane < m) io.wo_head[bo * m + lane] = h;
         for (int j = lane; j < N; j += 64) {
-          io.wo_st[(size_t)b * N + j] = C.st[j];
-          io.wo_d[(size_t)b * N + j] = C.d[j];
+          io.wo_st[bo * N + j] = C.st[j];
+          io.wo_d[bo * N + j] = C.d[j];
         }
         if (lane < m) {
-          double *dst = io.wo_binv + (size_t)b * m * m + lane;
+          double *dst = io.wo_binv + bo * m * m + lane;
   #pragma unroll
           for (int k = 0; k < M; ++k)
             if (k < m) dst[(size_t)k * m] = binv[k];   // column-major: coalesced

@@ -768,12 +768,13 @@ __global__ __launch_bounds__(kT) void lp_large_kernel(DevLP lp, LpIO io, double 
         for (int j = tid; j < N; j += kT)
           io.rc[(size_t)b * N + j] = s.st[j] == ST_BASIC ? 0.0 : s.d[j];
       if (io.wo_head != nullptr) {
-        for (int i = tid; i < m; i += kT) io.wo_head[(size_t)b * m + i] = s.head[i];
+        const size_t bo = io.wo_index != nullptr ? (size_t)io.wo_index[b] : (size_t)b;
+        for (int i = tid; i < m; i += kT) io.wo_head[bo * m + i] = s.head[i];
         for (int j = tid; j < N; j += kT) {
-          io.wo_st[(size_t)b * N + j] = s.st[j];
-          io.wo_d[(size_t)b * N + j] = s.d[j];
+          io.wo_st[bo * N + j] = s.st[j];
+          io.wo_d[bo * N + j] = s.d[j];
         }
-        double *dst = io.wo_binv + (size_t)b * mm;
+        double *dst = io.wo_binv + bo * mm;
         for (size_t e = tid; e < mm; e += kT) dst[e] = s.Bi[e];
       }
     } else if (tid == 0) {

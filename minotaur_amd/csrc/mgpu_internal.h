@@ -128,6 +128,8 @@ struct LpIO {
   double *wo_d;                 // [B][n+m]
   double *wo_binv;              // [B][m][m]
   double *rc;                   // [B][n+m] reduced costs out, 0 for basic columns (optional)
+  const int32_t *wo_index;      // [B] or null: LP b's warm start out goes to row wo_index[b]
+                                //   (chained strong branching: in place, the node's slot)
   // K3 and K3L: solve just the nodes node_list[list_lo .. min(*node_count,
   // list_hi)) (device memory; the overflow list of K3P / K3PW), null = every node
   // of the batch.  list_ws: the per-node warm start is indexed by list

@@ -568,15 +568,19 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     const int kcap = pfi_cap(c, &wide);
     const int m = c->lp.m, N = c->lp.n + c->lp.m;
     const size_t slot_bytes = (size_t)m * 4 + (size_t)N * 9 + (size_t)m * m * 8 + 48;
+    // continuation slots for a quarter of the batch (at least 4096): 1-3 %
+    // of the LPs fill the eta file on the hot path, so a slot per LP (35 KB
+    // each at m = 64: 18 GB for 524 288 LPs) would be memory held for
+    // nothing; overflows past the slots restart from the shared warm start
+    // (the same optimum, more pivots)
     const size_t max_slots = kPfiOvfBytes / slot_bytes;
-    const int cap = (size_t)io.batch < max_slots ? io.batch : (int)max_slots;
+    size_t want = (size_t)io.batch / 4 > 4096 ? (size_t)io.batch / 4 : 4096;
+    if (want > (size_t)io.batch) want = (size_t)io.batch;
+    const int cap = want < max_slots ? (int)want : (int)max_slots;
     HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 4) * sizeof(int32_t)));
     if (io.path.k != nullptr && (wide || kcap > kPathMax))
       return fail(c, MGPU_ERR_ARG, "%s: path warm starts run on K3P (m <= 64) with an eta cap "
                   "<= %d", who, kPathMax);
-    if (io.path.k != nullptr && cap < io.batch)
-      return fail(c, MGPU_ERR_NOMEM, "%s: path warm starts need a continuation slot per LP "
-                  "(%d LPs, %d slots)", who, io.batch, cap);
     const size_t sb_head = al16h((size_t)cap * m * 4), sb_st = al16h((size_t)cap * N),
                  sb_d = al16h((size_t)cap * N * 8), sb_binv = al16h((size_t)cap * m * m * 8),
                  sb_it = (size_t)cap * 4;

@@ -44,4 +44,6 @@ def solve(ctx, qp, batch=1024, capacity=None, max_rounds=10**9, incumbent=math.i
         if st.open == 0:
             break
     obj, x = ctx.glob_best()
-    return obj, (x if math.isfinite(obj) else None), st, time.perf_counter() - t0
+    # a finite objective from an outside incumbent comes without our point
+    ok = math.isfinite(obj) and x is not None and not any(math.isnan(v) for v in x)
+    return obj, (x if ok else None), st, time.perf_counter() - t0

@@ -225,8 +225,10 @@ class CpuBnbContext:
             w = wo[i] if self.warm == 1 else self.ws
             path = wo[i] if self.warm == 2 else None
             if dec == 5:
-                # ModifiedByBrancher: the node again with the bound change
-                nd = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth, w)
+                # ModifiedByBrancher: the node again with the bound change,
+                # from the basis its strong branching left (warm 1)
+                wm = self._chain[i] if self.warm == 1 else w
+                nd = _Node(f.lb[i].copy(), f.ub[i].copy(), obj[i], nodes[i].depth, wm)
                 if up_first:
                     nd.lb[j] = math.ceil(v)
                 else:
@@ -313,35 +315,6 @@ class CpuBnbContext:
                 out.append(((pv[2] + pv[3]) - 1e-5 * (pv[0] + pv[1]) - 1e-6 * max(dd, ud), j))
             return [j for _, j in sorted(out)]
 
-        kids_lb, kids_ub, kids_ws = [], [], []
-        for i in range(nb):
-            if decs[i] != 0:
-                continue
-            maxcnt = 0 if nodes[i].depth > REL_MAX_DEPTH else REL_MAX_CANDS
-            sb[i] = unrel_sorted(i)[:maxcnt]
-            for j in sb[i]:
-                v = x[i][j]
-                for up in (False, True):
-                    lb, ub = f.lb[i].copy(), f.ub[i].copy()
-                    if up:
-                        lb[j] = math.ceil(v)
-                    else:
-                        ub[j] = math.floor(v)
-                    kids_lb.append(lb)
-                    kids_ub.append(ub)
-                    kids_ws.append(wo[i])
-        cst = cobj = cit = None
-        if kids_lb:
-            ws = oracle.WarmStart(*(np.stack([getattr(w, a) for w in kids_ws])
-                                    for a in ('head', 'st', 'binv', 'd')))
-            cst, cobj, cit, _, _ = oracle.dual_simplex_nodes(
-                p, np.stack(kids_lb), np.stack(kids_ub), ws, iter_limit=REL_ITER)
-            self.tot.sb_lps += len(kids_lb)
-            self.tot.sb_pivots += int(np.sum(cit))
-        choice, events = {}, []
-        last_upd = {}
-        off = 0
-
         def sb_prune(chcut, change, st):
             if st in (3, 2, 5):
                 return True, True
@@ -350,6 +323,57 @@ class CpuBnbContext:
             if st == 6:
                 return False, True
             return False, False
+
+        # the strong-branching LPs, chained per node as the reference's engine
+        # runs them (strongBranch_ through one LPEngine, :469-506): each LP
+        # from the basis the previous optimal / iteration-limited one left
+        # (the first from the node's optimal basis), a node stopping after the
+        # first candidate with a verdict (findBestCandidate_ :111-118); step s
+        # is the s-th LP of every node still strong-branching (bnb_rel.hip)
+        for i in range(nb):
+            if decs[i] == 0:
+                maxcnt = 0 if nodes[i].depth > REL_MAX_DEPTH else REL_MAX_CANDS
+                sb[i] = unrel_sorted(i)[:maxcnt]
+        sbn = [i for i in range(nb) if decs[i] == 0 and sb[i]]
+        chain = {i: wo[i] for i in sbn}
+        res = {i: [] for i in sbn}
+        stopped = set()
+        for step in range(2 * max((len(sb[i]) for i in sbn), default=0)):
+            act = [i for i in sbn if i not in stopped and step < 2 * len(sb[i])]
+            if not act:
+                break
+            kl, ku = [], []
+            for i in act:
+                j = sb[i][step >> 1]
+                v = x[i][j]
+                lb, ub = f.lb[i].copy(), f.ub[i].copy()
+                if step & 1:
+                    lb[j] = math.ceil(v)
+                else:
+                    ub[j] = math.floor(v)
+                kl.append(lb)
+                ku.append(ub)
+            ws = oracle.WarmStart(*(np.stack([getattr(chain[i], a) for i in act])
+                                    for a in ('head', 'st', 'binv', 'd')))
+            cst, cobj, cit, _, w2 = oracle.dual_simplex_nodes(
+                p, np.stack(kl), np.stack(ku), ws, iter_limit=REL_ITER)
+            for t, i in enumerate(act):
+                res[i].append((int(cst[t]), float(cobj[t]), int(cit[t])))
+                chain[i] = oracle.WarmStart(w2.head[t].copy(), w2.st[t].copy(),
+                                            w2.binv[t].copy(), w2.d[t].copy())
+                if step & 1:
+                    (sd, od, _), (su, ou, _) = res[i][-2], res[i][-1]
+                    mc = self.inc - obj[i]
+                    pd_, rd = sb_prune(mc, max(od - obj[i], 0.0), sd)
+                    pu_, ru = sb_prune(mc, max(ou - obj[i], 0.0), su)
+                    if rd and ru and (pd_ or pu_):
+                        stopped.add(i)
+        for i in sbn:
+            self.tot.sb_lps += len(res[i])
+            self.tot.sb_pivots += sum(r[2] for r in res[i])
+        self._chain = chain
+        choice, events = {}, []
+        last_upd = {}
 
         for i in range(nb):
             if i in obs:
@@ -376,9 +400,9 @@ class CpuBnbContext:
             for k, j in enumerate(sb[i]):
                 v = xi[j]
                 dd, ud = v - math.floor(v), math.ceil(v) - v
-                sd, su = int(cst[off + 2 * k]), int(cst[off + 2 * k + 1])
-                cd = max(cobj[off + 2 * k] - objval, 0.0)
-                cu = max(cobj[off + 2 * k + 1] - objval, 0.0)
+                (sd, od, _), (su, ou, _) = res[i][2 * k], res[i][2 * k + 1]
+                cd = max(od - objval, 0.0)
+                cu = max(ou - objval, 0.0)
                 pd_, rel_d = sb_prune(maxchange, cd, sd)
                 pu_, rel_u = sb_prune(maxchange, cu, su)
                 if not (rel_d and rel_u):
@@ -414,7 +438,6 @@ class CpuBnbContext:
                 decs[i] = 5
                 choice[i] = mod
                 self.tot.sb_modified += 1
-            off += 2 * len(sb[i])
         for j, c in last_upd.items():   # the round's last writer (largest call number)
             self.last[j] = c
         for j, side, c in events:      # updatePCost_ in node order

@@ -4,13 +4,15 @@ node.
 Reference side (oracle/_ref/libminotaur_hip_integ.so, integ_bnb_tree): the
 unchanged BranchAndBound + TreeManager ("bfs" NodeHeap) + PCBProcessor
 (pres_freq 1: LinearHandler::presolveNode at every node) + NodeIncRelaxer
-(each node from its parent's warm start) + MaxVioBrancher + IntVarHandler
+(each node from its parent's warm start) + MaxVioBrancher or
+ReliabilityBrancher + IntVarHandler
 (guided dive on: the reference default), with the reference's own
 LinearHandler for FBBT and HipLPEngine for the LPs (Clp is absent).
 
 Batched side (libmgpu): mgpu_bnb_* at batch 1 with order 2 (the reference's
 NodeHeap order, lazy pruning, TreeManager's node ids), warm 1 (parent bases,
-root LP from the slack basis after its presolve), MaxVio.
+root LP from the slack basis after its presolve), MaxVio or the batched
+reliability brancher.
 
 Bar: the same number of nodes processed and created, the same number of LP
 solves, the same optimum bit for bit.  Larger batches run the same rounds
@@ -66,15 +68,20 @@ def reference_tree(integ, p, brancher=0, guided=1, hip_fbbt=0):
             "created": int(cnt[1]), "lps": int(cnt[2]), "sb_lps": int(cnt[3])}
 
 
-def batched_tree(ctx, p, batch=1, guided=1, warm=1):
+def batched_tree(ctx, p, batch=1, guided=1, warm=1, brancher=0):
+    """A node the brancher modified is solved again inside the same process()
+    call in the reference: it is not a processed or created node there."""
     ctx.load(p)
     ctx.bnb_guided_dive(guided)
     try:
-        obj, x, st, secs = bnb.solve(ctx, batch=batch, capacity=1 << 18, order=2, warm=warm)
+        obj, x, st, secs = bnb.solve(ctx, batch=batch, capacity=1 << 18, order=2, warm=warm,
+                                     brancher=brancher)
     finally:
         ctx.bnb_guided_dive(1)
-    return {"ub": obj, "processed": st.nodes, "created": 1 + 2 * st.ndec[0], "lps": st.lps,
-            "open": st.open, "x": x, "seconds": secs}
+    mod = st.sb_modified
+    return {"ub": obj, "processed": st.nodes - mod, "created": 1 + 2 * (st.ndec[0] - mod),
+            "lps": st.lps + st.sb_lps, "sb_lps": st.sb_lps, "open": st.open, "x": x,
+            "seconds": secs, "sb_modified": mod, "sb_pruned": st.sb_pruned}
 
 
 def _cases():
@@ -89,15 +96,20 @@ def _cases():
     }
 
 
+@pytest.mark.parametrize('brancher', [0, 1])
 @pytest.mark.parametrize('guided', [1, 0])
 @pytest.mark.parametrize('name', list(_cases()))
-def test_batch1_tree_is_the_reference_tree(integ, ctx, name, guided):
+def test_batch1_tree_is_the_reference_tree(integ, ctx, name, guided, brancher):
+    """brancher 0 MaxVioBrancher; 1 ReliabilityBrancher (strong-branching LPs
+    chained through the engine, stopping at the first verdict; a modified
+    node solved again from the last strong-branching basis): the reference's
+    lps count every LPEngine::solve call, strong branching included."""
     p = _cases()[name]
-    ref = reference_tree(integ, p, guided=guided)
-    gpu = batched_tree(ctx, p, guided=guided)
+    ref = reference_tree(integ, p, guided=guided, brancher=brancher)
+    gpu = batched_tree(ctx, p, guided=guided, brancher=brancher)
     assert gpu["open"] == 0
-    assert (gpu["processed"], gpu["created"], gpu["lps"]) == \
-        (ref["processed"], ref["created"], ref["lps"]), (gpu, ref)
+    assert (gpu["processed"], gpu["created"], gpu["lps"], gpu["sb_lps"]) == \
+        (ref["processed"], ref["created"], ref["lps"], ref["sb_lps"]), (gpu, ref)
     assert gpu["ub"] == ref["ub"]
     hs, hobj = oracle.highs_milp(p)
     assert hs == 0 and abs(gpu["ub"] - hobj) <= 1e-6 * max(1.0, abs(hobj))
