@@ -662,6 +662,26 @@ def qp_relaxation(ctx, dev, rank, world, args, B=1024, reps=3):
     return out
 
 
+def qp_tree(ctx, dev, rank, world, args, B=256, max_rounds=12):
+    """Supplementary (config 4 as a path): branch-and-bound over
+    QP relaxations of color_lab2_4x0 -- every round pops B nodes, K1 FBBT on
+    the equality rows, K5 (MFMA KKT) on the node QPs, decision + MaxVio
+    branching, children pushed -- for a bounded number of rounds."""
+    import torch
+    from minotaur_amd import qp as qpm
+    P = qpm.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'color_lab2_qp.npz'))
+    qpm.solve_tree(ctx, P, batch=16, capacity=1 << 12, max_rounds=1)     # warm-up
+    torch.cuda.synchronize()
+    obj, x, st, secs = qpm.solve_tree(ctx, P, batch=B, capacity=1 << 18, max_rounds=max_rounds)
+    torch.cuda.synchronize()
+    return {"instance": "color_lab2_4x0 (300 binaries, 61 rows, dense Q)", "batch_per_gpu": B,
+            "rounds": int(st.rounds), "nodes": int(st.nodes), "qp_solves": int(st.lps),
+            "ipm_iters_per_qp": st.pivots / max(st.lps, 1), "open": int(st.open),
+            "incumbent": obj, "seconds": secs, "nodes_per_s": st.nodes / secs,
+            "decisions": {"branched": int(st.ndec[0]), "infeasible": int(st.ndec[1]),
+                          "pruned_by_bound": int(st.ndec[2]), "feasible": int(st.ndec[3])}}
+
+
 def lp_flops_tableau(p, pivots):
     """SURVEY 8(d)'s LP flop count: the tableau rank-1 update, 2 m (n + m)
     per pivot (tls4: 19.8 kflop per pivot)."""
@@ -942,6 +962,7 @@ def compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, c
                                                    if ts else None),
             "convex_batch_nodes_per_s": rate("convex_batch"),
             "qp_per_s": rate("qp_relaxation", "qp_per_s"),
+            "qp_tree_nodes_per_s": rate("qp_tree"),
             "knapsack_nodes_per_s": rate("knapsack_nodes"),
             "glob_batch_nodes_per_s": rate("glob_batch"),
             "glob_tree_nodes_per_s": rate("glob_tree"),
@@ -1049,6 +1070,7 @@ def main():
             ("convex_batch", args.no_convex,
              lambda: convex_batch(ctx, dev, rank, world, TB, args)),
             ("qp_relaxation", args.no_qp, lambda: qp_relaxation(ctx, dev, rank, world, args)),
+            ("qp_tree", args.no_qp, lambda: qp_tree(ctx, dev, rank, world, args)),
             ("knapsack_nodes", args.no_knapsack,
              lambda: knapsack_nodes(ctx, dev, rank, world, args)),
             ("glob_batch", args.no_glob, lambda: glob_batch(ctx, dev, rank, world, args)),

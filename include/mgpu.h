@@ -395,6 +395,19 @@ typedef struct {
  *            146-150); the basis lives with the node in HBM, m*4 + (n+m)*9 +
  *            m*m*8 bytes per pool slot (K3 / K3L per-node warm starts). */
 int mgpu_bnb_config(mgpu_ctx *ctx, int order, int warm);
+/* Relaxation of the next mgpu_bnb_init's tree (default 0):
+ *   0: the loaded LP (K3P / K3 / K3L);
+ *   1: the loaded QP (mgpu_load_qp, same columns as the loaded rows): node
+ *      QPs by K5 on the FBBT-tightened boxes — QPDRelaxer + BqpdEngine
+ *      (examples/QPDRelaxer.cpp:56-126, BqpdEngine.cpp:449-534) batched.
+ *      The loaded LP supplies the rows for K1 (LinearHandler::presolveNode,
+ *      without objective propagation: the objective is quadratic) and the
+ *      column types; root warm starts (warm 0), MaxVio branching.  A node QP
+ *      the interior point does not solve within its iteration limit gets a
+ *      phase-1 LP over its box (min 0 s.t. the rows, K3 / K3L): infeasible
+ *      rows make it ProvenInfeasible; a feasible one it could not solve ends
+ *      the round with MGPU_ERR_ENGINE (decision 4). */
+int mgpu_bnb_relaxation(mgpu_ctx *ctx, int kind);
 /* order 2: the reference's own node order — TreeManager's "bfs" NodeHeap
  *          (NodeHeap.cpp:24-47: lowest bound within 1e-6, then shallower,
  *          then the larger node id) kept on the host with std::push_heap /

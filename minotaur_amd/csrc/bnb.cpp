@@ -52,6 +52,7 @@ struct BnbState {
   std::vector<double> best_x;
   mgpu_bnb_stats tot{};
   int order = 0, warm = 0;     // mgpu_bnb_config at init
+  int qp = 0;                  // mgpu_bnb_relaxation at init: node QPs by K5
   int rel = 0;                 // mgpu_bnb_brancher at init: 1 = reliability branching
   long long calls = 0;         // ReliabilityBrancher stats_->calls (findBranches calls)
   int maxsb = 0;               // strong-branching LP capacity of the child buffers
@@ -386,6 +387,14 @@ int mgpu_bnb_guided_dive(mgpu_ctx *c, int on) {
   return MGPU_OK;
 }
 
+int mgpu_bnb_relaxation(mgpu_ctx *c, int kind) {
+  if (!c) return MGPU_ERR_ARG;
+  if (kind < 0 || kind > 1)
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_relaxation: 0 (LP) or 1 (the loaded QP)");
+  c->bnb_relax = kind;
+  return MGPU_OK;
+}
+
 int mgpu_bnb_brancher(mgpu_ctx *c, int kind) {
   if (!c) return MGPU_ERR_ARG;
   if (kind < 0 || kind > 1)
@@ -411,7 +420,11 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   s->order = c->bnb_order;
   s->warm = c->bnb_warm;
   s->rel = c->bnb_brancher;
+  s->qp = c->bnb_relax;
   s->tot.incumbent = incumbent;
+  if (s->qp && (!c->qp || s->warm != 0 || s->rel))
+    return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: QP relaxations need mgpu_load_qp (same columns as "
+                "the loaded rows), root warm starts (warm 0) and MaxVio branching");
   if (s->warm == 2) {
     // path warm starts run on K3P's eta file: the tree hands children paths
     // of at most min(kPathInherit, eta cap) pivots
@@ -465,14 +478,16 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   const int32_t zero = 0;
   HIPCHK(c, hipMemcpyAsync(s->pnlb.p, &ninf, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(s->pdepth.p, &zero, 4, hipMemcpyHostToDevice, c->stream));
-  int rc = mgpu_lp_solve_dev(c, 1, s->plb.as<double>(), s->pub.as<double>(), nullptr, nullptr,
-                             nullptr, nullptr, nullptr, 1, 0, s->r_st.as<int32_t>(),
-                             s->r_obj.as<double>(), s->r_it.as<int32_t>(), nullptr,
-                             s->ws_head.as<int32_t>(), s->ws_st.as<int8_t>(),
-                             s->ws_d.as<double>(), s->ws_binv.as<double>());
-  if (rc != MGPU_OK) return rc;
-  int32_t rst = 0;
-  HIPCHK(c, hipMemcpyAsync(&rst, s->r_st.p, 4, hipMemcpyDeviceToHost, c->stream));
+  int32_t rst = -1;   // QP relaxations: no LP basis to share
+  if (!s->qp) {
+    int rc = mgpu_lp_solve_dev(c, 1, s->plb.as<double>(), s->pub.as<double>(), nullptr, nullptr,
+                               nullptr, nullptr, nullptr, 1, 0, s->r_st.as<int32_t>(),
+                               s->r_obj.as<double>(), s->r_it.as<int32_t>(), nullptr,
+                               s->ws_head.as<int32_t>(), s->ws_st.as<int8_t>(),
+                               s->ws_d.as<double>(), s->ws_binv.as<double>());
+    if (rc != MGPU_OK) return rc;
+    HIPCHK(c, hipMemcpyAsync(&rst, s->r_st.p, 4, hipMemcpyDeviceToHost, c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   s->root_ok = rst == 0;
   s->count = 1;
@@ -677,10 +692,20 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
     lb = s.wlb.as<double>();
     ub = s.wub.as<double>();
   }
-  rc = mgpu_fbbt_dev(c, nb, lb, ub, s.inc, s.wlb.as<double>(), s.wub.as<double>(),
-                     s.inf.as<int32_t>(), s.nm.as<int32_t>(), 0, nullptr, nullptr, nullptr);
+  // LinearHandler::varBndsFromObj_ propagates a linear objective only: a
+  // QP's node FBBT runs without the incumbent
+  rc = mgpu_fbbt_dev(c, nb, lb, ub, s.qp ? INFINITY : s.inc, s.wlb.as<double>(),
+                     s.wub.as<double>(), s.inf.as<int32_t>(), s.nm.as<int32_t>(), 0, nullptr,
+                     nullptr, nullptr);
   if (rc != MGPU_OK) return rc;
-  if (s.warm == 2) {
+  if (s.qp) {
+    // the node's QP relaxation (QPDRelaxer -> BqpdEngine::solve,
+    // examples/QPDRelaxer.cpp:56-126): K5 on the FBBT-tightened boxes, the
+    // FBBT-infeasible nodes skipped
+    rc = qp_solve_nodes(c, nb, s.wlb.as<double>(), s.wub.as<double>(), s.inf.as<int32_t>(), 0,
+                        s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
+                        s.x.as<double>());
+  } else if (s.warm == 2) {
     // each node from its parent's optimal basis (NodeIncRelaxer.cpp:146-150)
     // kept as its pivot path from the root basis; its own final path comes
     // back for its children

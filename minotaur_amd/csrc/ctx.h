@@ -61,6 +61,7 @@ struct mgpu_ctx {
   DevBuf scratch, flag_scratch;
   DevBuf fbbt_next;            // K1 persistent variant: node queue head
   int fbbt_variant = 0;
+  int bnb_relax = 0;          // mgpu_bnb_relaxation: 0 LP (K3P/K3/K3L), 1 QP (K5)
   int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L, 3 K3P
   int lp_pfi = kPfiMax;        // K3P eta-file cap (0: auto never picks K3P)
   int lp_pfi_wide = kPfiWideMax;  // K3PW eta-file cap (0: auto never picks K3PW)
@@ -143,6 +144,10 @@ hipError_t upload(DevBuf &b, const T *src, size_t count) {
 void quad_state_free(mgpu_ctx *c);  // quad_runtime.cpp
 void bnb_state_free(mgpu_ctx *c);   // bnb.cpp
 void qp_state_free(mgpu_ctx *c);    // qp_runtime.cpp
+// K5 over a batch of node boxes; skip[b] != 0 = not solved (qp_runtime.cpp)
+int qp_solve_nodes(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                   const int32_t *skip, int maxit, int32_t *status, double *obj, int32_t *iters,
+                   double *x);
 void glob_state_free(mgpu_ctx *c);  // glob_runtime.cpp
 // an LP batch with per-node warm starts through the K3 / K3L selection of
 // mgpu_lp_solve (mgpu_runtime.cpp); io.next is set here

@@ -161,6 +161,9 @@ struct LpIO {
 constexpr int kPathMax = 32;    // pivots per path warm start (MGPU_PATH_MAX)
 constexpr int kPathInherit = 24; // longest path the batched tree hands to children
 
+// K1: waves per CU a batch too small for one node per lane is spread over
+// (tuned on config 2's complete tree, tools/tree_probe.py)
+constexpr int kFbbtSmallWaves = 8;
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
 constexpr int kLpDefaultIterLimit = 10000;  // OsiLPEngine maxIterLimit_ (OsiLPEngine.cpp:99)

@@ -359,9 +359,21 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   // (best value - objective constant).
   io.has_inc = std::isfinite(incumbent) ? 1 : 0;
   io.inc_ub = io.has_inc ? incumbent - c->lp.objoff : 0.0;
-  // nodes per wave: fewer than 64 puts more waves in flight (latency-bound
-  // kernel); MGPU_FBBT_NPW overrides for experiments
+  // nodes per wave: one per lane fills the chip from kFbbtSmallWaves * CUs *
+  // 64 nodes on; a smaller batch (the narrow rounds of a complete tree)
+  // spreads its nodes over that many waves instead: a wave walks the union of
+  // its nodes' flagged rows, so fewer nodes per wave shorten the round's
+  // critical path (a forced variant keeps one node per lane);
+  // MGPU_FBBT_NPW overrides for experiments
   int npw = kLanes;
+  if (c->fbbt_variant == 0) {
+    const long target = (long)c->num_cus * kFbbtSmallWaves;
+    if ((long)batch < target * kLanes) {
+      const int want = (int)(((long)batch + target - 1) / target);
+      npw = 1;
+      while (npw < want) npw <<= 1;
+    }
+  }
   if (const char *e = getenv("MGPU_FBBT_NPW")) {
     const int v = atoi(e);
     if (v >= 1 && v <= kLanes) npw = v;

@@ -23,6 +23,7 @@ struct DevQP {
 
 struct QpWork {
   int B;
+  const int32_t *skip;       // [B] or null: nonzero = not solved (status 12, obj +inf)
   double *l, *u;             // [B][np] node boxes (padding fixed at 0)
   double *x, *zl, *zu;       // [B][np]
   double *y;                 // [B][mp]

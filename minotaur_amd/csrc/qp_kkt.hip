@@ -68,20 +68,28 @@ __device__ __forceinline__ double block_max(double v, double *red) {
 
 // ---- init ------------------------------------------------------------------
 __global__ __launch_bounds__(kT) void qp_init(DevQP q, QpWork w) {
+  __shared__ int s_empty;
   const int b = blockIdx.x;
   const size_t o = (size_t)b * q.np;
+  if (threadIdx.x == 0) s_empty = 0;
+  __syncthreads();
   for (int j = threadIdx.x; j < q.np; j += kT) {
     const double l = w.l[o + j], u = w.u[o + j];
     const bool fr = l < u;
+    if (l > u) s_empty = 1;
     w.x[o + j] = fr ? 0.5 * (l + u) : l;
     w.zl[o + j] = fr ? 1.0 : 0.0;
     w.zu[o + j] = fr ? 1.0 : 0.0;
   }
   for (int i = threadIdx.x; i < q.mp; i += kT) w.y[(size_t)b * q.mp + i] = 0.0;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    w.done[b] = 0;
+    // a skipped node (presolve found it infeasible) is not solved; an empty
+    // box is infeasible before any iteration
+    const bool skip = w.skip != nullptr && w.skip[b] != 0;
+    w.done[b] = skip || s_empty ? 1 : 0;
     w.iters[b] = 0;
-    w.status[b] = 6;
+    w.status[b] = skip ? 12 : s_empty ? 2 : 6;
   }
 }
 
@@ -614,7 +622,8 @@ __global__ __launch_bounds__(kT) void qp_final(DevQP q, QpWork w) {
     f += 0.5 * x[j] * qx + q.c[j] * x[j];
   }
   f = block_sum(f, red);
-  if (t == 0) w.obj[b] = f + q.k;
+  const int st = w.status[b];
+  if (t == 0) w.obj[b] = (st == 12 || st == 2) ? INFINITY : f + q.k;
 }
 
 }  // namespace

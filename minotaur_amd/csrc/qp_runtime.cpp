@@ -17,9 +17,11 @@ struct QpState {
   DevBuf l, u, x, zl, zu, y, rd, rp, K, W, WT, M, done, iters, status, obj;
   int maxB = 0;
   DevBuf h_l, h_u, h_st, h_obj, h_it, h_x;  // host-path device copies
+  DevBuf f_mask, f_st, f_obj, f_it;          // the tree's feasibility LPs
   void release() {
     for (DevBuf *p : {&Q, &c, &A, &AT, &b, &l, &u, &x, &zl, &zu, &y, &rd, &rp, &K, &W, &WT, &M,
-                      &done, &iters, &status, &obj, &h_l, &h_u, &h_st, &h_obj, &h_it, &h_x})
+                      &done, &iters, &status, &obj, &h_l, &h_u, &h_st, &h_obj, &h_it, &h_x,
+                      &f_mask, &f_st, &f_obj, &f_it})
       p->release();
   }
 };
@@ -50,6 +52,21 @@ __global__ void unpad_x(const double *px, int n, int np, int B, double *x) {
   x[e] = px[(e / n) * np + e % n];
 }
 
+// the tree's nodes whose QP neither converged nor was proven infeasible
+__global__ void qp_unsettled(const int32_t *st, int B, int32_t *skip) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) skip[b] = st[b] != 6;
+}
+
+// their feasibility LP decides: infeasible rows -> ProvenInfeasible; a
+// feasible QP the interior point did not solve -> EngineUnknownStatus
+__global__ void qp_settle(int32_t *st, double *obj, const int32_t *lst, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || st[b] != 6) return;
+  st[b] = lst[b] == 2 ? 2 : 12;
+  obj[b] = INFINITY;
+}
+
 int ensure_qp_batch(mgpu_ctx *c, QpState &s, int B) {
   if (B <= s.maxB) return MGPU_OK;
   const size_t np = s.dq.np, mp = s.dq.mp;
@@ -67,6 +84,90 @@ int ensure_qp_batch(mgpu_ctx *c, QpState &s, int B) {
 }
 
 }  // namespace
+
+// The batch solve with an optional skip list (the batched tree: nodes its
+// presolve found infeasible are not solved).
+int qp_solve_nodes(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                   const int32_t *skip, int maxit, int32_t *status, double *obj, int32_t *iters,
+                   double *x) {
+  QpState &s = *c->qp;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = ensure_qp_batch(c, s, batch);
+  if (rc != MGPU_OK) return rc;
+  const int np = s.dq.np;
+  QpWork w{};
+  w.B = batch;
+  w.skip = skip;
+  w.l = s.l.as<double>();
+  w.u = s.u.as<double>();
+  w.x = s.x.as<double>();
+  w.zl = s.zl.as<double>();
+  w.zu = s.zu.as<double>();
+  w.y = s.y.as<double>();
+  w.rd = s.rd.as<double>();
+  w.rp = s.rp.as<double>();
+  w.K = s.K.as<double>();
+  w.W = s.W.as<double>();
+  w.WT = s.WT.as<double>();
+  w.M = s.M.as<double>();
+  w.done = s.done.as<int32_t>();
+  w.iters = s.iters.as<int32_t>();
+  w.status = s.status.as<int32_t>();
+  w.obj = s.obj.as<double>();
+  const size_t tot = (size_t)batch * np;
+  hipLaunchKernelGGL(pad_boxes, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, lb,
+                     ub, s.n, np, batch, w.l, w.u);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev6, c->stream));
+  HIPCHK(c, launch_qp_init(s.dq, w, c->stream));
+  const int lim = maxit > 0 ? maxit : 80;
+  std::vector<int32_t> hd(batch);
+  for (int it = 0; it < lim; ++it) {
+    HIPCHK(c, launch_qp_iteration(s.dq, w, c->stream));
+    if (it % 4 == 3) {  // stop once every node has converged
+      HIPCHK(c, hipMemcpyAsync(hd.data(), w.done, (size_t)batch * 4, hipMemcpyDeviceToHost,
+                               c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      bool all = true;
+      for (int b = 0; b < batch && all; ++b) all = hd[b] != 0;
+      if (all) break;
+    }
+  }
+  // a final residual pass marks nodes that converged on the last step
+  HIPCHK(c, launch_qp_iteration_check(s.dq, w, c->stream));
+  HIPCHK(c, launch_qp_final(s.dq, w, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev7, c->stream));
+  HIPCHK(c, hipMemcpyAsync(status, w.status, (size_t)batch * 4, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(obj, w.obj, (size_t)batch * 8, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(iters, w.iters, (size_t)batch * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (x) {
+    const size_t tn = (size_t)batch * s.n;
+    hipLaunchKernelGGL(unpad_x, dim3((unsigned)((tn + 255) / 256)), dim3(256), 0, c->stream, w.x,
+                       s.n, np, batch, x);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (skip != nullptr) {
+    // the batched tree: a node QP still unsettled after the iteration limit
+    // (no convergence, no Farkas ray) gets a phase-1 answer from the loaded
+    // rows: the LP min 0 over the node box (K3 / K3L from the slack basis),
+    // as BQPD's own phase 1 would report an infeasible node QP
+    const unsigned g = (unsigned)((batch + 255) / 256);
+    for (DevBuf *p : {&s.f_mask, &s.f_st, &s.f_it}) HIPCHK(c, p->ensure((size_t)batch * 4));
+    HIPCHK(c, s.f_obj.ensure((size_t)batch * 8));
+    hipLaunchKernelGGL(qp_unsettled, dim3(g), dim3(256), 0, c->stream, status, batch,
+                       s.f_mask.as<int32_t>());
+    HIPCHK(c, hipGetLastError());
+    int rc2 = mgpu_lp_solve_dev(c, batch, lb, ub, s.f_mask.as<int32_t>(), nullptr, nullptr,
+                                nullptr, nullptr, 1, 0, s.f_st.as<int32_t>(),
+                                s.f_obj.as<double>(), s.f_it.as<int32_t>(), nullptr, nullptr,
+                                nullptr, nullptr, nullptr);
+    if (rc2 != MGPU_OK) return rc2;
+    hipLaunchKernelGGL(qp_settle, dim3(g), dim3(256), 0, c->stream, status, obj,
+                       s.f_st.as<int32_t>(), batch);
+    HIPCHK(c, hipGetLastError());
+  }
+  return MGPU_OK;
+}
 
 extern "C" {
 
@@ -128,62 +229,7 @@ int mgpu_qp_solve_dev(mgpu_ctx *c, int batch, const double *lb, const double *ub
   if (batch < 0 || (batch > 0 && (!lb || !ub || !status || !obj || !iters)))
     return fail(c, MGPU_ERR_ARG, "mgpu_qp_solve: bad argument");
   if (batch == 0) return MGPU_OK;
-  QpState &s = *c->qp;
-  HIPCHK(c, hipSetDevice(c->device));
-  int rc = ensure_qp_batch(c, s, batch);
-  if (rc != MGPU_OK) return rc;
-  const int np = s.dq.np;
-  QpWork w{};
-  w.B = batch;
-  w.l = s.l.as<double>();
-  w.u = s.u.as<double>();
-  w.x = s.x.as<double>();
-  w.zl = s.zl.as<double>();
-  w.zu = s.zu.as<double>();
-  w.y = s.y.as<double>();
-  w.rd = s.rd.as<double>();
-  w.rp = s.rp.as<double>();
-  w.K = s.K.as<double>();
-  w.W = s.W.as<double>();
-  w.WT = s.WT.as<double>();
-  w.M = s.M.as<double>();
-  w.done = s.done.as<int32_t>();
-  w.iters = s.iters.as<int32_t>();
-  w.status = s.status.as<int32_t>();
-  w.obj = s.obj.as<double>();
-  const size_t tot = (size_t)batch * np;
-  hipLaunchKernelGGL(pad_boxes, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, lb,
-                     ub, s.n, np, batch, w.l, w.u);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->ev6, c->stream));
-  HIPCHK(c, launch_qp_init(s.dq, w, c->stream));
-  const int lim = maxit > 0 ? maxit : 80;
-  std::vector<int32_t> hd(batch);
-  for (int it = 0; it < lim; ++it) {
-    HIPCHK(c, launch_qp_iteration(s.dq, w, c->stream));
-    if (it % 4 == 3) {  // stop once every node has converged
-      HIPCHK(c, hipMemcpyAsync(hd.data(), w.done, (size_t)batch * 4, hipMemcpyDeviceToHost,
-                               c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      bool all = true;
-      for (int b = 0; b < batch && all; ++b) all = hd[b] != 0;
-      if (all) break;
-    }
-  }
-  // a final residual pass marks nodes that converged on the last step
-  HIPCHK(c, launch_qp_iteration_check(s.dq, w, c->stream));
-  HIPCHK(c, launch_qp_final(s.dq, w, c->stream));
-  HIPCHK(c, hipEventRecord(c->ev7, c->stream));
-  HIPCHK(c, hipMemcpyAsync(status, w.status, (size_t)batch * 4, hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(obj, w.obj, (size_t)batch * 8, hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(iters, w.iters, (size_t)batch * 4, hipMemcpyDeviceToDevice, c->stream));
-  if (x) {
-    const size_t tn = (size_t)batch * s.n;
-    hipLaunchKernelGGL(unpad_x, dim3((unsigned)((tn + 255) / 256)), dim3(256), 0, c->stream, w.x,
-                       s.n, np, batch, x);
-    HIPCHK(c, hipGetLastError());
-  }
-  return MGPU_OK;
+  return qp_solve_nodes(c, batch, lb, ub, nullptr, maxit, status, obj, iters, x);
 }
 
 int mgpu_qp_solve(mgpu_ctx *c, int batch, const double *lb, const double *ub, int maxit,

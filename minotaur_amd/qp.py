@@ -114,3 +114,57 @@ def load(path) -> QpProblem:
     z = np.load(path, allow_pickle=False)
     return QpProblem(str(z['name']), z['Q'], z['c'], float(z['k']), z['A'], z['b'], z['l'],
                      z['u'], z['vtype'])
+
+
+def rows_problem(qp: QpProblem):
+    """The QP's equality rows as a LinProblem: what the batched tree's K1
+    (LinearHandler::presolveNode on the linear rows) and node decision
+    (IntVarHandler column types) read when the node relaxation is the QP
+    (mgpu_bnb_relaxation 1).  No linear objective: LinearHandler does not
+    propagate a quadratic objective."""
+    from .problem import LinProblem
+    rows, cols, vals = np.nonzero(qp.A)[0], np.nonzero(qp.A)[1], qp.A[np.nonzero(qp.A)]
+    rowptr = np.zeros(qp.m + 1, dtype=np.int32)
+    np.add.at(rowptr, rows + 1, 1)
+    rowptr = np.cumsum(rowptr).astype(np.int32)
+    return LinProblem(f'{qp.name}-rows', qp.n, qp.m, rowptr, cols.astype(np.int32),
+                      vals.astype(np.float64), qp.b.astype(np.float64), qp.b.astype(np.float64),
+                      qp.l.astype(np.float64), qp.u.astype(np.float64),
+                      qp.vtype.astype(np.int32), np.zeros(qp.n), 0.0)
+
+
+def solve_tree(ctx, qp: QpProblem, batch=1024, capacity=None, max_rounds=10**9, order=0,
+               incumbent=float('inf')):
+    """Branch-and-bound over QP relaxations (the batched tree with K5 as its
+    node relaxation, mgpu_bnb_relaxation 1): returns (incumbent, x, stats,
+    seconds).  QPDRelaxer (examples/QPDRelaxer.cpp:56-126) hands each node's
+    QP to BqpdEngine; here a round's nodes go to K5 in one batch."""
+    from . import bnb
+    ctx.load(rows_problem(qp))
+    ctx.load_qp(qp)
+    ctx.bnb_relaxation(1)
+    try:
+        return bnb.solve(ctx, batch=batch, capacity=capacity, max_rounds=max_rounds,
+                         incumbent=incumbent, order=order, warm=0)
+    finally:
+        ctx.bnb_relaxation(0)
+
+
+def random_miqp(seed: int, nbin: int = 8, ncont: int = 4, m: int = 2) -> QpProblem:
+    """A small convex MIQP whose optimum brute force over the binaries can
+    check: binaries x, continuous y in [0, 2], rows sum_j a_ij x_j +
+    sum_k c_ik y_k = b_i (some binary assignments infeasible), Q = G G'/n +
+    0.01 I."""
+    rng = np.random.default_rng(seed)
+    n = nbin + ncont
+    G = rng.normal(size=(n, n))
+    Q = G @ G.T / n + 0.01 * np.eye(n)
+    c = rng.normal(size=n)
+    A = np.zeros((m, n))
+    A[:, :nbin] = rng.uniform(0.5, 1.5, size=(m, nbin)) * (rng.random((m, nbin)) < 0.6)
+    A[:, nbin:] = rng.uniform(0.5, 1.5, size=(m, ncont))
+    b = A[:, :nbin].sum(axis=1) * 0.4 + A[:, nbin:].sum(axis=1) * 0.7
+    l = np.zeros(n)
+    u = np.concatenate([np.ones(nbin), np.full(ncont, 2.0)])
+    vtype = np.array([0] * nbin + [4] * ncont, dtype=np.int32)   # Binary, Continuous
+    return QpProblem(f'miqp{seed}', Q, c, 0.0, A, b, l, u, vtype)

@@ -36,6 +36,7 @@ EXPORTS = [
     'mgpu_bnb_import', 'mgpu_strong_branch',
     'mgpu_strong_branch_dev', 'mgpu_load_qp', 'mgpu_qp_solve', 'mgpu_qp_solve_dev',
     'mgpu_set_node_rows', 'mgpu_lp_solve_rows', 'mgpu_lp_solve_rows_dev', 'mgpu_bnb_brancher',
+    'mgpu_bnb_relaxation',
     'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
     'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive', 'mgpu_ws_alloc', 'mgpu_ws_free',
     'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1', 'mgpu_bnb_pick', 'mgpu_bnb_export_dev',
@@ -115,6 +116,7 @@ def load_library():
     lib.mgpu_bnb_init.argtypes = [_P, _I, _P, _P, _D]
     lib.mgpu_bnb_config.argtypes = [_P, _I, _I]
     lib.mgpu_bnb_brancher.argtypes = [_P, _I]
+    lib.mgpu_bnb_relaxation.argtypes = [_P, _I]
     lib.mgpu_bnb_guided_dive.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
     lib.mgpu_bnb_import.argtypes = [_P, _I, _P, _P, _P, _P]
@@ -621,6 +623,11 @@ class Context:
     def bnb_brancher(self, kind):
         """Next tree's brancher: 0 MaxVio, 1 reliability (mgpu_bnb_brancher)."""
         self._chk(self.lib.mgpu_bnb_brancher(self.h, int(kind)), 'mgpu_bnb_brancher')
+
+    def bnb_relaxation(self, kind):
+        """Next tree's relaxation: 0 the loaded LP, 1 the loaded QP by K5
+        (mgpu_bnb_relaxation)."""
+        self._chk(self.lib.mgpu_bnb_relaxation(self.h, int(kind)), 'mgpu_bnb_relaxation')
 
     def bnb_init(self, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
         p = self.problem
