@@ -73,6 +73,7 @@ struct mgpu_ctx {
   DevBuf lp_next;              // K3L: node counter of the dynamic schedule
   DevBuf pfi_ovf;              // K3P: overflow counter + node list
   DevBuf pfi_cont;             // K3P: continuation state of overflowing LPs
+  DevBuf pfi_t0;               // K3P: B0^{-1} a_q of every column [N][m]
   int num_cus = 256;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr,
             ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;

@@ -70,14 +70,15 @@ constexpr double kColrepTol = 1e-9;  // oracle COLREP_TOL
 constexpr double kArt0 = 1e7;
 constexpr double kInfB = 1e30;
 constexpr int kUnknownStatus = 12;
-// waves per workgroup (one workgroup per CU): with a 16-eta file 16 = 4 per
-// SIMD (<= 128 VGPRs) up to 3 column slots; the 4-slot build keeps 12 (3 per
-// SIMD) rather than spilling.  The 32-eta file (deep tree nodes are 15-20
-// pivots from the root basis) costs 32 more VGPRs: 12 waves (3 per SIMD).
-// A/B on tls4-lin (S = 3): 12 waves with a 24-eta file 2.12 ms, 16 waves
-// with a 16-eta file 1.75 ms + a longer overflow tail (0.16 ms).
+// waves per workgroup (one workgroup per CU): 16 = 4 per SIMD (<= 128 VGPRs)
+// up to 3 column slots; the 4-slot build keeps 12 (3 per SIMD).  The 32-eta
+// file does not fit 128 VGPRs (168 at 3 waves per SIMD): at 4 waves per SIMD
+// the compiler spills ~60 VGPRs (156 B per lane of scratch) and is still
+// faster: headline K3P 15.6 -> 14.5 ms (profiles/r04f_ab).  A/B on tls4-lin
+// (S = 3): 12 waves with a 24-eta file 2.12 ms, 16 waves with a 16-eta file
+// 1.75 ms + a longer overflow tail (0.16 ms).
 template <int S, int K>
-constexpr int waves_for() { return (S <= 3 && K <= 16) ? 16 : 12; }
+constexpr int waves_for() { return S <= 3 ? 16 : 12; }
 __host__ __device__ inline int slots_for(int N) { return (N + 63) / 64; }
 
 // packed column status: bits 0-1 status, 2-3 artificial-bound flags, 4 fixed
@@ -208,6 +209,43 @@ __device__ __forceinline__ double ftran_b0(const Prob &P, int q, int lane) {
     alq = -P.b0[(size_t)(q - P.n) * ld + li];
   }
   return lane < P.m ? alq : 0.0;
+}
+
+// B0^{-1} a_q from the launch's precomputed columns (launch_pfi_t0: the same
+// ftran_b0 arithmetic, once per column instead of once per use)
+__device__ __forceinline__ double ftran_col0(const Prob &P, const double *t0, int q, int lane) {
+  if (t0 == nullptr) return ftran_b0(P, q, lane);
+  return lane < P.m ? t0[(size_t)q * P.m + lane] : 0.0;
+}
+
+// t0[q][i] = (B0^{-1} a_q)_i, one wave per column, B0^{-1} read in place
+// (column-major, leading dimension m: the ABI layout) with ftran_b0's loop
+__global__ __launch_bounds__(256) void pfi_t0_kernel(DevLP lp, const double *binv, double *t0) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = lp.n, m = lp.m;
+  if (q >= n + m) return;
+  const int li = lane < m ? lane : 0;
+  double alq = 0.0;
+  if (q < n) {
+    int t = lp.colptr[q];
+    const int e = lp.colptr[q + 1];
+    for (; t + 4 <= e; t += 4) {
+      const int r0 = lp.rowidx[t], r1 = lp.rowidx[t + 1], r2 = lp.rowidx[t + 2],
+                r3 = lp.rowidx[t + 3];
+      const double c0 = lp.cval[t], c1 = lp.cval[t + 1], c2 = lp.cval[t + 2], c3 = lp.cval[t + 3];
+      const double b0 = binv[(size_t)r0 * m + li], b1 = binv[(size_t)r1 * m + li];
+      const double b2 = binv[(size_t)r2 * m + li], b3 = binv[(size_t)r3 * m + li];
+      alq += b0 * c0;
+      alq += b1 * c1;
+      alq += b2 * c2;
+      alq += b3 * c3;
+    }
+    for (; t < e; ++t) alq += binv[(size_t)lp.rowidx[t] * m + li] * lp.cval[t];
+  } else {
+    alq = -binv[(size_t)(q - n) * m + li];
+  }
+  if (lane < m) t0[(size_t)q * m + lane] = alq;
 }
 
 // u <- u' E_{k-1} ... E_0 (oracle pfi_btran's eta loop): each E_t' rewrites
@@ -429,7 +467,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         for (int i = 0; i < kRG; ++i) {
           const bool in = g + i < kpath;  // wave-uniform
           qg[i] = in ? (int)(ppath[g + i] & 0xFFFFu) : 0;
-          v[i] = in ? ftran_b0(P, qg[i], lane) : 0.0;
+          v[i] = in ? ftran_col0(P, px.t0, qg[i], lane) : 0.0;
         }
         apply_etas_n(v, eta, prow, g, lane);
 #pragma unroll
@@ -637,12 +675,10 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     double zB = 0.0;
     bool need = true;   // recompute before pricing
     int status = kUnknownStatus;
-    bool fresh = true;
     for (;;) {
       if (need) {
         zB = primals();
         PSTAMP(1);
-        fresh = true;
         need = false;
       }
       // ---- pricing: most infeasible basic row, lowest row on ties ----
@@ -656,10 +692,9 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       asm volatile("" : "+v"(best));
       PSTAMP(2);
       if (best == 0.0) {
-        if (!fresh) {
-          need = true;
-          continue;
-        }
+        // optimal on the maintained primal values: the product form holds at
+        // most kmax etas since the recompute at the solve's start, so no
+        // second recompute confirms them (oracle: pfi mode)
         bool g = false;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -769,7 +804,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       const int ql = q & 63, qs = q >> 6;
 
       // ---- FTRAN: alpha_q = E...E B0^{-1} a_q ----
-      const double alq = apply_etas(ftran_b0(P, q, lane), eta, prow, ne, lane);
+      const double alq = apply_etas(ftran_col0(P, px.t0, q, lane), eta, prow, ne, lane);
       const double arq = rld(alq, r);
       PSTAMP(6);
 
@@ -824,7 +859,6 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       if (lane == ne) prow = r;
       ++ne;
       ++iters;
-      fresh = false;
       PSTAMP(7);
     }
 
@@ -971,6 +1005,12 @@ extern "C" int mgpu_debug_pfi_stamps(unsigned long long *out, int reset) {
   return 0;
 }
 #endif
+
+hipError_t launch_pfi_t0(const DevLP &lp, const double *binv, double *t0, hipStream_t stream) {
+  const int N = lp.n + lp.m;
+  hipLaunchKernelGGL(pfi_t0_kernel, dim3((N + 3) / 4), dim3(256), 0, stream, lp, binv, t0);
+  return hipGetLastError();
+}
 
 size_t lp_pfi_lds_bytes(int n, int m, int nnz, int kmax) {
   const bool small = kmax <= kPfiSmall;

@@ -411,7 +411,6 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
 
     primals();
     int status = kUnknownStatus;
-    bool fresh = true;
     for (;;) {
       // ---- pricing: most infeasible basic row, lowest row on ties ----
       double inf[kR];
@@ -432,11 +431,7 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
       wave_argmax_idx(best, r);  // r used only when best > 0
       asm volatile("" : "+v"(best));
       if (best == 0.0) {
-        if (!fresh) {
-          primals();
-          fresh = true;
-          continue;
-        }
+        // optimal on the maintained primal values (K3P's rule, oracle pfi mode)
         bool g = false;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -456,7 +451,6 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
         art_bound *= 1e3;
         grow(art_bound);
         primals();
-        fresh = true;
         continue;
       }
       if (iters >= io.iter_limit) {
@@ -576,7 +570,6 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
         art_bound *= 1e3;
         grow(art_bound);
         primals();
-        fresh = true;
         continue;
       }
       // ---- Harris pass 2: largest |alpha| among ratios <= tmax; the owner
@@ -688,7 +681,6 @@ __global__ __launch_bounds__(64 * kWaves) void lp_pfiw_kernel(DevLP lp, LpIO io,
       }
       if (lane == iters) prow = r;
       ++iters;
-      fresh = false;
     }
 
     // ---- outputs ----

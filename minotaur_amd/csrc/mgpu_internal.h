@@ -192,7 +192,14 @@ struct PfiIO {
   int32_t *c_head;
   int8_t *c_st;
   double *c_d, *c_binv;
+  // B0^{-1} a_q of every column q of [A -I], column-major [N][m]: computed
+  // once per launch by launch_pfi_t0 with ftran_b0's arithmetic, so every
+  // FTRAN through B0^{-1} (the warm start's column replacements, each
+  // pivot's entering column) is one coalesced load (null: computed in place)
+  const double *t0;
 };
+// B0^{-1} a_q for every column into t0 [N][m] (K3P's ftran_b0, bit for bit)
+hipError_t launch_pfi_t0(const DevLP &lp, const double *binv, double *t0, hipStream_t stream);
 // continuation slots per LP call: one per LP of the batch, up to this many
 // bytes of HBM (K3P overflow beyond the slots restarts in K3 from the shared
 // warm start)

@@ -615,6 +615,13 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     if (wide) {
       HIPCHK(c, launch_lp_pfiw(c->lp, io, px, c->num_cus, c->stream));
     } else {
+      // every column's B0^{-1} a_q once per launch: headline K3P 13.8 ->
+      // 13.4 ms (profiles/r04g)
+      if (io.ws.binv != nullptr) {
+        HIPCHK(c, c->pfi_t0.ensure((size_t)N * m * 8));
+        HIPCHK(c, launch_pfi_t0(c->lp, io.ws.binv, c->pfi_t0.as<double>(), c->stream));
+        px.t0 = c->pfi_t0.as<double>();
+      }
       HIPCHK(c, launch_lp_pfi(c->lp, io, px, c->num_cus, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev8, c->stream));

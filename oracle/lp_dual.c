@@ -512,8 +512,10 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
         best = fabs(inf); r = i; delta = inf;
       }
     }
-    if (r < 0 && !fresh) {
-      /* confirm against freshly recomputed primal values */
+    if (r < 0 && !fresh && !W.pfi) {
+      /* confirm against freshly recomputed primal values (the product form,
+       * K3P / K3PW: at most pfi etas since the recompute at the solve's
+       * start, so its maintained values are declared final) */
       compute_primals(&W);
       fresh = 1;
       continue;
