@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, 'csrc')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 
-SOURCES = ['mgpu_runtime.cpp', 'quad_runtime.cpp', 'bnb.cpp', 'fbbt_linear.hip',
+SOURCES = ['mgpu_runtime.cpp', 'quad_runtime.cpp', 'bnb.cpp', 'fbbt_linear.hip', 'fbbt_group.hip',
            'lp_dual.hip', 'lp_pfi.hip', 'lp_pfi_wide.hip', 'lp_large.hip', 'node_decide.hip', 'quad_fbbt.hip', 'bnb.hip',
            'bnb_select.hip', 'qp_runtime.cpp', 'rows_runtime.cpp', 'lp_rows.hip', 'bnb_rel.hip', 'bnb_migrate.hip',
            'glob_tree.hip', 'glob_runtime.cpp',

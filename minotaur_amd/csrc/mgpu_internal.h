@@ -299,6 +299,10 @@ constexpr int kLdsStride = 65;  // padded [var][lane] stride (bank spread)
 
 hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
                               hipStream_t stream);
+// K1G (fbbt_group.hip): 16 lanes per node, bounds in LDS; m <= 64, no mod
+// log.  Waves per workgroup the LDS allows (0: not applicable).
+int fbbt_group_waves(const DevLP &lp);
+hipError_t launch_fbbt_group(const DevLP &lp, const FbbtIO &io, hipStream_t stream);
 size_t fbbt_lds_bytes(int n, int m);
 
 // ---- quadratic node FBBT (K2) ---------------------------------------------

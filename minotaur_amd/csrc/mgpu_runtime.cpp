@@ -273,7 +273,7 @@ static_assert(MGPU_PATH_MAX == kPathMax, "ABI path cap = kernel's");
 static_assert(MGPU_LP_PFI_WIDE_MAX == kPfiWideMax, "ABI eta-file cap = kernel's");
 
 int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
-  if (!c || variant < 0 || variant > 3) return MGPU_ERR_ARG;
+  if (!c || variant < 0 || variant > 4) return MGPU_ERR_ARG;
   c->fbbt_variant = variant;
   return MGPU_OK;
 }
@@ -390,6 +390,17 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   // 6.67 -> 5.58 ms; at 131 072 the one-shot kernel is faster, 1.87 vs
   // 2.17 ms; tools/fbbt_refill_probe.py).
   int variant = c->fbbt_variant;
+  // K1G (variant 4): four nodes per wave, 16 lanes each, bounds in LDS
+  static const bool group_auto = getenv("MGPU_FBBT_GROUP") != nullptr;  // A/B switch
+  if (variant == 4 || (variant == 0 && group_auto && io.mod_cap == 0 &&
+                       fbbt_group_waves(c->lp) > 0)) {
+    if (fbbt_group_waves(c->lp) <= 0 || io.mod_cap > 0)
+      return fail(c, MGPU_ERR_ARG, "mgpu_fbbt: K1G needs m <= 64, no mod log and LDS room");
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_fbbt_group(c->lp, io, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    return MGPU_OK;
+  }
   if (variant == 0)
     variant = (fits && waves <= c->num_cus) ? 1 : (waves > 8 * c->num_cus && npw == kLanes) ? 3 : 2;
   // persistent path: bit flags (m <= 64) and records staged in 64 KiB of LDS

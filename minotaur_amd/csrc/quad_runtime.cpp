@@ -303,7 +303,7 @@ int mgpu_quad_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double
   // 0 auto = LDS while it leaves room for several waves per CU.
   const size_t lds = quad_lds_bytes(q.dq);
   int variant = c->fbbt_variant;
-  if (variant == 0) variant = lds <= 40 * 1024 ? 1 : 2;
+  if (variant != 1 && variant != 2) variant = lds <= 40 * 1024 ? 1 : 2;  // 0 auto (3, 4: K1 only)
   if (variant == 1 && lds > 160 * 1024)
     return fail(c, MGPU_ERR_ARG, "quad LDS variant needs %zu B > 160 KiB", lds);
   if (variant == 2) {

@@ -49,6 +49,51 @@ def test_fbbt_matches_reference_golden(ctx, name, variant, monkeypatch):
     assert_mods_equal(r.nmods, r.mod_var, r.mod_lu, r.mod_val, g, g['mod_cap'])
 
 
+@pytest.mark.parametrize('name', cases())
+def test_fbbt_group_matches_reference_golden(ctx, name):
+    """K1G (variant 4: four nodes per wave, 16 lanes each, the activity
+    sums as DPP left folds) against the reference's own presolveNode
+    outputs: bounds bit for bit, verdicts and mod counts (K1G keeps no mod
+    log)."""
+    from minotaur_amd.runtime import MgpuError
+    p, g = load_fbbt(name)
+    if p.m > 64:
+        pytest.skip('K1G keeps row flags in one 64-bit mask')
+    ctx.load(p)
+    ctx.set_fbbt_variant(4)
+    try:
+        r = ctx.fbbt(g['lb_in'], g['ub_in'], _inc(g), mod_cap=0)
+    except MgpuError as e:
+        pytest.skip(str(e))
+    finally:
+        ctx.set_fbbt_variant(0)
+    assert bits_equal(r.lb, g['lb_out'])
+    assert bits_equal(r.ub, g['ub_out'])
+    assert np.array_equal(r.infeasible, g['infeas'])
+    assert np.array_equal(r.nmods, g['nmods'])
+
+
+@pytest.mark.parametrize('inst', ['tls4_lin', 'tls4_oa'])
+@pytest.mark.parametrize('inc', [math.inf, 20.0])
+def test_fbbt_group_large_batch_vs_oracle(ctx, inst, inc):
+    """K1G on 20 001 random-branching boxes (ragged last wave) against the
+    C restatement, with and without an incumbent."""
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    p = LinProblem.load(os.path.join(here, '..', 'minotaur_amd', 'instances', f'{inst}.npz'))
+    LB, UB = random_boxes(p, 20001, 4242)
+    ctx.load(p)
+    ctx.set_fbbt_variant(4)
+    try:
+        r = ctx.fbbt(LB, UB, inc)
+    finally:
+        ctx.set_fbbt_variant(0)
+    o = oracle.linear_fbbt(p, LB, UB, None if math.isinf(inc) else inc, nthreads=8)
+    assert bits_equal(r.lb, o.lb) and bits_equal(r.ub, o.ub)
+    assert np.array_equal(r.infeasible, o.infeas)
+    assert np.array_equal(r.nmods, o.nmods)
+
+
 def _tls4():
     import os
     here = os.path.dirname(os.path.abspath(__file__))
