@@ -164,6 +164,8 @@ constexpr int kPathInherit = 24; // longest path the batched tree hands to child
 // K1: waves per CU a batch too small for one node per lane is spread over
 // (tuned on config 2's complete tree, tools/tree_probe.py)
 constexpr int kFbbtSmallWaves = 8;
+// K1G is the auto choice up to this many nodes (mgpu_fbbt_dev)
+constexpr int kFbbtGroupMax = 65536;
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
 constexpr int kLpDefaultIterLimit = 10000;  // OsiLPEngine maxIterLimit_ (OsiLPEngine.cpp:99)

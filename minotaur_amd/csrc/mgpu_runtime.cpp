@@ -390,9 +390,13 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   // 6.67 -> 5.58 ms; at 131 072 the one-shot kernel is faster, 1.87 vs
   // 2.17 ms; tools/fbbt_refill_probe.py).
   int variant = c->fbbt_variant;
-  // K1G (variant 4): four nodes per wave, 16 lanes each, bounds in LDS
-  static const bool group_auto = getenv("MGPU_FBBT_GROUP") != nullptr;  // A/B switch
-  if (variant == 4 || (variant == 0 && group_auto && io.mod_cap == 0 &&
+  // K1G (variant 4): four nodes per wave, 16 lanes each, bounds in LDS.
+  // Auto below kFbbtGroupMax nodes: there one node's chain is the kernel's
+  // critical path and K1G shortens it (tls4-oa: 16 384 nodes 0.75 vs 2.25
+  // ms, 65 536 2.7 vs 3.2 ms); wider batches fill the chip and K1's lanes
+  // per node win (524 288: 7.1 vs 18.7 ms; tools/fbbt_batch_sweep.py,
+  // profiles/r04i)
+  if (variant == 4 || (variant == 0 && batch <= kFbbtGroupMax && io.mod_cap == 0 &&
                        fbbt_group_waves(c->lp) > 0)) {
     if (fbbt_group_waves(c->lp) <= 0 || io.mod_cap > 0)
       return fail(c, MGPU_ERR_ARG, "mgpu_fbbt: K1G needs m <= 64, no mod log and LDS room");
