@@ -1019,6 +1019,8 @@ def main():
                     help='skip the supplementary glob batch (QCQP: K2 -> per-node rows LP)')
     ap.add_argument('--no-fixed', action='store_true',
                     help='skip the supplementary fixed batch (K1 + K3P on tls4-lin boxes)')
+    ap.add_argument('--no-oa-tree', action='store_true',
+                    help="skip config 2's complete tree (tls4_oa_tree; profiling runs)")
     ap.add_argument('--no-knapsack', action='store_true',
                     help='skip the supplementary config-3 batch (1000 knapsack nodes)')
     args = ap.parse_args()
@@ -1061,8 +1063,8 @@ def main():
     progress(rank, f"headline done: {1e3 * elapsed / args.steps:.2f} ms/step, "
                    f"{nodes / elapsed / 1e6:.2f} M nodes/s")
     TB = args.tree_batch
-    oa_tree = tls4_oa_tree(ctx, dev, rank, world, args)
-    progress(rank, f"tls4_oa_tree done: {oa_tree['nodes_per_s'] / 1e6:.2f} M nodes/s")
+    oa_tree = {} if args.no_oa_tree else tls4_oa_tree(ctx, dev, rank, world, args)
+    progress(rank, f"tls4_oa_tree done: {oa_tree.get('nodes_per_s', 0.0) / 1e6:.2f} M nodes/s")
     supp = {}
     for key, skip, fn in (
             ("fixed_batch", args.no_fixed, lambda: fixed_batch(ctx, dev, rank, world, args)),

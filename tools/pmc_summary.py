@@ -16,7 +16,8 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
 
 
 def short(name):
-    for k in ('fbbt_linear_kernel', 'fbbt_linear_persist', 'lp_pfi_kernel', 'lp_dual_kernel',
+    for k in ('fbbt_linear_kernel', 'fbbt_linear_persist', 'fbbt_group_kernel', 'lp_pfi_kernel',
+              'lp_dual_kernel', 'pfi_t0_kernel',
               'node_decide_kernel', 'lp_large_kernel',
               'fbbt_quad_kernel',
               'obbt'):

@@ -6,7 +6,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=${OUT:-$R/gpurun_out/prof}
-ARGS=${BENCH_ARGS:---steps 5 --warmup 1 --batch 524288 --no-cpu-baseline --no-bnb --no-qp --no-convex --no-knapsack --no-glob --no-fixed}
+ARGS=${BENCH_ARGS:---steps 5 --warmup 1 --batch 524288 --no-cpu-baseline --no-bnb --no-qp --no-convex --no-knapsack --no-glob --no-fixed --no-oa-tree}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_trace.log 2>&1 || exit $?
