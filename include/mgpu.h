@@ -255,9 +255,9 @@ int mgpu_node_decide_dev(mgpu_ctx *ctx, int batch, const int32_t *d_fbbt_infeas,
 
 /* Which FBBT kernel variant the next calls use (linear K1 and quadratic
  * K2): 0 auto, 1 node state in LDS, 2 node state in a global scratch
- * (large n), 3 (K1) persistent lanes refilled from a node queue, 4 (K1)
- * K1G: 16 lanes per node, bounds in LDS (m <= 64, no mod log).  For
- * tests/benchmarks. */
+ * (large n), 3 (K1) persistent lanes refilled from a node queue, 4 / 5 / 6
+ * (K1) K1G with 16 / 8 / 4 lanes per node, bounds in LDS (m <= 64, no mod
+ * log).  For tests/benchmarks. */
 int mgpu_set_fbbt_variant(mgpu_ctx *ctx, int variant);
 
 /* Which LP kernel the next LP calls use: 0 auto, 1 K3, 2 K3L, 3 product

@@ -164,8 +164,10 @@ constexpr int kPathInherit = 24; // longest path the batched tree hands to child
 // K1: waves per CU a batch too small for one node per lane is spread over
 // (tuned on config 2's complete tree, tools/tree_probe.py)
 constexpr int kFbbtSmallWaves = 8;
-// K1G is the auto choice up to this many nodes (mgpu_fbbt_dev)
+// K1G is the auto choice up to this many nodes (mgpu_fbbt_dev), with
+// kFbbtGroupG lanes per node
 constexpr int kFbbtGroupMax = 65536;
+constexpr int kFbbtGroupG = 16;
 constexpr int kLpWaves = 4;     // nodes (waves) per workgroup
 constexpr int kLpMaxM = 64;     // basis rows held one per lane in VGPRs
 constexpr int kLpDefaultIterLimit = 10000;  // OsiLPEngine maxIterLimit_ (OsiLPEngine.cpp:99)
@@ -301,10 +303,12 @@ constexpr int kLdsStride = 65;  // padded [var][lane] stride (bank spread)
 
 hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
                               hipStream_t stream);
-// K1G (fbbt_group.hip): 16 lanes per node, bounds in LDS; m <= 64, no mod
-// log.  Waves per workgroup the LDS allows (0: not applicable).
-int fbbt_group_waves(const DevLP &lp);
-hipError_t launch_fbbt_group(const DevLP &lp, const FbbtIO &io, hipStream_t stream);
+// K1G (fbbt_group.hip): g = 16, 8 or 4 lanes per node, bounds in LDS;
+// m <= 64, no mod log.  Waves per workgroup the LDS allows (0: not
+// applicable).
+int fbbt_group_waves(const DevLP &lp, int g);
+hipError_t launch_fbbt_group(const DevLP &lp, const FbbtIO &io, int g, int num_cus,
+                             hipStream_t stream);
 size_t fbbt_lds_bytes(int n, int m);
 
 // ---- quadratic node FBBT (K2) ---------------------------------------------

@@ -273,7 +273,7 @@ static_assert(MGPU_PATH_MAX == kPathMax, "ABI path cap = kernel's");
 static_assert(MGPU_LP_PFI_WIDE_MAX == kPfiWideMax, "ABI eta-file cap = kernel's");
 
 int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
-  if (!c || variant < 0 || variant > 4) return MGPU_ERR_ARG;
+  if (!c || variant < 0 || variant > 6) return MGPU_ERR_ARG;
   c->fbbt_variant = variant;
   return MGPU_OK;
 }
@@ -396,12 +396,13 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   // ms, 65 536 2.7 vs 3.2 ms); wider batches fill the chip and K1's lanes
   // per node win (524 288: 7.1 vs 18.7 ms; tools/fbbt_batch_sweep.py,
   // profiles/r04i)
-  if (variant == 4 || (variant == 0 && batch <= kFbbtGroupMax && io.mod_cap == 0 &&
-                       fbbt_group_waves(c->lp) > 0)) {
-    if (fbbt_group_waves(c->lp) <= 0 || io.mod_cap > 0)
+  const int gg = variant == 4 ? 16 : variant == 5 ? 8 : variant == 6 ? 4 : kFbbtGroupG;
+  if (variant >= 4 || (variant == 0 && batch <= kFbbtGroupMax && io.mod_cap == 0 &&
+                       fbbt_group_waves(c->lp, gg) > 0)) {
+    if (fbbt_group_waves(c->lp, gg) <= 0 || io.mod_cap > 0)
       return fail(c, MGPU_ERR_ARG, "mgpu_fbbt: K1G needs m <= 64, no mod log and LDS room");
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_fbbt_group(c->lp, io, c->stream));
+    HIPCHK(c, launch_fbbt_group(c->lp, io, gg, c->num_cus, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     return MGPU_OK;
   }

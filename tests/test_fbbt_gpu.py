@@ -49,18 +49,19 @@ def test_fbbt_matches_reference_golden(ctx, name, variant, monkeypatch):
     assert_mods_equal(r.nmods, r.mod_var, r.mod_lu, r.mod_val, g, g['mod_cap'])
 
 
+@pytest.mark.parametrize('variant', [4, 5, 6])
 @pytest.mark.parametrize('name', cases())
-def test_fbbt_group_matches_reference_golden(ctx, name):
-    """K1G (variant 4: four nodes per wave, 16 lanes each, the activity
-    sums as DPP left folds) against the reference's own presolveNode
-    outputs: bounds bit for bit, verdicts and mod counts (K1G keeps no mod
-    log)."""
+def test_fbbt_group_matches_reference_golden(ctx, name, variant):
+    """K1G (variants 4 / 5 / 6: 16 / 8 / 4 lanes per node, the activity
+    sums added in term order from LDS product slots) against the
+    reference's own presolveNode outputs: bounds bit for bit, verdicts and
+    mod counts (K1G keeps no mod log)."""
     from minotaur_amd.runtime import MgpuError
     p, g = load_fbbt(name)
     if p.m > 64:
         pytest.skip('K1G keeps row flags in one 64-bit mask')
     ctx.load(p)
-    ctx.set_fbbt_variant(4)
+    ctx.set_fbbt_variant(variant)
     try:
         r = ctx.fbbt(g['lb_in'], g['ub_in'], _inc(g), mod_cap=0)
     except MgpuError as e:
@@ -73,9 +74,10 @@ def test_fbbt_group_matches_reference_golden(ctx, name):
     assert np.array_equal(r.nmods, g['nmods'])
 
 
+@pytest.mark.parametrize('variant', [4, 5, 6])
 @pytest.mark.parametrize('inst', ['tls4_lin', 'tls4_oa'])
 @pytest.mark.parametrize('inc', [math.inf, 20.0])
-def test_fbbt_group_large_batch_vs_oracle(ctx, inst, inc):
+def test_fbbt_group_large_batch_vs_oracle(ctx, inst, inc, variant):
     """K1G on 20 001 random-branching boxes (ragged last wave) against the
     C restatement, with and without an incumbent."""
     import os
@@ -83,7 +85,7 @@ def test_fbbt_group_large_batch_vs_oracle(ctx, inst, inc):
     p = LinProblem.load(os.path.join(here, '..', 'minotaur_amd', 'instances', f'{inst}.npz'))
     LB, UB = random_boxes(p, 20001, 4242)
     ctx.load(p)
-    ctx.set_fbbt_variant(4)
+    ctx.set_fbbt_variant(variant)
     try:
         r = ctx.fbbt(LB, UB, inc)
     finally:

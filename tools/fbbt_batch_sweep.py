@@ -1,7 +1,8 @@
 """K1 variants against batch size on config 2's instance (tls4-oa, random-
 branching boxes, with and without an incumbent): the auto choice of
-mgpu_fbbt_dev (K1: LDS / global / persistent lane-per-node) vs K1G (variant
-4: four nodes per wave, 16 lanes each).  Median kernel ms of 5 launches.
+mgpu_fbbt_dev (K1: LDS / global / persistent lane-per-node), the persistent
+K1 (variant 3) and K1G with 16 / 8 / 4 lanes per node (variants 4 / 5 / 6).
+Median kernel ms of 5 launches.
 
     python tools/fbbt_batch_sweep.py
 """
@@ -15,6 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+VARIANTS = (0, 3, 4, 5, 6)
+
+
 def main():
     import torch
     from minotaur_amd.problem import LinProblem, random_boxes
@@ -24,7 +28,7 @@ def main():
     ctx.load(p)
     dev = torch.device('cuda', 0)
     LBa, UBa = random_boxes(p, 524288, 20261017)
-    for B in (1024, 4096, 16384, 65536, 131072, 262144, 524288):
+    for B in (1024, 4096, 16384, 65536, 262144, 524288):
         lb = torch.from_numpy(LBa[:B]).to(dev)
         ub = torch.from_numpy(UBa[:B]).to(dev)
         lo, uo = torch.empty_like(lb), torch.empty_like(ub)
@@ -32,7 +36,7 @@ def main():
         nm = torch.zeros(B, dtype=torch.int32, device=dev)
         row = [B]
         for inc in (math.inf, 3.2):
-            for v in (0, 4):
+            for v in VARIANTS:
                 ctx.set_fbbt_variant(v)
                 ms = []
                 for _ in range(5):
@@ -41,8 +45,9 @@ def main():
                     ms.append(ctx.last_kernel_ms('fbbt'))
                 row.append(round(float(np.median(ms)), 3))
         ctx.set_fbbt_variant(0)
-        print("B %7d  no-inc: auto %.3f K1G %.3f ms   inc 3.2: auto %.3f K1G %.3f ms" % tuple(row),
-              flush=True)
+        print("B %7d " % B + "  ".join(
+            "%s v%d %.3f" % ("inc" if i >= len(VARIANTS) else "noinc", VARIANTS[i % len(VARIANTS)], t)
+            for i, t in enumerate(row[1:])), flush=True)
     ctx.close()
 
 

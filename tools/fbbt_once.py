@@ -1,5 +1,7 @@
 """Runs K1 alone (tls4-lin, B nodes, variant/npw from argv) a few times: a
-target for rocprofv3 counter passes.  python tools/fbbt_once.py B variant"""
+target for rocprofv3 counter passes.  python tools/fbbt_once.py B variant
+(MGPU_FBBT_INST names the instance, default tls4_lin; MGPU_FBBT_INC the
+incumbent, default 1.2)"""
 import os
 import sys
 
@@ -13,7 +15,7 @@ from minotaur_amd.runtime import Context  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 variant = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_lin.npz'))
+p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', os.environ.get('MGPU_FBBT_INST', 'tls4_lin') + '.npz'))
 ctx = Context(0)
 ctx.load(p)
 dev = torch.device('cuda', 0)
@@ -25,6 +27,6 @@ inf = torch.zeros(B, dtype=torch.int32, device=dev)
 nm = torch.zeros(B, dtype=torch.int32, device=dev)
 ctx.set_fbbt_variant(variant)
 for _ in range(3):
-    ctx.fbbt_dev(lb, ub, olb, oub, inf, nm, 1.2)
+    ctx.fbbt_dev(lb, ub, olb, oub, inf, nm, float(os.environ.get('MGPU_FBBT_INC', '1.2')))
     ctx.sync()
     print(f"fbbt B={B} variant={variant} {ctx.last_kernel_ms('fbbt'):.3f} ms", flush=True)
