@@ -7,9 +7,12 @@
 // Mehrotra predictor-corrector interior point, one node per workgroup.  The
 // Newton system is the KKT block [Q + D, A'; A, 0] (D = Z_l/S_l + Z_u/S_u),
 // reduced through its Schur complement:
-//   K = Q + D = L L'        qp_potrf   blocked right-looking Cholesky:
-//                                       16x16 tiles, trailing updates on
-//                                       v_mfma_f64_16x16x4_f64
+//   K = Q + D = L L'        qp_potrf_ll blocked left-looking Cholesky:
+//                                       16x16 tiles, each tile's update
+//                                       over all earlier column blocks on
+//                                       v_mfma_f64_16x16x4_f64, L written
+//                                       once (qp_potrf: the right-looking
+//                                       form, for n past its LDS panel)
 //   W = L^-1 A', M = W'W    qp_trsm_syrk  blocked forward substitution and
 //                                       the Gram product, both on MFMA
 //   M = Lm Lm', steps       qp_step    Lm in LDS, predictor + corrector
@@ -22,6 +25,7 @@
 // iterates up to rounding).
 #include "mgpu_internal.h"
 #include "qp_internal.h"
+#include "wave.h"
 
 namespace mgpu {
 namespace {
@@ -146,9 +150,11 @@ __global__ __launch_bounds__(kT) void qp_prep(DevQP q, QpWork w, int assemble) {
     return;
   }
   if (!assemble) return;
+  // assemble: bit 0 K, bit 1 W (qp_potrf_ll builds its K tiles from Q and
+  // qp_trsm_syrk_lds its W in LDS; the fallback kernels read these)
   // K = Q + diag(D), fixed rows/columns identity
   double *K = w.K + (size_t)b * np * np;
-  for (size_t e = t; e < (size_t)np * np; e += kT) {
+  for (size_t e = t; e < ((assemble & 1) ? (size_t)np * np : 0); e += kT) {
     const int i = (int)(e / np), j = (int)(e % np);
     const bool fi = w.l[o + i] < w.u[o + i], fj = w.l[o + j] < w.u[o + j];
     double v;
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(kT) void qp_prep(DevQP q, QpWork w, int assemble) {
   }
   // W = A' with the rows of fixed variables zeroed
   double *W = w.W + (size_t)b * np * mp;
-  for (size_t e = t; e < (size_t)np * mp; e += kT) {
+  for (size_t e = t; e < ((assemble & 2) ? (size_t)np * mp : 0); e += kT) {
     const int j = (int)(e / mp);
     W[e] = w.l[o + j] < w.u[o + j] ? q.AT[e] : 0.0;
   }
@@ -261,6 +267,145 @@ __global__ __launch_bounds__(kT) void qp_potrf(QpWork w, int np) {
   }
 }
 
+// ---- left-looking blocked Cholesky, K assembled on the fly ------------------
+// For column block j, every tile (i, j), i >= j, is K_ij - sum_k L_ik L_jk'
+// accumulated on MFMA over all k at once (L_ik and L_jk streamed from
+// HBM / L2, each 16x16 tile read as 16 rows of 128 contiguous bytes, four
+// column blocks' loads in flight together; the LDS holds only the tiles of
+// column block j, so three workgroups share a CU), the diagonal tile is factored and the tiles
+// below solved against it, and L_ij is written ONCE.  The right-looking
+// kernel above read and wrote the whole trailing matrix for every column
+// block (~9 MB per node at n = 304); this one reads ~2.3 MB of L and writes
+// its lower triangle.  K_ij itself is never stored: Q (shared by the batch,
+// L2-resident) plus the node's barrier diagonal, identity on fixed
+// variables, as qp_prep assembles it.
+constexpr int kPT = 512;   // 8 waves
+
+size_t potrf_ll_lds(int np) {
+  const int T = np / 16;
+  return sizeof(double) * (16 * 17 + (size_t)T * 256 + 2 * (size_t)np);
+}
+
+__global__ __launch_bounds__(kPT, 6) void qp_potrf_ll(DevQP q, QpWork w) {
+  extern __shared__ double sm[];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (w.done[b]) return;
+  const int np = q.np, T = np / 16;
+  const size_t o = (size_t)b * np;
+  double *K = w.K + (size_t)b * np * np;
+  double *D = sm;                       // [16][17] diagonal tile
+  double *P = D + 16 * 17;              // [T][16][16] tiles j..T-1 of column block j
+  double *dg = P + (size_t)T * 256;     // [np] barrier diagonal zl/sl + zu/su
+  double *fr = dg + np;                 // [np] 1 free, 0 fixed
+  for (int j = t; j < np; j += kPT) {
+    const double l = w.l[o + j], u = w.u[o + j], x = w.x[o + j];
+    const bool f = l < u;
+    fr[j] = f ? 1.0 : 0.0;
+    dg[j] = f ? w.zl[o + j] / (x - l) + w.zu[o + j] / (u - x) : 0.0;
+  }
+  __syncthreads();
+  const int row = lane & 15, kq = lane >> 4;
+  for (int jb = 0; jb < T; ++jb) {
+    const int c0 = jb * 16;
+    // (1) tiles i >= jb: acc = K_ij - sum_{k < jb} L_ik L_jk'
+    for (int i = jb + wave; i < T; i += kPT / 64) {
+      const int gi = i * 16;
+      d4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = gi + kq + 4 * r, gc = c0 + row;
+        double v;
+        if (fr[gr] == 0.0 || fr[gc] == 0.0) v = gr == gc ? 1.0 : 0.0;
+        else v = gr == gc ? q.Q[(size_t)gr * np + gc] + dg[gr] : q.Q[(size_t)gr * np + gc];
+        acc[r] = v;
+      }
+      // lane (row, kq) holds k = 16 kb + 4 kq + kk of A = L_ik and B = L_jk'
+      const double *ap = K + (size_t)(gi + row) * np + 4 * kq;
+      const double *bp = K + (size_t)(c0 + row) * np + 4 * kq;   // L_jk rows (L2 hits)
+      // four column blocks' loads in flight before their 16 MFMAs (one
+      // dependent HBM round trip per four blocks instead of per block)
+      int kb = 0;
+      for (; kb + 4 <= jb; kb += 4) {
+        double4 a[4], bb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a[u] = *reinterpret_cast<const double4 *>(ap + (kb + u) * 16);
+          bb[u] = *reinterpret_cast<const double4 *>(bp + (kb + u) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[u].x, bb[u].x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[u].y, bb[u].y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[u].z, bb[u].z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[u].w, bb[u].w, acc, 0, 0, 0);
+        }
+      }
+      for (; kb < jb; ++kb) {
+        const double4 a = *reinterpret_cast<const double4 *>(ap + kb * 16);
+        const double4 bq = *reinterpret_cast<const double4 *>(bp + kb * 16);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.x, bq.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.y, bq.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.z, bq.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.w, bq.w, acc, 0, 0, 0);
+      }
+      double *pt = P + (size_t)(i - jb) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pt[(kq + 4 * r) * 16 + row] = acc[r];
+    }
+    __syncthreads();
+    // (2) factor the diagonal tile (wave 0)
+    if (wave == 0) {
+      for (int e = lane; e < 256; e += 64) D[(e >> 4) * 17 + (e & 15)] = P[e];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int c = 0; c < 16; ++c) {
+        const double dd = sqrt(D[c * 17 + c]);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) D[c * 17 + c] = dd;
+        if (lane > c && lane < 16) D[lane * 17 + c] /= dd;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int e = lane; e < 256; e += 64) {
+          const int r = e >> 4, s2 = e & 15;
+          if (s2 > c && r >= s2) D[r * 17 + s2] -= D[r * 17 + c] * D[s2 * 17 + c];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      for (int e = lane; e < 256; e += 64) {
+        const int r = e >> 4, s2 = e & 15;
+        if (s2 <= r) K[(size_t)(c0 + r) * np + c0 + s2] = D[r * 17 + s2];
+      }
+    }
+    __syncthreads();
+    // (3) the tiles below: X = P L_jj^-T, one row per thread, written once
+    const int rows = np - c0 - 16;
+#pragma unroll 1
+    for (int r = t; r < rows; r += kPT) {
+      const int gr = c0 + 16 + r;
+      const double *pr = P + 256 + (size_t)(r >> 4) * 256 + (r & 15) * 16;
+      double a[16];
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) a[s2] = pr[s2];
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        double v = a[s2];
+        const double *dr = D + s2 * 17;   // re-read per row (LDS broadcast)
+#pragma unroll
+        for (int p2 = 0; p2 < s2; ++p2) v -= a[p2] * dr[p2];
+        a[s2] = v / dr[s2];
+        // keep the tile's loads in their row: hoisting all 136 of them
+        // (the compiler's choice) costs 250 VGPRs and spills at 8 waves
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) K[(size_t)gr * np + c0 + s2] = a[s2];
+    }
+    __syncthreads();
+  }
+}
+
 // ---- W = L^-1 A' (blocked forward substitution) and M = W'W, MFMA ---------
 __global__ __launch_bounds__(kT) void qp_trsm_syrk(QpWork w, int np, int mp) {
   extern __shared__ double sm[];
@@ -341,76 +486,217 @@ __global__ __launch_bounds__(kT) void qp_trsm_syrk(QpWork w, int np, int mp) {
   }
 }
 
+// ---- W = L^-1 A' and M = W'W with W resident in LDS -------------------------
+// The whole W (np x mp, row stride mp + 1) lives in LDS (156 KB at n = 304,
+// m = 61): assembled from A' there, solved block row by block row (diagonal
+// block by substitution, the rows below on MFMA with L_ik streamed from HBM
+// as 128-B row pieces), then written out once as W and W', and M = W'W
+// taken from LDS on MFMA.  qp_trsm_syrk above read and wrote W's trailing
+// rows in HBM for every block row.
+size_t trsm_lds_bytes(int np, int mp) {
+  return sizeof(double) * ((size_t)np * (mp + 1) + 16 * 17);
+}
+
+__global__ __launch_bounds__(kPT) void qp_trsm_syrk_lds(DevQP q, QpWork w) {
+  extern __shared__ double sm[];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (w.done[b]) return;
+  const int np = q.np, mp = q.mp, ld = mp + 1, T = np / 16, CB = mp / 16;
+  const size_t o = (size_t)b * np;
+  const double *K = w.K + (size_t)b * np * np;
+  double *Ws = sm;                 // [np][ld]
+  double *D = Ws + (size_t)np * ld; // [16][17]
+  for (int e = t; e < np * mp; e += kPT) {
+    const int j = e / mp, i = e - j * mp;
+    Ws[j * ld + i] = w.l[o + j] < w.u[o + j] ? q.AT[e] : 0.0;
+  }
+  const int row = lane & 15, kq = lane >> 4;
+  for (int kb = 0; kb < T; ++kb) {
+    const int r0 = kb * 16;
+    for (int e = t; e < 256; e += kPT) D[(e >> 4) * 17 + (e & 15)] = K[(size_t)(r0 + (e >> 4)) * np + r0 + (e & 15)];
+    __syncthreads();
+    // the diagonal block rows: one column per thread
+    for (int cidx = t; cidx < mp; cidx += kPT) {
+      double v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = Ws[(r0 + r) * ld + cidx];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double s2 = v[r];
+#pragma unroll
+        for (int p2 = 0; p2 < r; ++p2) s2 -= D[r * 17 + p2] * v[p2];
+        v[r] = s2 / D[r * 17 + r];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Ws[(r0 + r) * ld + cidx] = v[r];
+    }
+    __syncthreads();
+    // W_i -= L_ik W_k for row tiles i > kb (MFMA; lane (row, kq) holds
+    // k = 4 kq + kk of both operands)
+    // a wave owns a row tile i and all CB column tiles of it: L_ik is loaded
+    // once (and the next row tile's L prefetched) for CB x 4 MFMAs
+    const int nrow = T - kb - 1;
+    double4 an = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (wave < nrow)
+      an = *reinterpret_cast<const double4 *>(K + (size_t)((kb + 1 + wave) * 16 + row) * np + r0 + 4 * kq);
+    for (int ir = wave; ir < nrow; ir += kPT / 64) {
+      const int i = kb + 1 + ir;
+      const double4 a = an;
+      if (ir + kPT / 64 < nrow)
+        an = *reinterpret_cast<const double4 *>(K + (size_t)((i + kPT / 64) * 16 + row) * np + r0 + 4 * kq);
+      for (int cb = 0; cb < CB; ++cb) {
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = Ws[(i * 16 + kq + 4 * r) * ld + cb * 16 + row];
+        const double *bp = Ws + (r0 + 4 * kq) * ld + cb * 16 + row;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.x, bp[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.y, bp[ld], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.z, bp[2 * ld], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.w, bp[3 * ld], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ws[(i * 16 + kq + 4 * r) * ld + cb * 16 + row] = acc[r];
+      }
+    }
+    __syncthreads();
+  }
+  // W (step: W'v, coalesced over i) and W' (step: W dy, coalesced over j)
+  double *W = w.W + (size_t)b * np * mp;
+  double *WT = w.WT + (size_t)b * np * mp;
+  for (int e = t; e < np * mp; e += kPT) {
+    const int j = e / mp, i = e - j * mp;
+    W[e] = Ws[j * ld + i];
+  }
+  for (int e = t; e < np * mp; e += kPT) {
+    const int i = e / np, j = e - i * np;
+    WT[e] = Ws[j * ld + i];
+  }
+  // M = W'W: CB x CB tiles summed over np (A[i][k] = W[k][i], B[k][j] = W[k][j])
+  double *M = w.M + (size_t)b * mp * mp;
+  for (int tix = wave; tix < CB * CB; tix += kPT / 64) {
+    const int ib = tix / CB, jb = tix % CB;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < np; k0 += 16) {
+      const double *ap = Ws + (k0 + 4 * kq) * ld + ib * 16 + row;
+      const double *bp = Ws + (k0 + 4 * kq) * ld + jb * 16 + row;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[kk * ld], bp[kk * ld], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      M[(size_t)(ib * 16 + kq + 4 * r) * mp + jb * 16 + row] = acc[r];
+  }
+}
+
 // ---- per-node Newton steps ---------------------------------------------------
 struct StepSm {
   double *x, *l, *u, *zl, *zu, *rd, *v, *dx, *s2, *dzl, *dzu, *rl, *ru;
   double *y, *rp, *tt, *dy;
   double *Lm;     // [mp][mp+1]
-  double *part;   // [16][17] partial sums
-  double *dt;     // [16][17] diagonal tile of L
+  double *pre;    // [2][12][17] partial row sums (double-buffered)
+  double *dt;     // [2][16][17] diagonal tiles of L
+  double *xt;     // [2][16][17] the tiles between consecutive diagonal tiles
   double *red;    // [kT]
 };
 
-// v = L^-1 r, blocked by 16 rows: a GEMV of the block's rows against the
-// solved part (256 threads, 16 partial sums per row), then the diagonal
-// tile (staged in LDS) by a 16-lane substitution with v_readlane
-// broadcasts.  dt: [16][17] LDS tile.
-__device__ void fwd_L(const double *K, int np, const double *r, double *v, double *part,
-                      double *dt) {
-  const int t = threadIdx.x, rr = t & 15, pp = t >> 4;
+// The triangular solves with L, pipelined over 16-row blocks.  Block ib's
+// row sums split into the columns solved before the previous block (a GEMV
+// waves 1-3 compute while wave 0 is still substituting the previous block,
+// 12 partial sums per row) and the previous block's 16 columns (the tile
+// between the two diagonal tiles, prefetched into LDS by the same waves);
+// wave 0 adds the two parts, then substitutes the diagonal tile (staged
+// the same way) with v_readlane broadcasts.  One workgroup barrier per
+// block; nothing from HBM is on wave 0's critical path.  pre / dt / xt are
+// double-buffered [12|16][17] LDS tiles (StepSm::pre, dt, xt).
+__device__ void fwd_L(const double *K, int np, const double *r, double *v, const StepSm &s) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int T = np / 16;
+  if (wave > 0)
+    for (int e = t - 64; e < 256; e += kT - 64) s.dt[(e >> 4) * 17 + (e & 15)] = K[(size_t)(e >> 4) * np + (e & 15)];
+  __syncthreads();
   for (int ib = 0; ib < T; ++ib) {
+    const int cur = ib & 1, nxt = cur ^ 1;
     const int r0 = ib * 16;
-    double acc = 0.0;
-    for (int c = pp; c < r0; c += 16) acc += K[(size_t)(r0 + rr) * np + c] * v[c];
-    part[pp * 17 + rr] = acc;
-    dt[(t >> 4) * 17 + (t & 15)] = K[(size_t)(r0 + (t >> 4)) * np + r0 + (t & 15)];
-    __syncthreads();
-    if (t < 64) {
-      double val = 0.0;
-      if (t < 16) {
-        double sum = 0.0;
-        for (int q2 = 0; q2 < 16; ++q2) sum += part[q2 * 17 + t];
-        val = r[r0 + t] - sum;
+    if (wave == 0) {
+      const int i = lane & 15, q = lane >> 4;
+      double acc = 0.0;
+      if (ib > 0) {
+        const double *pre = s.pre + cur * 204, *xt = s.xt + cur * 272;
+        for (int k = q; k < 28; k += 4)
+          acc += k < 12 ? pre[k * 17 + i] : xt[i * 17 + (k - 12)] * v[r0 - 16 + (k - 12)];
       }
+      acc += __shfl_xor(acc, 16, 64);
+      acc += __shfl_xor(acc, 32, 64);
+      const double *dt = s.dt + cur * 272;
+      double val = lane < 16 ? r[r0 + lane] - acc : 0.0;
       double mine = 0.0;
+#pragma unroll
       for (int c = 0; c < 16; ++c) {
-        const double vc = __shfl(val, c, 64) / dt[c * 17 + c];
-        if (t == c) mine = vc;
-        if (t > c && t < 16) val -= dt[t * 17 + c] * vc;
+        const double vc = rld(val, c) / dt[c * 17 + c];   // v_readlane broadcast
+        if (lane == c) mine = vc;
+        if (lane > c && lane < 16) val -= dt[lane * 17 + c] * vc;
       }
-      if (t < 16) v[r0 + t] = mine;
+      if (lane < 16) v[r0 + lane] = mine;
+    } else if (ib + 1 < T) {
+      const int tt = t - 64, rr = tt & 15, pq = tt >> 4, r1 = r0 + 16;
+      double a = 0.0;
+      for (int c = pq; c < r0; c += 12) a += K[(size_t)(r1 + rr) * np + c] * v[c];
+      s.pre[nxt * 204 + pq * 17 + rr] = a;
+      for (int e = tt; e < 256; e += kT - 64) {
+        const int ei = e >> 4, ej = e & 15;
+        s.dt[nxt * 272 + ei * 17 + ej] = K[(size_t)(r1 + ei) * np + r1 + ej];
+        s.xt[nxt * 272 + ei * 17 + ej] = K[(size_t)(r1 + ei) * np + r0 + ej];
+      }
     }
     __syncthreads();
   }
 }
 
-// x = L^-T s (blocked, from the last row block up; same scheme)
-__device__ void bwd_LT(const double *K, int np, const double *s, double *xo, double *part,
-                       double *dt) {
-  const int t = threadIdx.x, rr = t & 15, pp = t >> 4;
+// x = L^-T s (from the last row block up; the same pipeline over columns of L)
+__device__ void bwd_LT(const double *K, int np, const double *sv, double *xo, const StepSm &s) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int T = np / 16;
-  for (int ib = T - 1; ib >= 0; --ib) {
+  if (wave > 0) {
+    const int d0 = (T - 1) * 16;
+    for (int e = t - 64; e < 256; e += kT - 64) s.dt[(e >> 4) * 17 + (e & 15)] = K[(size_t)(d0 + (e >> 4)) * np + d0 + (e & 15)];
+  }
+  __syncthreads();
+  for (int n = 0; n < T; ++n) {
+    const int ib = T - 1 - n;
+    const int cur = n & 1, nxt = cur ^ 1;
     const int r0 = ib * 16;
-    double acc = 0.0;
-    for (int k = r0 + 16 + pp; k < np; k += 16) acc += K[(size_t)k * np + r0 + rr] * xo[k];
-    part[pp * 17 + rr] = acc;
-    dt[(t >> 4) * 17 + (t & 15)] = K[(size_t)(r0 + (t >> 4)) * np + r0 + (t & 15)];
-    __syncthreads();
-    if (t < 64) {
-      double val = 0.0;
-      if (t < 16) {
-        double sum = 0.0;
-        for (int q2 = 0; q2 < 16; ++q2) sum += part[q2 * 17 + t];
-        val = s[r0 + t] - sum;
+    if (wave == 0) {
+      const int i = lane & 15, q = lane >> 4;
+      double acc = 0.0;
+      if (n > 0) {
+        const double *pre = s.pre + cur * 204, *xt = s.xt + cur * 272;
+        for (int k = q; k < 28; k += 4)
+          acc += k < 12 ? pre[k * 17 + i] : xt[(k - 12) * 17 + i] * xo[r0 + 16 + (k - 12)];
       }
+      acc += __shfl_xor(acc, 16, 64);
+      acc += __shfl_xor(acc, 32, 64);
+      const double *dt = s.dt + cur * 272;
+      double val = lane < 16 ? sv[r0 + lane] - acc : 0.0;
       double mine = 0.0;
+#pragma unroll
       for (int c = 15; c >= 0; --c) {
-        const double xc = __shfl(val, c, 64) / dt[c * 17 + c];
-        if (t == c) mine = xc;
-        if (t < c) val -= dt[c * 17 + t] * xc;
+        const double xc = rld(val, c) / dt[c * 17 + c];
+        if (lane == c) mine = xc;
+        if (lane < c) val -= dt[c * 17 + lane] * xc;
       }
-      if (t < 16) xo[r0 + t] = mine;
+      if (lane < 16) xo[r0 + lane] = mine;
+    } else if (ib > 0) {
+      // block ib - 1: rows k >= r0 + 16 of columns r0-16+rr (solved), the
+      // tile rows [r0, r0+16) for the combine, its diagonal tile
+      const int tt = t - 64, rr = tt & 15, pq = tt >> 4, c1 = r0 - 16;
+      double a = 0.0;
+      for (int k = r0 + 16 + pq; k < np; k += 12) a += K[(size_t)k * np + c1 + rr] * xo[k];
+      s.pre[nxt * 204 + pq * 17 + rr] = a;
+      for (int e = tt; e < 256; e += kT - 64) {
+        const int ei = e >> 4, ej = e & 15;
+        s.dt[nxt * 272 + ei * 17 + ej] = K[(size_t)(c1 + ei) * np + c1 + ej];
+        s.xt[nxt * 272 + ei * 17 + ej] = K[(size_t)(r0 + ei) * np + c1 + ej];
+      }
     }
     __syncthreads();
   }
@@ -421,7 +707,7 @@ __device__ void bwd_LT(const double *K, int np, const double *s, double *xo, dou
 __device__ void kkt_solve(const double *K, const double *W, const double *WT, int np, int mp,
                           const StepSm &s, const double *r1) {
   const int t = threadIdx.x;
-  fwd_L(K, np, r1, s.v, s.part, s.dt);
+  fwd_L(K, np, r1, s.v, s);
   // tt = rp - W'v (4 partial sums per column, coalesced over the column)
   {
     const int i = t & 63, pp = t >> 6;
@@ -433,27 +719,23 @@ __device__ void kkt_solve(const double *K, const double *W, const double *WT, in
     if (t < mp) s.tt[t] = s.rp[t] - (((s.red[t] + s.red[t + 64]) + s.red[t + 128]) + s.red[t + 192]);
     __syncthreads();
   }
-  // dy = Lm^-T Lm^-1 tt (wave 0, column sweeps in LDS)
+  // dy = Lm^-T Lm^-1 tt (wave 0: lane t holds tt[t] in a register, the
+  // pivot value broadcast by v_readlane; same operations in the same order
+  // as the column sweeps through LDS they replace)
   if (t < 64) {
     const int mpad = mp + 1;
+    double val = t < mp ? s.tt[t] : 0.0;
     for (int k = 0; k < mp; ++k) {
-      const double zk = s.tt[k] / s.Lm[k * mpad + k];
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (t == k) s.tt[k] = zk;
-      if (t > k && t < mp) s.tt[t] -= s.Lm[t * mpad + k] * zk;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+      const double zk = rld(val, k) / s.Lm[k * mpad + k];
+      if (t == k) val = zk;
+      else if (t > k && t < mp) val -= s.Lm[t * mpad + k] * zk;
     }
     for (int k = mp - 1; k >= 0; --k) {
-      const double zk = s.tt[k] / s.Lm[k * mpad + k];
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (t == k) s.dy[k] = zk;
-      if (t < k) s.tt[t] -= s.Lm[k * mpad + t] * zk;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+      const double zk = rld(val, k) / s.Lm[k * mpad + k];
+      if (t == k) val = zk;
+      else if (t < k) val -= s.Lm[k * mpad + t] * zk;
     }
+    if (t < mp) s.dy[t] = val;
   }
   __syncthreads();
   // s2 = v + W dy  (W' [mp][np] copy: coalesced across j)
@@ -463,7 +745,7 @@ __device__ void kkt_solve(const double *K, const double *W, const double *WT, in
     s.s2[j] = s.v[j] + acc;
   }
   __syncthreads();
-  bwd_LT(K, np, s.s2, s.dx, s.part, s.dt);
+  bwd_LT(K, np, s.s2, s.dx, s);
   for (int j = t; j < np; j += kT)
     if (!(s.l[j] < s.u[j])) s.dx[j] = 0.0;
   __syncthreads();
@@ -497,7 +779,8 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   s.rd = p; p += np; s.v = p; p += np; s.dx = p; p += np; s.s2 = p; p += np;
   s.dzl = p; p += np; s.dzu = p; p += np; s.rl = p; p += np; s.ru = p; p += np;
   s.y = p; p += mp; s.rp = p; p += mp; s.tt = p; p += mp; s.dy = p; p += mp;
-  s.Lm = p; p += mp * mpad; s.part = p; p += 16 * 17; s.dt = p; p += 16 * 17;
+  s.Lm = p; p += mp * mpad; s.pre = p; p += 2 * 204; s.dt = p; p += 2 * 272;
+  s.xt = p; p += 2 * 272;
   s.red = p; p += kT;
   double *r1 = s.s2;  // reuse: r1 is consumed by fwd_L before s2 is written
   const size_t o = (size_t)b * np, oy = (size_t)b * mp;
@@ -629,7 +912,7 @@ __global__ __launch_bounds__(kT) void qp_final(DevQP q, QpWork w) {
 }  // namespace
 
 size_t qp_step_lds(int np, int mp) {
-  return sizeof(double) * ((size_t)13 * np + 4 * mp + (size_t)mp * (mp + 1) + 2 * 16 * 17 + kT);
+  return sizeof(double) * ((size_t)13 * np + 4 * mp + (size_t)mp * (mp + 1) + 2 * 204 + 4 * 272 + kT);
 }
 
 hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s) {
@@ -645,15 +928,33 @@ hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s) {
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void *)qp_potrf,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void *)qp_potrf_ll,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void *)qp_trsm_syrk_lds,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const size_t lds_prep = sizeof(double) * (size_t)(q.np + q.mp);
   const size_t lds_potrf = sizeof(double) * (16 * 17 + (size_t)(q.np / 16) * 256);
   const size_t lds_trsm = sizeof(double) * (16 * 17 + (size_t)16 * q.mp);
-  hipLaunchKernelGGL(qp_prep, dim3(w.B), dim3(kT), lds_prep, s, q, w, 1);
-  hipLaunchKernelGGL(qp_potrf, dim3(w.B), dim3(kT), lds_potrf, s, w, q.np);
-  hipLaunchKernelGGL(qp_trsm_syrk, dim3(w.B), dim3(kT), lds_trsm, s, w, q.np, q.mp);
+  // left-looking factorization while its row panel fits the LDS (n <= ~580)
+  static const bool rl = getenv("MGPU_QP_RIGHT_LOOKING") != nullptr;   // A/B switch
+  const bool ll = !rl && potrf_ll_lds(q.np) <= 160 * 1024;
+  // W resident in LDS when it fits (n * (m + 1) <= ~20 000)
+  const bool wl = ll && trsm_lds_bytes(q.np, q.mp) <= 160 * 1024;
+  hipLaunchKernelGGL(qp_prep, dim3(w.B), dim3(kT), lds_prep, s, q, w, (ll ? 0 : 1) | (wl ? 0 : 2));
+  if (ll)
+    hipLaunchKernelGGL(qp_potrf_ll, dim3(w.B), dim3(kPT), potrf_ll_lds(q.np), s, q, w);
+  else
+    hipLaunchKernelGGL(qp_potrf, dim3(w.B), dim3(kT), lds_potrf, s, w, q.np);
+  if (wl)
+    hipLaunchKernelGGL(qp_trsm_syrk_lds, dim3(w.B), dim3(kPT), trsm_lds_bytes(q.np, q.mp), s, q,
+                       w);
+  else
+    hipLaunchKernelGGL(qp_trsm_syrk, dim3(w.B), dim3(kT), lds_trsm, s, w, q.np, q.mp);
   hipLaunchKernelGGL(qp_step, dim3(w.B), dim3(kT), qp_step_lds(q.np, q.mp), s, q, w);
   return hipGetLastError();
 }
