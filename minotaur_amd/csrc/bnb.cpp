@@ -86,8 +86,8 @@ struct BnbState {
   bool guided = true;          // IntVarHandler guided_dive (Environment.cpp:160-163)
   DevBuf cslots;               // [2 nb] child slots
   std::vector<int> pick;       // mgpu_bnb_pick: pool slots of the picked nodes, in pick order
-  void release() {
-    for (DevBuf *b : {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
+  std::vector<DevBuf *> bufs() {
+    return {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
                       &dec, &cand, &bvar, &bval, &bup, &depth_in, &pos, &bsum, &bidx, &boff,
                       &bmin, &bcnt, &out, &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj,
                       &r_it, &plive, &keys, &keys2, &vals, &vals2, &sort_tmp, &counts,
@@ -97,8 +97,20 @@ struct BnbState {
                       &nsb, &sb_off, &sb_var, &sb_val, &dec2, &nev, &ev_var, &ev_side, &ev_cost,
                       &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit, &ev_off, &cv_var, &cv_side,
                       &cv_cost, &ppk, &ppath, &ppst, &bpk, &bppath, &bpst, &opk, &oppath, &opst,
-                      &cslots, &ch_head, &ch_st, &ch_d, &ch_binv, &sbstop, &sblist, &sbcnt})
-      b->release();
+                      &cslots, &ch_head, &ch_st, &ch_d, &ch_binv, &sbstop, &sblist, &sbcnt};
+  }
+  void release() {
+    for (DevBuf *b : bufs()) b->release();
+  }
+  // takes over another state's device buffers (grow-only DevBufs): a new
+  // tree on the same context reuses the pool instead of freeing and
+  // allocating gigabytes again (mgpu_bnb_init)
+  void adopt(BnbState &o) {
+    std::vector<DevBuf *> a = bufs(), b = o.bufs();
+    for (size_t i = 0; i < a.size(); ++i) {
+      std::swap(a[i]->p, b[i]->p);
+      std::swap(a[i]->bytes, b[i]->bytes);
+    }
   }
 };
 
@@ -410,8 +422,12 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   if (capacity < 2 || !root_lb || !root_ub)
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: bad argument");
   HIPCHK(c, hipSetDevice(c->device));
-  bnb_state_free(c);
   BnbState *s = new BnbState();
+  if (c->bnb) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // the old tree's kernels are done with them
+    s->adopt(*c->bnb);
+  }
+  bnb_state_free(c);
   c->bnb = s;
   const int n = c->lp.n, m = c->lp.m, N = n + m;
   s->n = n;

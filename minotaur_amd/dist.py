@@ -112,6 +112,8 @@ class Comm:
             self.device = torch.device('cpu')
 
     def round_reduce(self, inc, n_open, err=0):
+        if not active():   # one rank: nothing to reduce (no device round trip per round)
+            return float(inc), float(n_open), float(n_open), float(err)
         t = torch.tensor([float(inc), -float(n_open), float(n_open), -float(err)],
                          dtype=torch.float64, device=self.device)
         if active():
