@@ -589,14 +589,23 @@ __global__ __launch_bounds__(kPT) void qp_trsm_syrk_lds(DevQP q, QpWork w) {
 }
 
 // ---- per-node Newton steps ---------------------------------------------------
+// LDS of the step kernel: only what crosses threads (the triangular solves'
+// vectors, the Schur factor and the solve pipeline's tiles); the per-column
+// state (x, bounds, duals, residual, steps) lives in registers, J columns
+// per thread (StepReg), so three workgroups share a CU.
 struct StepSm {
-  double *x, *l, *u, *zl, *zu, *rd, *v, *dx, *s2, *dzl, *dzu, *rl, *ru;
-  double *y, *rp, *tt, *dy;
+  double *v, *dx, *s2;
+  double *tt, *dy;
   double *Lm;     // [mp][mp+1]
   double *pre;    // [2][12][17] partial row sums (double-buffered)
   double *dt;     // [2][16][17] diagonal tiles of L
   double *xt;     // [2][16][17] the tiles between consecutive diagonal tiles
-  double *red;    // [kT]
+  double *red;    // [kT] (aliases pre: never live at the same time)
+};
+template <int J>
+struct StepReg {   // column j = threadIdx.x + k * kT, k < J
+  double x[J], l[J], u[J], zl[J], zu[J], rd[J], dzl[J], dzu[J], rl[J], ru[J];
+  __device__ __forceinline__ bool fr(int k) const { return l[k] < u[k]; }
 };
 
 // The triangular solves with L, pipelined over 16-row blocks.  Block ib's
@@ -704,8 +713,10 @@ __device__ void bwd_LT(const double *K, int np, const double *sv, double *xo, co
 
 // (dx, dy) for right-hand side r1: v = L^-1 r1, Lm Lm' dy = rp - W'v,
 // dx = L^-T (v + W dy), dx = 0 on fixed variables
-__device__ void kkt_solve(const double *K, const double *W, const double *WT, int np, int mp,
-                          const StepSm &s, const double *r1) {
+template <int J>
+__device__ void kkt_solve(const double *K, const double *W, const double *WT, const double *rp,
+                          int np, int mp, const StepSm &s, const StepReg<J> &g,
+                          const double *r1) {
   const int t = threadIdx.x;
   fwd_L(K, np, r1, s.v, s);
   // tt = rp - W'v (4 partial sums per column, coalesced over the column)
@@ -716,7 +727,7 @@ __device__ void kkt_solve(const double *K, const double *W, const double *WT, in
       for (int j = pp; j < np; j += 4) acc += W[(size_t)j * mp + i] * s.v[j];
     s.red[t] = acc;
     __syncthreads();
-    if (t < mp) s.tt[t] = s.rp[t] - (((s.red[t] + s.red[t + 64]) + s.red[t + 128]) + s.red[t + 192]);
+    if (t < mp) s.tt[t] = rp[t] - (((s.red[t] + s.red[t + 64]) + s.red[t + 128]) + s.red[t + 192]);
     __syncthreads();
   }
   // dy = Lm^-T Lm^-1 tt (wave 0: lane t holds tt[t] in a register, the
@@ -746,28 +757,35 @@ __device__ void kkt_solve(const double *K, const double *W, const double *WT, in
   }
   __syncthreads();
   bwd_LT(K, np, s.s2, s.dx, s);
-  for (int j = t; j < np; j += kT)
-    if (!(s.l[j] < s.u[j])) s.dx[j] = 0.0;
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    if (j < np && !g.fr(k)) s.dx[j] = 0.0;
+  }
   __syncthreads();
 }
 
-__device__ double max_step(const StepSm &s, int np, int which) {
+template <int J>
+__device__ double max_step(const StepSm &s, const StepReg<J> &g, int np, int which) {
   // which: 0 primal (sl with dx, su with -dx), 1 dual (zl with dzl, zu with dzu)
   double a = 1.0;
-  for (int j = threadIdx.x; j < np; j += kT) {
-    if (!(s.l[j] < s.u[j])) continue;
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = threadIdx.x + k * kT;
+    if (j >= np || !g.fr(k)) continue;
     if (which == 0) {
-      const double sl = s.x[j] - s.l[j], su = s.u[j] - s.x[j], d = s.dx[j];
+      const double sl = g.x[k] - g.l[k], su = g.u[k] - g.x[k], d = s.dx[j];
       if (d < 0) a = fmin(a, -sl / d);
       if (-d < 0) a = fmin(a, -su / -d);
     } else {
-      if (s.dzl[j] < 0) a = fmin(a, -s.zl[j] / s.dzl[j]);
-      if (s.dzu[j] < 0) a = fmin(a, -s.zu[j] / s.dzu[j]);
+      if (g.dzl[k] < 0) a = fmin(a, -g.zl[k] / g.dzl[k]);
+      if (g.dzu[k] < 0) a = fmin(a, -g.zu[k] / g.dzu[k]);
     }
   }
   return block_min(a, s.red);
 }
 
+template <int J>
 __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   extern __shared__ double sm[];
   const int b = blockIdx.x, t = threadIdx.x;
@@ -775,29 +793,28 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   const int np = q.np, mp = q.mp, mpad = mp + 1;
   StepSm s;
   double *p = sm;
-  s.x = p; p += np; s.l = p; p += np; s.u = p; p += np; s.zl = p; p += np; s.zu = p; p += np;
-  s.rd = p; p += np; s.v = p; p += np; s.dx = p; p += np; s.s2 = p; p += np;
-  s.dzl = p; p += np; s.dzu = p; p += np; s.rl = p; p += np; s.ru = p; p += np;
-  s.y = p; p += mp; s.rp = p; p += mp; s.tt = p; p += mp; s.dy = p; p += mp;
+  s.v = p; p += np; s.dx = p; p += np; s.s2 = p; p += np;
+  s.tt = p; p += mp; s.dy = p; p += mp;
   s.Lm = p; p += mp * mpad; s.pre = p; p += 2 * 204; s.dt = p; p += 2 * 272;
   s.xt = p; p += 2 * 272;
-  s.red = p; p += kT;
+  s.red = s.pre;   // kT = 256 <= 408 doubles
   double *r1 = s.s2;  // reuse: r1 is consumed by fwd_L before s2 is written
   const size_t o = (size_t)b * np, oy = (size_t)b * mp;
   const double *K = w.K + (size_t)b * np * np;
   const double *W = w.W + (size_t)b * np * mp;
   const double *WT = w.WT + (size_t)b * np * mp;
-  for (int j = t; j < np; j += kT) {
-    s.x[j] = w.x[o + j];
-    s.l[j] = w.l[o + j];
-    s.u[j] = w.u[o + j];
-    s.zl[j] = w.zl[o + j];
-    s.zu[j] = w.zu[o + j];
-    s.rd[j] = w.rd[o + j];
-  }
-  for (int i = t; i < mp; i += kT) {
-    s.y[i] = w.y[oy + i];
-    s.rp[i] = w.rp[oy + i];
+  const double *rp = w.rp + oy;
+  StepReg<J> g;
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    const bool in = j < np;
+    g.x[k] = in ? w.x[o + j] : 0.0;
+    g.l[k] = in ? w.l[o + j] : 0.0;
+    g.u[k] = in ? w.u[o + j] : 0.0;   // padding: l = u, a fixed column
+    g.zl[k] = in ? w.zl[o + j] : 0.0;
+    g.zu[k] = in ? w.zu[o + j] : 0.0;
+    g.rd[k] = in ? w.rd[o + j] : 0.0;
   }
   // Lm = chol(M + reg I)
   const double *M = w.M + (size_t)b * mp * mp;
@@ -825,66 +842,84 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   }
   // mu
   double comp = 0.0, nf = 0.0;
-  for (int j = t; j < np; j += kT)
-    if (s.l[j] < s.u[j]) {
-      comp += (s.x[j] - s.l[j]) * s.zl[j] + (s.u[j] - s.x[j]) * s.zu[j];
+#pragma unroll
+  for (int k = 0; k < J; ++k)
+    if (t + k * kT < np && g.fr(k)) {
+      comp += (g.x[k] - g.l[k]) * g.zl[k] + (g.u[k] - g.x[k]) * g.zu[k];
       nf += 1.0;
     }
   comp = block_sum(comp, s.red);
   nf = block_sum(nf, s.red);
   const double mu = comp / fmax(2.0 * nf, 1.0);
   // predictor
-  for (int j = t; j < np; j += kT)
-    r1[j] = s.l[j] < s.u[j] ? -s.rd[j] - s.zl[j] + s.zu[j] : 0.0;
-  __syncthreads();
-  kkt_solve(K, W, WT, np, mp, s, r1);
-  for (int j = t; j < np; j += kT) {
-    const bool fr = s.l[j] < s.u[j];
-    const double sl = s.x[j] - s.l[j], su = s.u[j] - s.x[j];
-    s.dzl[j] = fr ? -s.zl[j] - (s.zl[j] / sl) * s.dx[j] : 0.0;
-    s.dzu[j] = fr ? -s.zu[j] + (s.zu[j] / su) * s.dx[j] : 0.0;
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    if (j < np) r1[j] = g.fr(k) ? -g.rd[k] - g.zl[k] + g.zu[k] : 0.0;
   }
   __syncthreads();
-  const double ap0 = max_step(s, np, 0), ad0 = max_step(s, np, 1);
+  kkt_solve<J>(K, W, WT, rp, np, mp, s, g, r1);
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    if (j >= np) continue;
+    const bool fr = g.fr(k);
+    const double sl = g.x[k] - g.l[k], su = g.u[k] - g.x[k];
+    g.dzl[k] = fr ? -g.zl[k] - (g.zl[k] / sl) * s.dx[j] : 0.0;
+    g.dzu[k] = fr ? -g.zu[k] + (g.zu[k] / su) * s.dx[j] : 0.0;
+  }
+  const double ap0 = max_step<J>(s, g, np, 0), ad0 = max_step<J>(s, g, np, 1);
   double ca = 0.0;
-  for (int j = t; j < np; j += kT)
-    if (s.l[j] < s.u[j]) {
-      const double sl = s.x[j] - s.l[j], su = s.u[j] - s.x[j];
-      ca += (sl + ap0 * s.dx[j]) * (s.zl[j] + ad0 * s.dzl[j]) +
-            (su - ap0 * s.dx[j]) * (s.zu[j] + ad0 * s.dzu[j]);
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    if (j < np && g.fr(k)) {
+      const double sl = g.x[k] - g.l[k], su = g.u[k] - g.x[k];
+      ca += (sl + ap0 * s.dx[j]) * (g.zl[k] + ad0 * g.dzl[k]) +
+            (su - ap0 * s.dx[j]) * (g.zu[k] + ad0 * g.dzu[k]);
     }
+  }
   ca = block_sum(ca, s.red);
   const double mu_aff = ca / fmax(2.0 * nf, 1.0);
   const double ratio = mu > 0 ? mu_aff / mu : 0.0;
   const double sigma = mu > 0 ? ratio * ratio * ratio : 0.0;
-  // corrector
-  for (int j = t; j < np; j += kT) {
-    const bool fr = s.l[j] < s.u[j];
-    const double sl = s.x[j] - s.l[j], su = s.u[j] - s.x[j];
-    const double rl = sigma * mu - sl * s.zl[j] - s.dx[j] * s.dzl[j];
-    const double ru = sigma * mu - su * s.zu[j] + s.dx[j] * s.dzu[j];
-    s.rl[j] = rl;
-    s.ru[j] = ru;
-    r1[j] = fr ? -s.rd[j] + rl / sl - ru / su : 0.0;
+  // corrector (r1 = s2 is rewritten: every read of the predictor's s2 ended
+  // inside kkt_solve, before its closing barrier)
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    if (j >= np) continue;
+    const bool fr = g.fr(k);
+    const double sl = g.x[k] - g.l[k], su = g.u[k] - g.x[k];
+    const double rl = sigma * mu - sl * g.zl[k] - s.dx[j] * g.dzl[k];
+    const double ru = sigma * mu - su * g.zu[k] + s.dx[j] * g.dzu[k];
+    g.rl[k] = rl;
+    g.ru[k] = ru;
+    r1[j] = fr ? -g.rd[k] + rl / sl - ru / su : 0.0;
   }
   __syncthreads();
-  kkt_solve(K, W, WT, np, mp, s, r1);
-  for (int j = t; j < np; j += kT) {
-    const bool fr = s.l[j] < s.u[j];
-    const double sl = s.x[j] - s.l[j], su = s.u[j] - s.x[j];
-    s.dzl[j] = fr ? (s.rl[j] - s.zl[j] * s.dx[j]) / sl : 0.0;
-    s.dzu[j] = fr ? (s.ru[j] + s.zu[j] * s.dx[j]) / su : 0.0;
+  kkt_solve<J>(K, W, WT, rp, np, mp, s, g, r1);
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    if (j >= np) continue;
+    const bool fr = g.fr(k);
+    const double sl = g.x[k] - g.l[k], su = g.u[k] - g.x[k];
+    g.dzl[k] = fr ? (g.rl[k] - g.zl[k] * s.dx[j]) / sl : 0.0;
+    g.dzu[k] = fr ? (g.ru[k] + g.zu[k] * s.dx[j]) / su : 0.0;
   }
-  __syncthreads();
-  double ap = kQpStep * max_step(s, np, 0), ad = kQpStep * max_step(s, np, 1);
+  double ap = kQpStep * max_step<J>(s, g, np, 0), ad = kQpStep * max_step<J>(s, g, np, 1);
   ap = fmin(ap, 1.0);
   ad = fmin(ad, 1.0);
-  for (int j = t; j < np; j += kT) {
-    w.x[o + j] = s.x[j] + ap * s.dx[j];
-    w.zl[o + j] = s.zl[j] + ad * s.dzl[j];
-    w.zu[o + j] = s.zu[j] + ad * s.dzu[j];
+#pragma unroll
+  for (int k = 0; k < J; ++k) {
+    const int j = t + k * kT;
+    if (j >= np) continue;
+    w.x[o + j] = g.x[k] + ap * s.dx[j];
+    w.zl[o + j] = g.zl[k] + ad * g.dzl[k];
+    w.zu[o + j] = g.zu[k] + ad * g.dzu[k];
   }
-  for (int i = t; i < mp; i += kT) w.y[oy + i] = s.y[i] + ad * s.dy[i];
+  for (int i = t; i < mp; i += kT) w.y[oy + i] = w.y[oy + i] + ad * s.dy[i];
   if (t == 0) w.iters[b] += 1;
 }
 
@@ -912,7 +947,7 @@ __global__ __launch_bounds__(kT) void qp_final(DevQP q, QpWork w) {
 }  // namespace
 
 size_t qp_step_lds(int np, int mp) {
-  return sizeof(double) * ((size_t)13 * np + 4 * mp + (size_t)mp * (mp + 1) + 2 * 204 + 4 * 272 + kT);
+  return sizeof(double) * ((size_t)3 * np + 2 * mp + (size_t)mp * (mp + 1) + 2 * 204 + 4 * 272);
 }
 
 hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s) {
@@ -923,8 +958,11 @@ hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s) {
 hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void *)qp_step,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e = hipSuccess;
+    for (const void *f : {(const void *)qp_step<2>, (const void *)qp_step<4>,
+                          (const void *)qp_step<8>})
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void *)qp_potrf,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -955,7 +993,16 @@ hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s) {
                        w);
   else
     hipLaunchKernelGGL(qp_trsm_syrk, dim3(w.B), dim3(kT), lds_trsm, s, w, q.np, q.mp);
-  hipLaunchKernelGGL(qp_step, dim3(w.B), dim3(kT), qp_step_lds(q.np, q.mp), s, q, w);
+  // the step's per-column registers: J columns per thread
+  const size_t lstep = qp_step_lds(q.np, q.mp);
+  if (q.np <= 2 * kT)
+    hipLaunchKernelGGL(qp_step<2>, dim3(w.B), dim3(kT), lstep, s, q, w);
+  else if (q.np <= 4 * kT)
+    hipLaunchKernelGGL(qp_step<4>, dim3(w.B), dim3(kT), lstep, s, q, w);
+  else if (q.np <= 8 * kT)
+    hipLaunchKernelGGL(qp_step<8>, dim3(w.B), dim3(kT), lstep, s, q, w);
+  else
+    return hipErrorInvalidValue;   // n > 2048: mgpu_load_qp refuses it
   return hipGetLastError();
 }
 

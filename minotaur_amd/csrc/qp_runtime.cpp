@@ -174,8 +174,9 @@ extern "C" {
 int mgpu_load_qp(mgpu_ctx *c, int n, int m, const double *Q, const double *cvec, double k,
                  const double *A, const double *b) {
   if (!c) return MGPU_ERR_ARG;
-  if (n <= 0 || m < 0 || m > 64 || !Q || !cvec || (m > 0 && (!A || !b)))
-    return fail(c, MGPU_ERR_ARG, "mgpu_load_qp: bad argument (m <= 64 rows supported)");
+  if (n <= 0 || n > 2048 || m < 0 || m > 64 || !Q || !cvec || (m > 0 && (!A || !b)))
+    return fail(c, MGPU_ERR_ARG, "mgpu_load_qp: bad argument (n <= 2048 columns, m <= 64 rows "
+                "supported)");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   qp_state_free(c);

@@ -1,3 +1,13 @@
+"""K1G row-visit census ("Where K1G's time goes"): run with
+MGPU_LIB pointing at an instrumented variant built by tools/variant_build.py
+(the edits count row visits per wave, tightenings per node and s_memtime
+cycles of the activity / update phases, written into the infeas / nmods /
+lb_out[0..3] outputs), e.g.
+
+    python tools/variant_build.py k1gprobe fbbt_group.hip '<old>' '<new>' ...
+    MGPU_LIB=tools/_stamps/k1gprobe/libmgpu.so python tools/k1g_probe.py
+
+The outputs of such a build are NOT FBBT results."""
 import os, sys, math
 import numpy as np, torch
 ROOT = '/root/repo' if os.path.isdir('/root/repo') else os.getcwd()
