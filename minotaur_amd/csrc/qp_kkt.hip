@@ -360,10 +360,14 @@ __global__ __launch_bounds__(kPT, 6) void qp_potrf_ll(DevQP q, QpWork w) {
       __builtin_amdgcn_wave_barrier();
       for (int c = 0; c < 16; ++c) {
         const double dd = sqrt(D[c * 17 + c]);
+        const double rinv = 1.0 / dd;   // column 16 of the tile keeps 1 / L_cc
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) D[c * 17 + c] = dd;
-        if (lane > c && lane < 16) D[lane * 17 + c] /= dd;
+        if (lane == 0) {
+          D[c * 17 + c] = dd;
+          D[c * 17 + 16] = rinv;
+        }
+        if (lane > c && lane < 16) D[lane * 17 + c] *= rinv;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         for (int e = lane; e < 256; e += 64) {
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(kPT, 6) void qp_potrf_ll(DevQP q, QpWork w) {
         const double *dr = D + s2 * 17;   // re-read per row (LDS broadcast)
 #pragma unroll
         for (int p2 = 0; p2 < s2; ++p2) v -= a[p2] * dr[p2];
-        a[s2] = v / dr[s2];
+        a[s2] = v * dr[16];   // 1 / L_ss (no division on the row's chain)
         // keep the tile's loads in their row: hoisting all 136 of them
         // (the compiler's choice) costs 250 VGPRs and spills at 8 waves
         asm volatile("" ::: "memory");
@@ -513,7 +517,11 @@ __global__ __launch_bounds__(kPT) void qp_trsm_syrk_lds(DevQP q, QpWork w) {
   const int row = lane & 15, kq = lane >> 4;
   for (int kb = 0; kb < T; ++kb) {
     const int r0 = kb * 16;
-    for (int e = t; e < 256; e += kPT) D[(e >> 4) * 17 + (e & 15)] = K[(size_t)(r0 + (e >> 4)) * np + r0 + (e & 15)];
+    for (int e = t; e < 256; e += kPT) {
+      const double v = K[(size_t)(r0 + (e >> 4)) * np + r0 + (e & 15)];
+      D[(e >> 4) * 17 + (e & 15)] = v;
+      if ((e >> 4) == (e & 15)) D[(e >> 4) * 17 + 16] = 1.0 / v;
+    }
     __syncthreads();
     // the diagonal block rows: one column per thread
     for (int cidx = t; cidx < mp; cidx += kPT) {
@@ -525,7 +533,7 @@ __global__ __launch_bounds__(kPT) void qp_trsm_syrk_lds(DevQP q, QpWork w) {
         double s2 = v[r];
 #pragma unroll
         for (int p2 = 0; p2 < r; ++p2) s2 -= D[r * 17 + p2] * v[p2];
-        v[r] = s2 / D[r * 17 + r];
+        v[r] = s2 * D[r * 17 + 16];
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) Ws[(r0 + r) * ld + cidx] = v[r];
@@ -574,14 +582,16 @@ __global__ __launch_bounds__(kPT) void qp_trsm_syrk_lds(DevQP q, QpWork w) {
   double *M = w.M + (size_t)b * mp * mp;
   for (int tix = wave; tix < CB * CB; tix += kPT / 64) {
     const int ib = tix / CB, jb = tix % CB;
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    d4 acc = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     for (int k0 = 0; k0 < np; k0 += 16) {
       const double *ap = Ws + (k0 + 4 * kq) * ld + ib * 16 + row;
       const double *bp = Ws + (k0 + 4 * kq) * ld + jb * 16 + row;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[kk * ld], bp[kk * ld], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[0], bp[0], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[ld], bp[ld], acc1, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[2 * ld], bp[2 * ld], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ap[3 * ld], bp[3 * ld], acc1, 0, 0, 0);
     }
+    acc += acc1;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       M[(size_t)(ib * 16 + kq + 4 * r) * mp + jb * 16 + row] = acc[r];
@@ -621,7 +631,11 @@ __device__ void fwd_L(const double *K, int np, const double *r, double *v, const
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int T = np / 16;
   if (wave > 0)
-    for (int e = t - 64; e < 256; e += kT - 64) s.dt[(e >> 4) * 17 + (e & 15)] = K[(size_t)(e >> 4) * np + (e & 15)];
+    for (int e = t - 64; e < 256; e += kT - 64) {
+      const double v = K[(size_t)(e >> 4) * np + (e & 15)];
+      s.dt[(e >> 4) * 17 + (e & 15)] = v;
+      if ((e >> 4) == (e & 15)) s.dt[(e >> 4) * 17 + 16] = 1.0 / v;   // 1 / L_cc
+    }
   __syncthreads();
   for (int ib = 0; ib < T; ++ib) {
     const int cur = ib & 1, nxt = cur ^ 1;
@@ -641,7 +655,7 @@ __device__ void fwd_L(const double *K, int np, const double *r, double *v, const
       double mine = 0.0;
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        const double vc = rld(val, c) / dt[c * 17 + c];   // v_readlane broadcast
+        const double vc = rld(val, c) * dt[c * 17 + 16];   // v_readlane broadcast
         if (lane == c) mine = vc;
         if (lane > c && lane < 16) val -= dt[lane * 17 + c] * vc;
       }
@@ -653,7 +667,9 @@ __device__ void fwd_L(const double *K, int np, const double *r, double *v, const
       s.pre[nxt * 204 + pq * 17 + rr] = a;
       for (int e = tt; e < 256; e += kT - 64) {
         const int ei = e >> 4, ej = e & 15;
-        s.dt[nxt * 272 + ei * 17 + ej] = K[(size_t)(r1 + ei) * np + r1 + ej];
+        const double dv = K[(size_t)(r1 + ei) * np + r1 + ej];
+        s.dt[nxt * 272 + ei * 17 + ej] = dv;
+        if (ei == ej) s.dt[nxt * 272 + ei * 17 + 16] = 1.0 / dv;
         s.xt[nxt * 272 + ei * 17 + ej] = K[(size_t)(r1 + ei) * np + r0 + ej];
       }
     }
@@ -667,7 +683,11 @@ __device__ void bwd_LT(const double *K, int np, const double *sv, double *xo, co
   const int T = np / 16;
   if (wave > 0) {
     const int d0 = (T - 1) * 16;
-    for (int e = t - 64; e < 256; e += kT - 64) s.dt[(e >> 4) * 17 + (e & 15)] = K[(size_t)(d0 + (e >> 4)) * np + d0 + (e & 15)];
+    for (int e = t - 64; e < 256; e += kT - 64) {
+      const double v = K[(size_t)(d0 + (e >> 4)) * np + d0 + (e & 15)];
+      s.dt[(e >> 4) * 17 + (e & 15)] = v;
+      if ((e >> 4) == (e & 15)) s.dt[(e >> 4) * 17 + 16] = 1.0 / v;
+    }
   }
   __syncthreads();
   for (int n = 0; n < T; ++n) {
@@ -689,7 +709,7 @@ __device__ void bwd_LT(const double *K, int np, const double *sv, double *xo, co
       double mine = 0.0;
 #pragma unroll
       for (int c = 15; c >= 0; --c) {
-        const double xc = rld(val, c) / dt[c * 17 + c];
+        const double xc = rld(val, c) * dt[c * 17 + 16];
         if (lane == c) mine = xc;
         if (lane < c) val -= dt[c * 17 + lane] * xc;
       }
@@ -703,7 +723,9 @@ __device__ void bwd_LT(const double *K, int np, const double *sv, double *xo, co
       s.pre[nxt * 204 + pq * 17 + rr] = a;
       for (int e = tt; e < 256; e += kT - 64) {
         const int ei = e >> 4, ej = e & 15;
-        s.dt[nxt * 272 + ei * 17 + ej] = K[(size_t)(c1 + ei) * np + c1 + ej];
+        const double dv = K[(size_t)(c1 + ei) * np + c1 + ej];
+        s.dt[nxt * 272 + ei * 17 + ej] = dv;
+        if (ei == ej) s.dt[nxt * 272 + ei * 17 + 16] = 1.0 / dv;
         s.xt[nxt * 272 + ei * 17 + ej] = K[(size_t)(r0 + ei) * np + c1 + ej];
       }
     }
