@@ -159,7 +159,7 @@ struct LpIO {
   } path;
 };
 constexpr int kPathMax = 32;    // pivots per path warm start (MGPU_PATH_MAX)
-constexpr int kPathInherit = 24; // longest path the batched tree hands to children
+constexpr int kPathInherit = 32; // longest basis difference the batched tree hands to children (= the eta cap: profiles/r04q)
 
 // K1: waves per CU a batch too small for one node per lane is spread over
 // (tuned on config 2's complete tree, tools/tree_probe.py)

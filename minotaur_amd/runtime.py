@@ -22,7 +22,7 @@ _D = ctypes.c_double
 LP_PFI_MAX = 32  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
 LP_PFI_WIDE_MAX = 32  # MGPU_LP_PFI_WIDE_MAX: K3PW eta-file cap
 PATH_MAX = 32  # MGPU_PATH_MAX: columns per basis warm start
-PATH_INHERIT = 24  # the batched tree's largest basis difference handed to children (warm mode 2)
+PATH_INHERIT = 32  # the batched tree's largest basis difference handed to children (warm mode 2)
 
 # Every entry point declared in include/mgpu.h (checked by the CPU tests).
 EXPORTS = [

@@ -16,7 +16,8 @@ children), same pool order:
   optimal basis, whose own optimum is handed to both children; warm 2: from
   the parent's optimal basis kept as its pivot path from the root basis
   (oracle.dual_simplex_path, K3P's product form), paths of at most
-  min(24, pfi) pivots handed on, else the children restart from the root;
+  min(PATH_INHERIT = 32, pfi) basic columns handed on, else the children
+  restart from the root;
 * brancher 0: MaxVioBrancher; brancher 1: the batched ReliabilityBrancher of
   bnb_rel.hip (pseudocosts frozen at the round's start plus each node's own
   updateAfterSolve observation, strong-branching LPs from each node's optimal
@@ -70,7 +71,7 @@ class _Node:
 # ReliabilityBrancher defaults (ReliabilityBrancher.cpp:43-58)
 REL_MAX_CANDS, REL_ITER, REL_THRESH, REL_MIN_DIST, REL_ETOL = 20, 25, 4, 50, 1e-6
 REL_MAX_DEPTH = 1000   # maxDepth_: no strong branching below it (:105)
-PATH_INHERIT = 24      # warm 2: longest path handed to children (bnb.cpp kPathInherit)
+PATH_INHERIT = 32      # warm 2: longest basis difference handed to children (bnb.cpp kPathInherit)
 
 
 def _rel_score(up, down):
