@@ -414,11 +414,11 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
     variant = 2;
   int grid = waves;
   if (variant == 3) {
-    // persistent waves: 8 per CU (two per SIMD at the kernel's 177 VGPRs;
-    // more waves only enlarge the scratch working set, which already lives
-    // in the MALL: 3072-4096 waves measured slower), fewer for small
-    // batches; MGPU_FBBT_WAVES overrides
-    grid = c->num_cus * 8;
+    // persistent waves: 12 per CU (three per SIMD at the kernel's 168
+    // VGPRs: 524 288 tls4-OA nodes 8.29 -> 7.75 ms against 8 per CU at 179
+    // VGPRs, profiles/r04s; four per SIMD spills 284 VGPRs and is slower),
+    // fewer for small batches; MGPU_FBBT_WAVES overrides
+    grid = c->num_cus * 12;
     if (const char *e = getenv("MGPU_FBBT_WAVES")) {
       const int v = atoi(e);
       if (v >= 1) grid = v;
