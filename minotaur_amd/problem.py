@@ -198,7 +198,10 @@ def random_boxes(p: LinProblem, B: int, seed: int, max_depth: int = 20,
     each node gets a depth d in [1, max_depth]; each of the d steps picks a
     random integer column that is not fixed yet and either fixes a binary to
     0/1 or splits an integer (down: ub=floor(mid), up: lb=floor(mid)+1).
-    Vectorised over nodes.  Returns (lb[B,n], ub[B,n])."""
+    Vectorised over nodes; the column is drawn uniformly among the node's
+    free integer columns by rejection (round 4: 4 M boxes in seconds instead
+    of minutes; earlier rounds drew it by an arg-min over random keys, the
+    same distribution, other boxes).  Returns (lb[B,n], ub[B,n])."""
     rng = np.random.default_rng(seed)
     lb0 = p.vlb if root_lb is None else root_lb
     ub0 = p.vub if root_ub is None else root_ub
@@ -209,14 +212,34 @@ def random_boxes(p: LinProblem, B: int, seed: int, max_depth: int = 20,
         return LB, UB
     depth = rng.integers(1, max_depth + 1, size=B)
     rows = np.arange(B)
+    nint = ints.size
+
+    def is_free(r, c):
+        jj = ints[c]
+        return (UB[r, jj] - LB[r, jj]) >= 1.0
+
     for step in range(max_depth):
-        lo = LB[:, ints]
-        hi = UB[:, ints]
-        free = (hi - lo) >= 1.0
-        keys = rng.random((B, ints.size))
-        keys[~free] = 2.0
-        pick = np.argmin(keys, axis=1)
-        act = (depth > step) & free[rows, pick]
+        # a uniformly random free integer column per node, by rejection from
+        # uniform proposals (8 rounds; a node still without one -- most of
+        # its columns fixed -- takes the exact draw over its free columns)
+        pick = rng.integers(0, nint, size=B)
+        ok = is_free(rows, pick)
+        for _ in range(8):
+            miss = np.nonzero(~ok)[0]
+            if miss.size == 0:
+                break
+            cand = rng.integers(0, nint, size=miss.size)
+            good = is_free(miss, cand)
+            pick[miss[good]] = cand[good]
+            ok[miss[good]] = True
+        miss = np.nonzero(~ok)[0]
+        if miss.size:
+            fr = (UB[miss][:, ints] - LB[miss][:, ints]) >= 1.0
+            keys = rng.random((miss.size, nint))
+            keys[~fr] = 2.0
+            pick[miss] = np.argmin(keys, axis=1)
+            ok[miss] = fr[np.arange(miss.size), pick[miss]]
+        act = (depth > step) & ok
         j = ints[pick]
         l = np.where(np.isfinite(LB[rows, j]), LB[rows, j], -1e3)
         h = np.where(np.isfinite(UB[rows, j]), UB[rows, j], 1e3)
