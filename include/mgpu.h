@@ -497,17 +497,25 @@ int mgpu_bnb_import(mgpu_ctx *ctx, int k, const double *lb, const double *ub, co
  *                        The nodes stay in the pool.
  *   mgpu_bnb_export_dev: removes the picked nodes idx[0, k) (indices into the
  *                        last pick, host array) and packs them, in that
- *                        order, into device rows buf[k][2n + 2] =
+ *                        order, into device rows buf[k][W] =
  *                        [lb | ub | bound | depth] (Serializer.cpp:26-112's
- *                        content); the depth-first stack closes its gaps.
+ *                        content), in warm mode 2 followed by the node's
+ *                        warm start [k | path (MGPU_PATH_MAX) | column
+ *                        statuses, 16 two-bit codes per f64]: the basis
+ *                        relative to the root basis every rank shares;
+ *                        the depth-first stack closes its gaps.
  *   mgpu_bnb_import_dev: adds k nodes from device rows buf (best-first: the
  *                        lowest free pool slots, then past the high-water
- *                        mark; depth-first: on top), in row order; they
- *                        start from the root basis.
+ *                        mark; depth-first: on top), in row order; in warm
+ *                        mode 2 they start from the basis their row
+ *                        carries, otherwise from the root basis.
+ *   mgpu_bnb_row_width:  W, the row width in f64 (2n + 2, or 2n + 3 +
+ *                        MGPU_PATH_MAX + ceil((n + m) / 16) in warm mode 2).
  *   mgpu_bnb_count:      open nodes and pool slots left for imports. */
 int mgpu_bnb_pick(mgpu_ctx *ctx, int S, double *lbs, int *got);
 int mgpu_bnb_export_dev(mgpu_ctx *ctx, int k, const int32_t *idx, double *d_rows);
 int mgpu_bnb_import_dev(mgpu_ctx *ctx, int k, const double *d_rows);
+int mgpu_bnb_row_width(mgpu_ctx *ctx);
 int mgpu_bnb_count(mgpu_ctx *ctx, int *open, int *spare);
 
 /* ---- Batched spatial branch-and-bound (the glob path) --------------------

@@ -1060,7 +1060,8 @@ int mgpu_strong_branch(mgpu_ctx *c, const double *lb, const double *ub, int ncan
 // mgpu_bnb_pick is the pop (the nodes stay in the pool, only their bounds
 // leave), mgpu_bnb_export_dev packs the chosen ones into device rows and
 // removes them, mgpu_bnb_import_dev places received rows.  Rows are
-// [lb n | ub n | bound | depth] f64 (bnb_migrate.hip).
+// [lb n | ub n | bound | depth] f64, plus the node's basis in warm mode 2
+// (bnb_migrate.hip; mgpu_bnb_row_width).
 }  // extern "C"
 
 namespace {
@@ -1089,6 +1090,13 @@ std::vector<std::pair<DevBuf *, size_t>> slot_rows(BnbState &s, int m) {
   return r;
 }
 
+// migration row width in doubles: [lb | ub | bound | depth], plus in warm
+// mode 2 [k | path (kPathMax) | statuses, 16 per double] (bnb_migrate.hip)
+size_t mig_width(const BnbState &s, int m) {
+  const size_t N = (size_t)s.n + (size_t)m;
+  return 2 * (size_t)s.n + 2 + (s.warm == 2 ? 1 + (size_t)kPathMax + (N + 15) / 16 : 0);
+}
+
 inline double key_to_double(uint64_t k) {
   const uint64_t b = (k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
   double v;
@@ -1107,9 +1115,24 @@ int take_nodes(mgpu_ctx *c, BnbState &s, const std::vector<int32_t> &slots, int 
   HIPCHK(c, dsl.ensure((size_t)k * 4));
   HIPCHK(c, hipMemcpyAsync(dsl.p, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice,
                            c->stream));
-  HIPCHK(c, launch_bnb_pack(dsl.as<int32_t>(), k, s.n, s.plb.as<double>(), s.pub.as<double>(),
-                            s.pnlb.as<double>(), s.pdepth.as<int32_t>(),
-                            s.order == 1 ? s.plive.as<uint8_t>() : nullptr, buf, c->stream));
+  MigratePack pk{};
+  pk.k = k;
+  pk.n = s.n;
+  pk.N = s.n + c->lp.m;
+  pk.W = (int)mig_width(s, c->lp.m);
+  pk.slots = dsl.as<int32_t>();
+  pk.plb = s.plb.as<double>();
+  pk.pub = s.pub.as<double>();
+  pk.pnlb = s.pnlb.as<double>();
+  pk.pdepth = s.pdepth.as<int32_t>();
+  pk.plive = s.order == 1 ? s.plive.as<uint8_t>() : nullptr;
+  if (s.warm == 2) {
+    pk.ppk = s.ppk.as<int32_t>();
+    pk.ppath = s.ppath.as<uint32_t>();
+    pk.ppst = s.ppst.as<int8_t>();
+  }
+  pk.buf = buf;
+  HIPCHK(c, launch_bnb_pack(pk, c->stream));
   if (s.order == 0) {
     const int base = s.count - region;
     std::vector<uint8_t> gone((size_t)region, 0);
@@ -1184,6 +1207,7 @@ int place_nodes(mgpu_ctx *c, BnbState &s, int k, const double *buf) {
   io.n = s.n;
   io.m = m;
   io.N = N;
+  io.W = (int)mig_width(s, m);
   io.slots = dsl.as<int32_t>();
   io.buf = buf;
   io.plb = s.plb.as<double>();
@@ -1192,7 +1216,11 @@ int place_nodes(mgpu_ctx *c, BnbState &s, int k, const double *buf) {
   io.pdepth = s.pdepth.as<int32_t>();
   io.plive = s.order == 1 ? s.plive.as<uint8_t>() : nullptr;
   io.ppvar = s.rel ? s.ppvar.as<int32_t>() : nullptr;
-  io.ppk = s.warm == 2 ? s.ppk.as<int32_t>() : nullptr;
+  if (s.warm == 2) {  // the basis each row carries (k 0: the root basis)
+    io.ppk = s.ppk.as<int32_t>();
+    io.ppath = s.ppath.as<uint32_t>();
+    io.ppst = s.ppst.as<int8_t>();
+  }
   if (s.warm == 1) {  // a migrated node starts from the root basis
     io.ws_head = s.pws_head.as<int32_t>();
     io.ws_st = s.pws_st.as<int8_t>();
@@ -1316,6 +1344,12 @@ int mgpu_bnb_import_dev(mgpu_ctx *c, int k, const double *buf) {
   return place_nodes(c, s, k, buf);
 }
 
+int mgpu_bnb_row_width(mgpu_ctx *c) {
+  int rc = check_migrate(c, "mgpu_bnb_row_width");
+  if (rc != MGPU_OK) return rc;
+  return (int)mig_width(*c->bnb, c->lp.m);
+}
+
 int mgpu_bnb_count(mgpu_ctx *c, int *open, int *spare) {
   int rc = check_migrate(c, "mgpu_bnb_count");
   if (rc != MGPU_OK) return rc;
@@ -1351,7 +1385,7 @@ int mgpu_bnb_export(mgpu_ctx *c, int k, double *lb, double *ub, double *nlb, int
       if (live[(size_t)i]) slots.push_back(i);
     k = (int)slots.size();
   }
-  const size_t W = 2 * (size_t)n + 2;
+  const size_t W = mig_width(s, c->lp.m);
   DevBuf rows;
   HIPCHK(c, rows.ensure((size_t)k * W * 8));
   rc = take_nodes(c, s, slots, k, rows.as<double>());
@@ -1380,8 +1414,8 @@ int mgpu_bnb_import(mgpu_ctx *c, int k, const double *lb, const double *ub, cons
   HIPCHK(c, hipSetDevice(c->device));
   s.pick.clear();
   const int n = s.n;
-  const size_t W = 2 * (size_t)n + 2;
-  std::vector<double> h((size_t)k * W);
+  const size_t W = mig_width(s, c->lp.m);   // (host boxes: k 0, the root basis)
+  std::vector<double> h((size_t)k * W, 0.0);
   for (int t = 0; t < k; ++t) {
     double *r = h.data() + (size_t)t * W;
     std::memcpy(r, lb + (size_t)t * n, (size_t)n * 8);

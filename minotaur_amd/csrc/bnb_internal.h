@@ -188,15 +188,28 @@ hipError_t launch_bnb_shard(double *plb, double *pub, double *pnlb, int32_t *pde
 
 // Node migration (bnb_migrate.hip): packed rows [lb n | ub n | bound | depth]
 // into pool slots, per-node state reset for a migrated node.
+struct MigratePack {            // pool slots -> rows (bnb_pack)
+  int k, n, N, W;               // W: row width in doubles (mig_width)
+  const int32_t *slots;         // [k] source pool slots
+  const double *plb, *pub, *pnlb;
+  const int32_t *pdepth;
+  uint8_t *plive;               // best-first: the slot is freed (null: stack)
+  const int32_t *ppk;           // warm mode 2 (null: rows without a basis)
+  const uint32_t *ppath;
+  const int8_t *ppst;
+  double *buf;                  // [k][W]
+};
 struct MigrateIO {
-  int k, n, m, N;
+  int k, n, m, N, W;
   const int32_t *slots;         // [k] destination pool slots
-  const double *buf;            // [k][2n + 2]
+  const double *buf;            // [k][W]
   double *plb, *pub, *pnlb;
   int32_t *pdepth;
   uint8_t *plive;               // best-first pool flags (null: stack)
   int32_t *ppvar;               // reliability: parent branching variable (null: none)
-  int32_t *ppk;                 // path warm starts: path length (null: none)
+  int32_t *ppk;                 // warm mode 2: the rows' bases (null: none)
+  uint32_t *ppath;
+  int8_t *ppst;
   int32_t *ws_head;             // parent warm starts (null: none) <- the root basis r_*
   int8_t *ws_st;
   double *ws_d, *ws_binv;
@@ -204,9 +217,7 @@ struct MigrateIO {
   const int8_t *r_st;
   const double *r_d, *r_binv;
 };
-hipError_t launch_bnb_pack(const int32_t *slots, int k, int n, const double *plb,
-                           const double *pub, const double *pnlb, const int32_t *pdepth,
-                           uint8_t *plive, double *buf, hipStream_t stream);
+hipError_t launch_bnb_pack(const MigratePack &io, hipStream_t stream);
 hipError_t launch_bnb_unpack(const MigrateIO &io, hipStream_t stream);
 hipError_t launch_bnb_move_rows(unsigned char *rows, unsigned char *tmp, size_t row_bytes,
                                 const int32_t *from, const int32_t *to, int k,

@@ -5,8 +5,13 @@
 // per node.  Here the nodes a rank gives away are packed on the device into
 // one f64 row each,
 //     row t = [ lb (n) | ub (n) | node bound | depth ]      (2n + 2 doubles)
-// so the exchange is one collective over device buffers (RCCL over xGMI) and
-// no box crosses PCIe.  Three kernels, one wave per node:
+// and, in the tree's warm mode 2, the node's warm start behind it
+//     [ k | path (kPathMax) | statuses packed 16 per double (2 bits each) ]
+// (k 0 = the root basis; path entries past k and the statuses of k = 0
+// are 0), so a migrated node keeps its parent's basis: every rank solved
+// the same root LP, whose basis the path is relative to.  The exchange is
+// one collective over device buffers (RCCL over xGMI) and no box crosses
+// PCIe.  Three kernels, one wave per node:
 //   bnb_pack   : pool slot slots[t] -> row t (a best-first slot is freed);
 //   bnb_unpack : row t -> pool slot slots[t], with the slot's per-node state
 //                reset as a migrated node needs it (live flag, no parent
@@ -19,23 +24,38 @@
 namespace mgpu {
 namespace {
 
-__global__ __launch_bounds__(256) void bnb_pack(const int32_t *slots, int k, int n,
-                                                const double *plb, const double *pub,
-                                                const double *pnlb, const int32_t *pdepth,
-                                                uint8_t *plive, double *buf) {
+__global__ __launch_bounds__(256) void bnb_pack(MigratePack io) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= k) return;
-  const size_t s = (size_t)slots[t];
-  double *row = buf + (size_t)t * (2 * n + 2);
+  if (t >= io.k) return;
+  const int n = io.n;
+  const size_t s = (size_t)io.slots[t];
+  double *row = io.buf + (size_t)t * io.W;
   for (int j = lane; j < n; j += 64) {
-    row[j] = plb[s * n + j];
-    row[n + j] = pub[s * n + j];
+    row[j] = io.plb[s * n + j];
+    row[n + j] = io.pub[s * n + j];
+  }
+  if (io.ppk != nullptr) {   // warm mode 2: the node's basis travels with it
+    const int kp = io.ppk[s], N = io.N;
+    double *w = row + 2 * n + 2;
+    if (lane == 0) w[0] = (double)kp;
+    if (lane < kPathMax) w[1 + lane] = lane < kp ? (double)io.ppath[s * kPathMax + lane] : 0.0;
+    const int nq = (N + 15) / 16;
+    for (int q = lane; q < nq; q += 64) {
+      double v = 0.0;
+      if (kp > 0) {
+        uint32_t bits = 0;
+        for (int i = 0; i < 16 && q * 16 + i < N; ++i)
+          bits |= (uint32_t)(io.ppst[s * N + q * 16 + i] & 3) << (2 * i);
+        v = (double)bits;
+      }
+      w[1 + kPathMax + q] = v;
+    }
   }
   if (lane == 0) {
-    row[2 * n] = pnlb[s];
-    row[2 * n + 1] = (double)pdepth[s];
-    if (plive) plive[s] = 0;   // best-first pool: the slot becomes free
+    row[2 * n] = io.pnlb[s];
+    row[2 * n + 1] = (double)io.pdepth[s];
+    if (io.plive) io.plive[s] = 0;   // best-first pool: the slot becomes free
   }
 }
 
@@ -45,7 +65,7 @@ __global__ __launch_bounds__(256) void bnb_unpack(MigrateIO io) {
   if (t >= io.k) return;
   const int n = io.n;
   const size_t s = (size_t)io.slots[t];
-  const double *row = io.buf + (size_t)t * (2 * n + 2);
+  const double *row = io.buf + (size_t)t * io.W;
   for (int j = lane; j < n; j += 64) {
     io.plb[s * n + j] = row[j];
     io.pub[s * n + j] = row[n + j];
@@ -65,7 +85,19 @@ __global__ __launch_bounds__(256) void bnb_unpack(MigrateIO io) {
     io.pdepth[s] = (int32_t)row[2 * n + 1];
     if (io.plive) io.plive[s] = 1;
     if (io.ppvar) io.ppvar[s] = -1;   // no parent branching data
-    if (io.ppk) io.ppk[s] = 0;        // path warm start: the root basis
+  }
+  if (io.ppk) {   // warm mode 2: the basis the row carries (k 0: the root's)
+    const int N = io.N;
+    const double *w = row + 2 * n + 2;
+    const int kp = (int)w[0];
+    if (lane == 0) io.ppk[s] = kp;
+    if (lane < kPathMax) io.ppath[s * kPathMax + lane] = (uint32_t)w[1 + lane];
+    if (kp > 0) {
+      for (int j = lane; j < N; j += 64) {
+        const uint32_t bits = (uint32_t)w[1 + kPathMax + j / 16];
+        io.ppst[s * N + j] = (int8_t)((bits >> (2 * (j % 16))) & 3u);
+      }
+    }
   }
 }
 
@@ -90,12 +122,9 @@ __global__ __launch_bounds__(256) void bnb_move(const unsigned char *src, unsign
 
 }  // namespace
 
-hipError_t launch_bnb_pack(const int32_t *slots, int k, int n, const double *plb,
-                           const double *pub, const double *pnlb, const int32_t *pdepth,
-                           uint8_t *plive, double *buf, hipStream_t stream) {
-  if (k <= 0) return hipSuccess;
-  hipLaunchKernelGGL(bnb_pack, dim3((k + 3) / 4), dim3(256), 0, stream, slots, k, n, plb, pub,
-                     pnlb, pdepth, plive, buf);
+hipError_t launch_bnb_pack(const MigratePack &io, hipStream_t stream) {
+  if (io.k <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bnb_pack, dim3((io.k + 3) / 4), dim3(256), 0, stream, io);
   return hipGetLastError();
 }
 

@@ -158,7 +158,8 @@ def rebalance(ctx, comm, batch=0):
        rank i mod P; nodes whose owner is their receiver stay in place;
     4. a plan that would overflow some receiver's pool fails on EVERY rank
        (same data, same check), so no rank is left blocked in a collective;
-    5. the moving nodes leave as device rows (mgpu_bnb_export_dev), cross in
+    5. the moving nodes leave as device rows (mgpu_bnb_export_dev; in warm
+       mode 2 each row carries its node's basis), cross in
        ONE all-to-all (RCCL over xGMI on MI355X) and are imported in deal
        order (mgpu_bnb_import_dev).
 
@@ -189,7 +190,7 @@ def rebalance(ctx, comm, batch=0):
     src = owner[got]
     recv_counts = torch.bincount(src, minlength=P).tolist()
     rows = ctx.bnb_export_rows(idx)
-    width = 2 * ctx.problem.n + 2
+    width = ctx.bnb_row_width()
     out = comm.all_to_all_rows(rows, send_counts, recv_counts, width)
     # the all-to-all delivers rows grouped by sender; import them in deal order
     a2a = torch.sort(src, stable=True).indices               # a2a row -> deal position
@@ -198,5 +199,6 @@ def rebalance(ctx, comm, batch=0):
     ordered = out[inv.to(out.device)] if out.shape[0] else out
     ctx.bnb_import_rows(ordered)
     n_open = n_open - len(idx) + int(ordered.shape[0])
-    got_lbs = ordered[:, width - 2].cpu().numpy() if ordered.shape[0] else np.empty(0)
+    nb = 2 * ctx.problem.n   # the node bound's column
+    got_lbs = ordered[:, nb].cpu().numpy() if ordered.shape[0] else np.empty(0)
     return n_open, int(moved.sum().item()), lbs, got_lbs

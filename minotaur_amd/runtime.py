@@ -40,7 +40,7 @@ EXPORTS = [
     'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
     'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive', 'mgpu_ws_alloc', 'mgpu_ws_free',
     'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1', 'mgpu_bnb_pick', 'mgpu_bnb_export_dev',
-    'mgpu_bnb_import_dev', 'mgpu_bnb_count', 'mgpu_glob_init', 'mgpu_glob_round', 'mgpu_glob_best',
+    'mgpu_bnb_import_dev', 'mgpu_bnb_row_width', 'mgpu_bnb_count', 'mgpu_glob_init', 'mgpu_glob_round', 'mgpu_glob_best',
 ]
 
 
@@ -123,6 +123,7 @@ def load_library():
     lib.mgpu_bnb_pick.argtypes = [_P, _I, _P, _P]
     lib.mgpu_bnb_export_dev.argtypes = [_P, _I, _P, _P]
     lib.mgpu_bnb_import_dev.argtypes = [_P, _I, _P]
+    lib.mgpu_bnb_row_width.argtypes = [_P]
     lib.mgpu_bnb_count.argtypes = [_P, _P, _P]
     lib.mgpu_glob_init.argtypes = [_P, _I, _D]
     lib.mgpu_glob_round.argtypes = [_P, _I, _D, ctypes.POINTER(GlobStats)]
@@ -719,13 +720,22 @@ class Context:
                   'mgpu_bnb_pick')
         return lbs[:got.value].copy()
 
+    def bnb_row_width(self) -> int:
+        """mgpu_bnb_row_width: f64 per migration row (2n + 2; warm mode 2
+        appends the node's basis)."""
+        w = self.lib.mgpu_bnb_row_width(self.h)
+        self._chk(w if w < 0 else 0, 'mgpu_bnb_row_width')
+        return int(w)
+
     def bnb_export_rows(self, idx):
         """mgpu_bnb_export_dev: the picked nodes idx leave the pool as device
-        rows [k, 2n + 2] (a torch tensor on this context's device)."""
+        rows [k, W] (a torch tensor on this context's device; W =
+        bnb_row_width(): [lb | ub | bound | depth] and, in warm mode 2, the
+        node's basis)."""
         import torch
         idx = np.ascontiguousarray(idx, dtype=np.int32)
-        k, n = len(idx), self.problem.n
-        buf = torch.empty((k, 2 * n + 2), dtype=torch.float64,
+        k = len(idx)
+        buf = torch.empty((k, self.bnb_row_width()), dtype=torch.float64,
                           device=torch.device('cuda', self.device))
         self._chk(self.lib.mgpu_bnb_export_dev(self.h, k, _hp(idx) if k else None,
                                                buf.data_ptr() if k else None),
@@ -733,7 +743,7 @@ class Context:
         return buf
 
     def bnb_import_rows(self, rows):
-        """mgpu_bnb_import_dev: rows [k, 2n + 2] (torch; moved to this device)."""
+        """mgpu_bnb_import_dev: rows [k, W] (torch; moved to this device)."""
         import torch
         k = int(rows.shape[0])
         if k == 0:

@@ -71,6 +71,7 @@ class _Node:
 # ReliabilityBrancher defaults (ReliabilityBrancher.cpp:43-58)
 REL_MAX_CANDS, REL_ITER, REL_THRESH, REL_MIN_DIST, REL_ETOL = 20, 25, 4, 50, 1e-6
 REL_MAX_DEPTH = 1000   # maxDepth_: no strong branching below it (:105)
+PATH_MAX = oracle.PATH_MAX   # path slots per node (MGPU_PATH_MAX)
 PATH_INHERIT = 32      # warm 2: longest basis difference handed to children (bnb.cpp kPathInherit)
 
 
@@ -551,20 +552,40 @@ class CpuBnbContext:
             self.pick = live[:int(S)]
         return np.array([self.pool[i].nlb for i in self.pick], dtype=np.float64)
 
+    def bnb_row_width(self):
+        n, N = self.problem.n, self.problem.n + self.problem.m
+        return 2 * n + 2 + (1 + PATH_MAX + (N + 15) // 16 if self.warm == 2 else 0)
+
     def bnb_export_rows(self, idx):
-        """Rows [k, 2n + 2] = [lb | ub | bound | depth] of picked nodes idx,
-        removed from the pool (the stack keeps the others' order)."""
+        """Rows [k, W] = [lb | ub | bound | depth] of picked nodes idx, in
+        warm mode 2 followed by [k | path (PATH_MAX, zeros past k) | column
+        statuses, 16 two-bit codes per f64 (zeros for k = 0)]
+        (bnb_migrate.hip), removed from the pool (the stack keeps the
+        others' order)."""
         import torch
-        n = self.problem.n
+        n, N = self.problem.n, self.problem.n + self.problem.m
         slots = [self.pick[int(i)] for i in idx]
         assert len(set(slots)) == len(slots)
-        rows = torch.empty((len(slots), 2 * n + 2), dtype=torch.float64)
+        rows = torch.zeros((len(slots), self.bnb_row_width()), dtype=torch.float64)
         for t, sl in enumerate(slots):
             nd = self.pool[sl]
             rows[t, :n] = torch.from_numpy(np.asarray(nd.lb, dtype=np.float64))
             rows[t, n:2 * n] = torch.from_numpy(np.asarray(nd.ub, dtype=np.float64))
             rows[t, 2 * n] = float(nd.nlb)
             rows[t, 2 * n + 1] = float(nd.depth)
+            if self.warm == 2 and nd.path is not None and int(nd.path[0]) > 0:
+                k, pv, sv = nd.path
+                w = 2 * n + 2
+                rows[t, w] = float(k)
+                for i in range(int(k)):
+                    rows[t, w + 1 + i] = float(int(pv[i]))
+                sv = np.asarray(sv, dtype=np.int64) & 3
+                for q in range((N + 15) // 16):
+                    bits = 0
+                    for i in range(16):
+                        if q * 16 + i < N:
+                            bits |= int(sv[q * 16 + i]) << (2 * i)
+                    rows[t, w + 1 + PATH_MAX + q] = float(bits)
         if self.order == 0:
             gone = set(slots)
             self.pool = [nd for i, nd in enumerate(self.pool) if i not in gone]
@@ -576,9 +597,22 @@ class CpuBnbContext:
         return rows
 
     def bnb_import_rows(self, rows):
-        n = self.problem.n
+        n, N = self.problem.n, self.problem.n + self.problem.m
         v = rows.detach().cpu().numpy()
-        self._place([self._migrant(r[:n], r[n:2 * n], r[2 * n], int(r[2 * n + 1])) for r in v])
+        nodes = []
+        for r in v:
+            nd = self._migrant(r[:n], r[n:2 * n], r[2 * n], int(r[2 * n + 1]))
+            w = 2 * n + 2
+            if self.warm == 2 and int(r[w]) > 0:   # the basis the row carries
+                k = int(r[w])
+                pv = np.zeros(PATH_MAX, dtype=np.uint32)
+                pv[:] = r[w + 1:w + 1 + PATH_MAX].astype(np.uint64).astype(np.uint32)
+                sv = np.zeros(N, dtype=np.int8)
+                for j in range(N):
+                    sv[j] = (int(r[w + 1 + PATH_MAX + j // 16]) >> (2 * (j % 16))) & 3
+                nd.path = (k, pv, sv)
+            nodes.append(nd)
+        self._place(nodes)
 
     def bnb_count(self):
         live = sum(nd is not None for nd in self.pool)
