@@ -786,8 +786,11 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
         step(acc)
         if world > 1 and args.lb_every > 0 and (k + 1) % args.lb_every == 0:
             # one pool across the ranks: bound-aware rebalancing inside the
-            # timed loop (MpiBranchAndBound::LoadBalance_, dist.rebalance)
-            _, mv, _, _ = mdist.rebalance(ctx, comm, B)
+            # timed loop (MpiBranchAndBound::LoadBalance_, dist.rebalance);
+            # --lb-pick reference: each rank offers the reference's 50 P next
+            # candidates (:80-105); batch: max(50 P, B), the globally best
+            # P * B nodes dealt (~(P-1)/P of a batch crosses xGMI)
+            _, mv, _, _ = mdist.rebalance(ctx, comm, B if args.lb_pick == 'batch' else 0)
             moved += mv
     torch.cuda.synchronize()
     if world > 1:
@@ -1008,6 +1011,9 @@ def main():
     ap.add_argument('--supp-out', default=os.path.join('gpurun_out', 'bench_supplementary.json'),
                     help='where the supplementary objects (trees, configs 3/4/5, glob) are '
                          'written; the stdout line carries their headline numbers only')
+    ap.add_argument('--lb-pick', choices=('reference', 'batch'), default='reference',
+                    help="N > 1 headline: candidates each rank offers per rebalance: the "
+                         "reference's 50 P (default) or max(50 P, batch)")
     ap.add_argument('--warm', type=int, default=2,
                     help='headline tree warm starts: 2 parent basis as a pivot path (default; '
                          'NodeIncRelaxer semantics), 0 the root basis')
