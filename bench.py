@@ -41,7 +41,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PFI_CAP = 16                # MGPU_LP_PFI_MAX: K3P's eta-file cap (default)
+PFI_DEFAULT = 32            # MGPU_LP_PFI_MAX: K3P's default eta-file cap
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 dense (vector = matrix rate), spec
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec
 
@@ -346,9 +346,16 @@ def tls4_oa_tree(ctx, dev, rank, world, args):
     B = args.oa_tree_batch
     tr = []
     # the tree is solved once untimed (a warm process: kernels loaded, pool
-    # buffers in place, clocks up), then timed
-    inc, nodes, lps, piv, pruned, rounds, el, moved, _, _ = run_tree(
-        ctx, dev, rank, world, p, B, 0, 2, 1 << 21, 0, trace=tr, warm_rounds=None)
+    # buffers in place, clocks up), then timed.  Its rounds are narrow
+    # (~2 700 nodes): K3P's 48-eta build keeps the LPs that need 33-48 etas
+    # out of the dense continuation (the headline's wide rounds keep 32)
+    ctx.load(p)
+    ctx.set_lp_pfi(args.oa_tree_eta_cap)
+    try:
+        inc, nodes, lps, piv, pruned, rounds, el, moved, _, _ = run_tree(
+            ctx, dev, rank, world, p, B, 0, 2, 1 << 21, 0, trace=tr, warm_rounds=None)
+    finally:
+        ctx.set_lp_pfi(PFI_DEFAULT)
     tol = 1e-6 * max(1.0, abs(inc))
     tto = next((t for t, v in tr if v <= inc + tol), el)
     out = {"instance": f"tls4-oa ({p.m} rows, {p.n} cols)", "batch_per_gpu": B,
@@ -1011,6 +1018,8 @@ def main():
     ap.add_argument('--supp-out', default=os.path.join('gpurun_out', 'bench_supplementary.json'),
                     help='where the supplementary objects (trees, configs 3/4/5, glob) are '
                          'written; the stdout line carries their headline numbers only')
+    ap.add_argument('--oa-tree-eta-cap', type=int, default=48,
+                    help="K3P eta-file cap of config 2's complete tree (32 / 48 builds)")
     ap.add_argument('--lb-pick', choices=('reference', 'batch'), default='reference',
                     help="N > 1 headline: candidates each rank offers per rebalance: the "
                          "reference's 50 P (default) or max(50 P, batch)")

@@ -274,8 +274,10 @@ int mgpu_set_lp_variant(mgpu_ctx *ctx, int variant);
  * up to 24 GB; past that it restarts in K3 from the shared warm start).  The
  * eta file lives in VGPRs: caps <= 16 run the 16-eta build (4 waves per
  * SIMD), larger caps the 32-eta build (3 waves per SIMD).  0 keeps auto mode
- * off K3P; 1..MGPU_LP_PFI_MAX (default MGPU_LP_PFI_MAX). */
+ * off K3P; 1..MGPU_LP_PFI_BIG (default MGPU_LP_PFI_MAX; caps above it run
+ * the 48-eta build at two waves per SIMD, for narrow tree rounds). */
 #define MGPU_LP_PFI_MAX 32
+#define MGPU_LP_PFI_BIG 48   /* the largest cap mgpu_set_lp_pfi accepts */
 int mgpu_set_lp_pfi(mgpu_ctx *ctx, int kmax);
 
 /* K3PW (64 < m <= 128 rows, two basis rows per lane) eta-file cap: a node

@@ -445,14 +445,15 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
     // path warm starts run on K3P's eta file: the tree hands children paths
     // of at most min(kPathInherit, eta cap) pivots
     const int kcap = mgpu_lp_pfi_cap(c);
-    if (s->rel || m > kLpMaxM || kcap <= 0 || kcap > kPathMax)
+    if (s->rel || m > kLpMaxM || kcap <= 0 || kcap > kPfiBig)
       return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: path warm starts (warm 2) need MaxVio "
-                  "branching and K3P (m <= 64, eta cap 1..%d)", kPathMax);
+                  "branching and K3P (m <= 64, eta cap 1..%d)", kPfiBig);
     // MGPU_PATH_INHERIT (tuning experiments only; the CPU restatement
     // assumes the default) overrides the longest inherited path
     int inh = kPathInherit;
     if (const char *e = std::getenv("MGPU_PATH_INHERIT")) inh = std::atoi(e);
     if (inh < 0) inh = 0;
+    if (inh > kPathMax) inh = kPathMax;   // the path slots
     s->inherit = kcap < inh ? kcap : inh;
   }
   if (s->rel) {

@@ -77,15 +77,17 @@ constexpr int kUnknownStatus = 12;
 // faster: headline K3P 15.6 -> 14.5 ms (profiles/r04f_ab).  A/B on tls4-lin
 // (S = 3): 12 waves with a 24-eta file 2.12 ms, 16 waves with a 16-eta file
 // 1.75 ms + a longer overflow tail (0.16 ms).
+// The 48-eta build (caps above 32: narrow tree rounds, where a few LPs
+// would otherwise run dense past 32 etas) at two waves per SIMD.
 template <int S, int K>
-constexpr int waves_for() { return S <= 3 ? 16 : 12; }
+constexpr int waves_for() { return K > 32 ? 8 : S <= 3 ? 16 : 12; }
 __host__ __device__ inline int slots_for(int N) { return (N + 63) / 64; }
 
 // packed column status: bits 0-1 status, 2-3 artificial-bound flags, 4 fixed
 enum : int { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
 constexpr int kArtLo = 4, kArtHi = 8, kFixed = 16;
 
-static_assert(kPfiMax < 64, "K3P never reaches K3's 64-pivot primal refresh");
+static_assert(kPfiBig < 64, "K3P never reaches K3's 64-pivot primal refresh");
 constexpr int kPfiSmall = 16;   // the 16-eta build (4 waves per SIMD)
 
 __host__ __device__ constexpr size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
@@ -1013,10 +1015,11 @@ hipError_t launch_pfi_t0(const DevLP &lp, const double *binv, double *t0, hipStr
 }
 
 size_t lp_pfi_lds_bytes(int n, int m, int nnz, int kmax) {
-  const bool small = kmax <= kPfiSmall;
-  const int waves = slots_for(n + m) <= 3 ? (small ? waves_for<3, kPfiSmall>()
-                                                   : waves_for<3, kPfiMax>())
-                                          : waves_for<4, kPfiMax>();
+  const bool small = kmax <= kPfiSmall, big = kmax > kPfiMax;
+  const int waves = big ? waves_for<3, kPfiBig>()
+                    : slots_for(n + m) <= 3 ? (small ? waves_for<3, kPfiSmall>()
+                                                     : waves_for<3, kPfiMax>())
+                                            : waves_for<4, kPfiMax>();
   return pfi_shared_bytes(n, m, nnz) + (size_t)waves * pfi_wave_bytes(n + m);
 }
 
@@ -1030,12 +1033,13 @@ hipError_t launch_lp_pfi(const DevLP &lp, const LpIO &io, const PfiIO &px, int n
                          hipStream_t stream) {
   if (io.batch <= 0) return hipSuccess;
   if (!lp_pfi_fits(lp.n, lp.m, lp.nnz) || io.ws.head == nullptr || px.kmax < 1 ||
-      px.kmax > kPfiMax)
+      px.kmax > kPfiBig)
     return hipErrorInvalidValue;
-  // the eta file in VGPRs is sized at compile time: 16 (4 waves per SIMD)
-  // when the cap allows, else 32 (3 waves per SIMD)
-  return px.kmax <= kPfiSmall ? launch_k<kPfiSmall>(lp, io, px, num_cus, stream)
-                              : launch_k<kPfiMax>(lp, io, px, num_cus, stream);
+  // the eta file in VGPRs is sized at compile time: 16 when the cap allows,
+  // 32 (the default cap), 48 above it
+  if (px.kmax <= kPfiSmall) return launch_k<kPfiSmall>(lp, io, px, num_cus, stream);
+  if (px.kmax <= kPfiMax) return launch_k<kPfiMax>(lp, io, px, num_cus, stream);
+  return launch_k<kPfiBig>(lp, io, px, num_cus, stream);
 }
 
 }  // namespace mgpu

@@ -180,11 +180,12 @@ constexpr int kStallPivots = 128;
 
 // K3P (lp_pfi.hip): product-form dual simplex for a batch that shares its
 // warm start.  At most kPfiMax eta columns per node, n + m <= 64*kPfiSlots.
-constexpr int kPfiMax = 32;
-static_assert(kPfiMax < kStallPivots, "K3P never reaches the Bland switch");
+constexpr int kPfiMax = 32;   // the default cap (the headline's 32-eta build)
+constexpr int kPfiBig = 48;   // the largest cap: the 48-eta build (narrow tree rounds)
+static_assert(kPfiBig < kStallPivots, "K3P never reaches the Bland switch");
 constexpr int kPfiSlots = 4;
 struct PfiIO {
-  int kmax;                     // eta-file cap for this launch (1..kPfiMax)
+  int kmax;                     // eta-file cap for this launch (1..kPfiBig)
   int32_t *ovf_list;            // [B] nodes that needed more than kmax pivots
   int32_t *ovf_count;           // device counter, zeroed before the launch
   int32_t *next;                // device node counter (dynamic schedule), zeroed

@@ -257,7 +257,7 @@ int mgpu_set_lp_variant(mgpu_ctx *c, int variant) {
 }
 
 int mgpu_set_lp_pfi(mgpu_ctx *c, int kmax) {
-  if (!c || kmax < 0 || kmax > MGPU_LP_PFI_MAX) return MGPU_ERR_ARG;
+  if (!c || kmax < 0 || kmax > MGPU_LP_PFI_BIG) return MGPU_ERR_ARG;
   c->lp_pfi = kmax;
   return MGPU_OK;
 }
@@ -269,6 +269,7 @@ int mgpu_set_lp_pfi_wide(mgpu_ctx *c, int kmax) {
 }
 
 static_assert(MGPU_LP_PFI_MAX == kPfiMax, "ABI eta-file cap = kernel's");
+static_assert(MGPU_LP_PFI_BIG == kPfiBig, "ABI largest eta-file cap = kernel's");
 static_assert(MGPU_PATH_MAX == kPathMax, "ABI path cap = kernel's");
 static_assert(MGPU_LP_PFI_WIDE_MAX == kPfiWideMax, "ABI eta-file cap = kernel's");
 
@@ -606,9 +607,11 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     if (want > (size_t)io.batch) want = (size_t)io.batch;
     const int cap = want < max_slots ? (int)want : (int)max_slots;
     HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 4) * sizeof(int32_t)));
-    if (io.path.k != nullptr && (wide || kcap > kPathMax))
+    // (a node's basis difference handed on never exceeds the inherit cap,
+    // <= kPathMax, whatever the eta cap)
+    if (io.path.k != nullptr && (wide || kcap > kPfiBig))
       return fail(c, MGPU_ERR_ARG, "%s: path warm starts run on K3P (m <= 64) with an eta cap "
-                  "<= %d", who, kPathMax);
+                  "<= %d", who, kPfiBig);
     const size_t sb_head = al16h((size_t)cap * m * 4), sb_st = al16h((size_t)cap * N),
                  sb_d = al16h((size_t)cap * N * 8), sb_binv = al16h((size_t)cap * m * m * 8),
                  sb_it = (size_t)cap * 4;

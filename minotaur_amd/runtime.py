@@ -19,7 +19,8 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _D = ctypes.c_double
 
-LP_PFI_MAX = 32  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P eta-file cap
+LP_PFI_MAX = 32  # MGPU_LP_PFI_MAX (include/mgpu.h): K3P's default eta-file cap
+LP_PFI_BIG = 48  # MGPU_LP_PFI_BIG: the largest cap (the 48-eta build)
 LP_PFI_WIDE_MAX = 32  # MGPU_LP_PFI_WIDE_MAX: K3PW eta-file cap
 PATH_MAX = 32  # MGPU_PATH_MAX: columns per basis warm start
 PATH_INHERIT = 32  # the batched tree's largest basis difference handed to children (warm mode 2)

@@ -20,6 +20,7 @@ import pytest
 import oracle
 from golden_io import assert_lp_matches, load_lp
 from minotaur_amd.problem import LinProblem, random_boxes, random_mkp, random_problem
+from minotaur_amd.runtime import LP_PFI_BIG
 from minotaur_amd.runtime import LP_PFI_MAX as KCAP
 
 pytestmark = pytest.mark.gpu
@@ -108,10 +109,11 @@ def test_k3p_bench_boxes_vs_oracle(ctx, kmax):
         assert hs == 0 and abs(ho - r.obj[b]) <= 1e-6 * max(1.0, abs(ho))
 
 
-@pytest.mark.parametrize('kmax', [KCAP, 24, 16, 9])
+@pytest.mark.parametrize('kmax', [LP_PFI_BIG, 40, KCAP, 24, 16, 9])
 def test_k3p_tls4_oa_deep_boxes_vs_oracle(ctx, kmax):
     """Config 2's OA-LP boxes: 10.7 pivots from the root basis on average,
-    18 % above 16 (the 32-eta build for caps > 16, the 16-eta build below)."""
+    18 % above 16 (the 16-eta build for caps <= 16, the 32-eta build up to
+    32, the 48-eta build above)."""
     p = LinProblem.load(os.path.join(os.path.dirname(__file__), '..', 'minotaur_amd',
                                      'instances', 'tls4_oa.npz'))
     ctx.load(p)

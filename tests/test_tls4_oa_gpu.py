@@ -96,3 +96,24 @@ def test_tls4_oa_tree_proves_highs_optimum(ctx, order, warm, brancher, batch):
                              warm=warm, brancher=brancher)
     assert _sig(sg) == _sig(sc)
     assert og == oc                  # every LP kernel sums the objective as the oracle does
+
+
+def test_tls4_oa_tree_eta_cap_48_equals_restatement(ctx):
+    """The complete tree the bench times (depth-first, warm 2, batch 16 384)
+    with K3P's 48-eta build (mgpu_set_lp_pfi 48: caps above 32): the same
+    rounds, pivots and optimum bits as the CPU restatement with pfi 48."""
+    from bnb import CpuBnbContext
+    from minotaur_amd.runtime import LP_PFI_BIG, LP_PFI_MAX
+    p = _p()
+    ctx.load(p)
+    ctx.set_lp_pfi(LP_PFI_BIG)
+    try:
+        assert ctx.oracle_pfi() == LP_PFI_BIG
+        og, _, sg, _ = bnb.solve(ctx, batch=16384, capacity=1 << 20, order=0, warm=2)
+    finally:
+        ctx.set_lp_pfi(LP_PFI_MAX)
+    oc, _, sc, _ = bnb.solve(CpuBnbContext(p, LP_PFI_BIG), batch=16384, capacity=1 << 20,
+                             order=0, warm=2)
+    assert sg.open == 0 and sg.ndec[4] == 0
+    assert _sig(sg) == _sig(sc)
+    assert og == oc and abs(og - OA_MILP_OPT) <= 1e-6
