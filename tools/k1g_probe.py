@@ -17,8 +17,8 @@ from minotaur_amd.runtime import Context
 p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
 ctx = Context(0); ctx.load(p)
 LBa, UBa = random_boxes(p, 524288, 20261017)
-for B in (1024, 524288):
-    for v in (4, 5):
+for B in (1024, 16384):
+    for v in (4,):
         ctx.set_fbbt_variant(v)
         r = ctx.fbbt(LBa[:B], UBa[:B], math.inf)
         vis = r.infeasible // 16; it = r.infeasible % 16
