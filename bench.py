@@ -746,6 +746,7 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
     B = LB.shape[0]
     ctx.load(p)
     cap = B * (max(1, args.warmup) + args.steps + 2) + 2
+    ctx.set_lp_pfi(args.eta_cap)
     ctx.bnb_config(0, args.warm)
     ctx.bnb_brancher(0)
     ctx.bnb_init(cap)
@@ -1045,6 +1046,9 @@ def main():
                     help='skip the supplementary fixed batch (K1 + K3P on tls4-lin boxes)')
     ap.add_argument('--no-oa-tree', action='store_true',
                     help="skip config 2's complete tree (tls4_oa_tree; profiling runs)")
+    ap.add_argument('--eta-cap', type=int, default=PFI_DEFAULT,
+                    help="K3P's eta-file cap for the headline rounds (32; 33-48 select "
+                         'the 48-eta build)')
     ap.add_argument('--no-knapsack', action='store_true',
                     help='skip the supplementary config-3 batch (1000 knapsack nodes)')
     args = ap.parse_args()
@@ -1083,6 +1087,7 @@ def main():
     LB, UB = random_boxes(p, B * world, 20261017)
     LB, UB = LB[rank::world].copy(), UB[rank::world].copy()
     h = tree_rounds(ctx, dev, rank, world, p, LB, UB, args)
+    ctx.set_lp_pfi(PFI_DEFAULT)
     elapsed, nodes, lps = h["elapsed"], h["nodes"], h["lps"]
     progress(rank, f"headline done: {1e3 * elapsed / args.steps:.2f} ms/step, "
                    f"{nodes / elapsed / 1e6:.2f} M nodes/s")
