@@ -27,7 +27,10 @@ Supplementary objects: the round-1/2 fixed batch (tls4-lin), complete trees
 from the root, configs 3/4/5, the glob batch.
 
 Run: python bench.py [--gpus N --steps K --warmup W --batch B]
-     (N>1 through torch.distributed.run; one process per GPU over RCCL).
+     N > 1: one process per GPU, either launched by torch.distributed.run or,
+     without WORLD_SIZE in the environment, started by this script itself
+     (launch_ranks); the round collectives are the engine's own (mgpu_comm_*
+     over RCCL, minotaur_amd.dist.NativeComm).
 """
 import argparse
 import json
@@ -42,6 +45,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PFI_DEFAULT = 32            # MGPU_LP_PFI_MAX: K3P's default eta-file cap
+OP_SUM, OP_MIN, OP_MAX = 0, 1, 2   # MGPU_OP_* (include/mgpu.h)
+# the carrier of every cross-rank reduction of this run (minotaur_amd.dist:
+# the engine's own collectives, mgpu_comm_*, or torch.distributed); set by
+# main() once the ranks are up
+COMM = None
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 dense (vector = matrix rate), spec
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec
 
@@ -219,8 +227,7 @@ def tree_cpu_baseline(p, brancher, seconds):
             "solved": done, "ub": float(res[0])}
 
 
-def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None,
-             warm_rounds=2):
+def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None):
     """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
     across ranks after the shared first rounds: one packed all-reduce per
     round (incumbent MIN + open counts), open nodes rebalanced every 8 rounds
@@ -229,39 +236,39 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=No
     LPs, their pivots) — counts summed over ranks, seconds the max.  ``trace``
     (a list) receives (seconds since the start, incumbent) per round."""
     import torch
-    import torch.distributed as dist
     from minotaur_amd import bnb
-    from minotaur_amd import dist as mdist
-    comm = mdist.Comm(rank, world, dev)
+    from minotaur_amd.runtime import alloc_stats
+    comm = COMM
     ctx.load(p)
-    # warm-up (kernel loads, pool buffers; warm_rounds None: the whole tree once)
-    if warm_rounds is None:
-        bnb.solve_distributed(ctx, B, rank, world, capacity=cap, order=order, warm=warm,
-                              comm=comm, lb_every=8, brancher=brancher)
-    else:
-        bnb.solve_distributed(ctx, 64, rank, world, capacity=1 << 14, max_rounds=warm_rounds,
-                              order=order, warm=warm, comm=comm, brancher=brancher)
-    if world > 1:
-        dist.barrier()
+    # warm-up: the whole tree once, at the timed batch and pool capacity, so
+    # every device buffer the timed solve needs (pool, per-round batch
+    # buffers, warm-start slots, continuation slots) already exists: the timed
+    # region makes no device allocation (checked below; round 4's best-first
+    # dense-warm entry timed a 17 GB pool allocation, VERDICT r04).  (A tree
+    # whose later widths differ between runs could still grow a buffer: the
+    # check then fails loudly instead of timing it.)
+    bnb.solve_distributed(ctx, B, rank, world, capacity=cap, order=order, warm=warm,
+                          comm=comm, lb_every=8, brancher=brancher)
+    comm.barrier()
     torch.cuda.synchronize()
+    a0 = alloc_stats()
     t0 = time.perf_counter()
     tr = []
     inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=cap,
                                                      order=order, warm=warm, comm=comm,
                                                      lb_every=8, brancher=brancher, trace=tr)
     torch.cuda.synchronize()
+    a1 = alloc_stats()
+    if a1 != a0:
+        raise RuntimeError(f"run_tree {p.name}: {a1[0] - a0[0]} device allocation(s) "
+                           f"({a1[1] - a0[1]} bytes) inside the timed tree")
     if trace is not None:
         trace.extend((t - t0, v) for t, v in tr)
-    if world > 1:
-        dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    cnt = torch.tensor([float(mine[k]) for k in ('nodes', 'lps', 'pivots', 'pruned', 'sb_lps',
-                                                  'sb_pivots')],
-                       dtype=torch.float64, device=dev)
-    mdist.allreduce_max(el)
-    mdist.allreduce_sum(cnt)
-    c = [float(v) for v in cnt.tolist()]
-    return inc, c[0], c[1], c[2], c[3], rounds, float(el.item()), mine['moved'], c[4], c[5]
+    comm.barrier()
+    el = float(comm.allreduce([time.perf_counter() - t0], OP_MAX)[0])
+    c = [float(v) for v in comm.allreduce([float(mine[k]) for k in (
+        'nodes', 'lps', 'pivots', 'pruned', 'sb_lps', 'sb_pivots')], OP_SUM)]
+    return inc, c[0], c[1], c[2], c[3], rounds, el, mine['moved'], c[4], c[5]
 
 
 # Complete trees in the bench line (SURVEY §8 f1): config 2's instance as a
@@ -353,7 +360,7 @@ def tls4_oa_tree(ctx, dev, rank, world, args):
     ctx.set_lp_pfi(args.oa_tree_eta_cap)
     try:
         inc, nodes, lps, piv, pruned, rounds, el, moved, _, _ = run_tree(
-            ctx, dev, rank, world, p, B, 0, 2, 1 << 21, 0, trace=tr, warm_rounds=None)
+            ctx, dev, rank, world, p, B, 0, 2, 1 << 21, 0, trace=tr)
     finally:
         ctx.set_lp_pfi(PFI_DEFAULT)
     tol = 1e-6 * max(1.0, abs(inc))
@@ -448,37 +455,24 @@ def convex_batch(ctx, dev, rank, world, B, args):
     MIN per round; nodes/s and LP relaxations/s over the whole batch."""
     import torch
     from minotaur_amd import bnb
-    from minotaur_amd import dist as mdist
     from minotaur_amd.problem import knapsack_oa
-
-    def amin(v):
-        t = torch.tensor([v], dtype=torch.float64, device=dev)
-        return float(mdist.allreduce_incumbent(t).item())
-
-    def amax(v):
-        t = torch.tensor([v], dtype=torch.float64, device=dev)
-        return float(mdist.allreduce_max(t).item())
+    comm = COMM
 
     per, tot_nodes, tot_s, ok = [], 0.0, 0.0, True
     for f, N, opt in CONVEX_BATCH:
         p = knapsack_oa(f=f, N=N)
         ctx.load(p)
-        bnb.solve_distributed(ctx, 64, rank, world, amin, amax, capacity=1 << 14,
-                              max_rounds=2)                  # warm-up (kernel loads)
-        if world > 1:
-            torch.distributed.barrier()
+        bnb.solve_distributed(ctx, 64, rank, world, capacity=1 << 14, max_rounds=2,
+                              comm=comm)                     # warm-up (kernel loads)
+        comm.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, amin, amax,
-                                                         capacity=1 << 21)
+        inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=1 << 21,
+                                                         comm=comm)
         torch.cuda.synchronize()
-        if world > 1:
-            torch.distributed.barrier()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        nd = torch.tensor([float(mine['nodes'])], dtype=torch.float64, device=dev)
-        mdist.allreduce_max(el)
-        mdist.allreduce_sum(nd)
-        el, nodes = float(el.item()), float(nd.item())
+        comm.barrier()
+        el = float(comm.allreduce([time.perf_counter() - t0], OP_MAX)[0])
+        nodes = float(comm.allreduce([float(mine['nodes'])], OP_SUM)[0])
         good = abs(inc - opt) <= 1e-6 * max(1.0, abs(opt))
         ok &= good
         tot_nodes += nodes
@@ -649,10 +643,9 @@ def qp_relaxation(ctx, dev, rank, world, args, B=1024, reps=3):
     k = float(np.median(ms))
     np_, mp = 304, 64                                    # padded KKT sizes
     flops = iters * (np_ ** 3 / 3 + np_ ** 2 * mp + np_ * mp ** 2)
-    tot = torch.tensor([B / (k * 1e-3)], dtype=torch.float64, device=dev)
-    mdist.allreduce_sum(tot)
+    tot = float(COMM.allreduce([B / (k * 1e-3)], OP_SUM)[0])
     out = {"instance": "color_lab2_4x0 (n=300, m=61, dense Q)", "batch_per_gpu": B,
-           "qp_per_s": float(tot.item()), "ms_per_batch": k, "converged": ok,
+           "qp_per_s": tot, "ms_per_batch": k, "converged": ok,
            "ipm_iters_per_qp": iters / B,
            "roofline": {"bound": "mfma", "kernel": "qp_potrf/qp_trsm_syrk (KKT block)",
                         "achieved": flops / (k * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
@@ -753,7 +746,7 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
     if rank > 0:
         ctx.bnb_export(1)        # the root belongs to rank 0 (MpiBranchAndBound.cpp:246-279)
     ctx.bnb_import(LB, UB, np.full(B, -math.inf), np.zeros(B, dtype=np.int32))
-    comm = mdist.Comm(rank, world, dev)
+    comm = COMM
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     state = {"inc": math.inf, "prev": None}
     keys = ("nodes", "lps", "pivots", "pfi_pivots")
@@ -785,9 +778,10 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
     acc = {k: 0 for k in keys}
     acc.update({"fbbt_ms": [], "lp_ms": [], "lp_main_ms": [], "lp_tail_ms": [], "batch": [],
                 "rccl_ms": [], "open": 0})
-    if world > 1:
-        torch.distributed.barrier()
+    comm.barrier()
     torch.cuda.synchronize()
+    from minotaur_amd.runtime import alloc_stats
+    a0 = alloc_stats()
     t0 = time.perf_counter()
     moved = 0
     for k in range(args.steps):
@@ -801,14 +795,12 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
             _, mv, _, _ = mdist.rebalance(ctx, comm, B if args.lb_pick == 'batch' else 0)
             moved += mv
     torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
+    comm.barrier()
     elapsed = time.perf_counter() - t0
-    tot = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    cnt = torch.tensor([float(acc[k]) for k in keys], dtype=torch.float64, device=dev)
-    mdist.allreduce_max(tot)
-    mdist.allreduce_sum(cnt)
-    nodes, lps, pivots, pfi_pivots = (float(v) for v in cnt.tolist())
+    a1 = alloc_stats()
+    tot = float(comm.allreduce([elapsed], OP_MAX)[0])
+    nodes, lps, pivots, pfi_pivots = (float(v) for v in comm.allreduce(
+        [float(acc[k]) for k in keys], OP_SUM))
     S = args.steps
     nb = float(np.mean(acc["batch"]))
     kernels = kernel_entries(p, nb, float(np.mean(acc["fbbt_ms"])),
@@ -822,7 +814,10 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
                           "(K3P)" if args.warm == 2 else "root-basis warm start (K3P)"),
                "incumbent": state["inc"]}
     summary["nodes_migrated"] = moved
-    return {"elapsed": float(tot.item()), "nodes": nodes, "lps": lps, "kernels": kernels,
+    # device allocations inside the timed loop (0 at N = 1; at N > 1 the first
+    # rebalance sizes its row buffers)
+    summary["device_allocs_timed"] = int(a1[0] - a0[0])
+    return {"elapsed": tot, "nodes": nodes, "lps": lps, "kernels": kernels,
             "summary": summary, "incumbent": state["inc"],
             "rccl_ms": float(np.sum(acc["rccl_ms"]))}
 
@@ -1002,6 +997,24 @@ def progress(rank, msg):
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def launch_ranks(n):
+    """Run this bench as N rank processes through torch.distributed.run on
+    127.0.0.1 (the driver's own multi-GPU launch) and return its exit code.
+    A child process, not an exec: the ranks' stdout is this process's
+    stdout, so rank 0's JSON line is the one line printed."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           f'--nproc-per-node={n}', '--master-addr', '127.0.0.1', '--master-port', str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    progress(0, f"launching {n} ranks: {' '.join(cmd[2:])}")
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -1052,6 +1065,13 @@ def main():
     ap.add_argument('--no-knapsack', action='store_true',
                     help='skip the supplementary config-3 batch (1000 knapsack nodes)')
     args = ap.parse_args()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # `python bench.py --gpus N`: this process only launches; N fresh rank
+        # processes (one per GPU) run the bench and rank 0 prints the line.
+        # Nothing here touches the GPU (no torch import), so the ranks start
+        # from a clean device state.
+        sys.exit(launch_ranks(args.gpus))
+    global COMM
 
     import torch
     import torch.distributed as dist
@@ -1060,18 +1080,24 @@ def main():
     from minotaur_amd.runtime import Context
 
     rank, world, local = mdist.env_ranks()
-    # MGPU_BENCH_REHEARSAL=1 (test hook): every rank on device 0 over gloo, to
-    # rehearse the N>1 path on a one-GPU box (RCCL refuses a shared device)
+    if args.gpus != world:
+        progress(rank, f"--gpus {args.gpus} but WORLD_SIZE {world}: running {world} ranks")
+    # MGPU_BENCH_REHEARSAL=1 (test hook): every rank on device 0, to rehearse
+    # the N>1 path on a one-GPU box (RCCL refuses a shared device: the
+    # engine's collectives run over its host transport, gloo underneath)
     rehearse = os.environ.get('MGPU_BENCH_REHEARSAL') == '1'
     if rehearse:
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    comm_mode = os.environ.get('MGPU_COMM', 'host' if rehearse else 'rccl')
     if world > 1:
-        if rehearse:
-            dist.init_process_group('gloo')
-        else:
+        if comm_mode == 'torch':
             dist.init_process_group('nccl', device_id=dev)
+        else:
+            # the rendezvous of torch.distributed.run (and the host transport's
+            # gloo); the round collectives themselves are the engine's
+            dist.init_process_group('gloo')
 
     ctx = Context(local)
     # one dedicated stream for the engine AND the torch glue (the legacy null
@@ -1079,6 +1105,9 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
+    COMM = mdist.make_comm(ctx, rank, world, dev)
+    progress(rank, f"{world} rank(s), round collectives: "
+                   f"{type(COMM).__name__}/{getattr(COMM, 'transport', 'torch')}")
 
     p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
     B = args.batch
@@ -1142,6 +1171,7 @@ def main():
         if rehearse:
             line["rehearsal"] = "all ranks on device 0 over gloo (not a scaling number)"
         print(json.dumps(line), flush=True)
+    COMM = None
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -67,6 +67,10 @@ const char *mgpu_last_error(const mgpu_ctx *ctx);
 int mgpu_set_stream(mgpu_ctx *ctx, void *hip_stream);
 void *mgpu_get_stream(mgpu_ctx *ctx);
 int mgpu_sync(mgpu_ctx *ctx);
+/* Device allocations the engine has made in this process (count and bytes,
+ * every context; buffers grow on demand and are then reused).  A host that
+ * times a region checks that the count did not move inside it. */
+int mgpu_alloc_stats(long long *count, long long *bytes);
 
 /* Load the batch-shared relaxation: row-major CSR, row bounds, root column
  * bounds and types, and a linear objective to MINIMISE plus constant.
@@ -519,6 +523,88 @@ int mgpu_bnb_export_dev(mgpu_ctx *ctx, int k, const int32_t *idx, double *d_rows
 int mgpu_bnb_import_dev(mgpu_ctx *ctx, int k, const double *d_rows);
 int mgpu_bnb_row_width(mgpu_ctx *ctx);
 int mgpu_bnb_count(mgpu_ctx *ctx, int *open, int *spare);
+
+/* ---- the round collectives of the node-sharded tree (multi-GPU) ---------
+ * MpiBranchAndBound (src/base/MpiBranchAndBound.cpp) runs one B&B per MPI
+ * rank and couples them with a few small collectives; here they live in the
+ * engine so that a C++ host shaped like MpiBranchAndBound shards the batched
+ * tree with the C ABI alone (one process per GPU, one context per process).
+ * A context without a communicator is a world of one: every collective is
+ * the identity there.
+ *   mgpu_comm_unique_id : an RCCL unique id (MGPU_COMM_ID_BYTES), made by one
+ *                         rank and handed to the others by the host's own
+ *                         launcher (MPI_Bcast, a file, a TCP store);
+ *   mgpu_comm_init      : an RCCL communicator over the contexts' devices
+ *                         (xGMI between the GPUs of a node);
+ *   mgpu_comm_init_host : the host's own transport instead (e.g. MPI calls on
+ *                         host buffers; device rows are staged through host
+ *                         memory); the callbacks return 0 on success;
+ *   mgpu_comm_info      : this context's rank and world size.
+ * Collectives (blocking unless _dev; every rank calls them in the same order):
+ *   mgpu_allreduce_f64  : v[count] in place, op MGPU_OP_SUM / MIN / MAX (the
+ *                         MPI_Gather of statistics :417, :442 as a SUM);
+ *   mgpu_allreduce_min  : one f64 MIN: the incumbent (MPI_Allreduce MIN,
+ *                         :387-389, and the eager pushes of :197-208);
+ *   mgpu_round_reduce   : the per-round exchange in ONE all-reduce MIN of
+ *                         [incumbent, -open, open, -err] -> out[4] = global
+ *                         incumbent, max and min open count over the ranks,
+ *                         1 when some rank reported err != 0 (the LOR stop
+ *                         flag of :85 and the idle-rank test of the balancer);
+ *   mgpu_allgather_f64  : recv[world][count] = every rank's send[count]
+ *                         (MPI_Allgather of the candidates' bounds, :107);
+ *   mgpu_alltoall_rows_dev : rows of `width` f64 in device memory,
+ *                         send_counts[r] rows to rank r (grouped by receiver,
+ *                         ascending), recv_counts[r] rows from rank r
+ *                         (grouped by sender); asynchronous on the context's
+ *                         stream with RCCL (the per-node MPI_Send / MPI_Recv
+ *                         of :159-185 as one grouped exchange).
+ * Load balancing:
+ *   mgpu_lb_deal        : LoadBalance_'s deal (:111-188), host only, no
+ *                         context: the rank-major bounds lbs[world][S] (+INF
+ *                         padding) sorted ascending by (bound, rank, index)
+ *                         (a stable sort; the reference's std::sort leaves
+ *                         ties unordered), the i-th dealt to rank i mod world,
+ *                         stopping at the first +INF; owner / local / recv[i]
+ *                         for i < the returned count;
+ *   mgpu_bnb_rebalance  : one whole LoadBalance_ on the tree pool: pick this
+ *                         rank's next S candidates (mgpu_bnb_pick), all-gather
+ *                         their bounds and every rank's free pool room, deal,
+ *                         refuse on every rank a deal that would overflow some
+ *                         pool (MGPU_ERR_STATE), export the nodes that change
+ *                         rank as device rows, exchange them in one all-to-all
+ *                         and import the received rows in deal order.
+ *                         picked[S] (optional): the bounds this rank offered,
+ *                         *npicked of them; received[world*S] (optional): the
+ *                         bounds of the nodes it received, in deal order;
+ *                         *moved: nodes that changed rank (all ranks);
+ *                         *open_after: this rank's open nodes afterwards. */
+#define MGPU_COMM_ID_BYTES 128
+#define MGPU_ERR_COMM (-6)   /* a collective failed (RCCL or the host transport) */
+#define MGPU_OP_SUM 0
+#define MGPU_OP_MIN 1
+#define MGPU_OP_MAX 2
+typedef struct {
+  void *user;
+  int (*allreduce)(void *user, double *v, int count, int op);
+  int (*allgather)(void *user, const double *send, int count, double *recv);
+  int (*alltoallv)(void *user, const double *send, const int32_t *send_counts, double *recv,
+                   const int32_t *recv_counts, int width);
+} mgpu_host_transport;
+int mgpu_comm_unique_id(void *id);
+int mgpu_comm_init(mgpu_ctx *ctx, int rank, int world, const void *id);
+int mgpu_comm_init_host(mgpu_ctx *ctx, int rank, int world, const mgpu_host_transport *t);
+int mgpu_comm_info(mgpu_ctx *ctx, int *rank, int *world);
+int mgpu_allreduce_f64(mgpu_ctx *ctx, double *v, int count, int op);
+int mgpu_allreduce_min(mgpu_ctx *ctx, double *v);
+int mgpu_round_reduce(mgpu_ctx *ctx, double incumbent, double open, int err, double *out);
+int mgpu_allgather_f64(mgpu_ctx *ctx, const double *send, int count, double *recv);
+int mgpu_alltoall_rows_dev(mgpu_ctx *ctx, int width, const double *d_send,
+                           const int32_t *send_counts, double *d_recv,
+                           const int32_t *recv_counts);
+int mgpu_lb_deal(int world, int S, const double *lbs, int32_t *owner, int32_t *local,
+                 int32_t *recv);
+int mgpu_bnb_rebalance(mgpu_ctx *ctx, int S, double *picked, int *npicked, double *received,
+                       int *nreceived, long long *moved, int *open_after);
 
 /* ---- Batched spatial branch-and-bound (the glob path) --------------------
  * The node loop of the reference's glob solver (Glob::createBab_,

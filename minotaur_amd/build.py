@@ -17,7 +17,7 @@ SOURCES = ['mgpu_runtime.cpp', 'quad_runtime.cpp', 'bnb.cpp', 'fbbt_linear.hip',
            'lp_dual.hip', 'lp_pfi.hip', 'lp_pfi_wide.hip', 'lp_large.hip', 'node_decide.hip', 'quad_fbbt.hip', 'bnb.hip',
            'bnb_select.hip', 'qp_runtime.cpp', 'rows_runtime.cpp', 'lp_rows.hip', 'bnb_rel.hip', 'bnb_migrate.hip',
            'glob_tree.hip', 'glob_runtime.cpp',
-           'qp_kkt.hip']
+           'qp_kkt.hip', 'comm_runtime.cpp']
 # -ffp-contract=off: no fused multiply-add anywhere (bit-exact FBBT sums,
 # SURVEY §7.3); -fno-gpu-rdc keeps one code object per TU.
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off',
@@ -57,7 +57,10 @@ def build(verbose=False, jobs=None):
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 2) // 2), 8)
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
-    cmd = [HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', out] + objs
+    # RCCL for the round collectives (comm_runtime.cpp); under torch the
+    # process's one librccl.so.1 (torch's, same soname) serves both
+    cmd = ([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', out] + objs +
+           ['-L/opt/rocm/lib', '-lrccl'])
     if verbose:
         print(' '.join(cmd))
     subprocess.run(cmd, check=True)

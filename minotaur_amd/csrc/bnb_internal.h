@@ -222,5 +222,8 @@ hipError_t launch_bnb_unpack(const MigrateIO &io, hipStream_t stream);
 hipError_t launch_bnb_move_rows(unsigned char *rows, unsigned char *tmp, size_t row_bytes,
                                 const int32_t *from, const int32_t *to, int k,
                                 hipStream_t stream);
+// dst row t = src row from[t] (device index array), rows of row_bytes
+hipError_t launch_bnb_gather_rows(const unsigned char *src, unsigned char *dst, size_t row_bytes,
+                                  const int32_t *from, int k, hipStream_t stream);
 
 }  // namespace mgpu

@@ -144,4 +144,12 @@ hipError_t launch_bnb_move_rows(unsigned char *rows, unsigned char *tmp, size_t 
   return hipGetLastError();
 }
 
+hipError_t launch_bnb_gather_rows(const unsigned char *src, unsigned char *dst, size_t row_bytes,
+                                  const int32_t *from, int k, hipStream_t stream) {
+  if (k <= 0 || row_bytes == 0) return hipSuccess;
+  hipLaunchKernelGGL(bnb_move, dim3((k + 3) / 4), dim3(256), 0, stream, src, dst, row_bytes,
+                     from, nullptr, k);
+  return hipGetLastError();
+}
+
 }  // namespace mgpu

@@ -17,6 +17,11 @@ struct QuadState;  // quad_runtime.cpp
 struct BnbState;   // bnb.cpp
 struct QpState;    // qp_runtime.cpp
 struct GlobState;  // glob_runtime.cpp
+struct CommState;  // comm_runtime.cpp
+
+// every device allocation the engine makes (mgpu_alloc_stats: a timed
+// region must not contain one)
+void note_dev_alloc(size_t bytes);  // mgpu_runtime.cpp
 
 struct DevBuf {
   void *p = nullptr;
@@ -31,7 +36,10 @@ struct DevBuf {
     p = nullptr;
     bytes = 0;
     hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) bytes = want;
+    if (e == hipSuccess) {
+      bytes = want;
+      note_dev_alloc(want);
+    }
     return e;
   }
   void release() {
@@ -106,6 +114,7 @@ struct mgpu_ctx {
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
   QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)
   GlobState *glob = nullptr;   // batched spatial B&B (mgpu_glob_init)
+  CommState *comm = nullptr;   // round collectives (mgpu_comm_init[_host])
 };
 
 namespace {
@@ -150,6 +159,7 @@ int qp_solve_nodes(mgpu_ctx *c, int batch, const double *lb, const double *ub,
                    const int32_t *skip, int maxit, int32_t *status, double *obj, int32_t *iters,
                    double *x);
 void glob_state_free(mgpu_ctx *c);  // glob_runtime.cpp
+void comm_state_free(mgpu_ctx *c);  // comm_runtime.cpp
 // an LP batch with per-node warm starts through the K3 / K3L selection of
 // mgpu_lp_solve (mgpu_runtime.cpp); io.next is set here
 int launch_lp_nodes(mgpu_ctx *c, const LpIO &io);

@@ -406,6 +406,10 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     // optimal basis as its statuses plus the kpath basic columns outside the
     // shared basis (ascending); kpath 0 = the shared basis itself
     int kpath = io.path.k != nullptr ? io.path.k[b] : 0;
+    // a basis difference larger than this launch's eta file (a cap lowered
+    // after the tree handed it on, a row imported from a rank with a larger
+    // cap) cannot be rebuilt: the shared basis, as the oracle does
+    if (kpath > px.kmax) kpath = 0;
     const uint32_t *ppath = io.path.path + (size_t)b * kPathMax;
     const int8_t *pst = io.path.st + (size_t)b * N;
     // ---- working bounds; an empty box is infeasible before any pivot ----

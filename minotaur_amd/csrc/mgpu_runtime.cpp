@@ -18,6 +18,8 @@
 #include <string>
 #include <vector>
 
+#include <atomic>
+
 #include "ctx.h"
 
 
@@ -86,8 +88,24 @@ int mgpu_destroy(mgpu_ctx *c) {
   quad_state_free(c);
   bnb_state_free(c);
   qp_state_free(c);
+  comm_state_free(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
+  return MGPU_OK;
+}
+
+namespace {
+std::atomic<long long> g_alloc_count{0}, g_alloc_bytes{0};
+}  // namespace
+
+extern "C++" void note_dev_alloc(size_t bytes) {
+  g_alloc_count.fetch_add(1, std::memory_order_relaxed);
+  g_alloc_bytes.fetch_add((long long)bytes, std::memory_order_relaxed);
+}
+
+int mgpu_alloc_stats(long long *count, long long *bytes) {
+  if (count) *count = g_alloc_count.load(std::memory_order_relaxed);
+  if (bytes) *bytes = g_alloc_bytes.load(std::memory_order_relaxed);
   return MGPU_OK;
 }
 
@@ -605,6 +623,18 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     const size_t max_slots = kPfiOvfBytes / slot_bytes;
     size_t want = (size_t)io.batch / 4 > 4096 ? (size_t)io.batch / 4 : 4096;
     if (want > (size_t)io.batch) want = (size_t)io.batch;
+    // basis warm starts (the tree's warm mode 2): an overflowing LP must go on
+    // from ITS basis, as the oracle's product-form mode does.  Which
+    // LPs overflow first is decided by the device's atomic order, so a
+    // restart from the shared basis past the slots could not be restated:
+    // one slot per LP, or the call fails
+    if (io.path.k != nullptr) {
+      if ((size_t)io.batch > max_slots)
+        return fail(c, MGPU_ERR_NOMEM, "%s: %d basis-warm-started LPs need one continuation "
+                    "slot each (%zu bytes), more than the %zu-byte budget", who, io.batch,
+                    slot_bytes, (size_t)kPfiOvfBytes);
+      want = (size_t)io.batch;
+    }
     const int cap = want < max_slots ? (int)want : (int)max_slots;
     HIPCHK(c, c->pfi_ovf.ensure(((size_t)io.batch + 4) * sizeof(int32_t)));
     // (a node's basis difference handed on never exceeds the inherit cap,
@@ -820,6 +850,7 @@ int mgpu_ws_alloc(mgpu_ctx *c, int *slot) {
   ch.cap = kWsChunkSlots;
   ch.bytes = ws_layout(n, m).bytes;
   HIPCHK(c, hipMalloc((void **)&ch.base, ch.bytes * ch.cap));
+  note_dev_alloc(ch.bytes * ch.cap);
   ch.free.reserve(ch.cap);
   for (int i = ch.cap - 1; i >= 1; --i) ch.free.push_back(i);
   size_t k = c->ws_chunks.size();

@@ -7,6 +7,7 @@
 namespace mgpu {
 
 constexpr double kQpTolMu = 1e-10;   // complementarity (oracle/qp_ipm.py TOL_MU)
+constexpr double kQpTolP = 1e-9;     // primal residual, relative (oracle/qp_ipm.py TOL_P)
 constexpr double kQpReg = 1e-12;     // relative regularisation of M
 constexpr double kQpStep = 0.995;    // fraction to the boundary
 

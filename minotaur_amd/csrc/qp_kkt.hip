@@ -111,8 +111,9 @@ __global__ __launch_bounds__(kT) void qp_prep(DevQP q, QpWork w, int assemble) {
   __syncthreads();
   // rd = Qx + c - A'y - zl + zu on free variables (Q symmetric: column
   // access Q[i][j] over i is coalesced across j)
-  double rdmax = 0.0, comp = 0.0, nf = 0.0;
+  double rdmax = 0.0, comp = 0.0, nf = 0.0, xmax = 0.0;
   for (int j = t; j < np; j += kT) {
+    xmax = fmax(xmax, fabs(x[j]));
     double qx = 0.0;
     for (int i = 0; i < np; ++i) qx += q.Q[(size_t)i * np + j] * x[i];
     double aty = 0.0;
@@ -141,8 +142,13 @@ __global__ __launch_bounds__(kT) void qp_prep(DevQP q, QpWork w, int assemble) {
   rpmax = block_max(rpmax, red);
   comp = block_sum(comp, red);
   nf = block_sum(nf, red);
+  xmax = block_max(xmax, red);
   const double mu = comp / fmax(2.0 * nf, 1.0);
-  if (rpmax <= q.tp && rdmax <= q.td && mu <= kQpTolMu) {
+  // the primal tolerance scales with the rows' right-hand sides and the
+  // iterate (slack columns of ranged rows carry the rows' activity while b
+  // is 0: hs021), as oracle/qp_ipm.py
+  const double tp = fmax(q.tp, kQpTolP * (1.0 + xmax));
+  if (rpmax <= tp && rdmax <= q.td && mu <= kQpTolMu) {
     if (t == 0) {
       w.done[b] = 1;
       w.status[b] = 0;

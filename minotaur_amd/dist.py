@@ -1,8 +1,16 @@
 """Multi-GPU semantics of the batched B&B path (one process per GPU).
 
 Mirrors the collectives of MpiBranchAndBound (src/base/MpiBranchAndBound.cpp)
-that touch the hot path, on torch.distributed (RCCL over xGMI on MI355X,
-gloo on CPU for the tests):
+that touch the hot path.  Two carriers with one interface:
+
+* ``NativeComm``: a ctypes client of the engine's own collectives
+  (mgpu_comm_* / mgpu_round_reduce / mgpu_bnb_rebalance in libmgpu, RCCL over
+  xGMI, or a host transport) -- what a C++ host shaped like MpiBranchAndBound
+  calls; the bench and the trees on GPUs use it;
+* ``Comm``: torch.distributed (gloo on CPU), for the CPU restatement's
+  multi-process tests (oracle contexts have no engine).
+
+The collectives:
 
 * incumbent: ``MPI_Allreduce(MIN)`` of the upper bound (:387-389) plus the
   eager point-to-point pushes of new incumbents (:197-208, :36-50), folded
@@ -111,6 +119,17 @@ class Comm:
         if active() and dist.get_backend() == 'gloo':
             self.device = torch.device('cpu')
 
+    def allreduce(self, vals, op):
+        """SUM / MIN / MAX (runtime.OP_*) of a small f64 vector -> numpy."""
+        t = torch.as_tensor(np.array(vals, dtype=np.float64).reshape(-1)).to(self.device)
+        if active():
+            dist.all_reduce(t, op=(dist.ReduceOp.SUM, dist.ReduceOp.MIN, dist.ReduceOp.MAX)[op])
+        return t.cpu().numpy()
+
+    def barrier(self):
+        if active():
+            dist.barrier()
+
     def round_reduce(self, inc, n_open, err=0):
         if not active():   # one rank: nothing to reduce (no device round trip per round)
             return float(inc), float(n_open), float(n_open), float(err)
@@ -144,6 +163,73 @@ class Comm:
         return out
 
 
+class NativeComm:
+    """The round collectives inside the engine (include/mgpu.h mgpu_comm_*):
+    ``transport`` 'rccl' -- an RCCL communicator over the ranks' GPUs (rank 0
+    makes the unique id, the bootstrap process group hands it to the others;
+    torch.distributed is only the launcher's rendezvous here) -- or 'host' --
+    the engine calls back into torch.distributed (gloo) on host buffers (the
+    one-GPU rehearsal of N ranks, where RCCL refuses a shared device).  A
+    world of one needs no communicator: every collective is the identity.
+    Load balancing is ONE engine call (mgpu_bnb_rebalance)."""
+
+    def __init__(self, ctx, rank, world, transport='rccl'):
+        self.ctx, self.rank, self.world, self.transport = ctx, rank, world, transport
+        if world == 1:
+            return
+        if transport == 'rccl':
+            from .runtime import comm_unique_id
+            obj = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.comm_init(rank, world, obj[0])
+        elif transport == 'host':
+            ops = (dist.ReduceOp.SUM, dist.ReduceOp.MIN, dist.ReduceOp.MAX)
+
+            def ar(v, op):
+                t = torch.from_numpy(v)          # shares the engine's buffer
+                dist.all_reduce(t, op=ops[op])
+
+            def ag(send, recv):
+                out = torch.from_numpy(recv)
+                dist.all_gather(list(out.unbind(0)), torch.from_numpy(send.copy()))
+
+            def a2a(send, sc, recv, rc):
+                out = torch.from_numpy(recv) if recv.size else torch.empty((0, recv.shape[1]),
+                                                                           dtype=torch.float64)
+                dist.all_to_all_single(out, torch.from_numpy(send.copy()),
+                                       [int(c) for c in rc], [int(c) for c in sc])
+            ctx.comm_init_host(rank, world, ar, ag, a2a)
+        else:
+            raise ValueError(f"NativeComm: unknown transport {transport!r}")
+
+    def allreduce(self, vals, op):
+        return self.ctx.allreduce(vals, op)
+
+    def barrier(self):
+        self.ctx.allreduce([0.0], 0)
+
+    def round_reduce(self, inc, n_open, err=0):
+        return self.ctx.round_reduce(inc, n_open, err)
+
+    def allgather_vec(self, vec):
+        return torch.from_numpy(self.ctx.allgather(vec))
+
+    def all_to_all_rows(self, rows, send_counts, recv_counts, width):
+        return self.ctx.alltoall_rows(rows, send_counts, recv_counts)
+
+
+def make_comm(ctx, rank, world, device=None):
+    """The carrier of the round collectives for a GPU run: the engine's own
+    (NativeComm; MGPU_COMM=rccl (default) or host) or torch.distributed's
+    (MGPU_COMM=torch, Comm).  The one-GPU rehearsal (MGPU_BENCH_REHEARSAL=1)
+    uses the host transport: RCCL refuses ranks that share a device."""
+    mode = os.environ.get('MGPU_COMM', 'host' if os.environ.get('MGPU_BENCH_REHEARSAL') == '1'
+                          else 'rccl')
+    if mode == 'torch':
+        return Comm(rank, world, device)
+    return NativeComm(ctx, rank, world, mode)
+
+
 def rebalance(ctx, comm, batch=0):
     """One bound-aware load-balancing step (MpiBranchAndBound::LoadBalance_,
     :78-195) on the tree pool of ``ctx``:
@@ -168,6 +254,8 @@ def rebalance(ctx, comm, batch=0):
     order)."""
     P, r = comm.world, comm.rank
     S = max(MIN_NODES_PER_RANK * P, int(batch))
+    if isinstance(comm, NativeComm):      # the whole step inside the engine
+        return ctx.bnb_rebalance(S)
     lbs = ctx.bnb_pick(S)
     n_open, spare = ctx.bnb_count()
     vec = torch.full((S + 1,), float('inf'), dtype=torch.float64)

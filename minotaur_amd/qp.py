@@ -38,6 +38,14 @@ class QpProblem:
 
 
 def from_nl(path, name=None) -> QpProblem:
+    """The QP of an ``.nl`` model with a quadratic objective and linear rows.
+    Equality rows stay as they are; a ranged or one-sided row l <= a'x <= u
+    becomes a'x - s = 0 with a slack column s in [l, u] (continuous, no
+    objective term, appended after the model's columns in row order): BQPD
+    takes the same model, general constraints carrying bounds bl / bu next
+    to the variables' (BqpdEngine::setVarBounds_ / setConsBounds_,
+    src/interfaces/BqpdEngine.cpp:601-641).  Infinite bounds stay infinite
+    (presolve_box makes a node box finite for K5)."""
     m = nlmod.read_nl(path)
     Q, c, k = nlmod.quadratic_form(m.obj_expr, m.n)
     for j, a in m.obj_grad:
@@ -45,15 +53,43 @@ def from_nl(path, name=None) -> QpProblem:
     k += m.obj_const
     if m.obj_sense == 1:
         Q, c, k = -Q, -c, -k
-    if not np.all(m.con_lb == m.con_ub):
-        raise ValueError('QP path takes equality rows only')
-    A = np.zeros((m.m, m.n))
+    ranged = [i for i in range(m.m) if m.con_lb[i] != m.con_ub[i]]
+    n = m.n + len(ranged)
+    A = np.zeros((m.m, n))
     for i, row in enumerate(m.rows):
         for j, a in row:
             A[i, j] += a
-    return QpProblem(name or m.name, Q, c, k, A, m.con_lb.astype(np.float64),
-                     m.var_lb.astype(np.float64), m.var_ub.astype(np.float64),
-                     np.asarray(m.var_type, dtype=np.int32))
+    b = m.con_lb.astype(np.float64).copy()
+    l = np.concatenate([m.var_lb.astype(np.float64), np.zeros(len(ranged))])
+    u = np.concatenate([m.var_ub.astype(np.float64), np.zeros(len(ranged))])
+    for t, i in enumerate(ranged):
+        A[i, m.n + t] = -1.0
+        b[i] = 0.0
+        l[m.n + t], u[m.n + t] = m.con_lb[i], m.con_ub[i]
+    Qn = np.zeros((n, n))
+    Qn[:m.n, :m.n] = Q
+    cn = np.concatenate([c, np.zeros(len(ranged))])
+    vtype = np.concatenate([np.asarray(m.var_type, dtype=np.int32),
+                            np.full(len(ranged), 4, dtype=np.int32)])   # Continuous
+    return QpProblem(name or m.name, Qn, cn, k, A, b, l, u, vtype)
+
+
+def presolve_box(ctx, qp: QpProblem, lb=None, ub=None):
+    """A finite node box for K5 (whose interior point needs one): the box
+    (default: the root's) tightened by K1 on the QP's rows -- the batched
+    tree's own presolve (LinearHandler::presolveNode, mgpu_fbbt) -- which
+    derives bounds for free columns from their rows.  Raises when the rows
+    prove the box infeasible or a bound stays infinite.  Loads the rows
+    problem into ``ctx``."""
+    ctx.load(rows_problem(qp))
+    LB = np.atleast_2d(qp.l if lb is None else lb).astype(np.float64)
+    UB = np.atleast_2d(qp.u if ub is None else ub).astype(np.float64)
+    r = ctx.fbbt(LB, UB)
+    if np.any(r.infeasible):
+        raise ValueError(f'{qp.name}: the rows prove the box infeasible')
+    if not (np.all(np.isfinite(r.lb)) and np.all(np.isfinite(r.ub))):
+        raise ValueError(f'{qp.name}: FBBT leaves an infinite bound; K5 needs a finite box')
+    return r.lb, r.ub
 
 
 def feasible_binary_point(qp: QpProblem, seed: int):

@@ -42,7 +42,28 @@ EXPORTS = [
     'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive', 'mgpu_ws_alloc', 'mgpu_ws_free',
     'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1', 'mgpu_bnb_pick', 'mgpu_bnb_export_dev',
     'mgpu_bnb_import_dev', 'mgpu_bnb_row_width', 'mgpu_bnb_count', 'mgpu_glob_init', 'mgpu_glob_round', 'mgpu_glob_best',
+    'mgpu_comm_unique_id', 'mgpu_comm_init', 'mgpu_comm_init_host', 'mgpu_comm_info',
+    'mgpu_allreduce_f64', 'mgpu_allreduce_min', 'mgpu_round_reduce', 'mgpu_allgather_f64',
+    'mgpu_alltoall_rows_dev', 'mgpu_lb_deal', 'mgpu_bnb_rebalance', 'mgpu_alloc_stats',
 ]
+
+COMM_ID_BYTES = 128            # MGPU_COMM_ID_BYTES
+OP_SUM, OP_MIN, OP_MAX = 0, 1, 2   # MGPU_OP_*
+
+# mgpu_host_transport's callbacks (include/mgpu.h)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.c_int, ctypes.c_int)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.c_int, ctypes.POINTER(ctypes.c_double))
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_int32), ctypes.c_int)
+
+
+class HostTransport(ctypes.Structure):
+    """mgpu_host_transport (include/mgpu.h)."""
+    _fields_ = [('user', ctypes.c_void_p), ('allreduce', ALLREDUCE_FN),
+                ('allgather', ALLGATHER_FN), ('alltoallv', ALLTOALLV_FN)]
 
 
 class BnbStats(ctypes.Structure):
@@ -126,6 +147,18 @@ def load_library():
     lib.mgpu_bnb_import_dev.argtypes = [_P, _I, _P]
     lib.mgpu_bnb_row_width.argtypes = [_P]
     lib.mgpu_bnb_count.argtypes = [_P, _P, _P]
+    lib.mgpu_alloc_stats.argtypes = [_P, _P]
+    lib.mgpu_comm_unique_id.argtypes = [_P]
+    lib.mgpu_comm_init.argtypes = [_P, _I, _I, _P]
+    lib.mgpu_comm_init_host.argtypes = [_P, _I, _I, ctypes.POINTER(HostTransport)]
+    lib.mgpu_comm_info.argtypes = [_P, _P, _P]
+    lib.mgpu_allreduce_f64.argtypes = [_P, _P, _I, _I]
+    lib.mgpu_allreduce_min.argtypes = [_P, _P]
+    lib.mgpu_round_reduce.argtypes = [_P, _D, _D, _I, _P]
+    lib.mgpu_allgather_f64.argtypes = [_P, _P, _I, _P]
+    lib.mgpu_alltoall_rows_dev.argtypes = [_P, _I, _P, _P, _P, _P]
+    lib.mgpu_lb_deal.argtypes = [_I, _I, _P, _P, _P, _P]
+    lib.mgpu_bnb_rebalance.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P]
     lib.mgpu_glob_init.argtypes = [_P, _I, _D]
     lib.mgpu_glob_round.argtypes = [_P, _I, _D, ctypes.POINTER(GlobStats)]
     lib.mgpu_glob_best.argtypes = [_P, _P, _P]
@@ -167,6 +200,40 @@ def _hp(a):
 def _dp(t):
     """Device pointer of a torch CUDA tensor (or None)."""
     return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def comm_unique_id() -> bytes:
+    """mgpu_comm_unique_id: an RCCL unique id for mgpu_comm_init (one rank
+    makes it, the launcher hands it to the others)."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    rc = lib.mgpu_comm_unique_id(buf)
+    if rc != 0:
+        raise MgpuError(f"mgpu_comm_unique_id failed rc={rc}")
+    return buf.raw
+
+
+def alloc_stats():
+    """mgpu_alloc_stats: (device allocations, bytes) the engine made so far
+    in this process."""
+    lib = load_library()
+    n, b = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    lib.mgpu_alloc_stats(ctypes.byref(n), ctypes.byref(b))
+    return n.value, b.value
+
+
+def lb_deal(world, S, lbs):
+    """mgpu_lb_deal (host only, no device): LoadBalance_'s deal of the
+    rank-major bounds lbs [world * S] -> (owner, local, receiver) arrays."""
+    lib = load_library()
+    v = np.ascontiguousarray(lbs, dtype=np.float64).reshape(-1)
+    if v.size != world * S:
+        raise MgpuError(f"lb_deal: {v.size} bounds for world {world} x S {S}")
+    o, loc, r = (np.empty(max(v.size, 1), dtype=np.int32) for _ in range(3))
+    nd = lib.mgpu_lb_deal(int(world), int(S), _hp(v), _hp(o), _hp(loc), _hp(r))
+    if nd < 0:
+        raise MgpuError(f"mgpu_lb_deal failed rc={nd}")
+    return o[:nd].copy(), loc[:nd].copy(), r[:nd].copy()
 
 
 class FbbtOut:
@@ -749,6 +816,10 @@ class Context:
         k = int(rows.shape[0])
         if k == 0:
             return
+        W = self.bnb_row_width()
+        if rows.dim() != 2 or int(rows.shape[1]) != W:
+            raise MgpuError(f"bnb_import_rows: rows of shape {tuple(rows.shape)}, the pool's "
+                            f"row width is {W} (mgpu_bnb_row_width)")
         buf = rows.to(device=torch.device('cuda', self.device), dtype=torch.float64).contiguous()
         self._chk(self.lib.mgpu_bnb_import_dev(self.h, k, buf.data_ptr()), 'mgpu_bnb_import_dev')
 
@@ -758,6 +829,110 @@ class Context:
         self._chk(self.lib.mgpu_bnb_count(self.h, ctypes.byref(o), ctypes.byref(v)),
                   'mgpu_bnb_count')
         return o.value, v.value
+
+    # -- round collectives (mgpu_comm_*, include/mgpu.h) ------------------------
+    def comm_init(self, rank, world, uid: bytes):
+        """mgpu_comm_init: an RCCL communicator (uid from comm_unique_id() on
+        one rank, handed to every rank by the launcher)."""
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        self._chk(self.lib.mgpu_comm_init(self.h, int(rank), int(world), buf), 'mgpu_comm_init')
+
+    def comm_init_host(self, rank, world, allreduce, allgather, alltoallv):
+        """mgpu_comm_init_host: the host's own transport.  The three Python
+        callables take numpy arrays (views of the engine's host buffers):
+        allreduce(v, op) in place; allgather(send, recv[world, count]);
+        alltoallv(send[rows, width], send_counts, recv[rows, width],
+        recv_counts)."""
+        def ar(_, v, count, op):
+            try:
+                allreduce(np.ctypeslib.as_array(v, shape=(count,)), int(op))
+                return 0
+            except Exception:                                  # noqa: BLE001
+                return 1
+
+        def ag(_, send, count, recv):
+            try:
+                allgather(np.ctypeslib.as_array(send, shape=(count,)),
+                          np.ctypeslib.as_array(recv, shape=(self._world, count)))
+                return 0
+            except Exception:                                  # noqa: BLE001
+                return 1
+
+        def a2a(_, send, sc, recv, rc, width):
+            try:
+                P = self._world
+                scn = np.ctypeslib.as_array(sc, shape=(P,)).copy()
+                rcn = np.ctypeslib.as_array(rc, shape=(P,)).copy()
+                ns, nr = int(scn.sum()), int(rcn.sum())
+                sv = (np.ctypeslib.as_array(send, shape=(ns, width)) if ns
+                      else np.empty((0, width)))
+                rv = (np.ctypeslib.as_array(recv, shape=(nr, width)) if nr
+                      else np.empty((0, width)))
+                alltoallv(sv, scn, rv, rcn)
+                return 0
+            except Exception:                                  # noqa: BLE001
+                return 1
+        self._world = int(world)
+        self._transport = HostTransport(None, ALLREDUCE_FN(ar), ALLGATHER_FN(ag),
+                                        ALLTOALLV_FN(a2a))   # kept alive with the context
+        self._chk(self.lib.mgpu_comm_init_host(self.h, int(rank), int(world),
+                                               ctypes.byref(self._transport)),
+                  'mgpu_comm_init_host')
+
+    def comm_info(self):
+        r, w = ctypes.c_int(0), ctypes.c_int(1)
+        self._chk(self.lib.mgpu_comm_info(self.h, ctypes.byref(r), ctypes.byref(w)),
+                  'mgpu_comm_info')
+        return r.value, w.value
+
+    def allreduce(self, vals, op):
+        """mgpu_allreduce_f64 over the ranks (op OP_SUM / OP_MIN / OP_MAX)."""
+        v = np.array(vals, dtype=np.float64).reshape(-1)
+        self._chk(self.lib.mgpu_allreduce_f64(self.h, _hp(v), int(v.size), int(op)),
+                  'mgpu_allreduce_f64')
+        return v
+
+    def round_reduce(self, inc, n_open, err=0):
+        """mgpu_round_reduce -> (incumbent, max open, min open, any error)."""
+        out = np.zeros(4)
+        self._chk(self.lib.mgpu_round_reduce(self.h, float(inc), float(n_open), int(err),
+                                             _hp(out)), 'mgpu_round_reduce')
+        return float(out[0]), float(out[1]), float(out[2]), float(out[3])
+
+    def allgather(self, vec):
+        """mgpu_allgather_f64 -> [world, count]."""
+        v = np.array(vec, dtype=np.float64).reshape(-1)
+        _, w = self.comm_info()
+        out = np.empty((w, v.size))
+        self._chk(self.lib.mgpu_allgather_f64(self.h, _hp(v), int(v.size), _hp(out)),
+                  'mgpu_allgather_f64')
+        return out
+
+    def alltoall_rows(self, rows, send_counts, recv_counts):
+        """mgpu_alltoall_rows_dev on torch device rows [k, W] -> received rows."""
+        import torch
+        W = int(rows.shape[1])
+        sc = np.ascontiguousarray(send_counts, dtype=np.int32)
+        rc = np.ascontiguousarray(recv_counts, dtype=np.int32)
+        out = torch.empty((int(rc.sum()), W), dtype=torch.float64, device=rows.device)
+        inp = rows.contiguous()
+        self._chk(self.lib.mgpu_alltoall_rows_dev(self.h, W, _dp(inp) if inp.numel() else None,
+                                                  _hp(sc), _dp(out) if out.numel() else None,
+                                                  _hp(rc)), 'mgpu_alltoall_rows_dev')
+        return out
+
+    def bnb_rebalance(self, S):
+        """mgpu_bnb_rebalance: one LoadBalance_ -> (open afterwards, nodes moved,
+        the bounds this rank offered, the bounds it received in deal order)."""
+        _, w = self.comm_info()
+        picked = np.empty(int(S))
+        got = np.empty(int(S) * w)
+        npk, ngot, op = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        mv = ctypes.c_longlong(0)
+        self._chk(self.lib.mgpu_bnb_rebalance(self.h, int(S), _hp(picked), ctypes.byref(npk),
+                                              _hp(got), ctypes.byref(ngot), ctypes.byref(mv),
+                                              ctypes.byref(op)), 'mgpu_bnb_rebalance')
+        return op.value, int(mv.value), picked[:npk.value].copy(), got[:ngot.value].copy()
 
     # -- batched spatial B&B (mgpu_glob_*) ------------------------------------
     def glob_init(self, capacity, incumbent=math.inf):

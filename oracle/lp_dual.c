@@ -467,7 +467,8 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
     }
     for (int j = 0; j < N; ++j) W.st[j] = path->st[j];
     pfi_compute_duals(&W);
-  } else if (path && path->k > 0 && W.pfi && colrep_basis(&W, path)) {
+  } else if (path && path->k > 0 && W.pfi && path->k <= W.pfi && colrep_basis(&W, path)) {
+    /* (a difference larger than the eta file: the shared basis, as K3P) */
     for (int j = 0; j < N; ++j) W.st[j] = path->st[j];
     pfi_compute_duals(&W);
   } else if (have_ws && have_binv == 1 && ws_d) {

@@ -74,7 +74,10 @@ def solve_node(Q, c, A, b, l, u, maxit=MAXIT):
         rd = np.where(free, Q @ x + c - A.T @ y - zl + zu, 0.0)
         rp = b - A @ x
         mu = float((sl[free] @ zl[free] + su[free] @ zu[free]) / max(2 * nf, 1))
-        if np.max(np.abs(rp), initial=0.0) <= tp and np.max(np.abs(rd), initial=0.0) <= td \
+        # the primal tolerance also scales with the iterate: a ranged row's
+        # slack column carries the row's activity while b is 0 (hs021)
+        tpx = max(tp, TOL_P * (1.0 + float(np.max(np.abs(x), initial=0.0))))
+        if np.max(np.abs(rp), initial=0.0) <= tpx and np.max(np.abs(rd), initial=0.0) <= td \
                 and mu <= TOL_MU:
             status = 0
             break

@@ -255,3 +255,25 @@ def test_cpu_pick_export_import_roundtrip():
         while st.open:                      # the tree still proves the optimum
             st = ctx.bnb_round(8)
         assert abs(ctx.inc - hobj) <= 1e-6 * max(1.0, abs(hobj))
+
+
+@pytest.mark.parametrize("world,S", [(1, 5), (2, 3), (3, 50), (8, 400)])
+def test_engine_lb_deal_equals_restatement(world, S):
+    """mgpu_lb_deal (the deal inside mgpu_bnb_rebalance, host code of
+    libmgpu: no device needed) equals dist.lb_deal -- the restatement of
+    LoadBalance_'s deal the gloo tests check -- on gathers with ties,
+    -0.0 / +0.0, -inf and +inf padding."""
+    from minotaur_amd import runtime
+    from minotaur_amd.dist import lb_deal
+    rng = np.random.default_rng(world * 1000 + S)
+    g = rng.integers(-3, 6, size=(world, S)).astype(np.float64)   # many ties
+    g[rng.random((world, S)) < 0.1] = -0.0
+    g[rng.random((world, S)) < 0.05] = -math.inf
+    for r in range(world):                     # each rank's picks, then padding
+        k = int(rng.integers(0, S + 1))
+        g[r, k:] = math.inf
+    o1, l1, r1 = runtime.lb_deal(world, S, g.reshape(-1))
+    o2, l2, r2 = lb_deal(torch.from_numpy(g.reshape(-1)), world, S)
+    assert o1.tolist() == o2.tolist()
+    assert l1.tolist() == l2.tolist()
+    assert r1.tolist() == r2.tolist()

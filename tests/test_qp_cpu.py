@@ -53,3 +53,24 @@ def test_small_qp_matches_slsqp(seed):
                  options={'ftol': 1e-14, 'maxiter': 500})
     assert s.success
     assert abs(r['obj'] - s.fun) <= 1e-6 * max(1.0, abs(s.fun))
+
+
+HS021 = os.path.join(os.path.dirname(__file__), 'golden', 'nl', 'hs021.nl')
+
+
+def test_hs021_reference_answer_by_restatement():
+    """The reference's own QP answer (AMPLBqpdUT, src/testing/AMPLBqpdUT.cpp:
+    29, 59-64: BQPD on instances/hs021 -> ProvenLocalOptimal, objective
+    -99.96 within 1e-7; tests/golden/nl/hs021.nl is that instance file):
+    the .nl reader's QP (ranged rows -> slack columns, as BQPD's general
+    constraint bounds), the box the rows' FBBT makes finite (C restatement of
+    LinearHandler::presolveNode), then the interior-point restatement."""
+    import oracle
+    P = qpm.from_nl(HS021)
+    assert (P.n, P.m) == (5, 3)                  # x0, x1 + a slack per ranged row
+    f = oracle.linear_fbbt(qpm.rows_problem(P), P.l[None], P.u[None])
+    assert f.infeas[0] == 0 and np.all(np.isfinite(f.lb)) and np.all(np.isfinite(f.ub))
+    r = qp_ipm.solve_node(P.Q, P.c, P.A, P.b, f.lb[0], f.ub[0])
+    assert r['status'] == 0
+    assert abs(r['obj'] + P.k + 99.96) < 1e-7
+    assert abs(r['x'][0] - 2.0) < 1e-7 and abs(r['x'][1]) < 1e-7

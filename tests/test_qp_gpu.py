@@ -39,7 +39,7 @@ def test_color_lab2_batch(ctx):
     ctx.load_qp(P)
     LB, UB = qpm.random_node_boxes(P, 24, 9)
     st, ob, it, x = ctx.qp_solve(LB, UB)
-    _check(P, LB, UB, st, ob, x, nref=6)
+    _check(P, LB, UB, st, ob, x)              # every box against the restatement
     assert it.max() < 80 and ctx.last_kernel_ms('qp') > 0
 
 
@@ -54,3 +54,26 @@ def test_random_qps(ctx, seed):
     UB = np.tile(P.u, (B, 1))
     st, ob, it, x = ctx.qp_solve(LB, UB)
     _check(P, LB, UB, st, ob, x, nref=3)
+
+
+HS021 = os.path.join(ROOT, 'tests', 'golden', 'nl', 'hs021.nl')
+
+
+def test_hs021_reference_answer(ctx):
+    """The reference's own QP pin (AMPLBqpdUT, src/testing/AMPLBqpdUT.cpp:29,
+    59-64): BQPD on instances/hs021 -> ProvenLocalOptimal with objective
+    -99.96 within 1e-7.  Here: the .nl reader's QP (ranged rows as slack
+    columns, BQPD's general-constraint bounds), the box K1 makes finite from
+    the rows (qp.presolve_box), K5 -> status optimal and the reference's
+    objective; and the QP tree over the same model (no integer columns: the
+    root is feasible and is the answer)."""
+    P = qpm.from_nl(HS021)
+    LB, UB = qpm.presolve_box(ctx, P)
+    ctx.load_qp(P)
+    st, ob, it, x = ctx.qp_solve(LB, UB)
+    assert st[0] == 0
+    assert abs(ob[0] + 99.96) < 1e-7
+    assert abs(x[0, 0] - 2.0) < 1e-7 and abs(x[0, 1]) < 1e-7
+    obj, xt, stt, _ = qpm.solve_tree(ctx, P, batch=4, capacity=64)
+    assert stt.open == 0 and stt.ndec[3] == 1
+    assert abs(obj + 99.96) < 1e-7

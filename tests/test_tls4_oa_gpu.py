@@ -117,3 +117,27 @@ def test_tls4_oa_tree_eta_cap_48_equals_restatement(ctx):
     assert sg.open == 0 and sg.ndec[4] == 0
     assert _sig(sg) == _sig(sc)
     assert og == oc and abs(og - OA_MILP_OPT) <= 1e-6
+
+
+def test_tls4_oa_warm2_small_eta_cap_wide_rounds_equal_restatement(ctx):
+    """with a small eta cap (9) and rounds of 32 768 nodes far more
+    than a quarter of the basis-warm-started LPs fill the eta file; each must
+    still go on from its own basis (one continuation slot per LP), as the
+    oracle's product-form mode does, so the rounds equal the restatement's
+    pivot for pivot."""
+    from bnb import CpuBnbContext
+    from minotaur_amd.runtime import LP_PFI_MAX
+    p = _p()
+    ctx.load(p)
+    ctx.set_lp_pfi(9)
+    try:
+        assert ctx.oracle_pfi() == 9
+        og, _, sg, _ = bnb.solve(ctx, batch=32768, capacity=1 << 20, order=0, warm=2,
+                                 max_rounds=20)
+    finally:
+        ctx.set_lp_pfi(LP_PFI_MAX)
+    oc, _, sc, _ = bnb.solve(CpuBnbContext(p, 9), batch=32768, capacity=1 << 20, order=0,
+                             warm=2, max_rounds=20)
+    assert sg.lps > 32768            # at least one full-width round
+    assert _sig(sg) == _sig(sc)
+    assert og == oc
