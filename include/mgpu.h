@@ -383,9 +383,10 @@ typedef struct {
                                    with the one-sided bound change from the
                                    last strong-branching basis; counted in
                                    nodes and ndec[0] once more)           */
-  long long pfi_pivots;         /* node-LP pivots run by the product-form
-                                   kernel itself (K3P / K3PW: at most its
-                                   eta cap per LP; 0 for dense kernels)   */
+  long long pfi_pivots;         /* node-LP pivots run by K3P itself (its
+                                   own counter: warm-start column
+                                   replacements are not pivots; 0 for K3PW
+                                   and the dense kernels)                 */
 } mgpu_bnb_stats;
 
 /* Search options of the next mgpu_bnb_init (default 0, 0):

@@ -801,6 +801,7 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   // the shared-root-basis node LPs ran the product form (K3P / K3PW) when the
   // context selects it; per-node bases (warm 1, reliability) run K3 / K3L
   io.pfi_cap = ((s.warm == 0 || s.warm == 2) && !s.rel && s.root_ok) ? mgpu_lp_pfi_cap(c) : 0;
+  io.pfi_piv = io.pfi_cap > 0 && c->last_lp_pfi ? c->pfi_piv.as<unsigned long long>() : nullptr;
   io.cand_obj = s.cand.as<double>();
   io.obj = s.obj.as<double>();
   io.bvar = s.bvar.as<int32_t>();

@@ -48,11 +48,9 @@ __global__ __launch_bounds__(kScanBlock) void bnb_scan_block(BnbIO io) {
   const bool lp = live && io.status[i] != 12;
   s_cnt[t][5] = lp ? 1 : 0;
   s_cnt[t][6] = lp ? io.iters[i] : 0;
-  // pivots the product-form kernel ran itself (an overflowing LP's first
-  // pfi_cap - k pivots after its k warm-start etas; the rest ran in the
-  // dense continuation)
-  const int kin = (lp && io.kin != nullptr) ? io.kin[i] : 0;
-  s_cnt[t][7] = lp ? min(io.iters[i], max(io.pfi_cap - kin, 0)) : 0;
+  // (slot 7 unused: the pivots the product-form kernel ran itself come from
+  // its own counter, BnbIO::pfi_piv)
+  s_cnt[t][7] = 0;
   __syncthreads();
   // Hillis-Steele inclusive scan of the flags
   for (int o = 1; o < kScanBlock; o <<= 1) {
@@ -142,8 +140,11 @@ __global__ __launch_bounds__(1024) void bnb_scan_top(BnbIO io, int nblk) {
                         (unsigned long long)cnt[5]);
   if (cnt[6]) atomicAdd(reinterpret_cast<unsigned long long *>(&io.out->pivots),
                         (unsigned long long)cnt[6]);
-  if (cnt[7]) atomicAdd(reinterpret_cast<unsigned long long *>(&io.out->pfi_pivots),
-                        (unsigned long long)cnt[7]);
+  // the product-form kernel's own pivots (K3P counts them: a basis warm
+  // start's column replacements are not pivots, a reinversion keeps going,
+  // an overflowing LP's later pivots ran in the dense continuation)
+  if (t == 0 && io.pfi_piv != nullptr)
+    io.out->pfi_pivots = (long long)*io.pfi_piv;
   if (t == 0) {
     io.out->nchild = s_carry;
     io.out->best = s_min[0];

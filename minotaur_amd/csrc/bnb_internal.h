@@ -58,6 +58,7 @@ struct BnbIO {
   const int32_t *status;        // [nb] LP status (12 = not solved: FBBT-infeasible)
   const int32_t *iters;         // [nb] LP pivots
   int pfi_cap;                  // product-form eta cap of the round's LP call (0: dense)
+  const unsigned long long *pfi_piv;   // K3P's pivot counter of that call (null: none)
   const int32_t *kin;           // warm 2: each node's warm-start eta count (batch-indexed)
   const double *cand_obj;       // [nb]
   const double *obj;            // [nb] relaxation values (children's bound)

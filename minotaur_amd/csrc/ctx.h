@@ -82,6 +82,7 @@ struct mgpu_ctx {
   DevBuf pfi_ovf;              // K3P: overflow counter + node list
   DevBuf pfi_cont;             // K3P: continuation state of overflowing LPs
   DevBuf pfi_t0;               // K3P: B0^{-1} a_q of every column [N][m]
+  DevBuf pfi_piv;              // K3P: pivots of the last product-form call (u64)
   int num_cus = 256;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr,
             ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;

@@ -34,6 +34,8 @@
 // Arithmetic: oracle/lp_dual.c in product-form mode (dual_simplex_impl with
 // pfi > 0: pfi_btran, ftran_col, pfi_apply_etas, compute_primals), loop for
 // loop, so the GPU follows the oracle pivot for pivot (tests/test_lp_pfi_gpu.py).
+#include <type_traits>
+
 #include "mgpu_internal.h"
 #include "wave.h"
 
@@ -88,6 +90,7 @@ enum : int { ST_LB = 0, ST_UB = 1, ST_FREE = 2, ST_BASIC = 3 };
 constexpr int kArtLo = 4, kArtHi = 8, kFixed = 16;
 
 static_assert(kPfiBig < 64, "K3P never reaches K3's 64-pivot primal refresh");
+// (a reinversion is taken only while the refresh stays out of reach, below)
 constexpr int kPfiSmall = 16;   // the 16-eta build (4 waves per SIMD)
 
 __host__ __device__ constexpr size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
@@ -376,6 +379,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
 
   // persistent waves over nodes (no workgroup barrier below this point)
   PSTAMP_DECL
+  unsigned long long wave_piv = 0;   // pivots this wave ran (PfiIO::pivots)
   // Nodes are taken from a device counter: a wave that finishes early takes
   // the next node, so the kernel ends with the last node, not with the wave
   // that drew the longest static share (pivot counts range 0..24+).
@@ -448,37 +452,36 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     int prow = 0;  // lane t: pivot row of eta t
     int ne = 0;    // eta columns: the warm start's column replacements, then this solve's
 
-    // ---- basis rows: head, the warm start's column replacements, bounds
-    // (basic columns carry no artificial box)
+    // Column replacement with partial pivoting (oracle colrep_basis), from
+    // the shared basis (head s_whead, no etas): the shared basis's columns
+    // that are nonbasic in the target basis free their rows (freem); each
+    // listed column q = colq(i), ascending (FTRAN through B0^{-1} and the etas
+    // so far) takes the free row with the largest |alpha| (lowest row on
+    // ties) and becomes an eta exactly as a pivot on it would.  kRG columns
+    // at a time: the etas of the earlier groups go into them as kRG
+    // independent chains (apply_etas_n); inside the group each new eta is
+    // applied to the group's later columns, so every column sees the
+    // operations of one apply_etas call in order.  false: no usable pivot
+    // (< kColrepTol) for some column.  Used by the basis warm start and by
+    // the reinversion when the eta file is full.
     int h = lane < m ? s_whead[lane] : -1;
-    if (kpath > 0) {
-      // Column replacement with partial pivoting (oracle colrep_basis): the
-      // root's basic columns that are nonbasic in the node free their rows;
-      // each entering column q (FTRAN through B0^{-1} and the etas so far)
-      // takes the free row with the largest |alpha| (lowest row on ties) and
-      // becomes an eta exactly as a pivot on it would.  kRG columns at a
-      // time: the etas of the earlier groups go into them as kRG independent
-      // chains (apply_etas_n); inside the group each new eta is applied to
-      // the group's later columns, so every column sees the operations of
-      // one apply_etas call in order.  No usable pivot (< kColrepTol): the
-      // shared basis instead.
-      uint64_t freem = __ballot(lane < m && pst[h] != ST_BASIC);
+    auto colrep = [&](int k, uint64_t freem, auto colq, auto group) -> bool {
+      constexpr int kRG = decltype(group)::value;
       bool ok = true;
-      constexpr int kRG = 4;
 #pragma unroll 1
-      for (int g = 0; g < kpath && ok; g += kRG) {
+      for (int g = 0; g < k && ok; g += kRG) {
         double v[kRG];
         int qg[kRG];
 #pragma unroll
         for (int i = 0; i < kRG; ++i) {
-          const bool in = g + i < kpath;  // wave-uniform
-          qg[i] = in ? (int)(ppath[g + i] & 0xFFFFu) : 0;
+          const bool in = g + i < k;  // wave-uniform
+          qg[i] = in ? colq(g + i) : 0;
           v[i] = in ? ftran_col0(P, px.t0, qg[i], lane) : 0.0;
         }
         apply_etas_n(v, eta, prow, g, lane);
 #pragma unroll
         for (int i = 0; i < kRG; ++i) {
-          if (ok && g + i < kpath) {
+          if (ok && g + i < k) {
             const int s = g + i, q = qg[i];
             double best = ((freem >> lane) & 1ull) ? fabs(v[i]) : 0.0;
             const int r = wave_argmax_lane(best);
@@ -503,7 +506,15 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
           }
         }
       }
-      if (ok) {
+      return ok;
+    };
+
+    // ---- basis rows: head, the warm start's column replacements, bounds
+    // (basic columns carry no artificial box)
+    if (kpath > 0) {
+      const uint64_t freem = __ballot(lane < m && pst[h] != ST_BASIC);
+      if (colrep(kpath, freem, [&](int i) { return (int)(ppath[i] & 0xFFFFu); },
+                 std::integral_constant<int, 4>())) {
         ne = kpath;
       } else {  // the shared basis, its statuses and reduced costs
         kpath = 0;
@@ -726,7 +737,76 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         status = 6;
         break;
       }
-      if (ne >= kmax) {  // eta file full: the dense K3 continues this node
+      if (ne >= kmax) {
+        // eta file full.  Reinversion (oracle: the same rule): the current
+        // basis rebuilt as column replacements on B0 -- its basic columns
+        // outside the shared basis, ascending, exactly as a basis warm start
+        // -- when that difference leaves a quarter of the file free and the
+        // solve stays short of the 64-pivot primal refresh; the primal values
+        // are then recomputed, the reduced costs kept.  Otherwise (or for
+        // bound LPs, whose reduced costs are rebuilt per objective) the dense
+        // K3 continues this node from its basis and explicit inverse.
+        bool again = false;
+        if (io.ws.d != nullptr) {
+          uint64_t bm[S], nrm[S];
+          int kb = 0;
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const int j = s * 64 + lane;
+            bm[s] = __ballot(j < N && (sa[s] & 3) == ST_BASIC);
+            nrm[s] = bm[s] & ~__ballot(j < N && s_wst[j] == ST_BASIC);
+            kb += __popcll(nrm[s]);
+          }
+          const int room = kmax / 4 > 1 ? kmax / 4 : 1;
+          if (kb <= kmax - room && iters + (kmax - kb) < 64) {
+            // the listed columns into the (free) rho slice, ascending
+            int *cl = reinterpret_cast<int *>(rho);
+            int base = 0;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+              if ((nrm[s] >> lane) & 1ull)
+                cl[base + __popcll(nrm[s] & ((1ull << lane) - 1ull))] = s * 64 + lane;
+              base += __popcll(nrm[s]);
+            }
+            wave_sync();
+            // rows whose shared-basis column is nonbasic now are free
+            const int hc = lane < m ? s_whead[lane] : 0;
+            bool bnow = false;
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+              if ((hc >> 6) == s) bnow = ((bm[s] >> (hc & 63)) & 1ull) != 0;
+            const uint64_t freem = __ballot(lane < m && !bnow);
+            h = lane < m ? s_whead[lane] : -1;
+            ne = 0;
+            // (one column at a time: the main loop's state is live here)
+            if (colrep(kb, freem, [&](int i) { return cl[i]; },
+                       std::integral_constant<int, 1>())) {
+              ne = kb;
+              if (lane < m) {
+                lbB = lo[h];
+                ubB = hi[h];
+              }
+              again = true;
+            } else {
+              // no usable pivot: the dense continuation restarts from the
+              // shared basis (head, statuses, reduced costs), the pivots counted
+              h = lane < m ? s_whead[lane] : -1;
+#pragma unroll
+              for (int s = 0; s < S; ++s) {
+                const int j = s * 64 + lane;
+                if (j < N) {
+                  sa[s] = s_wst[j];
+                  d[s] = s_wst[j] == ST_BASIC ? 0.0 : s_wd[j];
+                }
+              }
+            }
+            wave_sync();
+          }
+        }
+        if (again) {
+          need = true;
+          continue;
+        }
         status = -1;
         break;
       }
@@ -868,6 +948,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       PSTAMP(7);
     }
 
+    wave_piv += (unsigned long long)iters;   // this kernel's own pivots
     // ---- outputs ----
     if (status == -1) {
       // overflow: take a list slot; within the slot capacity, hand K3 this
@@ -964,6 +1045,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     wave_sync();
     PSTAMP(8);
   }
+  if (lane0 == 0 && px.pivots != nullptr && wave_piv != 0) atomicAdd(px.pivots, wave_piv);
   PSTAMP_FLUSH
 }
 

@@ -202,6 +202,9 @@ struct PfiIO {
   // FTRAN through B0^{-1} (the warm start's column replacements, each
   // pivot's entering column) is one coalesced load (null: computed in place)
   const double *t0;
+  // pivots the product-form kernel ran itself, summed over the launch (K3P;
+  // null: not counted): the dense continuation's pivots are not in it
+  unsigned long long *pivots;
 };
 // B0^{-1} a_q for every column into t0 [N][m] (K3P's ftran_b0, bit for bit)
 hipError_t launch_pfi_t0(const DevLP &lp, const double *binv, double *t0, hipStream_t stream);

@@ -64,7 +64,7 @@ int mgpu_destroy(mgpu_ctx *c) {
                     &c->lp_ost, &c->lp_od, &c->lp_ob, &c->lp_slots, &c->io_lb_in,
                     &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
                     &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch,
-                    &c->fbbt_next, &c->nr_map, &c->nr_ws, &c->nr_vals})
+                    &c->fbbt_next, &c->nr_map, &c->nr_ws, &c->nr_vals, &c->pfi_piv})
     b->release();
   for (auto &ch : c->ws_chunks)
     if (ch.base) (void)hipFree(ch.base);
@@ -651,6 +651,9 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     HIPCHK(c, hipMemsetAsync(cnt, 0, 4 * sizeof(int32_t), c->stream));
     PfiIO px{};
     px.kmax = kcap;
+    HIPCHK(c, c->pfi_piv.ensure(sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(c->pfi_piv.p, 0, sizeof(unsigned long long), c->stream));
+    px.pivots = wide ? nullptr : c->pfi_piv.as<unsigned long long>();
     px.ovf_count = cnt;
     px.next = cnt + 1;
     px.ovf_list = cnt + 4;

@@ -386,6 +386,46 @@ static int colrep_basis(lpw *W, const orc_path *path) {
   return ok;
 }
 
+/* K3P's reinversion when the eta file is full (lp_pfi.hip, the same rule):
+ * the current basis as column replacements on B0 -- its basic columns
+ * outside B0 in ascending order, from B0's head, exactly as a basis warm
+ * start (colrep_basis) -- when that difference kb leaves a quarter of the
+ * file free (kb <= pfi - max(1, pfi / 4)) and pivots + (pfi - kb) < 64 (the
+ * product form never reaches the 64-pivot refresh).  Returns 1 when the etas
+ * were rebuilt; 0 with the state untouched when the rule declines; -1 after
+ * a failed replacement (no usable pivot) with the SHARED basis in place
+ * (B0's head, the shared statuses and reduced costs): the dense
+ * continuation then restarts from it, the pivots so far counted. */
+static int reinvert(lpw *W, const int *hroot, const unsigned char *rootb,
+                    const signed char *ws_st, const double *ws_d, int iters) {
+  int m = W->P->m, N = W->N, kb = 0;
+  int room = W->pfi / 4 > 1 ? W->pfi / 4 : 1;
+  for (int j = 0; j < N; ++j) kb += W->st[j] == ST_BASIC && !rootb[j];
+  if (kb > W->pfi - room || iters + (W->pfi - kb) >= 64) return 0;
+  unsigned *cols = (unsigned *) malloc(sizeof(unsigned) * (size_t) (kb + 1));
+  signed char *stc = (signed char *) malloc((size_t) N);
+  for (int j = 0, t = 0; j < N; ++j) {
+    stc[j] = W->st[j];
+    if (W->st[j] == ST_BASIC && !rootb[j]) cols[t++] = (unsigned) j;
+  }
+  orc_path tp;
+  memset(&tp, 0, sizeof tp);
+  tp.k = kb;
+  tp.path = cols;
+  tp.st = stc;
+  memcpy(W->head, hroot, sizeof(int) * (size_t) m);
+  W->neta = 0;
+  int ok = colrep_basis(W, &tp) ? 1 : -1;
+  if (ok < 0) {   /* the shared basis (colrep_basis restored B0's head) */
+    for (int j = 0; j < N; ++j) W->st[j] = ws_st[j] == ST_BASIC ? ST_LB : ws_st[j];
+    for (int i = 0; i < m; ++i) W->st[W->head[i]] = ST_BASIC;
+    for (int j = 0; j < N; ++j) W->d[j] = W->st[j] == ST_BASIC ? 0.0 : ws_d[j];
+  }
+  free(cols);
+  free(stc);
+  return ok;
+}
+
 static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub,
                              int *ws_head, signed char *ws_st, double *ws_binv, double *ws_d,
                              int have_ws, int have_binv, int iter_limit, double *obj_out,
@@ -397,6 +437,7 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
   int status = 12, iters = 0, fresh = 1;
   double art_bound = ART_BOUND;
   unsigned char *rootb = 0;   /* basis warm start output: basic in B0 */
+  int *hroot = 0;             /* product form: B0's head */
   memset(&W, 0, sizeof W);
   W.P = P; W.N = N; W.lb = lb; W.ub = ub;
   if (pfi > 0 && have_ws && have_binv) {
@@ -448,9 +489,13 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
     for (int i = 0; i < m * m; ++i) W.binv[i] = 0.0;
     for (int i = 0; i < m; ++i) W.binv[i * m + i] = -1.0;
   }
-  if (path && path->k_out) {
+  if ((path && path->k_out) || W.pfi) {
     rootb = (unsigned char *) calloc((size_t) N, 1);
     for (int i = 0; i < m; ++i) rootb[W.head[i]] = 1;
+  }
+  if (W.pfi) {   /* the shared basis's head, for a reinversion */
+    hroot = (int *) malloc(sizeof(int) * (size_t) m + 4);
+    memcpy(hroot, W.head, sizeof(int) * (size_t) m);
   }
   if (path && path->k > 0 && W.pfi && g_path_pivots) {
     /* pivot path: replay each pivot on the root basis (FTRAN of its entering
@@ -537,7 +582,20 @@ static int dual_simplex_impl(const orc_lp *P, const double *lb, const double *ub
       continue;
     }
     if (iters >= iter_limit) { status = 6; break; }   /* EngineIterationLimit */
-    if (W.pfi && W.neta >= W.pfi) {
+    int to_dense = 0;
+    if (W.pfi && W.neta >= W.pfi && ws_d && m <= 64) {
+      /* K3P's reinversion: the eta file rebuilt from B0, primal values
+       * recomputed, reduced costs kept (-1: failed, the shared basis in
+       * place for the dense continuation) */
+      const int re = reinvert(&W, hroot, rootb, ws_st, ws_d, iters);
+      if (re > 0) {
+        compute_primals(&W);
+        fresh = 1;
+        continue;
+      }
+      to_dense = re < 0;
+    }
+    if (W.pfi && (W.neta >= W.pfi || to_dense)) {
       /* eta file full: the dense solve continues from this basis with its
        * explicit inverse E_{k-1}...E_0 B0^{-1}, column by column */
       for (int c = 0; c < m; ++c) {
@@ -701,6 +759,7 @@ done:
     if (ko) for (int j = 0; j < N; ++j) path->st_out[j] = W.st[j];
   }
   free(rootb);
+  free(hroot);
   free(W.blo); free(W.bhi); free(W.art); free(W.z); free(W.d); free(W.binv);
   free(W.head); free(W.st); free(W.rho); free(W.w); free(W.alpha_r); free(W.alpha_q);
   free(W.eta); free(W.prow); free(W.pq); free(W.u);
