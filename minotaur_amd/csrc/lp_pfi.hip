@@ -104,8 +104,11 @@ __host__ __device__ inline size_t pfi_shared_bytes(int n, int m, int nnz) {
          al16((size_t)m * (m + 1) * 8) + al16((size_t)N * 8) + al16((size_t)N * 4) +
          al16((size_t)m * 4) + al16((size_t)n * 4) + al16((size_t)n * 8) + 16;
 }
-// per wave: rho [64] + column values, lower and upper working bounds [N]
-__host__ __device__ inline size_t pfi_wave_bytes(int N) { return 64 * 8 + 3 * al16((size_t)N * 8); }
+// per wave: rho [64] + column values, lower and upper working bounds [N],
+// a node pair's reduced costs [N] and head [64]
+__host__ __device__ inline size_t pfi_wave_bytes(int N) {
+  return 64 * 8 + 4 * al16((size_t)N * 8) + 64 * 4;
+}
 
 __device__ __forceinline__ double art_lo(double thi, double ab) {
   return (thi < kInfB ? thi : 0.0) - ab;
@@ -376,6 +379,8 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
   double *zc = rho + 64;   // value of each nonbasic column, 0 for basic ones
   double *lo = zc + Np;    // working bounds (artificial where marked)
   double *hi = lo + Np;
+  double *sib_d = hi + Np;                            // a pair's shared reduced costs
+  int *sib_h = reinterpret_cast<int *>(sib_d + Np);   // and basis head [64]
 
   // persistent waves over nodes (no workgroup barrier below this point)
   PSTAMP_DECL
@@ -383,13 +388,30 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
   // Nodes are taken from a device counter: a wave that finishes early takes
   // the next node, so the kernel ends with the last node, not with the wave
   // that drew the longest static share (pivot counts range 0..24+).
+  //
+  // Nodes come in PAIRS (2p, 2p + 1): the batched tree pops children pairs
+  // that start from the same parent basis, and the column replacements of a
+  // basis warm start and the reduced costs they give depend on the basis
+  // alone, so the second node of a pair with the first's basis reuses them
+  // (eta columns [0, k) stay intact under the first node's pivots; head and
+  // reduced costs are kept in the wave's LDS slice).  The same operations,
+  // so the same bits as computing them again.
+  double eta[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) eta[t] = 0.0;
+  int prow = 0;      // lane t: pivot row of eta t
+  int sib = -1;      // the node whose column replacements eta [0, ksib) hold
+  int ksib = 0;
   for (;;) {
-    int b = 0;
-    if (lane0 == 0) b = atomicAdd(px.next, 1);
-    b = __builtin_amdgcn_readfirstlane(b);
-    if (b >= io.batch) break;
+    int pr = 0;
+    if (lane0 == 0) pr = atomicAdd(px.next, 1);
+    pr = __builtin_amdgcn_readfirstlane(pr);
+    if (2 * pr >= io.batch) break;
+  for (int b = 2 * pr; b < 2 * pr + 2 && b < io.batch; ++b) {
     int lane = lane0;
     asm volatile("" : "+v"(lane));
+    const int prev_sib = sib;   // reusable by this node only
+    sib = -1;
     P.nlb = io.lb + (size_t)b * io.box_stride;
     P.nub = io.ub + (size_t)b * io.box_stride;
     P.ocol = io.obj_col != nullptr ? io.obj_col[b] : -1;
@@ -446,10 +468,6 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     }
     wave_sync();
 
-    double eta[K];
-#pragma unroll
-    for (int t = 0; t < K; ++t) eta[t] = 0.0;
-    int prow = 0;  // lane t: pivot row of eta t
     int ne = 0;    // eta columns: the warm start's column replacements, then this solve's
 
     // Column replacement with partial pivoting (oracle colrep_basis), from
@@ -511,11 +529,31 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
 
     // ---- basis rows: head, the warm start's column replacements, bounds
     // (basic columns carry no artificial box)
-    if (kpath > 0) {
+    bool reuse = false;
+    if (kpath > 0 && prev_sib == b - 1 && ksib == kpath) {
+      // the previous node's basis?  (path columns and statuses equal)
+      const uint32_t *pp1 = ppath - kPathMax;
+      const int8_t *ps1 = pst - N;
+      bool diff = lane < kpath && ppath[lane] != pp1[lane];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = s * 64 + lane;
+        diff |= j < N && pst[j] != ps1[j];
+      }
+      reuse = !__any(diff);
+    }
+    if (reuse) {
+      ne = kpath;
+      h = lane < m ? sib_h[lane] : -1;
+      sib = b;
+    } else if (kpath > 0) {
       const uint64_t freem = __ballot(lane < m && pst[h] != ST_BASIC);
       if (colrep(kpath, freem, [&](int i) { return (int)(ppath[i] & 0xFFFFu); },
                  std::integral_constant<int, 4>())) {
         ne = kpath;
+        if (lane < m) sib_h[lane] = h;
+        sib = b;
+        ksib = kpath;
       } else {  // the shared basis, its statuses and reduced costs
         kpath = 0;
         h = lane < m ? s_whead[lane] : -1;
@@ -533,7 +571,13 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       ubB = hi[h];
     }
     double d[S];
-    if (kpath > 0) {
+    if (reuse) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = s * 64 + lane;
+        d[s] = j < N ? sib_d[j] : 0.0;
+      }
+    } else if (kpath > 0) {
       // reduced costs of the path's basis (oracle pfi_compute_duals): u = c_B
       // through the etas backwards (BTRAN), rho = u' B0^{-1}, d = c - rho' A
       double u = (lane < m && h < n) ? P.c[h] : 0.0;
@@ -546,6 +590,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         d[s] = 0.0;
         if (j < N && sa[s] != ST_BASIC)
           d[s] = (j < n ? P.c[j] : 0.0) - (j >= n ? -rho[j - n] : P.col_dot(rho, j));
+        if (j < N) sib_d[j] = d[s];
       }
       wave_sync();
       PSTAMP(11);
@@ -778,6 +823,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
             const uint64_t freem = __ballot(lane < m && !bnow);
             h = lane < m ? s_whead[lane] : -1;
             ne = 0;
+            sib = -1;   // the column replacements are gone
             // (one column at a time: the main loop's state is live here)
             if (colrep(kb, freem, [&](int i) { return cl[i]; },
                        std::integral_constant<int, 1>())) {
@@ -1044,6 +1090,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     }
     wave_sync();
     PSTAMP(8);
+  }
   }
   if (lane0 == 0 && px.pivots != nullptr && wave_piv != 0) atomicAdd(px.pivots, wave_piv);
   PSTAMP_FLUSH
