@@ -227,7 +227,7 @@ def tree_cpu_baseline(p, brancher, seconds):
             "solved": done, "ub": float(res[0])}
 
 
-def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None):
+def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None, growth=0):
     """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
     across ranks after the shared first rounds: one packed all-reduce per
     round (incumbent MIN + open counts), open nodes rebalanced every 8 rounds
@@ -248,7 +248,7 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=No
     # whose later widths differ between runs could still grow a buffer: the
     # check then fails loudly instead of timing it.)
     bnb.solve_distributed(ctx, B, rank, world, capacity=cap, order=order, warm=warm,
-                          comm=comm, lb_every=8, brancher=brancher)
+                          comm=comm, lb_every=8, brancher=brancher, growth=growth)
     comm.barrier()
     torch.cuda.synchronize()
     a0 = alloc_stats()
@@ -256,7 +256,8 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=No
     tr = []
     inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=cap,
                                                      order=order, warm=warm, comm=comm,
-                                                     lb_every=8, brancher=brancher, trace=tr)
+                                                     lb_every=8, brancher=brancher, trace=tr,
+                                                     growth=growth)
     torch.cuda.synchronize()
     a1 = alloc_stats()
     if a1 != a0:
@@ -276,20 +277,24 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=No
 # its linear rows alone (tls4-lin, trivial: LP bound = optimum 0), config 1's
 # OA-LP, and a weak-bound MILP whose tree is large enough to time the
 # driver's throughput (multi-dimensional knapsack n = 60, m = 8).
-# (name, kind, order, warm, optimum, brancher): brancher 1 = the reference's
-# default ReliabilityBrancher (strong-branching LPs count as relaxations).
-TREES = [("tls4_oa", "instance", 0, 0, 3.2, 0),
-         ("tls4_oa", "instance", 0, 2, 3.2, 0),
-         ("tls4_oa", "instance", 1, 0, 3.2, 0),
-         ("tls4_oa", "instance", 1, 1, 3.2, 0),
-         ("tls4_oa", "instance", 1, 2, 3.2, 0),
-         ("tls4_oa", "instance", 1, 0, 3.2, 1),
-         ("tls4_lin", "instance", 1, 0, 0.0, 1),
-         ("nvs08_oa", "instance", 1, 0, None, 0),
-         ("mkp-1-n60-m8", "mkp", 0, 0, -1915.0, 0),
-         ("mkp-1-n60-m8", "mkp", 1, 0, -1915.0, 0),
-         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0, 0),
-         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0, 1)]
+# (name, kind, order, warm, optimum, brancher, growth): brancher 1 = the
+# reference's default ReliabilityBrancher (strong-branching LPs count as
+# relaxations); growth 2 (mgpu_bnb_growth): rounds of at most half the nodes
+# evaluated so far, so the reliability brancher's decisions rest on earlier
+# rounds' pseudocosts (a fixed wide batch grew tls4-OA's tree to 4.9x the
+# reference's)
+TREES = [("tls4_oa", "instance", 0, 0, 3.2, 0, 0),
+         ("tls4_oa", "instance", 0, 2, 3.2, 0, 0),
+         ("tls4_oa", "instance", 1, 0, 3.2, 0, 0),
+         ("tls4_oa", "instance", 1, 1, 3.2, 0, 0),
+         ("tls4_oa", "instance", 1, 2, 3.2, 0, 0),
+         ("tls4_oa", "instance", 1, 1, 3.2, 1, 2),
+         ("tls4_lin", "instance", 1, 1, 0.0, 1, 2),
+         ("nvs08_oa", "instance", 1, 0, None, 0, 0),
+         ("mkp-1-n60-m8", "mkp", 0, 0, -1915.0, 0, 0),
+         ("mkp-1-n60-m8", "mkp", 1, 0, -1915.0, 0, 0),
+         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0, 0, 0),
+         ("mkp-1-n60-m8", "mkp", 1, 1, -1915.0, 1, 2)]
 
 
 def tree_search(ctx, dev, rank, world, B, args):
@@ -299,7 +304,7 @@ def tree_search(ctx, dev, rank, world, B, args):
     from minotaur_amd.problem import LinProblem, random_mkp
     out = []
     cpu_trees = {}
-    for name, kind, order, warm, opt, br in TREES:
+    for name, kind, order, warm, opt, br, grow in TREES:
         if kind == "mkp":
             p = random_mkp(1, 60, 8)
         else:
@@ -312,7 +317,7 @@ def tree_search(ctx, dev, rank, world, B, args):
         # 32 KB for tls4-oa), so those pools are sized to the tree
         cap = 1 << 19 if warm and p.m > 16 else 1 << 23
         inc, nodes, lps, piv, pruned, rounds, el, moved, sbl, sbp = run_tree(
-            ctx, dev, rank, world, p, B, order, warm, cap, br)
+            ctx, dev, rank, world, p, B, order, warm, cap, br, growth=grow)
         progress(rank, f"tree {p.name} order {order} warm {warm} brancher {br}: "
                        f"{nodes:.0f} nodes in {el:.2f}s")
         out.append({"instance": p.name, "vars": p.n, "rows": p.m,
@@ -321,7 +326,8 @@ def tree_search(ctx, dev, rank, world, B, args):
                                ", parent-basis warm starts" if warm else
                                ", root-basis warm start") +
                               (", reliability branching (strong branching + pseudocosts)"
-                               if br else ", MaxVio branching"),
+                               if br else ", MaxVio branching") +
+                              (f", batch growth {grow}" if grow else ""),
                     "nodes": nodes, "lp_solves": lps, "pivots_per_lp": piv / max(lps, 1.0),
                     "strong_branching_lps": sbl,
                     "pruned_open": pruned, "rounds": rounds, "seconds": el,
@@ -379,6 +385,34 @@ def tls4_oa_tree(ctx, dev, rank, world, args):
                                                                  "nodes", "seconds", "solved",
                                                                  "ub")}
             out["vs_reference_one_core"] = out["nodes_per_s"] / max(c1["value"], 1e-9)
+    return out
+
+
+def tls4_oa_rel_tree(ctx, dev, rank, world, args):
+    """Config 2's tree with the reference's DEFAULT brancher (VERDICT r04 item
+    3): reliability branching (Environment.cpp:574-576 sets "rel"), best-
+    first, parent-basis warm starts, batch growth 2 -- its node count and
+    time to proof (the whole tree: the optimum proven) next to the
+    reference's own BranchAndBound + ReliabilityBrancher on one core
+    (oracle/_ref, LP restatement behind CpuLPEngine)."""
+    from minotaur_amd.problem import LinProblem
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
+    B = args.tree_batch
+    inc, nodes, lps, piv, pruned, rounds, el, moved, sbl, sbp = run_tree(
+        ctx, dev, rank, world, p, B, 1, 1, 1 << 20, 1, growth=2)
+    out = {"instance": f"tls4-oa ({p.m} rows, {p.n} cols)", "batch_cap_per_gpu": B,
+           "search": "best-first, reliability branching (strong branching + pseudocosts), "
+                     "parent-basis warm starts, batch growth 2",
+           "nodes": nodes, "rounds": rounds, "lp_solves": lps, "strong_branching_lps": sbl,
+           "time_to_proof_s": el, "optimum": inc,
+           "optimum_matches_highs": bool(abs(inc - 3.2) <= 1e-6 * 3.2)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        c1 = tree_cpu_baseline(p, 1, 4 * args.tree_cpu_seconds)
+        if c1 is not None:
+            out["reference_one_core"] = {"nodes": c1["nodes"], "seconds": c1["seconds"],
+                                         "solved": c1["solved"], "ub": c1["ub"]}
+            out["nodes_vs_reference"] = nodes / max(c1["nodes"], 1)
+            out["time_to_proof_speedup"] = c1["seconds"] / max(el, 1e-9)
     return out
 
 
@@ -893,7 +927,7 @@ LINE_MAX = 6000   # the driver keeps the tail of stdout: the line must stay shor
 
 
 def compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, cpu, oa_tree,
-                 supp, supp_path):
+                 supp, supp_path, rel_tree=None):
     """The ONE stdout JSON line (< 6 KB so the driver's
     stdout tail holds it whole): the metric, the roofline of the dominant
     kernel, the CPU baselines, config 2's complete tree and one number per
@@ -969,6 +1003,9 @@ def compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, c
         "kernels": ks,
         "cpu_baseline": cb,
         "tls4_oa_tree": oa,
+        "tls4_oa_rel_tree": ({k: (_r(v) if isinstance(v, float) else v)
+                              for k, v in rel_tree.items() if k not in ("instance", "search")}
+                             if rel_tree else None),
         "supplementary": {
             "file": supp_path,
             "fixed_batch_nodes_per_s": rate("fixed_batch"),
@@ -984,7 +1021,7 @@ def compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, c
         },
     }
     # keep the line under the driver's limit whatever the supplementary holds
-    for drop in ("supplementary", "tree_rounds", "tls4_oa_tree"):
+    for drop in ("supplementary", "tree_rounds", "tls4_oa_rel_tree", "tls4_oa_tree"):
         if len(json.dumps(line)) <= LINE_MAX:
             break
         line[drop] = "see " + str(supp_path)
@@ -1123,6 +1160,8 @@ def main():
     TB = args.tree_batch
     oa_tree = {} if args.no_oa_tree else tls4_oa_tree(ctx, dev, rank, world, args)
     progress(rank, f"tls4_oa_tree done: {oa_tree.get('nodes_per_s', 0.0) / 1e6:.2f} M nodes/s")
+    rel_tree = {} if args.no_oa_tree else tls4_oa_rel_tree(ctx, dev, rank, world, args)
+    progress(rank, f"tls4_oa_rel_tree done: {rel_tree}")
     supp = {}
     for key, skip, fn in (
             ("fixed_batch", args.no_fixed, lambda: fixed_batch(ctx, dev, rank, world, args)),
@@ -1157,7 +1196,8 @@ def main():
             # the same instance's tree on one core by the reference's own
             # BranchAndBound (nodes/s like value; not the same node boxes)
             cpu["reference_tree_one_core"] = tree_cpu_baseline(p, 0, 2 * args.tree_cpu_seconds)
-        full = {"headline_kernels": kernels, "cpu_baseline": cpu, "tls4_oa_tree": oa_tree}
+        full = {"headline_kernels": kernels, "cpu_baseline": cpu, "tls4_oa_tree": oa_tree,
+                "tls4_oa_rel_tree": rel_tree}
         full.update(supp)
         supp_path = os.path.abspath(args.supp_out)
         try:
@@ -1167,7 +1207,7 @@ def main():
         except OSError as e:
             supp_path = f"not written ({e})"
         line = compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, cpu,
-                            oa_tree, supp, supp_path)
+                            oa_tree, supp, supp_path, rel_tree)
         if rehearse:
             line["rehearsal"] = "all ranks on device 0 over gloo (not a scaling number)"
         print(json.dumps(line), flush=True)

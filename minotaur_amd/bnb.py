@@ -16,14 +16,16 @@ import time
 
 
 def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
-          root_lb=None, root_ub=None, order=0, warm=0, brancher=0):
+          root_lb=None, root_ub=None, order=0, warm=0, brancher=0, growth=0):
     """Tree search on the loaded LinProblem: returns (obj, x, stats, seconds).
     order 0 depth-first / 1 best-first; warm 0 root basis / 1 parent basis
-    (mgpu_bnb_config); brancher 0 MaxVio / 1 reliability (mgpu_bnb_brancher)."""
+    (mgpu_bnb_config); brancher 0 MaxVio / 1 reliability (mgpu_bnb_brancher);
+    growth > 0: rounds of at most nodes-so-far // growth (mgpu_bnb_growth)."""
     cap = capacity or 64 * batch
     t0 = time.perf_counter()
     ctx.bnb_config(order, warm)
     ctx.bnb_brancher(brancher)
+    ctx.bnb_growth(growth)
     ctx.bnb_init(cap, root_lb, root_ub, incumbent)
     st = None
     for _ in range(max_rounds):
@@ -36,7 +38,7 @@ def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
 
 def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max=None,
                       capacity=None, max_rounds=10**9, shard_at=None, order=0, warm=0,
-                      comm=None, lb_every=0, brancher=0, trace=None):
+                      comm=None, lb_every=0, brancher=0, trace=None, growth=0):
     """Node-sharded tree search.  Every rank runs the same deterministic
     rounds until the pool holds at least ``shard_at`` (default 4 * world)
     open nodes, then keeps nodes i = rank (mod world) (mgpu_bnb_shard) and
@@ -60,6 +62,7 @@ def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max
     shard_at = shard_at or 4 * world
     ctx.bnb_config(order, warm)
     ctx.bnb_brancher(brancher)
+    ctx.bnb_growth(growth)
     ctx.bnb_init(cap, None, None, math.inf)
     inc = math.inf
     sharded = world == 1

@@ -47,6 +47,7 @@ static bool heap_greater(const HeapNode &a, const HeapNode &b) {
 
 struct BnbState {
   int n = 0, cap = 0, count = 0, maxb = 0;
+  int grow = 0;                // mgpu_bnb_growth of this tree
   bool root_ok = false;
   double inc = INFINITY;
   std::vector<double> best_x;
@@ -407,6 +408,13 @@ int mgpu_bnb_relaxation(mgpu_ctx *c, int kind) {
   return MGPU_OK;
 }
 
+int mgpu_bnb_growth(mgpu_ctx *c, int div) {
+  if (!c) return MGPU_ERR_ARG;
+  if (div < 0) return fail(c, MGPU_ERR_ARG, "mgpu_bnb_growth: div must be >= 0");
+  c->bnb_grow = div;
+  return MGPU_OK;
+}
+
 int mgpu_bnb_brancher(mgpu_ctx *c, int kind) {
   if (!c) return MGPU_ERR_ARG;
   if (kind < 0 || kind > 1)
@@ -437,6 +445,7 @@ int mgpu_bnb_init(mgpu_ctx *c, int capacity, const double *root_lb, const double
   s->warm = c->bnb_warm;
   s->rel = c->bnb_brancher;
   s->qp = c->bnb_relax;
+  s->grow = c->bnb_grow;
   s->tot.incumbent = incumbent;
   if (s->qp && (!c->qp || s->warm != 0 || s->rel))
     return fail(c, MGPU_ERR_ARG, "mgpu_bnb_init: QP relaxations need mgpu_load_qp (same columns as "
@@ -575,6 +584,10 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
   BnbState &s = *c->bnb;
   HIPCHK(c, hipSetDevice(c->device));
   if (incumbent < s.inc) s.inc = incumbent;
+  if (s.grow > 0) {   // mgpu_bnb_growth: at most 1/grow of the nodes so far
+    const long long g = s.tot.nodes / s.grow;
+    if ((long long)batch > (g > 1 ? g : 1)) batch = (int)(g > 1 ? g : 1);
+  }
   const int n = s.n, m = c->lp.m, N = n + m;
   const bool bfs = s.order >= 1;      // the round's nodes are gathered from pool slots
   const bool heap = s.order == 2;

@@ -77,6 +77,7 @@ struct mgpu_ctx {
   int bnb_warm = 0;            // mgpu_bnb_config: 0 root basis, 1 parent basis
   int bnb_brancher = 0;        // mgpu_bnb_brancher: 0 MaxVio, 1 reliability
   int bnb_guided = 1;          // mgpu_bnb_guided_dive (order 2: child order by the incumbent)
+  int bnb_grow = 0;            // mgpu_bnb_growth: batch <= nodes so far / div (0: off)
   DevBuf lp_slots;             // K3L: one B^-1 [m][m] per resident workgroup
   DevBuf lp_next;              // K3L: node counter of the dynamic schedule
   DevBuf pfi_ovf;              // K3P: overflow counter + node list

@@ -45,6 +45,7 @@ EXPORTS = [
     'mgpu_comm_unique_id', 'mgpu_comm_init', 'mgpu_comm_init_host', 'mgpu_comm_info',
     'mgpu_allreduce_f64', 'mgpu_allreduce_min', 'mgpu_round_reduce', 'mgpu_allgather_f64',
     'mgpu_alltoall_rows_dev', 'mgpu_lb_deal', 'mgpu_bnb_rebalance', 'mgpu_alloc_stats',
+    'mgpu_bnb_growth',
 ]
 
 COMM_ID_BYTES = 128            # MGPU_COMM_ID_BYTES
@@ -138,6 +139,7 @@ def load_library():
     lib.mgpu_bnb_init.argtypes = [_P, _I, _P, _P, _D]
     lib.mgpu_bnb_config.argtypes = [_P, _I, _I]
     lib.mgpu_bnb_brancher.argtypes = [_P, _I]
+    lib.mgpu_bnb_growth.argtypes = [_P, _I]
     lib.mgpu_bnb_relaxation.argtypes = [_P, _I]
     lib.mgpu_bnb_guided_dive.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
@@ -692,6 +694,11 @@ class Context:
     def bnb_brancher(self, kind):
         """Next tree's brancher: 0 MaxVio, 1 reliability (mgpu_bnb_brancher)."""
         self._chk(self.lib.mgpu_bnb_brancher(self.h, int(kind)), 'mgpu_bnb_brancher')
+
+    def bnb_growth(self, div):
+        """Next tree's batch growth (mgpu_bnb_growth): a round evaluates at most
+        max(1, nodes so far // div) nodes; 0 = off."""
+        self._chk(self.lib.mgpu_bnb_growth(self.h, int(div)), 'mgpu_bnb_growth')
 
     def bnb_relaxation(self, kind):
         """Next tree's relaxation: 0 the loaded LP, 1 the loaded QP by K5

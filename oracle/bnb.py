@@ -90,12 +90,17 @@ class CpuBnbContext:
         self.pfi = pfi   # node LPs in K3P's product form (Context.oracle_pfi())
         self.order, self.warm = order, warm
         self.brancher = brancher
+        self.grow_next = 0
 
     def bnb_config(self, order=0, warm=0):
         self.order, self.warm = int(order), int(warm)
 
     def bnb_brancher(self, kind):
         self.brancher = int(kind)
+
+    def bnb_growth(self, div):
+        """mgpu_bnb_growth: rounds of at most max(1, nodes so far // div)."""
+        self.grow_next = int(div)
 
     # -- mgpu_bnb_init ------------------------------------------------------
     def bnb_init(self, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
@@ -110,6 +115,7 @@ class CpuBnbContext:
         self.best_x = np.full(p.n, np.nan)
         self.tot = _Stats()
         self.tot.incumbent = incumbent
+        self.grow = self.grow_next
         self.rel = self.brancher == 1
         if self.rel:   # ReliabilityBrancher::initialize (:384-398)
             n = p.n
@@ -143,6 +149,8 @@ class CpuBnbContext:
         p = self.problem
         if incumbent < self.inc:
             self.inc = incumbent
+        if self.grow > 0:     # mgpu_bnb_growth (bnb.cpp mgpu_bnb_round)
+            batch = min(batch, max(1, self.tot.nodes // self.grow))
         if self.order == 0:
             count = len(self.pool)
             nb = min(batch, count, self.cap - count)

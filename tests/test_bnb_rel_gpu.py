@@ -79,3 +79,38 @@ def test_rel_tls4_lin_tree(ctx):
     og, _, sg, _ = bnb.solve(ctx, batch=4096, capacity=1 << 18, order=1, brancher=1)
     assert sg.open == 0 and hs == 0
     assert abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
+
+
+@pytest.mark.parametrize('warm', [0, 1])
+def test_rel_tree_growth_tls4_oa(ctx, warm):
+    """with a fixed batch the round's nodes share one
+    pseudocost state and config 2's reliability tree grows to 4.9x the
+    reference's.  mgpu_bnb_growth 2 (a round evaluates at most half the
+    nodes evaluated so far) keeps it near the reference's own tree: the GPU
+    tree equals the CPU restatement round for round, proves HiGHS' optimum,
+    and with parent warm starts stays within 1.5x the reference
+    BranchAndBound's processed nodes (integ_bnb_tree_cpu, one core)."""
+    import os
+    from bnb import CpuBnbContext
+    from minotaur_amd.problem import LinProblem
+    root = os.path.join(os.path.dirname(__file__), '..')
+    p = LinProblem.load(os.path.join(root, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
+    hs, hobj = oracle.highs_milp(p)
+    ctx.load(p)
+    og, _, sg, _ = bnb.solve(ctx, batch=131072, capacity=1 << 20, order=1, warm=warm,
+                             brancher=1, growth=2)
+    oc, _, sc, _ = bnb.solve(CpuBnbContext(p), batch=131072, capacity=1 << 20, order=1,
+                             warm=warm, brancher=1, growth=2)
+    assert sg.open == sc.open == 0
+    assert _sig(sg) == _sig(sc) and sg.sb_pivots == sc.sb_pivots
+    assert og == oc and abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
+    if warm == 1:
+        from test_ref_tree_cpu import LIB, cpu_tree
+        if os.path.exists(LIB):
+            import ctypes
+            lib = ctypes.CDLL(LIB, mode=os.RTLD_LAZY | os.RTLD_GLOBAL)
+            lib.integ_bnb_tree_cpu.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 9 + \
+                [ctypes.c_double] * 2 + [ctypes.c_void_p] * 2
+            ref = cpu_tree(lib, p, 1)
+            assert abs(ref["ub"] - hobj) <= 1e-6 * max(1.0, abs(hobj))
+            assert sg.nodes <= 1.5 * ref["processed"], (sg.nodes, ref["processed"])

@@ -70,3 +70,27 @@ def test_cpu_reference_tree_time_limit(integ):
     p = random_mkp(1, 60, 8)
     r = cpu_tree(integ, p, 0, 1, time_limit=0.5)
     assert 0.45 <= r["seconds"] <= 1.5 and r["processed"] > 100
+
+
+def test_growth_caps_each_round():
+    """mgpu_bnb_growth restated (oracle/bnb.py): with div 2 every round
+    evaluates at most max(1, nodes so far // 2) nodes, and the tree still
+    proves HiGHS' optimum."""
+    from bnb import CpuBnbContext
+    p = random_mkp(2, 18, 3)
+    hs, hobj = oracle.highs_milp(p)
+    c = CpuBnbContext(p)
+    c.bnb_config(1, 1)
+    c.bnb_brancher(1)
+    c.bnb_growth(2)
+    c.bnb_init(1 << 14)
+    before = 0
+    while True:
+        st = c.bnb_round(4096)
+        if st.open == 0 and st.last_batch == 0:
+            break
+        assert st.last_batch <= max(1, before // 2)
+        before = st.nodes
+        if st.open == 0:
+            break
+    assert abs(c.inc - hobj) <= 1e-6 * max(1.0, abs(hobj))
