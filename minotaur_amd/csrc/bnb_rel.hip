@@ -33,10 +33,12 @@
 //                           = down first when change_up > change_down;
 //   pc_fold               : the round's observations into the pseudocosts,
 //                           per variable in node order (updatePCost_).
-// One thread per node in rel_prepare / rel_decide: the logic is a short
-// serial scan over the integer columns with data-dependent exits, not
-// arithmetic that rewards lanes.
+// One wave per node in rel_prepare / rel_decide (round 5; one thread per node
+// before): the candidate scans are wave reductions over the reference's
+// (score, index) keys, which took the per-round latency of the two kernels
+// from ~90 us each on a tree's narrow rounds.
 #include "bnb_internal.h"
+#include "wave.h"
 
 #include <climits>
 
@@ -140,8 +142,31 @@ __global__ __launch_bounds__(1024) void excl_scan(const int32_t *in, int32_t *ou
   if (t == 0) *total = carry;
 }
 
+// Lexicographic (u, j) minimum over the wave: the smallest u, the smallest j
+// among its holders (u = +INF, j = INT_MAX: no candidate).  Wave uniform.
+__device__ __forceinline__ void wave_min_key(double &u, int &j) {
+  const double mu = wave_min_dpp(u);
+  j = wave_min_i32_dpp(u == mu ? j : INT_MAX);
+  u = mu;
+}
+// (v, key u, j) maximum over the wave: the largest v, then the smallest (u, j)
+// among its holders.  v = -INF: no candidate.  Wave uniform.
+__device__ __forceinline__ void wave_max_key(double &v, double &u, int &j) {
+  const double mv = wave_max_dpp(v);
+  double uu = v == mv ? u : INFINITY;
+  int jj = v == mv ? j : INT_MAX;
+  wave_min_key(uu, jj);
+  v = mv;
+  u = uu;
+  j = jj;
+}
+
+// One wave per node: the candidates are spread over the lanes (column j of
+// lane j % 64); every selection is a wave reduction over (score, index) keys,
+// the same keys and the same order as the reference's serial scans.
 __global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
-  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= io.nb) return;
   int nsb = 0;
   if (io.decision[b] == 0) {
@@ -159,7 +184,7 @@ __global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
     for (int k = 0; k < maxcnt; ++k) {
       double bs = INFINITY;
       int bj = INT_MAX;
-      for (int j = 0; j < io.n; ++j) {
+      for (int j = lane; j < io.n; j += 64) {
         if (!is_int(io.vtype[j])) continue;
         const double v = x[j];
         if (!fractional(v)) continue;
@@ -172,16 +197,21 @@ __global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
           bj = j;
         }
       }
+      wave_min_key(bs, bj);
       if (bj == INT_MAX) break;
-      io.sb_var[(size_t)b * kRelMaxCands + k] = bj;
-      io.sb_val[(size_t)b * kRelMaxCands + k] = x[bj];
+      if (lane == 0) {
+        io.sb_var[(size_t)b * kRelMaxCands + k] = bj;
+        io.sb_val[(size_t)b * kRelMaxCands + k] = x[bj];
+      }
       ++nsb;
       ps = bs;
       pj = bj;
     }
   }
-  io.nsb[b] = nsb;
-  if (nsb > 0) atomicMax(io.nsb_max, nsb);
+  if (lane == 0) {
+    io.nsb[b] = nsb;
+    if (nsb > 0) atomicMax(io.nsb_max, nsb);
+  }
 }
 
 // one wave per strong-branching child: the node's (FBBT-tightened) box with
@@ -254,17 +284,26 @@ __device__ __forceinline__ int sb_outcome(const RelIO &io, size_t off, int k, do
   return (pu && pd) ? 1 : pu ? 2 : pd ? 3 : 0;
 }
 
+// One wave per node (as rel_prepare): the candidate scans are wave
+// reductions, the strong-branching results a uniform loop; the winner is the
+// first maximum of the reference's scan order -- reliable candidates by
+// ascending index, then the strong-branched ones, then the remaining
+// unreliable ones in CompareScore order -- which the reductions restate as
+// (score max, order key min).
 __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
-  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= io.nb) return;
   const size_t e0 = (size_t)b * kRelEvents;
   int ov = -1, os = 0, nev = 0;
   double oc = 0.0;
   const bool own = after_solve_obs(io, b, ov, os, oc);
   if (own) {  // updateAfterSolve comes first (PCBProcessor.cpp:245-248)
-    io.ev_var[e0] = ov;
-    io.ev_side[e0] = (int8_t)os;
-    io.ev_cost[e0] = oc;
+    if (lane == 0) {
+      io.ev_var[e0] = ov;
+      io.ev_side[e0] = (int8_t)os;
+      io.ev_cost[e0] = oc;
+    }
     nev = 1;
   }
   int dec = io.decision[b];
@@ -272,11 +311,11 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
     const double *x = io.x + (size_t)b * io.n;
     const long long calls = calls_of(io, b);
     const double objval = io.obj[b];
-    double best = -INFINITY;
-    int bj = -1;
-    bool down_first = false;
-    // reliable candidates, ascending index (:84-96)
-    for (int j = 0; j < io.n; ++j) {
+    // reliable candidates, ascending index (:84-96): the largest score, the
+    // lowest index on ties (a NaN score never wins a strict comparison)
+    double rs = -INFINITY, ru = 0.0;
+    int rj = INT_MAX;
+    for (int j = lane; j < io.n; j += 64) {
       if (!is_int(io.vtype[j])) continue;
       const double v = x[j];
       if (!fractional(v)) continue;
@@ -284,13 +323,24 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
       if (!reliable(io, j, calls, pv)) continue;
       const double cd = (v - floor(v)) * pv.pd, cu = (ceil(v) - v) * pv.pu;
       const double sc = rel_score(cu, cd);
-      if (sc > best) {
-        best = sc;
-        bj = j;
-        down_first = cu > cd;
+      if (sc > rs) {   // lanes visit ascending j: the first maximum
+        rs = sc;
+        rj = j;
       }
     }
-    // strong-branched candidates (:98-128)
+    wave_max_key(rs, ru, rj);
+    double best = -INFINITY;
+    int bj = -1;
+    bool down_first = false;
+    if (rj != INT_MAX) {
+      const double v = x[rj];
+      const PcView pv = pc_view(io, rj, own, ov, os, oc);
+      const double cd = (v - floor(v)) * pv.pd, cu = (ceil(v) - v) * pv.pu;
+      best = rs;
+      bj = rj;
+      down_first = cu > cd;
+    }
+    // strong-branched candidates (:98-128), in order
     const double maxchange = io.cutoff - objval;
     const int nsb = io.nsb[b];
     const size_t off = 2 * (size_t)io.sb_off[b];
@@ -302,33 +352,35 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
       const double v = io.sb_val[(size_t)b * kRelMaxCands + k];
       const double dd = v - floor(v), ud = ceil(v) - v;
       double cd, cu;
-      const int oc = sb_outcome(io, off, k, objval, maxchange, cd, cu);
+      const int oc2 = sb_outcome(io, off, k, objval, maxchange, cd, cu);
       ran = k + 1;
-      if (oc < 0) {
+      if (oc2 < 0) {
         // an unreliable side: no verdict, no observation
-      } else if (oc == 1) {
+      } else if (oc2 == 1) {
         status = 1;
-      } else if (oc == 2) {
+      } else if (oc2 == 2) {
         status = 2;       // the down branch's bound change
         mvar = j;
         mup = 0;
-      } else if (oc == 3) {
+      } else if (oc2 == 3) {
         status = 2;       // the up branch's bound change
         mvar = j;
         mup = 1;
       } else if (nev + 2 <= kRelEvents) {
-        io.ev_var[e0 + nev] = j;
-        io.ev_side[e0 + nev] = 0;
-        io.ev_cost[e0 + nev] = fabs(cd) / (fabs(dd) + kRelETol);
-        io.ev_var[e0 + nev + 1] = j;
-        io.ev_side[e0 + nev + 1] = 1;
-        io.ev_cost[e0 + nev + 1] = fabs(cu) / (fabs(ud) + kRelETol);
+        if (lane == 0) {
+          io.ev_var[e0 + nev] = j;
+          io.ev_side[e0 + nev] = 0;
+          io.ev_cost[e0 + nev] = fabs(cd) / (fabs(dd) + kRelETol);
+          io.ev_var[e0 + nev + 1] = j;
+          io.ev_side[e0 + nev + 1] = 1;
+          io.ev_cost[e0 + nev + 1] = fabs(cu) / (fabs(ud) + kRelETol);
+        }
         nev += 2;
       }
       const double sc = rel_score(cu, cd);
       // lastStrBranched_ = calls: within the round the last writer is the
       // largest call number (pc_fold stores it)
-      atomicMax(&io.last_new[j], (int)calls);
+      if (lane == 0) atomicMax(&io.last_new[j], (int)calls);
       if (status != 0) break;
       if (sc > best) {
         best = sc;
@@ -338,63 +390,74 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
     }
     if (status == 0) {
       // the remaining unreliable candidates by pseudocost (:129-147), in
-      // CompareScore order after the first nsb
+      // CompareScore order after the first nsb (the strong-branched ones:
+      // rel_prepare chose them with the same keys): the largest score, the
+      // earliest key on ties; it wins only above the best so far
       double ps = -INFINITY;
       int pj = -1;
-      for (int k = 0;; ++k) {
-        double bs = INFINITY;
-        int kj = INT_MAX;
-        for (int j = 0; j < io.n; ++j) {
-          if (!is_int(io.vtype[j])) continue;
-          const double v = x[j];
-          if (!fractional(v)) continue;
-          const PcView pv = pc_view(io, j, own, ov, os, oc);
-          if (reliable(io, j, calls, pv)) continue;
-          const double sc = unrel_score(pv, v - floor(v), ceil(v) - v);
-          const bool after = sc > ps || (sc == ps && j > pj);
-          if (after && (sc < bs || (sc == bs && j < kj))) {
-            bs = sc;
-            kj = j;
-          }
-        }
-        if (kj == INT_MAX) break;
-        ps = bs;
-        pj = kj;
-        if (k < nsb) continue;   // strong-branched above
-        const double v = x[kj];
-        const PcView pv = pc_view(io, kj, own, ov, os, oc);
+      if (nsb > 0) {
+        pj = io.sb_var[(size_t)b * kRelMaxCands + nsb - 1];
+        const double v = x[pj];
+        ps = unrel_score(pc_view(io, pj, own, ov, os, oc), v - floor(v), ceil(v) - v);
+      }
+      double us = -INFINITY, uk = INFINITY;
+      int uj = INT_MAX;
+      for (int j = lane; j < io.n; j += 64) {
+        if (!is_int(io.vtype[j])) continue;
+        const double v = x[j];
+        if (!fractional(v)) continue;
+        const PcView pv = pc_view(io, j, own, ov, os, oc);
+        if (reliable(io, j, calls, pv)) continue;
+        const double key = unrel_score(pv, v - floor(v), ceil(v) - v);
+        if (!(key > ps || (key == ps && j > pj))) continue;   // strong-branched, or unordered
         const double cd = (v - floor(v)) * pv.pd, cu = (ceil(v) - v) * pv.pu;
         const double sc = rel_score(cu, cd);
-        if (sc > best) {
-          best = sc;
-          bj = kj;
-          down_first = cu > cd;
+        if (!(sc > -INFINITY)) continue;
+        if (sc > us || (sc == us && (key < uk || (key == uk && j < uj)))) {
+          us = sc;
+          uk = key;
+          uj = j;
         }
       }
-      io.bvar[b] = bj;
-      io.bval[b] = x[bj];
-      io.bup[b] = down_first ? 0 : 1;
+      wave_max_key(us, uk, uj);
+      if (uj != INT_MAX && us > best) {
+        const double v = x[uj];
+        const PcView pv = pc_view(io, uj, own, ov, os, oc);
+        const double cd = (v - floor(v)) * pv.pd, cu = (ceil(v) - v) * pv.pu;
+        best = us;
+        bj = uj;
+        down_first = cu > cd;
+      }
+      if (lane == 0) {
+        io.bvar[b] = bj;
+        io.bval[b] = x[bj];
+        io.bup[b] = down_first ? 0 : 1;
+      }
     } else if (status == 1) {
       dec = 1;   // PrunedByBrancher -> NodeInfeasible (PCBProcessor.cpp:284-294)
-      atomicAdd(&io.counters[1], 1ull);
+      if (lane == 0) atomicAdd(&io.counters[1], 1ull);
     } else {
       // ModifiedByBrancher: the node again with the one-sided bound change
       // (PCBProcessor.cpp:295-305); the tail writes it as a single child
       dec = 5;
-      io.bvar[b] = mvar;
-      io.bval[b] = x[mvar];
-      io.bup[b] = (int8_t)mup;
-      atomicAdd(&io.counters[2], 1ull);
+      if (lane == 0) {
+        io.bvar[b] = mvar;
+        io.bval[b] = x[mvar];
+        io.bup[b] = (int8_t)mup;
+        atomicAdd(&io.counters[2], 1ull);
+      }
     }
-    if (ran > 0) {  // the LPs the reference solves: up to the verdict
+    if (ran > 0 && lane == 0) {  // the LPs the reference solves: up to the verdict
       unsigned long long piv = 0;
       for (int c = 0; c < 2 * ran; ++c) piv += (unsigned long long)io.c_iters[off + c];
       atomicAdd(&io.counters[0], (unsigned long long)(2 * ran));
       atomicAdd(&io.counters[3], piv);
     }
   }
-  io.dec_out[b] = dec;
-  io.nev[b] = nev;
+  if (lane == 0) {
+    io.dec_out[b] = dec;
+    io.nev[b] = nev;
+  }
 }
 
 // ---- chained strong branching (ReliabilityBrancher::strongBranch_, :469-506):
@@ -504,7 +567,7 @@ hipError_t launch_rel_rank(const RelIO &io, int32_t *flag, int32_t *rank, int32_
 hipError_t launch_rel_prepare(const RelIO &io, int32_t *sb_off, int32_t *total,
                               hipStream_t stream) {
   if (io.nb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rel_prepare, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  hipLaunchKernelGGL(rel_prepare, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
   hipLaunchKernelGGL(excl_scan, dim3(1), dim3(1024), 0, stream, io.nsb, sb_off, io.nb, total);
   return hipGetLastError();
 }
@@ -543,7 +606,7 @@ hipError_t launch_rel_chain_stop(const RelIO &io, int c, uint8_t *stopped, hipSt
 
 hipError_t launch_rel_decide(const RelIO &io, hipStream_t stream) {
   if (io.nb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rel_decide, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  hipLaunchKernelGGL(rel_decide, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
   hipLaunchKernelGGL(excl_scan, dim3(1), dim3(1024), 0, stream, io.nev, io.ev_off, io.nb,
                      io.ev_total);
   hipLaunchKernelGGL(rel_compact, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);

@@ -21,7 +21,7 @@ def build():
     from minotaur_amd import build as b
     srcs = [os.path.join(b.CSRC, x) for x in b.SOURCES]
     cmd = [b.HIPCC] + b.FLAGS + ['-DMGPU_STAMPS', '-I', os.path.join(ROOT, 'include'),
-                                 '-o', OUT] + srcs
+                                 '-o', OUT] + srcs + ['-L/opt/rocm/lib', '-lrccl']
     subprocess.run(cmd, check=True)
 
 

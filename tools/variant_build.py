@@ -44,7 +44,8 @@ def main():
         else:
             objs.append(os.path.join(b.HERE, 'build', s + '.o'))
     lib = os.path.join(out, 'libmgpu.so')
-    subprocess.run([b.HIPCC, '-shared', '-fPIC', f'--offload-arch={b.ARCH}', '-o', lib] + objs,
+    subprocess.run([b.HIPCC, '-shared', '-fPIC', f'--offload-arch={b.ARCH}', '-o', lib] + objs +
+                   ['-L/opt/rocm/lib', '-lrccl'],
                    check=True)
     print(lib)
 
