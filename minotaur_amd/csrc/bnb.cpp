@@ -728,6 +728,26 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
                      s.wub.as<double>(), s.inf.as<int32_t>(), s.nm.as<int32_t>(), 0, nullptr,
                      nullptr, nullptr);
   if (rc != MGPU_OK) return rc;
+  // the node decision (shouldPrune_ + isFeasible + MaxVio), fused into K3P's
+  // epilogue when the round's LPs run the product form (no x read back)
+  DecideIO d{};
+  d.batch = nb;
+  d.fbbt_infeas = s.inf.as<int32_t>();
+  d.status = s.st.as<int32_t>();
+  d.obj = s.obj.as<double>();
+  d.x = s.x.as<double>();
+  d.incumbent = s.inc;
+  d.abs_tol = 1e-6;
+  d.rel_tol = 1e-6;
+  d.cutoff = INFINITY;
+  d.int_tol = 1e-6;
+  d.decision = s.dec.as<int32_t>();
+  d.cand_obj = s.cand.as<double>();
+  d.bvar = s.bvar.as<int32_t>();
+  d.bval = s.bval.as<double>();
+  d.bup = s.bup.as<int8_t>();
+  c->lp_decided = false;
+  c->pfi_decide = (!s.qp && !s.rel && (s.warm == 0 || s.warm == 2)) ? &d : nullptr;
   if (s.qp) {
     // the node's QP relaxation (QPDRelaxer -> BqpdEngine::solve,
     // examples/QPDRelaxer.cpp:56-126): K5 on the FBBT-tightened boxes, the
@@ -776,24 +796,10 @@ int mgpu_bnb_round(mgpu_ctx *c, int batch, double incumbent, mgpu_bnb_stats *sta
                            s.rel ? s.wo_d.as<double>() : nullptr,
                            s.rel ? s.wo_binv.as<double>() : nullptr);
   }
+  c->pfi_decide = nullptr;
   if (rc != MGPU_OK) return rc;
-  DecideIO d{};
-  d.batch = nb;
-  d.fbbt_infeas = s.inf.as<int32_t>();
-  d.status = s.st.as<int32_t>();
-  d.obj = s.obj.as<double>();
-  d.x = s.x.as<double>();
-  d.incumbent = s.inc;
-  d.abs_tol = 1e-6;
-  d.rel_tol = 1e-6;
-  d.cutoff = INFINITY;
-  d.int_tol = 1e-6;
-  d.decision = s.dec.as<int32_t>();
-  d.cand_obj = s.cand.as<double>();
-  d.bvar = s.bvar.as<int32_t>();
-  d.bval = s.bval.as<double>();
-  d.bup = s.bup.as<int8_t>();
-  HIPCHK(c, launch_node_decide(c->lp, d, c->stream));
+  if (!c->lp_decided) HIPCHK(c, launch_node_decide(c->lp, d, c->stream));
+  c->lp_decided = false;
   const int32_t *decision = s.dec.as<int32_t>();
   unsigned long long rcnt[4] = {0, 0, 0, 0};
   if (s.rel) {

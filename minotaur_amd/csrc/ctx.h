@@ -89,6 +89,10 @@ struct mgpu_ctx {
             ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;
   hipEvent_t ev8 = nullptr;    // between K3P and its dense overflow re-solve
   bool last_lp_pfi = false;    // the last LP call ran K3P or K3PW
+  // the batched tree's node decision for K3P to fuse into its epilogue (set
+  // around one LP call by bnb.cpp); lp_decided: that call did decide
+  const DecideIO *pfi_decide = nullptr;
+  bool lp_decided = false;
   double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0, last_qp_ms = 0.0;
   // per-node rows (mgpu_set_node_rows): device maps csc_pos, csr_pos,
   // coef_src, row, lo_src, hi_src; K3R's per-node warm starts; host-path

@@ -423,6 +423,10 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         io.obj[b] = INFINITY;
         io.iters[b] = 0;
         if (io.path.k_out != nullptr) io.path.k_out[b] = 0;
+        if (px.decide) {   // presolveNode found it infeasible (node_decide: 1)
+          px.dec.decision[b] = 1;
+          if (px.dec.cand_obj != nullptr) px.dec.cand_obj[b] = INFINITY;
+        }
       }
       PSTAMP(9);
       continue;
@@ -462,6 +466,10 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         io.obj[b] = INFINITY;
         io.iters[b] = 0;
         if (io.path.k_out != nullptr) io.path.k_out[b] = 0;
+        if (px.decide) {   // ProvenInfeasible (node_decide: 1)
+          px.dec.decision[b] = 1;
+          if (px.dec.cand_obj != nullptr) px.dec.cand_obj[b] = INFINITY;
+        }
       }
       PSTAMP(9);
       continue;
@@ -548,8 +556,9 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       sib = b;
     } else if (kpath > 0) {
       const uint64_t freem = __ballot(lane < m && pst[h] != ST_BASIC);
+      // (two columns per group: four measured 0.8 % slower, profiles/r05f)
       if (colrep(kpath, freem, [&](int i) { return (int)(ppath[i] & 0xFFFFu); },
-                 std::integral_constant<int, 4>())) {
+                 std::integral_constant<int, 2>())) {
         ne = kpath;
         if (lane < m) sib_h[lane] = h;
         sib = b;
@@ -786,7 +795,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         // eta file full.  Reinversion (oracle: the same rule): the current
         // basis rebuilt as column replacements on B0 -- its basic columns
         // outside the shared basis, ascending, exactly as a basis warm start
-        // -- when that difference leaves a quarter of the file free and the
+        // -- when that difference leaves an eighth of the file free and the
         // solve stays short of the 64-pivot primal refresh; the primal values
         // are then recomputed, the reduced costs kept.  Otherwise (or for
         // bound LPs, whose reduced costs are rebuilt per objective) the dense
@@ -802,7 +811,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
             nrm[s] = bm[s] & ~__ballot(j < N && s_wst[j] == ST_BASIC);
             kb += __popcll(nrm[s]);
           }
-          const int room = kmax / 4 > 1 ? kmax / 4 : 1;
+          const int room = kmax / 8 > 1 ? kmax / 8 : 1;
           if (kb <= kmax - room && iters + (kmax - kb) < 64) {
             // the listed columns into the (free) rho slice, ascending
             int *cl = reinterpret_cast<int *>(rho);
@@ -1051,11 +1060,68 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
           for (int i = 0; i < cnt; ++i) sum += rld(pr, i);
         }
       }
-      if (lane == 0) io.obj[b] = P.ocol < 0 ? sum + lp.objoff : sum;
-      if (io.x != nullptr)
+      const double solval = P.ocol < 0 ? sum + lp.objoff : sum;
+      if (lane == 0) io.obj[b] = solval;
+      int dec = -1;
+      if (px.decide) {
+        // node_decide_kernel's decision on the values in LDS (the same
+        // tests in the same order): the bound test of shouldPrune_, then
+        // IntVarHandler::isFeasible, then MaxVioBrancher's choice
+        const DecideIO &dd = px.dec;
+        const double cut = dd.incumbent;
+        if (solval >= cut - dd.abs_tol || solval >= cut - fabs(cut) * dd.rel_tol ||
+            solval >= dd.cutoff) {
+          dec = 2;
+        } else {
+          bool frac = false;
+          for (int j = lane; j < n; j += 64) {
+            const uint8_t t = lp.vtype[j];
+            if (t == kBinary || t == kInteger) {
+              const double v = zc[j];
+              frac |= fabs(v - floor(v + 0.5)) > dd.int_tol;
+            }
+          }
+          dec = __any(frac) ? 0 : 3;
+          if (dec == 0 && dd.bvar != nullptr) {
+            double best = -INFINITY;
+            int bj = INT_MAX;
+            for (int j = lane; j < n; j += 64) {
+              const uint8_t t = lp.vtype[j];
+              if (t != kBinary && t != kInteger) continue;
+              const double v = zc[j];
+              if (!(fabs(floor(v + 0.5) - v) > dd.int_tol)) continue;
+              const double dn = v - floor(v), up = ceil(v) - v;
+              const double lo_ = (up < dn) ? up : dn, hi_ = (dn < up) ? up : dn;
+              const double sc = 0.1 * (0.8 * lo_ + 0.2 * hi_);
+              if (sc > best) {
+                best = sc;
+                bj = j;
+              }
+            }
+            wave_argmax(best, bj);
+            if (lane == 0) {
+              const double v = zc[bj];
+              dd.bvar[b] = bj;
+              dd.bval[b] = v;
+              dd.bup[b] = (v - floor(v)) > (ceil(v) - v) ? 1 : 0;
+            }
+          }
+        }
+        if (lane == 0) {
+          dd.decision[b] = dec;
+          if (dd.cand_obj != nullptr) dd.cand_obj[b] = dec == 3 ? solval : INFINITY;
+        }
+      }
+      // x for the caller; with the fused decision only an incumbent
+      // candidate's (the tree reads no other node's x)
+      if (io.x != nullptr && (!px.decide || dec == 3))
         for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = zc[j];
-    } else if (lane == 0) {
-      io.obj[b] = status == 2 ? INFINITY : -INFINITY;
+    } else {
+      if (lane == 0) io.obj[b] = status == 2 ? INFINITY : -INFINITY;
+      if (px.decide && lane == 0) {   // 2 infeasible -> 1; 4 unbounded -> 4 (engine)
+        px.dec.decision[b] = status == 2 ? 1 : 4;
+        if (px.dec.cand_obj != nullptr) px.dec.cand_obj[b] = INFINITY;
+      }
     }
     if (lane == 0) {
       io.status[b] = status;

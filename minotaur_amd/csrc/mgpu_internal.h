@@ -184,6 +184,27 @@ constexpr int kPfiMax = 32;   // the default cap (the headline's 32-eta build)
 constexpr int kPfiBig = 48;   // the largest cap: the 48-eta build (narrow tree rounds)
 static_assert(kPfiBig < kStallPivots, "K3P never reaches the Bland switch");
 constexpr int kPfiSlots = 4;
+struct DecideIO {
+  int batch;
+  const int32_t *fbbt_infeas;   // [B] or null
+  const int32_t *status;        // [B] LP status
+  const double *obj;            // [B]
+  const double *x;              // [B][n]
+  double incumbent;             // best known objective (+inf if none)
+  double abs_tol, rel_tol;      // solAbs_tol / solRel_tol (1e-6)
+  double cutoff;                // obj_cut_off (+inf)
+  double int_tol;               // int_tol (1e-6)
+  int32_t *decision;            // [B]
+  double *inf_meas;             // [B] or null
+  double *cand_obj;             // [B] or null: obj if integer feasible else +inf
+  int32_t *bvar;                // [B] or null: branching variable when decision 0
+  double *bval;                 // [B] its LP value
+  int8_t *bup;                  // [B] 1: up branch preferred (dd > ud)
+  // list mode (node_list != null): decide only nodes node_list[i], i <
+  // *node_count (device count), e.g. the product form's overflow list
+  const int32_t *node_list;
+  const int32_t *node_count;
+};
 struct PfiIO {
   int kmax;                     // eta-file cap for this launch (1..kPfiBig)
   int32_t *ovf_list;            // [B] nodes that needed more than kmax pivots
@@ -205,6 +226,13 @@ struct PfiIO {
   // pivots the product-form kernel ran itself, summed over the launch (K3P;
   // null: not counted): the dense continuation's pivots are not in it
   unsigned long long *pivots;
+  // decide != 0 (K3P): the node decision of node_decide (shouldPrune_ +
+  // isFeasible + MaxVio) in the kernel's epilogue, on the primal values in
+  // LDS, for every node that does not overflow; x is then written only for
+  // integer-feasible nodes (the incumbent candidates).  The overflow list is
+  // decided after its dense continuation (launch_node_decide, list mode).
+  int decide;
+  DecideIO dec;
 };
 // B0^{-1} a_q for every column into t0 [N][m] (K3P's ftran_b0, bit for bit)
 hipError_t launch_pfi_t0(const DevLP &lp, const double *binv, double *t0, hipStream_t stream);
@@ -225,23 +253,7 @@ bool lp_pfiw_fits(int n, int m, int nnz);
 hipError_t launch_lp_pfiw(const DevLP &lp, const LpIO &io, const PfiIO &px, int num_cus,
                           hipStream_t stream);
 
-struct DecideIO {
-  int batch;
-  const int32_t *fbbt_infeas;   // [B] or null
-  const int32_t *status;        // [B] LP status
-  const double *obj;            // [B]
-  const double *x;              // [B][n]
-  double incumbent;             // best known objective (+inf if none)
-  double abs_tol, rel_tol;      // solAbs_tol / solRel_tol (1e-6)
-  double cutoff;                // obj_cut_off (+inf)
-  double int_tol;               // int_tol (1e-6)
-  int32_t *decision;            // [B]
-  double *inf_meas;             // [B] or null
-  double *cand_obj;             // [B] or null: obj if integer feasible else +inf
-  int32_t *bvar;                // [B] or null: branching variable when decision 0
-  double *bval;                 // [B] its LP value
-  int8_t *bup;                  // [B] 1: up branch preferred (dd > ud)
-};
+
 
 hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t stream);
 

@@ -654,6 +654,10 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
     HIPCHK(c, c->pfi_piv.ensure(sizeof(unsigned long long)));
     HIPCHK(c, hipMemsetAsync(c->pfi_piv.p, 0, sizeof(unsigned long long), c->stream));
     px.pivots = wide ? nullptr : c->pfi_piv.as<unsigned long long>();
+    if (!wide && c->pfi_decide != nullptr) {   // the tree's decision in K3P's epilogue
+      px.decide = 1;
+      px.dec = *c->pfi_decide;
+    }
     px.ovf_count = cnt;
     px.next = cnt + 1;
     px.ovf_list = cnt + 4;
@@ -711,6 +715,13 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
       io3.list_hi = 0x7fffffff;
       io3.next = cnt + 3;
       HIPCHK(c, dense(io3));
+    }
+    if (px.decide) {   // the overflow list, after its dense continuation
+      DecideIO d2 = px.dec;
+      d2.node_list = px.ovf_list;
+      d2.node_count = px.ovf_count;
+      HIPCHK(c, launch_node_decide(c->lp, d2, c->stream));
+      c->lp_decided = true;
     }
     return MGPU_OK;
   }

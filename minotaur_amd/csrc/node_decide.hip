@@ -21,8 +21,10 @@ constexpr int kNodesPerBlock = 4;
 __global__ __launch_bounds__(64 * kNodesPerBlock) void node_decide_kernel(DevLP lp,
                                                                            DecideIO io) {
   const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * kNodesPerBlock + (threadIdx.x >> 6);
-  if (b >= io.batch) return;
+  const int nn = io.node_list != nullptr ? *io.node_count : io.batch;
+  for (int t = blockIdx.x * kNodesPerBlock + (threadIdx.x >> 6); t < nn;
+       t += gridDim.x * kNodesPerBlock) {
+  const int b = io.node_list != nullptr ? io.node_list[t] : t;
   const int st = io.status[b];
   const double solval = io.obj[b];
   int dec;
@@ -107,13 +109,16 @@ __global__ __launch_bounds__(64 * kNodesPerBlock) void node_decide_kernel(DevLP 
     if (io.inf_meas != nullptr) io.inf_meas[b] = inf_meas;
     if (io.cand_obj != nullptr) io.cand_obj[b] = dec == 3 ? solval : INFINITY;
   }
+  }
 }
 
 }  // namespace
 
 hipError_t launch_node_decide(const DevLP &lp, const DecideIO &io, hipStream_t stream) {
   if (io.batch <= 0) return hipSuccess;
-  const int blocks = (io.batch + kNodesPerBlock - 1) / kNodesPerBlock;
+  int blocks = (io.batch + kNodesPerBlock - 1) / kNodesPerBlock;
+  // list mode: the count is on the device; a grid-stride loop over it
+  if (io.node_list != nullptr && blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(node_decide_kernel, dim3(blocks), dim3(64 * kNodesPerBlock), 0, stream,
                      lp, io);
   return hipGetLastError();

@@ -389,8 +389,8 @@ static int colrep_basis(lpw *W, const orc_path *path) {
 /* K3P's reinversion when the eta file is full (lp_pfi.hip, the same rule):
  * the current basis as column replacements on B0 -- its basic columns
  * outside B0 in ascending order, from B0's head, exactly as a basis warm
- * start (colrep_basis) -- when that difference kb leaves a quarter of the
- * file free (kb <= pfi - max(1, pfi / 4)) and pivots + (pfi - kb) < 64 (the
+ * start (colrep_basis) -- when that difference kb leaves an eighth of the
+ * file free (kb <= pfi - max(1, pfi / 8)) and pivots + (pfi - kb) < 64 (the
  * product form never reaches the 64-pivot refresh).  Returns 1 when the etas
  * were rebuilt; 0 with the state untouched when the rule declines; -1 after
  * a failed replacement (no usable pivot) with the SHARED basis in place
@@ -399,7 +399,7 @@ static int colrep_basis(lpw *W, const orc_path *path) {
 static int reinvert(lpw *W, const int *hroot, const unsigned char *rootb,
                     const signed char *ws_st, const double *ws_d, int iters) {
   int m = W->P->m, N = W->N, kb = 0;
-  int room = W->pfi / 4 > 1 ? W->pfi / 4 : 1;
+  int room = W->pfi / 8 > 1 ? W->pfi / 8 : 1;
   for (int j = 0; j < N; ++j) kb += W->st[j] == ST_BASIC && !rootb[j];
   if (kb > W->pfi - room || iters + (W->pfi - kb) >= 64) return 0;
   unsigned *cols = (unsigned *) malloc(sizeof(unsigned) * (size_t) (kb + 1));
