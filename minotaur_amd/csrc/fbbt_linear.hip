@@ -27,6 +27,8 @@
 //    reference's x86-64 build (no FMA without -march).
 #include "mgpu_internal.h"
 
+#include <type_traits>
+
 namespace mgpu {
 namespace {
 
@@ -48,18 +50,34 @@ __device__ __forceinline__ uint64_t rlu64(uint64_t v, int k) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Per-lane slice of a chunk of up to 64 term records.
+// v_readfirstlane: the value of the first ACTIVE lane, so it is correct
+// under any EXEC mask (v_readlane of a fixed lane is not: inside a
+// divergent region the compiler may copy or reload a VGPR for the active
+// lanes only, and a fixed lane may be inactive -- round 5 met exactly that)
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double rfld(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ uint64_t rflu64(uint64_t v) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffffu));
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Per-lane slice of a chunk of up to 64 term records (tightenInts_'s column
+// list, read with v_readlane in uniform control flow only).
 struct TermChunk {
-  double a;
   uint64_t cmask;
   int j, cs, ce, isint;
 };
 
 __device__ __forceinline__ TermChunk load_terms(const TermRec *base, int cnt, int lane) {
-  TermChunk c{0.0, 0ull, 0, 0, 0, 0};
+  TermChunk c{0ull, 0, 0, 0, 0};
   if (lane < cnt) {
     const TermRec r = base[lane];
-    c.a = r.a;
     c.cmask = r.cmask;
     c.j = r.j;
     c.cs = r.cs;
@@ -75,23 +93,20 @@ struct Term1 {  // one term, every field wave-uniform
   int j, cs, ce, isint;
 };
 
-// Calls f(Term1) for every term of a term list, in order.  Chunk 0 (the
-// first 64 terms) comes from `pre`, which the caller loaded with the FULL
-// wave active (v_readlane reads lanes regardless of EXEC, so the source
-// VGPR must have been written by every lane); longer lists read the rest
-// straight from memory with wave-uniform addresses, which is correct under
-// any EXEC mask.
+// Term k of a record list (LDS in the persistent and staged kernels, HBM
+// otherwise): a wave-uniform address read by every active lane, made
+// uniform with readfirstlane.  Row visits run in divergent code (only the
+// lanes whose node flagged the row), so every record read there goes this
+// way.
+__device__ __forceinline__ Term1 term_at(const TermRec *base, int k) {
+  const TermRec r = base[k];
+  return Term1{rfld(r.a), rflu64(r.cmask), rfl(r.j), rfl(r.cs), rfl(r.ce), rfl(r.isint)};
+}
+
+// Calls f(Term1) for every term of a term list, in order.
 template <class F>
-__device__ __forceinline__ void for_terms(const TermRec *base, int nt, const TermChunk &pre,
-                                          F &&f) {
-  const int cnt = nt < kLanes ? nt : kLanes;
-  for (int k = 0; k < cnt; ++k)
-    f(Term1{rld(pre.a, k), rlu64(pre.cmask, k), rl(pre.j, k), rl(pre.cs, k), rl(pre.ce, k),
-            rl(pre.isint, k)});
-  for (int k = kLanes; k < nt; ++k) {
-    const TermRec r = base[k];
-    f(Term1{r.a, r.cmask, r.j, r.cs, r.ce, r.isint});
-  }
+__device__ __forceinline__ void for_terms(const TermRec *base, int nt, F &&f) {
+  for (int k = 0; k < nt; ++k) f(term_at(base, k));
 }
 
 // ---- per-lane node view ----------------------------------------------------
@@ -106,6 +121,7 @@ struct NodeView {
   int stride;        // elements between consecutive variables (same lane)
   int lane;
   const int32_t *rowidx;
+  static constexpr bool kBits = kBitFlags;
   __device__ __forceinline__ double &L(int j) const {
     if constexpr (kIL) return lb[((size_t)j * kLanes + lane) * 2];
     else return lb[j * stride + lane];
@@ -198,10 +214,10 @@ struct ModLog {
 
 // getLfBnds_ (LinearHandler.cpp:1237-1258): ascending-column f64 sums.
 template <class V>
-__device__ __forceinline__ void lf_bnds(const TermRec *base, int nt, const TermChunk &pre,
-                                        const V &v, double &lo, double &up) {
+__device__ __forceinline__ void lf_bnds(const TermRec *base, int nt, const V &v, double &lo,
+                                        double &up) {
   double l = 0.0, u = 0.0;
-  for_terms(base, nt, pre, [&](const Term1 &t) {
+  for_terms(base, nt, [&](const Term1 &t) {
     const double vl = v.L(t.j), vu = v.U(t.j);
     if (t.a > 0) {
       l += t.a * vl;
@@ -218,11 +234,11 @@ __device__ __forceinline__ void lf_bnds(const TermRec *base, int nt, const TermC
 // getSingLfBnds_ (LinearHandler.cpp:1261-1319): sums that skip a single
 // infinite term; a second infinite term makes the side infinite.
 template <class V>
-__device__ __forceinline__ void sing_lf_bnds(const TermRec *base, int nt, const TermChunk &pre, const V &v,
-                             double &lo, double &up) {
+__device__ __forceinline__ void sing_lf_bnds(const TermRec *base, int nt, const V &v, double &lo,
+                                             double &up) {
   double l = 0.0, u = 0.0;
   bool lo_sing = false, up_sing = false, lo_fin = true, up_fin = true;
-  for_terms(base, nt, pre, [&](const Term1 &t) {
+  for_terms(base, nt, [&](const Term1 &t) {
     const double c = t.a;
     const double vl = v.L(t.j), vu = v.U(t.j);
     if (c > kETol) {
@@ -261,16 +277,6 @@ __device__ __forceinline__ void sing_lf_bnds(const TermRec *base, int nt, const 
   up = u;
 }
 
-// Term k of a list: from the preloaded chunk (k < 64, v_readlane) or from
-// memory (uniform address).
-__device__ __forceinline__ Term1 term_at(const TermRec *base, const TermChunk &pre, int k) {
-  if (k < kLanes)
-    return Term1{rld(pre.a, k), rlu64(pre.cmask, k), rl(pre.j, k), rl(pre.cs, k),
-                 rl(pre.ce, k), rl(pre.isint, k)};
-  const TermRec r = base[k];
-  return Term1{r.a, r.cmask, r.j, r.cs, r.ce, r.isint};
-}
-
 // updateLfBoundsFromLb_ (LinearHandler.cpp:1048-1134) when from_lb, with
 // diff = lb - uu; updateLfBoundsFromUb_ (:1137-1226) otherwise, with
 // diff = ub - ll.  A term with coef > 0 (from_lb) / coef < 0 (from_ub)
@@ -283,7 +289,7 @@ __device__ __forceinline__ Term1 term_at(const TermRec *base, const TermChunk &p
 // its own column's bounds; the order-dependent effects (mod log, nintmods)
 // are produced in phase B in term order.
 template <class V>
-__device__ __forceinline__ void upd_side(const TermRec *base, int nt, const TermChunk &pre, V &v,
+__device__ __forceinline__ void upd_side(const TermRec *base, int nt, V &v,
                          NodeState &s, const ModLog &log, double diff, bool from_lb,
                          bool is_sing, bool &changed, bool count_int) {
   for (int k0 = 0; k0 < nt; k0 += 4) {
@@ -297,11 +303,10 @@ __device__ __forceinline__ void upd_side(const TermRec *base, int nt, const Term
       cand[u] = 0.0;
       cur[u] = 0.0;
       if (k0 + u < nt) {
-        t[u] = term_at(base, pre, k0 + u);
+        t[u] = term_at(base, k0 + u);
         const double c = t[u].a;
         if (c > kETol || c < -kETol) {
-          const int j = t[u].j;
-          const double vl = v.L(j), vu = v.U(j);
+          const double vl = v.L(t[u].j), vu = v.U(t[u].j);
           low[u] = from_lb ? c > 0 : c < 0;
           if (low[u]) {
             // new lower bound: diff/c + (vub, or 0 for a singleton infinity)
@@ -343,22 +348,6 @@ __device__ __forceinline__ void upd_side(const TermRec *base, int nt, const Term
   }
 }
 
-template <class V>
-__device__ __forceinline__ void upd_from_lb(const TermRec *base, int nt, const TermChunk &pre,
-                                            V &v, NodeState &s, const ModLog &log, double lb,
-                                            double uu, bool is_sing, bool &changed,
-                                            bool count_int) {
-  upd_side(base, nt, pre, v, s, log, lb - uu, true, is_sing, changed, count_int);
-}
-
-template <class V>
-__device__ __forceinline__ void upd_from_ub(const TermRec *base, int nt, const TermChunk &pre,
-                                            V &v, NodeState &s, const ModLog &log, double ub,
-                                            double ll, bool is_sing, bool &changed,
-                                            bool count_int) {
-  upd_side(base, nt, pre, v, s, log, ub - ll, false, is_sing, changed, count_int);
-}
-
 // ---- register-cached rows ---------------------------------------------------
 // A row of nt <= RC terms is tightened with all of its bounds gathered into
 // registers ONCE (2*RC independent loads in flight), reused by the 4-5 passes
@@ -373,13 +362,14 @@ struct RowCache {
 };
 
 template <int RC, class V>
-__device__ __forceinline__ void rc_load(RowCache<RC> &c, const TermChunk &pre, int nt,
+__device__ __forceinline__ void rc_load(RowCache<RC> &c, const TermRec *base, int nt,
                                         const V &v) {
 #pragma unroll
   for (int k = 0; k < RC; ++k) {
     const int kk = k < nt ? k : 0;   // clamped: loads are unconditional
-    const int j = rl(pre.j, kk);
-    c.a[k] = k < nt ? rld(pre.a, kk) : 0.0;
+    const TermRec *r = base + kk;    // the record's first 16 B: a, j
+    const int j = rfl(r->j);
+    c.a[k] = k < nt ? rfld(r->a) : 0.0;
     c.l[k] = v.L(j);
     c.u[k] = v.U(j);
   }
@@ -453,7 +443,7 @@ __device__ __forceinline__ void rc_sing_lf_bnds(const RowCache<RC> &c, int nt, d
 // upd_side on the cache: phase A computes every slot's candidate (RC
 // independent divisions), phase B applies hits in term order.
 template <int RC, class V>
-__device__ __forceinline__ void rc_upd_side(RowCache<RC> &c, int nt, const TermChunk &pre, V &v,
+__device__ __forceinline__ void rc_upd_side(RowCache<RC> &c, const TermRec *base, int nt, V &v,
                             NodeState &s, const ModLog &log, double diff, bool from_lb,
                             bool is_sing, bool &changed, bool count_int) {
   double cand[RC];
@@ -480,8 +470,7 @@ __device__ __forceinline__ void rc_upd_side(RowCache<RC> &c, int nt, const TermC
 #pragma unroll
   for (int k = 0; k < RC; ++k) {
     if (k < nt && hit[k]) {
-      const Term1 t{c.a[k], rlu64(pre.cmask, k), rl(pre.j, k), rl(pre.cs, k), rl(pre.ce, k),
-                    rl(pre.isint, k)};
+      const Term1 t = term_at(base, k);   // t.a == c.a[k]
       const bool low = from_lb ? t.a > 0 : t.a < 0;
       double nb = cand[k];
       if (low) {
@@ -505,33 +494,32 @@ __device__ __forceinline__ void rc_upd_side(RowCache<RC> &c, int nt, const TermC
 
 // linBndTighten_ (LinearHandler.cpp:952-1045) on a register-cached row.
 template <int RC, class V>
-__device__ __forceinline__ bool rc_lin_bnd_tighten(int nt, const TermChunk &pre, double lb, double ub, V &v,
+__device__ __forceinline__ bool rc_lin_bnd_tighten(int nt, const TermRec *base, double lb, double ub, V &v,
                                    NodeState &s, const ModLog &log, bool &changed) {
   RowCache<RC> c;
-  rc_load<RC>(c, pre, nt, v);
-  double ll, uu, sing_ll = -INFINITY, sing_uu = INFINITY;
+  rc_load<RC>(c, base, nt, v);
+  double ll = 0.0, uu = 0.0, sing_ll = -INFINITY, sing_uu = INFINITY;
   changed = false;
-  rc_lf_bnds<RC>(c, nt, ll, uu);
-  if (ll < -kInfty || uu > kInfty) rc_sing_lf_bnds<RC>(c, nt, sing_ll, sing_uu);
-  if (ll > ub + kETol) return true;
-  if (uu < lb - kETol) return true;
-  if (lb > -kInfty) {
-    if (uu < kInfty) {
-      rc_upd_side<RC>(c, nt, pre, v, s, log, lb - uu, true, false, changed, true);
-    } else if (sing_uu < kInfty) {
-      rc_upd_side<RC>(c, nt, pre, v, s, log, lb - sing_uu, true, true, changed, true);
+  // pass 0: the lb side (updateLfBoundsFromLb_ with lb - uu, or lb - the
+  // singleton sum), pass 1: the ub side; the activity sums are recomputed
+  // before pass 1 only if pass 0 changed a bound.  The side and the
+  // singleton case are run-time values, so each pass holds one copy of the
+  // update (two before: the code is half the size, same operations)
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (p == 0 || changed) {
+      rc_lf_bnds<RC>(c, nt, ll, uu);
+      if (ll < -kInfty || uu > kInfty) rc_sing_lf_bnds<RC>(c, nt, sing_ll, sing_uu);
     }
-  }
-  if (changed) {
-    rc_lf_bnds<RC>(c, nt, ll, uu);
-    if (ll < -kInfty || uu > kInfty) rc_sing_lf_bnds<RC>(c, nt, sing_ll, sing_uu);
-  }
-  if (ub < kInfty) {
-    if (ll > -kInfty) {
-      rc_upd_side<RC>(c, nt, pre, v, s, log, ub - ll, false, false, changed, true);
-    } else if (sing_ll > -kInfty) {
-      rc_upd_side<RC>(c, nt, pre, v, s, log, ub - sing_ll, false, true, changed, true);
-    }
+    if (p == 0 && (ll > ub + kETol || uu < lb - kETol)) return true;
+    const bool lo_side = p == 0;
+    const bool side_fin = lo_side ? lb > -kInfty : ub < kInfty;
+    const double act = lo_side ? uu : ll, sact = lo_side ? sing_uu : sing_ll;
+    const bool act_fin = lo_side ? act < kInfty : act > -kInfty;
+    const bool sact_fin = lo_side ? sact < kInfty : sact > -kInfty;
+    if (side_fin && (act_fin || sact_fin))
+      rc_upd_side<RC>(c, base, nt, v, s, log, (lo_side ? lb : ub) - (act_fin ? act : sact), lo_side,
+                      !act_fin, changed, true);
   }
   return false;
 }
@@ -539,10 +527,10 @@ __device__ __forceinline__ bool rc_lin_bnd_tighten(int nt, const TermChunk &pre,
 // varBndsFromObj_ (LinearHandler.cpp:544-597) on a register-cached
 // objective (nobj <= RC).
 template <int RC, class V>
-__device__ __forceinline__ void rc_bnds_from_obj(int nobj, const TermChunk &pre, V &v, NodeState &s,
+__device__ __forceinline__ void rc_bnds_from_obj(int nobj, const TermRec *base, V &v, NodeState &s,
                                  const ModLog &log, double ub, bool &changed) {
   RowCache<RC> c;
-  rc_load<RC>(c, pre, nobj, v);
+  rc_load<RC>(c, base, nobj, v);
   bool tch = true;
   long guard = 0;
   while (tch) {
@@ -551,11 +539,9 @@ __device__ __forceinline__ void rc_bnds_from_obj(int nobj, const TermChunk &pre,
     rc_lf_bnds<RC>(c, nobj, ll, uu);
     if (ll < -kInfty || uu > kInfty) rc_sing_lf_bnds<RC>(c, nobj, sing_ll, sing_uu);
     if (ll > ub + kETol) return;
-    if (ll > -kInfty) {
-      rc_upd_side<RC>(c, nobj, pre, v, s, log, ub - ll, false, false, tch, false);
-    } else if (sing_ll > -kInfty) {
-      rc_upd_side<RC>(c, nobj, pre, v, s, log, ub - sing_ll, false, true, tch, false);
-    }
+    const bool fin = ll > -kInfty;
+    if (fin || sing_ll > -kInfty)
+      rc_upd_side<RC>(c, base, nobj, v, s, log, ub - (fin ? ll : sing_ll), false, !fin, tch, false);
     if (tch) changed = true;
     if (++guard > 100000L) break;
   }
@@ -564,32 +550,27 @@ __device__ __forceinline__ void rc_bnds_from_obj(int nobj, const TermChunk &pre,
 // linBndTighten_ in node mode (LinearHandler.cpp:952-1045).  Returns true if
 // the row proves the node infeasible.
 template <class V>
-__device__ __forceinline__ bool lin_bnd_tighten(const TermRec *base, int nt, const TermChunk &pre, double lb,
+__device__ __forceinline__ bool lin_bnd_tighten(const TermRec *base, int nt, double lb,
                                 double ub, V &v, NodeState &s, const ModLog &log,
                                 bool &changed) {
-  double ll, uu, sing_ll = -INFINITY, sing_uu = INFINITY;
+  double ll = 0.0, uu = 0.0, sing_ll = -INFINITY, sing_uu = INFINITY;
   changed = false;
-  lf_bnds(base, nt, pre, v, ll, uu);
-  if (ll < -kInfty || uu > kInfty) sing_lf_bnds(base, nt, pre, v, sing_ll, sing_uu);
-  if (ll > ub + kETol) return true;
-  if (uu < lb - kETol) return true;
-  if (lb > -kInfty) {
-    if (uu < kInfty) {
-      upd_from_lb(base, nt, pre, v, s, log, lb, uu, false, changed, true);
-    } else if (sing_uu < kInfty) {
-      upd_from_lb(base, nt, pre, v, s, log, lb, sing_uu, true, changed, true);
+  // the two sides as in rc_lin_bnd_tighten
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (p == 0 || changed) {
+      lf_bnds(base, nt, v, ll, uu);
+      if (ll < -kInfty || uu > kInfty) sing_lf_bnds(base, nt, v, sing_ll, sing_uu);
     }
-  }
-  if (changed) {
-    lf_bnds(base, nt, pre, v, ll, uu);
-    if (ll < -kInfty || uu > kInfty) sing_lf_bnds(base, nt, pre, v, sing_ll, sing_uu);
-  }
-  if (ub < kInfty) {
-    if (ll > -kInfty) {
-      upd_from_ub(base, nt, pre, v, s, log, ub, ll, false, changed, true);
-    } else if (sing_ll > -kInfty) {
-      upd_from_ub(base, nt, pre, v, s, log, ub, sing_ll, true, changed, true);
-    }
+    if (p == 0 && (ll > ub + kETol || uu < lb - kETol)) return true;
+    const bool lo_side = p == 0;
+    const bool side_fin = lo_side ? lb > -kInfty : ub < kInfty;
+    const double act = lo_side ? uu : ll, sact = lo_side ? sing_uu : sing_ll;
+    const bool act_fin = lo_side ? act < kInfty : act > -kInfty;
+    const bool sact_fin = lo_side ? sact < kInfty : sact > -kInfty;
+    if (side_fin && (act_fin || sact_fin))
+      upd_side(base, nt, v, s, log, (lo_side ? lb : ub) - (act_fin ? act : sact), lo_side,
+               !act_fin, changed, true);
   }
   return false;
 }
@@ -598,21 +579,19 @@ __device__ __forceinline__ bool lin_bnd_tighten(const TermRec *base, int nt, con
 // change; the 100000 cap is a safety net never reached on real data (the
 // oracle uses the same cap).
 template <class V>
-__device__ __forceinline__ void bnds_from_obj(const DevLP &lp, const TermChunk &pre, V &v, NodeState &s,
+__device__ __forceinline__ void bnds_from_obj(const TermRec *orec, int nobj, V &v, NodeState &s,
                               const ModLog &log, double ub, bool &changed) {
   bool tch = true;
   long guard = 0;
   while (tch) {
     double ll, uu, sing_ll = INFINITY, sing_uu = INFINITY;
     tch = false;
-    lf_bnds(lp.orec, lp.nobj, pre, v, ll, uu);
-    if (ll < -kInfty || uu > kInfty) sing_lf_bnds(lp.orec, lp.nobj, pre, v, sing_ll, sing_uu);
+    lf_bnds(orec, nobj, v, ll, uu);
+    if (ll < -kInfty || uu > kInfty) sing_lf_bnds(orec, nobj, v, sing_ll, sing_uu);
     if (ll > ub + kETol) return;  // SolvedInfeasible, ignored by the caller
-    if (ll > -kInfty) {
-      upd_from_ub(lp.orec, lp.nobj, pre, v, s, log, ub, ll, false, tch, false);
-    } else if (sing_ll > -kInfty) {
-      upd_from_ub(lp.orec, lp.nobj, pre, v, s, log, ub, sing_ll, true, tch, false);
-    }
+    const bool fin = ll > -kInfty;
+    if (fin || sing_ll > -kInfty)
+      upd_side(orec, nobj, v, s, log, ub - (fin ? ll : sing_ll), false, !fin, tch, false);
     if (tch) changed = true;
     if (++guard > 100000L) break;
   }
@@ -621,13 +600,14 @@ __device__ __forceinline__ void bnds_from_obj(const DevLP &lp, const TermChunk &
 // tightenInts_ in node mode (LinearHandler.cpp:415-490), over the list of
 // Binary/Integer columns in ascending order.
 template <class V>
-__device__ __forceinline__ bool tighten_ints(const DevLP &lp, V &v, NodeState &s, const ModLog &log,
+__device__ __forceinline__ bool tighten_ints(const DevLP &lp, const TermRec *irec, V &v, NodeState &s, const ModLog &log,
                              bool act, bool &changed) {
   bool bad = false;  // checkBounds_ over the integer columns, after tightening
   // called with the full wave active: `act` predicates this lane's updates
   for (int c0 = 0; c0 < lp.nint; c0 += kLanes) {
     const int cnt = lp.nint - c0 < kLanes ? lp.nint - c0 : kLanes;
-    const TermChunk ch = load_terms(lp.irec + c0, cnt, v.lane);
+    // full wave active here: the column records broadcast with v_readlane
+    const TermChunk ch = load_terms(irec + c0, cnt, v.lane);
     // the columns are distinct, so the bounds of 8 of them are loaded before
     // any is written: one memory round trip per 8 columns instead of one per
     // column (the compiler cannot prove the stores do not alias later loads)
@@ -778,7 +758,6 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
   // returns of varBndsFromCons_/varBndsFromObj_ are ignored (:1630, :1637);
   // only checkBounds_ ends the loop as infeasible.
   // objective terms for varBndsFromObj_, loaded once with the full wave
-  const TermChunk opre = load_terms(lp.orec, lp.nobj < kLanes ? lp.nobj : kLanes, lane);
   bool changed = live;
   bool infeas = false;
   unsigned iters = 1;
@@ -803,21 +782,21 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
         if (!__any(mine)) continue;
         // full wave active here: load the row's first 64 terms for broadcast
         const int k0 = rl(rr.k0, q), nt = rl(rr.nt, q);
-        const TermChunk pre = load_terms(trec + k0, nt < kLanes ? nt : kLanes, lane);
+        // the row bounds broadcast here, in uniform control flow
+        const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
         if (mine) {
-          const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
           bool tch;
           v.clear(r);
           bool inf;
           // row-length classes: fewer masked slots (each costs a division)
-          if (nt <= 3) inf = rc_lin_bnd_tighten<3>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 5) inf = rc_lin_bnd_tighten<5>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 6) inf = rc_lin_bnd_tighten<6>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 11) inf = rc_lin_bnd_tighten<11>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
-          else inf = lin_bnd_tighten(trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
+          if (nt <= 3) inf = rc_lin_bnd_tighten<3>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 5) inf = rc_lin_bnd_tighten<5>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 6) inf = rc_lin_bnd_tighten<6>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 11) inf = rc_lin_bnd_tighten<11>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else inf = lin_bnd_tighten(trec + k0, nt, rlo, rhi, v, s, log, tch);
           if (inf) {
             cons_on = false;
           } else if (tch) {
@@ -827,11 +806,11 @@ __global__ __launch_bounds__(kLanes) void fbbt_linear_kernel(DevLP lp, FbbtIO io
       }
     }
     if (go && io.has_inc && lp.nobj > 0) {
-      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
-      else bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
+      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, lp.orec, v, s, log, io.inc_ub, changed);
+      else bnds_from_obj(lp.orec, lp.nobj, v, s, log, io.inc_ub, changed);
     }
     // both called with the full wave active (v_readlane broadcasts inside)
-    const bool bad = check_bounds_rest(lp, v, tighten_ints(lp, v, s, log, go, changed));
+    const bool bad = check_bounds_rest(lp, v, tighten_ints(lp, lp.irec, v, s, log, go, changed));
     if (go) infeas = bad;
   }
   if (live) {
@@ -882,9 +861,12 @@ __global__ __launch_bounds__(kLanes * kWG, 3) void fbbt_linear_persist(DevLP lp,
   v.ub = v.lb + (size_t)n * kLanes;
   v.flag = nullptr;
   // row and term records staged once into LDS
+  // row, term, objective and integer-column records staged once into LDS
   RowRec *s_rows = reinterpret_cast<RowRec *>(lds);
   TermRec *s_trec = reinterpret_cast<TermRec *>(reinterpret_cast<char *>(lds) +
                                                 (size_t)m * sizeof(RowRec));
+  TermRec *s_orec = s_trec + lp.nnz;
+  TermRec *s_irec = s_orec + lp.nobj;
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(lp.rows);
     uint4 *dst = reinterpret_cast<uint4 *>(s_rows);
@@ -892,13 +874,18 @@ __global__ __launch_bounds__(kLanes * kWG, 3) void fbbt_linear_persist(DevLP lp,
     src = reinterpret_cast<const uint4 *>(lp.trec);
     dst = reinterpret_cast<uint4 *>(s_trec);
     for (int i = threadIdx.x; i < 2 * lp.nnz; i += kLanes * kWG) dst[i] = src[i];
+    src = reinterpret_cast<const uint4 *>(lp.orec);
+    dst = reinterpret_cast<uint4 *>(s_orec);
+    for (int i = threadIdx.x; i < 2 * lp.nobj; i += kLanes * kWG) dst[i] = src[i];
+    src = reinterpret_cast<const uint4 *>(lp.irec);
+    dst = reinterpret_cast<uint4 *>(s_irec);
+    for (int i = threadIdx.x; i < 2 * lp.nint; i += kLanes * kWG) dst[i] = src[i];
   }
   __syncthreads();
   if (wave >= io.npw) return;   // the grid is rounded up to whole workgroups
   const TermRec *trec = s_trec;
   const RowRec *rows = s_rows;
   const uint64_t all_rows = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
-  const TermChunk opre = load_terms(lp.orec, lp.nobj < kLanes ? lp.nobj : kLanes, lane);
   const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 
   int node = -1;
@@ -972,20 +959,20 @@ __global__ __launch_bounds__(kLanes * kWG, 3) void fbbt_linear_persist(DevLP lp,
         const bool mine = cons_on && v.flagged(r);
         if (!__any(mine)) continue;
         const int k0 = rl(rr.k0, q), nt = rl(rr.nt, q);
-        const TermChunk pre = load_terms(trec + k0, nt < kLanes ? nt : kLanes, lane);
+        // the row bounds broadcast here, in uniform control flow
+        const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
         if (mine) {
-          const double rlo = rld(rr.lo, q), rhi = rld(rr.hi, q);
           bool tch;
           v.clear(r);
           bool inf;
-          if (nt <= 3) inf = rc_lin_bnd_tighten<3>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 5) inf = rc_lin_bnd_tighten<5>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 6) inf = rc_lin_bnd_tighten<6>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 11) inf = rc_lin_bnd_tighten<11>(nt, pre, rlo, rhi, v, s, log, tch);
-          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, pre, rlo, rhi, v, s, log, tch);
-          else inf = lin_bnd_tighten(trec + k0, nt, pre, rlo, rhi, v, s, log, tch);
+          if (nt <= 3) inf = rc_lin_bnd_tighten<3>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 4) inf = rc_lin_bnd_tighten<4>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 5) inf = rc_lin_bnd_tighten<5>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 6) inf = rc_lin_bnd_tighten<6>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 8) inf = rc_lin_bnd_tighten<8>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 11) inf = rc_lin_bnd_tighten<11>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else if (nt <= 16) inf = rc_lin_bnd_tighten<16>(nt, trec + k0, rlo, rhi, v, s, log, tch);
+          else inf = lin_bnd_tighten(trec + k0, nt, rlo, rhi, v, s, log, tch);
           if (inf) {
             cons_on = false;
           } else if (tch) {
@@ -995,10 +982,10 @@ __global__ __launch_bounds__(kLanes * kWG, 3) void fbbt_linear_persist(DevLP lp,
       }
     }
     if (go && io.has_inc && lp.nobj > 0) {
-      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, opre, v, s, log, io.inc_ub, changed);
-      else bnds_from_obj(lp, opre, v, s, log, io.inc_ub, changed);
+      if (lp.nobj <= 16) rc_bnds_from_obj<16>(lp.nobj, s_orec, v, s, log, io.inc_ub, changed);
+      else bnds_from_obj(s_orec, lp.nobj, v, s, log, io.inc_ub, changed);
     }
-    const bool bad = check_bounds_rest(lp, v, tighten_ints(lp, v, s, log, go, changed));
+    const bool bad = check_bounds_rest(lp, v, tighten_ints(lp, s_irec, v, s, log, go, changed));
     if (go) infeas = bad;
   }
 }
@@ -1023,6 +1010,10 @@ hipError_t launch_variant(const DevLP &lp, const FbbtIO &io, size_t lds, hipStre
 
 }  // namespace
 
+size_t fbbt_persist_lds(const DevLP &lp) {
+  return (size_t)lp.m * sizeof(RowRec) + (size_t)(lp.nnz + lp.nobj + lp.nint) * sizeof(TermRec);
+}
+
 size_t fbbt_lds_bytes(int n, int m) {
   return (size_t)2 * n * kLdsStride * sizeof(double) + (m > 64 ? (size_t)m * kLanes : 0);
 }
@@ -1045,7 +1036,8 @@ hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
   }
   if (io.scratch == nullptr || (!bits && io.flag_scratch == nullptr)) return hipErrorInvalidValue;
   if (variant == 3) {  // persistent refill (caller sized the grid in io.npw units)
-    if (!bits || io.next == nullptr || tab > 64 * 1024) return hipErrorInvalidValue;
+    const size_t ptab = fbbt_persist_lds(lp);
+    if (!bits || io.next == nullptr || ptab > 64 * 1024) return hipErrorInvalidValue;
     static const int wg = getenv("MGPU_FBBT_WG") ? atoi(getenv("MGPU_FBBT_WG")) : 4;
     static bool attr_set = false;
     if (!attr_set) {
@@ -1058,9 +1050,9 @@ hipError_t launch_fbbt_linear(const DevLP &lp, const FbbtIO &io, int variant,
       attr_set = true;
     }
     if (wg == 1)
-      hipLaunchKernelGGL(fbbt_linear_persist<1>, dim3(io.npw), dim3(kLanes), tab, stream, lp, io);
+      hipLaunchKernelGGL(fbbt_linear_persist<1>, dim3(io.npw), dim3(kLanes), ptab, stream, lp, io);
     else
-      hipLaunchKernelGGL(fbbt_linear_persist<4>, dim3((io.npw + 3) / 4), dim3(4 * kLanes), tab,
+      hipLaunchKernelGGL(fbbt_linear_persist<4>, dim3((io.npw + 3) / 4), dim3(4 * kLanes), ptab,
                          stream, lp, io);
     return hipGetLastError();
   }

@@ -33,12 +33,12 @@ struct alignas(16) RowRec {   // 32 B
   int32_t k0, nt;             // first term, term count
   int32_t pad0, pad1;
 };
-struct alignas(16) TermRec {  // 32 B
+struct alignas(16) TermRec {  // 32 B; a, j, isint in the first 16 B (one read in a row visit)
   double a;                   // coefficient (0 for the integer-column list)
-  uint64_t cmask;             // rows holding column j (bitmask, m <= 64)
   int32_t j;                  // column
-  int32_t cs, ce;             // CSC range of column j (m > 64)
   int32_t isint;              // column is Binary/Integer
+  uint64_t cmask;             // rows holding column j (bitmask, m <= 64)
+  int32_t cs, ce;             // CSC range of column j (m > 64)
 };
 
 // Batch-shared linear relaxation, resident in HBM after mgpu_load_lp.
@@ -326,6 +326,7 @@ int fbbt_group_waves(const DevLP &lp, int g);
 hipError_t launch_fbbt_group(const DevLP &lp, const FbbtIO &io, int g, int num_cus,
                              hipStream_t stream);
 size_t fbbt_lds_bytes(int n, int m);
+size_t fbbt_persist_lds(const DevLP &lp);   // records staged by K1's persistent kernel
 
 // ---- quadratic node FBBT (K2) ---------------------------------------------
 // One tightenQuad_ term, pre-classified on the host (QuadHandler.cpp:

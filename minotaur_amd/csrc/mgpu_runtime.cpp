@@ -428,8 +428,7 @@ int mgpu_fbbt_dev(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_
   if (variant == 0)
     variant = (fits && waves <= c->num_cus) ? 1 : (waves > 8 * c->num_cus && npw == kLanes) ? 3 : 2;
   // persistent path: bit flags (m <= 64) and records staged in 64 KiB of LDS
-  if (variant == 3 && (c->lp.m > 64 || (size_t)c->lp.m * sizeof(RowRec) +
-                                            (size_t)c->lp.nnz * sizeof(TermRec) > 64 * 1024))
+  if (variant == 3 && (c->lp.m > 64 || fbbt_persist_lds(c->lp) > 64 * 1024))
     variant = 2;
   int grid = waves;
   if (variant == 3) {

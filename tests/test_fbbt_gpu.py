@@ -125,6 +125,49 @@ def test_fbbt_large_batch_vs_oracle(ctx, inc, waves, monkeypatch):
     assert np.array_equal(r.nmods, o.nmods)
 
 
+@pytest.mark.parametrize('inc', [math.inf, 20.0])
+def test_fbbt_persistent_odd_bounds(ctx, inc, monkeypatch):
+    """The persistent kernel on boxes whose [0,1] integer columns take the
+    other values a bound can hold -- -0.0, fractions, an inverted pair,
+    values just off 0 and 1 -- against the restatement, mod log entry by
+    entry.  (Round 5 tried keeping such columns' bounds as bits in VGPRs with
+    these values as escapes; this test pinned it, DESIGN §3 K1 has why it did
+    not ship.)"""
+    p = _tls4()
+    LB, UB = random_boxes(p, 6000, 777)
+    rng = np.random.default_rng(5)
+    slots = np.nonzero(((p.vtype == 0) | (p.vtype == 1)) & (p.vlb >= 0) & (p.vub <= 1))[0]
+    odd = np.array([-0.0, 0.25, 0.5, 1 - 2 ** -52, 2 ** -60, 0.999999, 1e-7, 1.0 + 2 ** -52])
+    for b in range(LB.shape[0]):
+        for j in rng.choice(slots, size=rng.integers(0, 6), replace=False):
+            k = rng.integers(0, 4)
+            if k == 0:
+                LB[b, j] = odd[rng.integers(0, odd.size)]
+            elif k == 1:
+                UB[b, j] = odd[rng.integers(0, odd.size)]
+            elif k == 2:
+                LB[b, j], UB[b, j] = 1.0, 0.0
+            else:
+                LB[b, j] = -0.0
+                UB[b, j] = -0.0 if rng.integers(0, 2) else 0.0
+    ctx.load(p)
+    ctx.set_fbbt_variant(3)
+    monkeypatch.setenv('MGPU_FBBT_WAVES', '37')
+    try:
+        r = ctx.fbbt(LB, UB, inc, mod_cap=48)
+    finally:
+        ctx.set_fbbt_variant(0)
+    o = oracle.linear_fbbt(p, LB, UB, None if math.isinf(inc) else inc, 48, nthreads=8)
+    assert bits_equal(r.lb, o.lb) and bits_equal(r.ub, o.ub)
+    assert np.array_equal(r.infeasible, o.infeas)
+    assert np.array_equal(r.nmods, o.nmods)
+    for b in range(LB.shape[0]):
+        k = min(int(o.nmods[b]), 48)
+        assert np.array_equal(r.mod_var[b, :k], o.mod_var[b, :k])
+        assert np.array_equal(r.mod_lu[b, :k], o.mod_lu[b, :k])
+        assert bits_equal(r.mod_val[b, :k], o.mod_val[b, :k])
+
+
 def test_fbbt_global_variant_large_problem(ctx):
     """n=400 does not fit LDS: the global-scratch kernel runs automatically."""
     p = random_problem(77, n=400, m=300, density=0.02)

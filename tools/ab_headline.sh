@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of libmgpu variants on the headline (run on the GPU box from the repo
 # root): VARIANTS="base name1 name2 ..." (base = minotaur_amd/libmgpu.so,
-# others tools/_stamps/<name>/libmgpu.so from tools/variant_build.py); each
+# others tools/_stamps/<name>/libmgpu.so from tools/variant_build.py; name+VAR=1
+# adds environment settings); each
 # runs the headline twice, one JSON summary line per run.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -9,8 +10,10 @@ O=$R/gpurun_out/${TAG:-ab}; mkdir -p $O; cd $R; export TMPDIR=/tmp
 ARGS=${ARGS:---steps 10 --warmup 2 --no-cpu-baseline --no-bnb --no-qp --no-convex --no-knapsack --no-glob --no-fixed}
 for rep in 1 2; do
 for v in ${VARIANTS:-base}; do
-  if [ "$v" = base ]; then L=$R/minotaur_amd/libmgpu.so; else L=$R/tools/_stamps/$v/libmgpu.so; fi
-  MGPU_LIB=$L timeout -k 10 300 python -u bench.py $ARGS --supp-out $O/${v}_supp.json > $O/$v.json 2> $O/$v.err || { tail -5 $O/$v.err; exit 1; }
+  # a variant is a library name, optionally followed by +VAR=value env settings
+  lib=${v%%+*}; envs=""; [ "$lib" != "$v" ] && envs=$(echo "${v#*+}" | tr '+' ' ')
+  if [ "$lib" = base ]; then L=$R/minotaur_amd/libmgpu.so; else L=$R/tools/_stamps/$lib/libmgpu.so; fi
+  env $envs MGPU_LIB=$L timeout -k 10 300 python -u bench.py $ARGS --supp-out $O/${v}_supp.json > $O/$v.json 2> $O/$v.err || { tail -5 $O/$v.err; exit 1; }
   python3 -c "
 import json
 d = json.loads([l for l in open('$O/$v.json') if l.startswith('{')][-1])

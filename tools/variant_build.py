@@ -4,6 +4,8 @@ translation units reuse minotaur_amd/build/*.o).  Run a bench or probe with
 MGPU_LIB=tools/_stamps/<name>/libmgpu.so to time the variant.
 
     python tools/variant_build.py NAME FILE 'old' 'new' [FILE 'old' 'new' ...]
+
+(OLD = @FILE replaces FILE with the contents of the file at path NEW.)
 """
 import os
 import shutil
@@ -28,8 +30,11 @@ def main():
         f, old, new = edits[k:k + 3]
         p = os.path.join(src, f)
         s = open(p).read()
-        assert s.count(old) >= 1, f"{f}: pattern not found: {old!r}"
-        open(p, 'w').write(s.replace(old, new))
+        if old == '@FILE':   # replace the whole file with the file at path NEW
+            open(p, 'w').write(open(new).read())
+        else:
+            assert s.count(old) >= 1, f"{f}: pattern not found: {old!r}"
+            open(p, 'w').write(s.replace(old, new))
         changed.add(f)
     b.build()   # the reference objects are current
     objs = []
