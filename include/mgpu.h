@@ -736,8 +736,16 @@ int mgpu_quad_fbbt_dev(mgpu_ctx *ctx, int batch, const double *d_lb_in, const do
  * mgpu_lp_solve_rows), measured with hipEvents on the context stream.
  * "lp" is the whole LP call; "lp_main" its first kernel (K3P, or the only
  * one) and "lp_tail" the dense K3 re-solve of K3P's overflow list (0 when
- * K3P did not run). */
+ * K3P did not run).  With mgpu_set_qp_ktime on, "qp_potrf", "qp_trsm" and
+ * "qp_step" are the summed times of those K5 kernels over the last QP
+ * solve's interior-point iterations. */
 double mgpu_last_kernel_ms(mgpu_ctx *ctx, const char *which);
+
+/* Per-kernel event timing of K5's iteration kernels (the KKT factor, the
+ * W / Schur products, the Newton steps): on = 1 records events around each
+ * of them in every iteration (a measurement mode; the solve itself is
+ * unchanged).  Not a reference interface: the bench's per-kernel roofline. */
+int mgpu_set_qp_ktime(mgpu_ctx *ctx, int on);
 
 #ifdef __cplusplus
 }

@@ -94,6 +94,8 @@ struct mgpu_ctx {
   const DecideIO *pfi_decide = nullptr;
   bool lp_decided = false;
   double last_fbbt_ms = 0.0, last_lp_ms = 0.0, last_quad_ms = 0.0, last_qp_ms = 0.0;
+  bool qp_ktime = false;          // mgpu_set_qp_ktime
+  double last_qp_kms[3] = {0.0, 0.0, 0.0};   // K5 factor / W+Schur / step, summed
   // per-node rows (mgpu_set_node_rows): device maps csc_pos, csr_pos,
   // coef_src, row, lo_src, hi_src; K3R's per-node warm starts; host-path
   // staging of the node records

@@ -297,6 +297,12 @@ int mgpu_set_fbbt_variant(mgpu_ctx *c, int variant) {
   return MGPU_OK;
 }
 
+int mgpu_set_qp_ktime(mgpu_ctx *c, int on) {
+  if (!c) return MGPU_ERR_ARG;
+  c->qp_ktime = on != 0;
+  return MGPU_OK;
+}
+
 double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
   if (!c || !which) return -1.0;
   if (!strcmp(which, "fbbt")) {
@@ -306,6 +312,9 @@ double mgpu_last_kernel_ms(mgpu_ctx *c, const char *which) {
       c->last_fbbt_ms = ms;
     return c->last_fbbt_ms;
   }
+  if (!strcmp(which, "qp_potrf")) return c->last_qp_kms[0];
+  if (!strcmp(which, "qp_trsm")) return c->last_qp_kms[1];
+  if (!strcmp(which, "qp_step")) return c->last_qp_kms[2];
   if (!strcmp(which, "refactor")) {  // K3R of the last mgpu_lp_solve_rows
     float ms = 0.f;
     if (hipEventSynchronize(c->ev10) == hipSuccess &&

@@ -40,7 +40,10 @@ struct QpWork {
 
 size_t qp_step_lds(int np, int mp);
 hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s);
-hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s);
+// ev (optional): four events recorded before the factor kernel, after it,
+// after the W / Schur kernel and after the step kernel
+hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s,
+                               hipEvent_t *ev = nullptr);
 hipError_t launch_qp_iteration_check(const DevQP &q, const QpWork &w, hipStream_t s);
 hipError_t launch_qp_final(const DevQP &q, const QpWork &w, hipStream_t s);
 

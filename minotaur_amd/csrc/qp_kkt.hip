@@ -983,7 +983,7 @@ hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s) {
+hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s, hipEvent_t *ev) {
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipSuccess;
@@ -1012,15 +1012,18 @@ hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s) {
   // W resident in LDS when it fits (n * (m + 1) <= ~20 000)
   const bool wl = ll && trsm_lds_bytes(q.np, q.mp) <= 160 * 1024;
   hipLaunchKernelGGL(qp_prep, dim3(w.B), dim3(kT), lds_prep, s, q, w, (ll ? 0 : 1) | (wl ? 0 : 2));
+  if (ev) (void)hipEventRecord(ev[0], s);
   if (ll)
     hipLaunchKernelGGL(qp_potrf_ll, dim3(w.B), dim3(kPT), potrf_ll_lds(q.np), s, q, w);
   else
     hipLaunchKernelGGL(qp_potrf, dim3(w.B), dim3(kT), lds_potrf, s, w, q.np);
+  if (ev) (void)hipEventRecord(ev[1], s);
   if (wl)
     hipLaunchKernelGGL(qp_trsm_syrk_lds, dim3(w.B), dim3(kPT), trsm_lds_bytes(q.np, q.mp), s, q,
                        w);
   else
     hipLaunchKernelGGL(qp_trsm_syrk, dim3(w.B), dim3(kT), lds_trsm, s, w, q.np, q.mp);
+  if (ev) (void)hipEventRecord(ev[2], s);
   // the step's per-column registers: J columns per thread
   const size_t lstep = qp_step_lds(q.np, q.mp);
   if (q.np <= 2 * kT)
@@ -1031,6 +1034,7 @@ hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s) {
     hipLaunchKernelGGL(qp_step<8>, dim3(w.B), dim3(kT), lstep, s, q, w);
   else
     return hipErrorInvalidValue;   // n > 2048: mgpu_load_qp refuses it
+  if (ev) (void)hipEventRecord(ev[3], s);
   return hipGetLastError();
 }
 

@@ -18,7 +18,10 @@ struct QpState {
   int maxB = 0;
   DevBuf h_l, h_u, h_st, h_obj, h_it, h_x;  // host-path device copies
   DevBuf f_mask, f_st, f_obj, f_it;          // the tree's feasibility LPs
+  std::vector<hipEvent_t> kev;               // mgpu_set_qp_ktime: 4 per iteration
   void release() {
+    for (hipEvent_t e : kev) (void)hipEventDestroy(e);
+    kev.clear();
     for (DevBuf *p : {&Q, &c, &A, &AT, &b, &l, &u, &x, &zl, &zu, &y, &rd, &rp, &K, &W, &WT, &M,
                       &done, &iters, &status, &obj, &h_l, &h_u, &h_st, &h_obj, &h_it, &h_x,
                       &f_mask, &f_st, &f_obj, &f_it})
@@ -122,8 +125,15 @@ int qp_solve_nodes(mgpu_ctx *c, int batch, const double *lb, const double *ub,
   HIPCHK(c, launch_qp_init(s.dq, w, c->stream));
   const int lim = maxit > 0 ? maxit : 80;
   std::vector<int32_t> hd(batch);
+  if (c->qp_ktime && s.kev.size() < (size_t)4 * lim) {
+    const size_t have = s.kev.size();
+    s.kev.resize((size_t)4 * lim, nullptr);
+    for (size_t e = have; e < s.kev.size(); ++e) HIPCHK(c, hipEventCreate(&s.kev[e]));
+  }
+  int nit = 0;
   for (int it = 0; it < lim; ++it) {
-    HIPCHK(c, launch_qp_iteration(s.dq, w, c->stream));
+    HIPCHK(c, launch_qp_iteration(s.dq, w, c->stream, c->qp_ktime ? &s.kev[(size_t)4 * it] : nullptr));
+    nit = it + 1;
     if (it % 4 == 3) {  // stop once every node has converged
       HIPCHK(c, hipMemcpyAsync(hd.data(), w.done, (size_t)batch * 4, hipMemcpyDeviceToHost,
                                c->stream));
@@ -137,6 +147,16 @@ int qp_solve_nodes(mgpu_ctx *c, int batch, const double *lb, const double *ub,
   HIPCHK(c, launch_qp_iteration_check(s.dq, w, c->stream));
   HIPCHK(c, launch_qp_final(s.dq, w, c->stream));
   HIPCHK(c, hipEventRecord(c->ev7, c->stream));
+  if (c->qp_ktime) {   // per-kernel sums over the iterations (measurement mode)
+    HIPCHK(c, hipEventSynchronize(s.kev[(size_t)4 * nit - 1]));
+    for (int k = 0; k < 3; ++k) c->last_qp_kms[k] = 0.0;
+    for (int it = 0; it < nit; ++it)
+      for (int k = 0; k < 3; ++k) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, s.kev[(size_t)4 * it + k], s.kev[(size_t)4 * it + k + 1]));
+        c->last_qp_kms[k] += ms;
+      }
+  }
   HIPCHK(c, hipMemcpyAsync(status, w.status, (size_t)batch * 4, hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(obj, w.obj, (size_t)batch * 8, hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(iters, w.iters, (size_t)batch * 4, hipMemcpyDeviceToDevice, c->stream));

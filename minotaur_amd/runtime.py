@@ -30,6 +30,7 @@ EXPORTS = [
     'mgpu_create', 'mgpu_destroy', 'mgpu_last_error', 'mgpu_set_stream',
     'mgpu_get_stream', 'mgpu_sync', 'mgpu_load_lp', 'mgpu_fbbt', 'mgpu_fbbt_dev',
     'mgpu_set_fbbt_variant', 'mgpu_set_lp_variant', 'mgpu_set_lp_pfi', 'mgpu_last_kernel_ms',
+    'mgpu_set_qp_ktime',
     'mgpu_lp_solve', 'mgpu_lp_solve_dev',
     'mgpu_node_decide_dev', 'mgpu_load_quad', 'mgpu_quad_rows', 'mgpu_quad_fbbt',
     'mgpu_quad_fbbt_dev', 'mgpu_lp_bound', 'mgpu_lp_bound_dev', 'mgpu_bnb_init',
@@ -183,6 +184,7 @@ def load_library():
     lib.mgpu_ws_read.argtypes = [_P, _I, _P, _P, _P, _P]
     lib.mgpu_ws_write.argtypes = [_P, _I, _P, _P, _P, _P]
     lib.mgpu_lp_solve1.argtypes = [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]
+    lib.mgpu_set_qp_ktime.argtypes = [_P, _I]
     lib.mgpu_last_kernel_ms.argtypes = [_P, ctypes.c_char_p]
     lib.mgpu_last_kernel_ms.restype = _D
     for name in EXPORTS:
@@ -345,6 +347,11 @@ class Context:
         if k < 0:
             raise MgpuError(f"mgpu_lp_pfi_cap failed ({k})")
         return int(k)
+
+    def set_qp_ktime(self, on):
+        """Per-kernel event timing of K5's iteration kernels (last_kernel_ms
+        'qp_potrf' / 'qp_trsm' / 'qp_step')."""
+        self._chk(self.lib.mgpu_set_qp_ktime(self.h, 1 if on else 0), 'mgpu_set_qp_ktime')
 
     def set_fbbt_variant(self, v: int):
         self._chk(self.lib.mgpu_set_fbbt_variant(self.h, int(v)), 'mgpu_set_fbbt_variant')
