@@ -729,11 +729,14 @@ def qp_relaxation(ctx, dev, rank, world, args, B=1024, reps=3):
     return out
 
 
-def qp_tree(ctx, dev, rank, world, args, B=256, max_rounds=12):
+def qp_tree(ctx, dev, rank, world, args, B=256, max_rounds=200):
     """Supplementary (config 4 as a path): branch-and-bound over
     QP relaxations of color_lab2_4x0 -- every round pops B nodes, K1 FBBT on
     the equality rows, K5 (MFMA KKT) on the node QPs, decision + MaxVio
-    branching, children pushed -- for a bounded number of rounds."""
+    branching, children pushed -- for a bounded number of rounds.  200
+    depth-first rounds reach leaves: the run finds incumbents and prunes by
+    bound (12 rounds, round 4's bound, branched every node and found none;
+    tools/qp_tree_probe.py)."""
     import torch
     from minotaur_amd import qp as qpm
     P = qpm.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'color_lab2_qp.npz'))
