@@ -612,12 +612,17 @@ __global__ __launch_bounds__(kPT) void qp_trsm_syrk_lds(DevQP q, QpWork w) {
 struct StepSm {
   double *v, *dx, *s2;
   double *tt, *dy;
-  double *Lm;     // [mp][mp+1]
+  double *Lm;     // lower triangle of [mp][mp], packed by rows (lt(i, j), j <= i)
   double *pre;    // [2][12][17] partial row sums (double-buffered)
   double *dt;     // [2][16][17] diagonal tiles of L
   double *xt;     // [2][16][17] the tiles between consecutive diagonal tiles
   double *red;    // [kT] (aliases pre: never live at the same time)
 };
+// packed lower-triangle index: the Schur factor takes mp (mp + 1) / 2
+// doubles of LDS instead of mp (mp + 1), so four step workgroups fit a CU
+// instead of two (the same values, the same operations)
+__device__ __forceinline__ int lt(int i, int j) { return i * (i + 1) / 2 + j; }
+
 template <int J>
 struct StepReg {   // column j = threadIdx.x + k * kT, k < J
   double x[J], l[J], u[J], zl[J], zu[J], rd[J], dzl[J], dzu[J], rl[J], ru[J];
@@ -762,17 +767,16 @@ __device__ void kkt_solve(const double *K, const double *W, const double *WT, co
   // pivot value broadcast by v_readlane; same operations in the same order
   // as the column sweeps through LDS they replace)
   if (t < 64) {
-    const int mpad = mp + 1;
     double val = t < mp ? s.tt[t] : 0.0;
     for (int k = 0; k < mp; ++k) {
-      const double zk = rld(val, k) / s.Lm[k * mpad + k];
+      const double zk = rld(val, k) / s.Lm[lt(k, k)];
       if (t == k) val = zk;
-      else if (t > k && t < mp) val -= s.Lm[t * mpad + k] * zk;
+      else if (t > k && t < mp) val -= s.Lm[lt(t, k)] * zk;
     }
     for (int k = mp - 1; k >= 0; --k) {
-      const double zk = rld(val, k) / s.Lm[k * mpad + k];
+      const double zk = rld(val, k) / s.Lm[lt(k, k)];
       if (t == k) val = zk;
-      else if (t < k) val -= s.Lm[k * mpad + t] * zk;
+      else if (t < k) val -= s.Lm[lt(k, t)] * zk;
     }
     if (t < mp) s.dy[t] = val;
   }
@@ -818,12 +822,12 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   extern __shared__ double sm[];
   const int b = blockIdx.x, t = threadIdx.x;
   if (w.done[b]) return;
-  const int np = q.np, mp = q.mp, mpad = mp + 1;
+  const int np = q.np, mp = q.mp;
   StepSm s;
   double *p = sm;
   s.v = p; p += np; s.dx = p; p += np; s.s2 = p; p += np;
   s.tt = p; p += mp; s.dy = p; p += mp;
-  s.Lm = p; p += mp * mpad; s.pre = p; p += 2 * 204; s.dt = p; p += 2 * 272;
+  s.Lm = p; p += mp * (mp + 1) / 2; s.pre = p; p += 2 * 204; s.dt = p; p += 2 * 272;
   s.xt = p; p += 2 * 272;
   s.red = s.pre;   // kT = 256 <= 408 doubles
   double *r1 = s.s2;  // reuse: r1 is consumed by fwd_L before s2 is written
@@ -849,22 +853,22 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   double dmax = 0.0;
   for (int e = t; e < mp * mp; e += kT) {
     const int i = e / mp, j = e % mp;
-    s.Lm[i * mpad + j] = M[e];
+    if (j <= i) s.Lm[lt(i, j)] = M[e];
     if (i == j) dmax = fmax(dmax, M[e]);
   }
   dmax = block_max(dmax, s.red);
-  for (int i = t; i < mp; i += kT) s.Lm[i * mpad + i] += kQpReg * (1.0 + dmax);
+  for (int i = t; i < mp; i += kT) s.Lm[lt(i, i)] += kQpReg * (1.0 + dmax);
   __syncthreads();
   for (int k = 0; k < mp; ++k) {
-    if (t == 0) s.Lm[k * mpad + k] = sqrt(s.Lm[k * mpad + k]);
+    if (t == 0) s.Lm[lt(k, k)] = sqrt(s.Lm[lt(k, k)]);
     __syncthreads();
-    const double dk = s.Lm[k * mpad + k];
-    for (int i = k + 1 + t; i < mp; i += kT) s.Lm[i * mpad + k] /= dk;
+    const double dk = s.Lm[lt(k, k)];
+    for (int i = k + 1 + t; i < mp; i += kT) s.Lm[lt(i, k)] /= dk;
     __syncthreads();
     const int nt = mp - k - 1;
     for (int e = t; e < nt * nt; e += kT) {
       const int i = k + 1 + e / nt, j = k + 1 + e % nt;
-      if (j <= i) s.Lm[i * mpad + j] -= s.Lm[i * mpad + k] * s.Lm[j * mpad + k];
+      if (j <= i) s.Lm[lt(i, j)] -= s.Lm[lt(i, k)] * s.Lm[lt(j, k)];
     }
     __syncthreads();
   }
@@ -975,7 +979,7 @@ __global__ __launch_bounds__(kT) void qp_final(DevQP q, QpWork w) {
 }  // namespace
 
 size_t qp_step_lds(int np, int mp) {
-  return sizeof(double) * ((size_t)3 * np + 2 * mp + (size_t)mp * (mp + 1) + 2 * 204 + 4 * 272);
+  return sizeof(double) * ((size_t)3 * np + 2 * mp + (size_t)mp * (mp + 1) / 2 + 2 * 204 + 4 * 272);
 }
 
 hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s) {
