@@ -38,7 +38,7 @@ struct QpWork {
   double *obj;
 };
 
-size_t qp_step_lds(int np, int mp);
+size_t qp_step_lds(int np, int mp, int m);
 hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s);
 // ev (optional): four events recorded before the factor kernel, after it,
 // after the W / Schur kernel and after the step kernel

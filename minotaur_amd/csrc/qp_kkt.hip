@@ -610,17 +610,20 @@ __global__ __launch_bounds__(kPT) void qp_trsm_syrk_lds(DevQP q, QpWork w) {
 // state (x, bounds, duals, residual, steps) lives in registers, J columns
 // per thread (StepReg), so three workgroups share a CU.
 struct StepSm {
-  double *v, *dx, *s2;
-  double *tt, *dy;
+  double *v, *dx;  // v: L^-1 r, then v + W dy in place; dx: the right-hand side, then the step
+  double *tt, *dy; // dy aliases tt (wave 0 reads tt into registers, writes dy)
   double *Lm;     // lower triangle of [mp][mp], packed by rows (lt(i, j), j <= i)
   double *pre;    // [2][12][17] partial row sums (double-buffered)
   double *dt;     // [2][16][17] diagonal tiles of L
   double *xt;     // [2][16][17] the tiles between consecutive diagonal tiles
   double *red;    // [kT] (aliases pre: never live at the same time)
 };
-// packed lower-triangle index: the Schur factor takes mp (mp + 1) / 2
-// doubles of LDS instead of mp (mp + 1), so four step workgroups fit a CU
-// instead of two (the same values, the same operations)
+// packed lower-triangle index: the Schur factor of the m real rows takes
+// m (m + 1) / 2 doubles of LDS instead of mp (mp + 1).  With the step's
+// vectors aliased (the right-hand side in dx, v + W dy in place, dy over
+// tt) a step workgroup takes 32.5 KB, so five fit a CU (two before).
+// The padded rows of M are zero, so their dy is 0 and the real rows'
+// factor and solves are the same operations as with the padding.
 __device__ __forceinline__ int lt(int i, int j) { return i * (i + 1) / 2 + j; }
 
 template <int J>
@@ -748,7 +751,7 @@ __device__ void bwd_LT(const double *K, int np, const double *sv, double *xo, co
 // dx = L^-T (v + W dy), dx = 0 on fixed variables
 template <int J>
 __device__ void kkt_solve(const double *K, const double *W, const double *WT, const double *rp,
-                          int np, int mp, const StepSm &s, const StepReg<J> &g,
+                          int np, int mp, int mr, const StepSm &s, const StepReg<J> &g,
                           const double *r1) {
   const int t = threadIdx.x;
   fwd_L(K, np, r1, s.v, s);
@@ -767,13 +770,13 @@ __device__ void kkt_solve(const double *K, const double *W, const double *WT, co
   // pivot value broadcast by v_readlane; same operations in the same order
   // as the column sweeps through LDS they replace)
   if (t < 64) {
-    double val = t < mp ? s.tt[t] : 0.0;
-    for (int k = 0; k < mp; ++k) {
+    double val = t < mr ? s.tt[t] : 0.0;
+    for (int k = 0; k < mr; ++k) {
       const double zk = rld(val, k) / s.Lm[lt(k, k)];
       if (t == k) val = zk;
-      else if (t > k && t < mp) val -= s.Lm[lt(t, k)] * zk;
+      else if (t > k && t < mr) val -= s.Lm[lt(t, k)] * zk;
     }
-    for (int k = mp - 1; k >= 0; --k) {
+    for (int k = mr - 1; k >= 0; --k) {
       const double zk = rld(val, k) / s.Lm[lt(k, k)];
       if (t == k) val = zk;
       else if (t < k) val -= s.Lm[lt(k, t)] * zk;
@@ -781,14 +784,14 @@ __device__ void kkt_solve(const double *K, const double *W, const double *WT, co
     if (t < mp) s.dy[t] = val;
   }
   __syncthreads();
-  // s2 = v + W dy  (W' [mp][np] copy: coalesced across j)
+  // v += W dy  (W' [mp][np] copy: coalesced across j; each j by one thread)
   for (int j = t; j < np; j += kT) {
     double acc = 0.0;
     for (int i = 0; i < mp; ++i) acc += WT[(size_t)i * np + j] * s.dy[i];
-    s.s2[j] = s.v[j] + acc;
+    s.v[j] = s.v[j] + acc;
   }
   __syncthreads();
-  bwd_LT(K, np, s.s2, s.dx, s);
+  bwd_LT(K, np, s.v, s.dx, s);
 #pragma unroll
   for (int k = 0; k < J; ++k) {
     const int j = t + k * kT;
@@ -822,15 +825,18 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   extern __shared__ double sm[];
   const int b = blockIdx.x, t = threadIdx.x;
   if (w.done[b]) return;
-  const int np = q.np, mp = q.mp;
+  const int np = q.np, mp = q.mp, mr = q.m;
   StepSm s;
   double *p = sm;
-  s.v = p; p += np; s.dx = p; p += np; s.s2 = p; p += np;
-  s.tt = p; p += mp; s.dy = p; p += mp;
-  s.Lm = p; p += mp * (mp + 1) / 2; s.pre = p; p += 2 * 204; s.dt = p; p += 2 * 272;
+  s.v = p; p += np; s.dx = p; p += np;
+  s.tt = p; s.dy = p; p += mp;
+  s.Lm = p; p += mr * (mr + 1) / 2; s.pre = p; p += 2 * 204; s.dt = p; p += 2 * 272;
   s.xt = p; p += 2 * 272;
   s.red = s.pre;   // kT = 256 <= 408 doubles
-  double *r1 = s.s2;  // reuse: r1 is consumed by fwd_L before s2 is written
+  // the right-hand side in dx: fwd_L consumes it before bwd_LT writes the
+  // step there, and the corrector's right-hand side reads the predictor's
+  // dx[j] in the same thread that overwrites it
+  double *r1 = s.dx;
   const size_t o = (size_t)b * np, oy = (size_t)b * mp;
   const double *K = w.K + (size_t)b * np * np;
   const double *W = w.W + (size_t)b * np * mp;
@@ -853,19 +859,19 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
   double dmax = 0.0;
   for (int e = t; e < mp * mp; e += kT) {
     const int i = e / mp, j = e % mp;
-    if (j <= i) s.Lm[lt(i, j)] = M[e];
+    if (i < mr && j <= i) s.Lm[lt(i, j)] = M[e];
     if (i == j) dmax = fmax(dmax, M[e]);
   }
   dmax = block_max(dmax, s.red);
-  for (int i = t; i < mp; i += kT) s.Lm[lt(i, i)] += kQpReg * (1.0 + dmax);
+  for (int i = t; i < mr; i += kT) s.Lm[lt(i, i)] += kQpReg * (1.0 + dmax);
   __syncthreads();
-  for (int k = 0; k < mp; ++k) {
+  for (int k = 0; k < mr; ++k) {
     if (t == 0) s.Lm[lt(k, k)] = sqrt(s.Lm[lt(k, k)]);
     __syncthreads();
     const double dk = s.Lm[lt(k, k)];
-    for (int i = k + 1 + t; i < mp; i += kT) s.Lm[lt(i, k)] /= dk;
+    for (int i = k + 1 + t; i < mr; i += kT) s.Lm[lt(i, k)] /= dk;
     __syncthreads();
-    const int nt = mp - k - 1;
+    const int nt = mr - k - 1;
     for (int e = t; e < nt * nt; e += kT) {
       const int i = k + 1 + e / nt, j = k + 1 + e % nt;
       if (j <= i) s.Lm[lt(i, j)] -= s.Lm[lt(i, k)] * s.Lm[lt(j, k)];
@@ -890,7 +896,7 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
     if (j < np) r1[j] = g.fr(k) ? -g.rd[k] - g.zl[k] + g.zu[k] : 0.0;
   }
   __syncthreads();
-  kkt_solve<J>(K, W, WT, rp, np, mp, s, g, r1);
+  kkt_solve<J>(K, W, WT, rp, np, mp, mr, s, g, r1);
 #pragma unroll
   for (int k = 0; k < J; ++k) {
     const int j = t + k * kT;
@@ -930,7 +936,7 @@ __global__ __launch_bounds__(kT) void qp_step(DevQP q, QpWork w) {
     r1[j] = fr ? -g.rd[k] + rl / sl - ru / su : 0.0;
   }
   __syncthreads();
-  kkt_solve<J>(K, W, WT, rp, np, mp, s, g, r1);
+  kkt_solve<J>(K, W, WT, rp, np, mp, mr, s, g, r1);
 #pragma unroll
   for (int k = 0; k < J; ++k) {
     const int j = t + k * kT;
@@ -978,8 +984,8 @@ __global__ __launch_bounds__(kT) void qp_final(DevQP q, QpWork w) {
 
 }  // namespace
 
-size_t qp_step_lds(int np, int mp) {
-  return sizeof(double) * ((size_t)3 * np + 2 * mp + (size_t)mp * (mp + 1) / 2 + 2 * 204 + 4 * 272);
+size_t qp_step_lds(int np, int mp, int m) {
+  return sizeof(double) * ((size_t)2 * np + mp + (size_t)m * (m + 1) / 2 + 2 * 204 + 4 * 272);
 }
 
 hipError_t launch_qp_init(const DevQP &q, const QpWork &w, hipStream_t s) {
@@ -1029,7 +1035,7 @@ hipError_t launch_qp_iteration(const DevQP &q, const QpWork &w, hipStream_t s, h
     hipLaunchKernelGGL(qp_trsm_syrk, dim3(w.B), dim3(kT), lds_trsm, s, w, q.np, q.mp);
   if (ev) (void)hipEventRecord(ev[2], s);
   // the step's per-column registers: J columns per thread
-  const size_t lstep = qp_step_lds(q.np, q.mp);
+  const size_t lstep = qp_step_lds(q.np, q.mp, q.m);
   if (q.np <= 2 * kT)
     hipLaunchKernelGGL(qp_step<2>, dim3(w.B), dim3(kT), lstep, s, q, w);
   else if (q.np <= 4 * kT)
