@@ -112,7 +112,26 @@ def host_cpu():
     return model, max(1, min(want, avail))
 
 
-def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
+def pool_rows_decode(p, rows):
+    """Migration rows of warm mode 2 ([lb | ub | bound | depth | k | path |
+    packed statuses], bnb_migrate.hip) -> (lb, ub, k_in, path_in, st_in) for
+    oracle.dual_simplex_path (the decoding of CpuBnbContext.bnb_import_rows,
+    vectorised)."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle
+    n, N = p.n, p.n + p.m
+    w = 2 * n + 2
+    k_in = rows[:, w].astype(np.int32)
+    path = rows[:, w + 1:w + 1 + oracle.PATH_MAX].astype(np.uint64).astype(np.uint32)
+    words = rows[:, w + 1 + oracle.PATH_MAX:w + 1 + oracle.PATH_MAX + (N + 15) // 16]
+    words = words.astype(np.int64)
+    j = np.arange(N)
+    st = ((words[:, j // 16] >> (2 * (j % 16))) & 3).astype(np.int8)
+    return (np.ascontiguousarray(rows[:, :n]), np.ascontiguousarray(rows[:, n:2 * n]), k_in,
+            path, st)
+
+
+def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin", pool=None):
     """Rank 0, N=1, the same node boxes on the host:
 
     * all-cores leg (the reported value): the C restatement of the FBBT
@@ -167,18 +186,77 @@ def cpu_baseline(p, LB, UB, budget_s, what_inst="tls4-lin"):
         progress(0, f"cpu baseline leg done: {tf + tl:.2f}s")
         return S, tf, tl, solved, what
 
-    S, tf, tl, solved, what = leg(T, False, 0.5 * budget_s)
-    S1, tf1, tl1, solved1, what1 = leg(1, use_ref, 0.5 * budget_s)
+    def pool_leg(budget, parent):
+        """The GPU's own next nodes after the timed rounds (the work its next
+        rounds would do), every LP warm-started either from the node's parent
+        basis as K3P starts it (basis difference from the root rebuilt by
+        column replacement, product form with the same eta cap, dense
+        continuation past it) or from the root basis."""
+        rows, inc, cap = pool
+        lb, ub, k_in, path, st = pool_rows_decode(p, rows)
+        inc_ = inc if math.isfinite(inc) else None
+
+        def run_pool(idx):
+            t0 = time.perf_counter()
+            f = oracle.linear_fbbt(p, lb[idx], ub[idx], inc_, nthreads=T)
+            t1 = time.perf_counter()
+            keep = f.infeas == 0
+            ki = idx[keep]
+            if parent:
+                oracle.dual_simplex_path(p, f.lb[keep], f.ub[keep], ws, k_in[ki], path[ki],
+                                         st[ki], cap, min(32, cap), nthreads=T, want_x=False)
+            else:
+                oracle.dual_simplex(p, f.lb[keep], f.ub[keep], ws, nthreads=T)
+            return t1 - t0, time.perf_counter() - t1, int(keep.sum())
+        probe = np.arange(min(256 * T, lb.shape[0]))
+        a, b, _ = run_pool(probe)
+        per = (a + b) / len(probe)
+        S = int(min(64 * lb.shape[0], max(len(probe), budget / max(per, 1e-9))))
+        progress(0, f"cpu baseline pool leg ({T} threads, parent={parent}): probe "
+                    f"{len(probe)} nodes {a + b:.2f}s -> sample {S}")
+        tf, tl, solved = run_pool(np.arange(S) % lb.shape[0])
+        progress(0, f"cpu baseline pool leg done: {tf + tl:.2f}s")
+        return S, tf, tl, solved, lb.shape[0]
+
     fb1 = ('the reference LinearHandler::presolveNode (oracle/_ref)' if use_ref
            else 'the C restatement')
+    if pool is not None and pool[0] is not None and len(pool[0]):
+        # the GPU's own next nodes, both warm starts; the value is the faster
+        # (the host's best choice: the restatement's column-replacement
+        # rebuild of a parent basis costs more on a CPU than the pivots it saves)
+        legs = {}
+        for parent in (True, False):
+            Sp, tfp, tlp, solvedp, npool = pool_leg(0.3 * budget_s, parent)
+            legs[parent] = {
+                "value": Sp / (tfp + tlp), "unit": "nodes/s", "cores": T,
+                "relaxations_per_s": solvedp / (tfp + tlp),
+                "sample": (f"{Sp} nodes: the {npool} next open nodes of the GPU's own pool "
+                           f"after the timed rounds (cycled), {T} threads (OpenMP over nodes): "
+                           f"FBBT by the C restatement (bit-identical to the reference) "
+                           f"{tfp:.2f}s, then {solvedp} LPs by the dual-simplex restatement "
+                           f"(Clp absent) warm-started from "
+                           + ("the parent basis each node carries, as K3P starts them "
+                              "(column replacement from the root inverse, product form, the "
+                              "same eta cap)" if parent else "the root basis")
+                           + f" {tlp:.2f}s")}
+        S1, tf1, tl1, solved1, what1 = leg(1, use_ref, 0.4 * budget_s)
+        best = legs[True] if legs[True]["value"] >= legs[False]["value"] else legs[False]
+        head = dict(best, kind="port", cpu_model=model,
+                    parent_warm=legs[True], root_warm=legs[False])
+    else:
+        S, tf, tl, solved, what = leg(T, False, 0.5 * budget_s)
+        S1, tf1, tl1, solved1, what1 = leg(1, use_ref, 0.5 * budget_s)
+        head = {
+            "value": S / (tf + tl), "unit": "nodes/s", "cores": T, "kind": "port",
+            "cpu_model": model,
+            "sample": (f"{what} ({what_inst}), {T} threads (OpenMP over nodes): FBBT by the C "
+                       f"restatement (bit-identical to the reference) {tf:.2f}s, then {solved} "
+                       f"root-warm-started LPs by the dual-simplex restatement (Clp absent) "
+                       f"{tl:.2f}s"),
+            "relaxations_per_s": solved / (tf + tl),
+        }
     return {
-        "value": S / (tf + tl), "unit": "nodes/s", "cores": T, "kind": "port",
-        "cpu_model": model,
-        "sample": (f"{what} ({what_inst}), {T} threads (OpenMP over nodes): FBBT by the C "
-                   f"restatement (bit-identical to the reference) {tf:.2f}s, then {solved} "
-                   f"root-warm-started LPs by the dual-simplex restatement (Clp absent) "
-                   f"{tl:.2f}s"),
-        "relaxations_per_s": solved / (tf + tl),
+        **head,
         "one_core": {
             "value": S1 / (tf1 + tl1), "unit": "nodes/s", "cores": 1,
             "kind": "reference" if use_ref else "port",
@@ -878,9 +956,18 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
     # device allocations inside the timed loop (0 at N = 1; at N > 1 the first
     # rebalance sizes its row buffers)
     summary["device_allocs_timed"] = int(a1[0] - a0[0])
+    # after the timed rounds: the next nodes of this pool, with the parent
+    # bases they carry, for the CPU baseline (exported and imported back)
+    pool_sample = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.warm == 2:
+        lbs = ctx.bnb_pick(args.cpu_pool_nodes)
+        if len(lbs):
+            rows = ctx.bnb_export_rows(np.arange(len(lbs)))
+            pool_sample = rows.cpu().numpy()
+            ctx.bnb_import_rows(rows)
     return {"elapsed": tot, "nodes": nodes, "lps": lps, "kernels": kernels,
             "summary": summary, "incumbent": state["inc"],
-            "rccl_ms": float(np.sum(acc["rccl_ms"]))}
+            "rccl_ms": float(np.sum(acc["rccl_ms"])), "pool_sample": pool_sample}
 
 
 def fixed_batch(ctx, dev, rank, world, args, reps=10):
@@ -975,6 +1062,9 @@ def compact_line(args, world, B, p, h, elapsed, nodes, lps, roofline, kernels, c
               "relaxations_per_s": _r(cpu["relaxations_per_s"]),
               "one_core": {k: (_r(v) if k != "sample" else v[:200])
                            for k, v in cpu["one_core"].items()}}
+        for key in ("parent_warm", "root_warm"):
+            if key in cpu:
+                cb[key] = _r(cpu[key]["value"])
         rt = cpu.get("reference_tree_one_core")
         if rt:
             cb["reference_tree_one_core"] = {"value": _r(rt["value"]), "nodes": rt["nodes"],
@@ -1111,6 +1201,9 @@ def main():
                     help='N > 1: rebalance the open nodes across the ranks every this many '
                          'headline rounds (dist.rebalance; 0 = never)')
     ap.add_argument('--cpu-seconds', type=float, default=16.0)
+    ap.add_argument('--cpu-pool-nodes', type=int, default=65536,
+                    help="open nodes (with their parent bases) exported after the headline's "
+                         "timed rounds for the all-cores CPU baseline")
     ap.add_argument('--tree-cpu-seconds', type=float, default=3.0,
                     help="time_limit of each tree_search entry's one-core reference tree")
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -1222,7 +1315,8 @@ def main():
                                 "2m(n+m) flops per pivot K3P ran / its HIP-event time")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(p, LB, UB, args.cpu_seconds, "tls4-oa")
+            cpu = cpu_baseline(p, LB, UB, args.cpu_seconds, "tls4-oa",
+                               pool=(h["pool_sample"], h["incumbent"], args.eta_cap))
             # the same instance's tree on one core by the reference's own
             # BranchAndBound (nodes/s like value; not the same node boxes)
             cpu["reference_tree_one_core"] = tree_cpu_baseline(p, 0, 2 * args.tree_cpu_seconds)

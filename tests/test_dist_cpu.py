@@ -277,3 +277,36 @@ def test_engine_lb_deal_equals_restatement(world, S):
     assert o1.tolist() == o2.tolist()
     assert l1.tolist() == l2.tolist()
     assert r1.tolist() == r2.tolist()
+
+
+def test_bench_pool_rows_decode_equals_restatement():
+    """bench.py's CPU baseline decodes the headline pool's warm-mode-2 rows
+    (the parent basis each node carries) vectorised; the result equals the
+    restatement's own per-row import (CpuBnbContext.bnb_import_rows)."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+    import bench
+    from bnb import CpuBnbContext
+    from minotaur_amd.problem import random_mkp
+    p = random_mkp(2, 18, 3)
+    ctx = CpuBnbContext(p, 32)          # product form, 32 etas (K3P's)
+    ctx.bnb_config(0, 2)
+    ctx.bnb_brancher(0)
+    ctx.bnb_init(1 << 12)
+    for _ in range(5):
+        ctx.bnb_round(8)
+    lbs = ctx.bnb_pick(12)
+    picked = [ctx.pool[ctx.pick[i]] for i in range(len(lbs))]
+    rows = ctx.bnb_export_rows(list(range(len(lbs)))).numpy()
+    lb, ub, k_in, path, st = bench.pool_rows_decode(p, rows)
+    assert any(int(k) > 0 for k in k_in)
+    for t, nd in enumerate(picked):
+        assert np.array_equal(lb[t], nd.lb) and np.array_equal(ub[t], nd.ub)
+        if nd.path is None or int(nd.path[0]) == 0:
+            assert k_in[t] == 0
+            continue
+        k, pv, sv = nd.path
+        assert k_in[t] == k
+        assert np.array_equal(path[t, :k], np.asarray(pv, dtype=np.uint32)[:k])
+        assert np.array_equal(st[t], np.asarray(sv, dtype=np.int8) & 3)
