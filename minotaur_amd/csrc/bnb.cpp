@@ -289,17 +289,21 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
     io.wo_binv = s.ch_binv.as<double>();
     io.wo_index = s.cnode.as<int32_t>();
     io.node_list = s.sblist.as<int32_t>();
-    io.node_count = s.sbcnt.as<int32_t>();
     io.list_lo = 0;
     io.list_hi = 0x7fffffff;
     io.iter_limit = kRelIterLimit;
     io.status = s.cst.as<int32_t>();
     io.obj = s.cobj.as<double>();
     io.iters = s.cit.as<int32_t>();
-    for (int step = 0; step < 2 * h_tot[3]; ++step) {
-      HIPCHK(c, hipMemsetAsync(s.sbcnt.p, 0, 4, c->stream));
+    // one list counter per chain step, zeroed together (one fill per round
+    // instead of one per step: the rounds of a reliability tree are short)
+    const int nsteps = 2 * h_tot[3];
+    HIPCHK(c, s.sbcnt.ensure((size_t)(nsteps > 4 ? nsteps : 4) * 4));
+    if (nsteps > 0) HIPCHK(c, hipMemsetAsync(s.sbcnt.p, 0, (size_t)nsteps * 4, c->stream));
+    for (int step = 0; step < nsteps; ++step) {
+      io.node_count = s.sbcnt.as<int32_t>() + step;
       HIPCHK(c, launch_rel_chain_list(r, step, s.sbstop.as<uint8_t>(), s.sblist.as<int32_t>(),
-                                      s.sbcnt.as<int32_t>(), c->stream));
+                                      s.sbcnt.as<int32_t>() + step, c->stream));
       const int lrc = launch_lp_nodes(c, io);
       if (lrc != MGPU_OK) return lrc;
       if (step & 1)

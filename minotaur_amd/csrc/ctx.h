@@ -68,6 +68,7 @@ struct mgpu_ctx {
   DevBuf io_lb_in, io_ub_in, io_lb_out, io_ub_out, io_inf, io_nmods, io_mv, io_ml, io_mval;
   DevBuf scratch, flag_scratch;
   DevBuf fbbt_next;            // K1 persistent variant: node queue head
+  DevBuf lp_next3;             // K3's self-resetting node counter [next, exited waves]
   int fbbt_variant = 0;
   int bnb_relax = 0;          // mgpu_bnb_relaxation: 0 LP (K3P/K3/K3L), 1 QP (K5)
   int lp_variant = 0;          // 0 auto, 1 K3 (m <= 64), 2 K3L, 3 K3P

@@ -236,7 +236,19 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     nsolve = *io.node_count;
     if (nsolve > io.list_hi) nsolve = io.list_hi;
   }
-  if (lo + (int)blockIdx.x * W >= nsolve) return;
+  // self-resetting node counter: every wave counts itself out, the last one
+  // zeroes the counter for the next launch on the stream (no fill kernel)
+  auto leave = [&]() {
+    if (io.next_exit != nullptr && lane0 == 0 &&
+        atomicAdd(io.next_exit, 1) == (int)gridDim.x * W - 1) {
+      atomicExch(io.next, 0);
+      atomicExch(io.next_exit, 0);
+    }
+  };
+  if (lo + (int)blockIdx.x * W >= nsolve) {
+    leave();
+    return;
+  }
 
   // ---- stage the constraint matrix (CSC + CSR) once per workgroup ----
   unsigned char *p = smem;
@@ -758,6 +770,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     }
     STAMP(9);
   }
+  leave();
   STAMP_FLUSH
 }
 

@@ -142,6 +142,9 @@ struct LpIO {
   // null = iter_base); the iteration limit and the Bland switch count them
   const int32_t *iter_base_list;
   int32_t *next;                // K3L: zeroed device node counter (dynamic schedule) or null
+  // K3 only: next[1] counts exited waves; the last one zeroes next[0..1],
+  // so the counter needs no fill before the next launch (null: not used)
+  int32_t *next_exit;
   // Path warm starts (K3P only; path.k == null: none).  Node b starts from
   // the shared warm start (the root basis) after its k[b] pivots path[b]
   // (entering column | row << 16, stride kPathMax) with column statuses

@@ -64,7 +64,7 @@ int mgpu_destroy(mgpu_ctx *c) {
                     &c->lp_ost, &c->lp_od, &c->lp_ob, &c->lp_slots, &c->io_lb_in,
                     &c->io_ub_in, &c->io_lb_out, &c->io_ub_out, &c->io_inf, &c->io_nmods,
                     &c->io_mv, &c->io_ml, &c->io_mval, &c->scratch, &c->flag_scratch,
-                    &c->fbbt_next, &c->nr_map, &c->nr_ws, &c->nr_vals, &c->pfi_piv})
+                    &c->fbbt_next, &c->lp_next3, &c->nr_map, &c->nr_ws, &c->nr_vals, &c->pfi_piv})
     b->release();
   for (auto &ch : c->ws_chunks)
     if (ch.base) (void)hipFree(ch.base);
@@ -740,10 +740,15 @@ int launch_lp(mgpu_ctx *c, const LpIO &io, const char *who) {
   if (!use_large_lp(c)) {
     if (c->lp.m > kLpMaxM || lp_lds_bytes(c->lp.n, c->lp.m, c->lp.nnz) > 160 * 1024)
       return fail(c, MGPU_ERR_ARG, "%s: problem too large for K3 (m=%d)", who, c->lp.m);
-    HIPCHK(c, c->lp_next.ensure(sizeof(int32_t)));  // dynamic node schedule
-    HIPCHK(c, hipMemsetAsync(c->lp_next.p, 0, sizeof(int32_t), c->stream));
+    // dynamic node schedule: a counter of its own that the kernel leaves
+    // zeroed (filled once, when allocated)
+    if (c->lp_next3.p == nullptr) {
+      HIPCHK(c, c->lp_next3.ensure(2 * sizeof(int32_t)));
+      HIPCHK(c, hipMemsetAsync(c->lp_next3.p, 0, 2 * sizeof(int32_t), c->stream));
+    }
     LpIO iod = io;
-    iod.next = c->lp_next.as<int32_t>();
+    iod.next = c->lp_next3.as<int32_t>();
+    iod.next_exit = c->lp_next3.as<int32_t>() + 1;
     HIPCHK(c, launch_lp_dual(c->lp, iod, c->num_cus, c->stream));
     return MGPU_OK;
   }
