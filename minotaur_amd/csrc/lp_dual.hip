@@ -201,7 +201,21 @@ __device__ __forceinline__ double compute_primals(const Ctx &C, const double (&b
   double w = 0.0;
   const int k = C.lane;
   if (k < C.m) {
-    for (int t = C.rowptr[k]; t < C.rowptr[k + 1]; ++t) {
+    // four entries' loads in flight (column, then its status and value),
+    // the adds in CSR order as before
+    int t = C.rowptr[k];
+    const int e = C.rowptr[k + 1];
+    for (; t + 4 <= e; t += 4) {
+      const int j0 = C.ccol[t], j1 = C.ccol[t + 1], j2 = C.ccol[t + 2], j3 = C.ccol[t + 3];
+      const double r0 = C.rval[t], r1 = C.rval[t + 1], r2 = C.rval[t + 2], r3 = C.rval[t + 3];
+      const int8_t s0 = C.st[j0], s1 = C.st[j1], s2 = C.st[j2], s3 = C.st[j3];
+      const double z0 = C.z[j0], z1 = C.z[j1], z2 = C.z[j2], z3 = C.z[j3];
+      if (s0 != ST_BASIC && z0 != 0.0) w += r0 * z0;
+      if (s1 != ST_BASIC && z1 != 0.0) w += r1 * z1;
+      if (s2 != ST_BASIC && z2 != 0.0) w += r2 * z2;
+      if (s3 != ST_BASIC && z3 != 0.0) w += r3 * z3;
+    }
+    for (; t < e; ++t) {
       const int j = C.ccol[t];
       if (C.st[j] == ST_BASIC) continue;
       const double zj = C.z[j];
