@@ -302,6 +302,12 @@ int mgpu_bnb_rebalance(mgpu_ctx *c, int S, double *picked, int *npicked, double 
   if (rc != MGPU_OK) return rc;
   if (picked) std::memcpy(picked, vec.data(), (size_t)k * 8);
   if (npicked) *npicked = k;
+  if (P == 1) {   // solo: the deal keeps every node where it is
+    if (nreceived) *nreceived = 0;
+    if (moved) *moved = 0;
+    if (open_after) *open_after = open;
+    return MGPU_OK;
+  }
   vec[(size_t)S] = (double)spare;
   // 2. one all-gather of the bounds and the pool room (:107)
   std::vector<double> g((size_t)P * (S + 1));
@@ -355,8 +361,7 @@ int mgpu_bnb_rebalance(mgpu_ctx *c, int S, double *picked, int *npicked, double 
   if (nreceived) *nreceived = (int)got_at.size();
   const int W = mgpu_bnb_row_width(c);
   if (W < 0) return W;
-  CommState local_state;
-  CommState &s = c->comm ? *c->comm : local_state;
+  CommState &s = *c->comm;   // P > 1: a communicator is set
   const size_t rowb = (size_t)W * 8;
   const int ks = (int)idx.size(), kr = (int)got_at.size();
   HIPCHK(c, hipSetDevice(c->device));
