@@ -70,12 +70,17 @@ def lp_flops(p, pivots, solves):
     return pivots * per_pivot + solves * per_solve
 
 
-def pmc_traffic(kernel, batch, tree=False):
+def pmc_traffic(kernel, batch, eta_cap, tree=False):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3
-    FETCH_SIZE/WRITE_SIZE passes of this same bench at the same batch; tree:
-    summaries of the tree-round headline, marked "workload": "tree_rounds")."""
+    FETCH_SIZE/WRITE_SIZE passes of this same bench at the same batch and
+    eta cap; tree: summaries of the tree-round headline, marked "workload":
+    "tree_rounds").  Returns (bytes, file, fresh): fresh is True when the
+    summary's source digest equals this tree's engine sources, False when
+    the counters were taken on other code (reported as stale), None when the
+    summary predates the digest."""
     import glob
+    from minotaur_amd.build import source_digest
     keys = {'fbbt': ('fbbt_linear_persist', 'fbbt_linear_kernel'), 'lp_dual': ('lp_dual_kernel',),
             'lp_pfi': ('lp_pfi_kernel',)}[kernel]
     for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')), reverse=True):
@@ -87,11 +92,16 @@ def pmc_traffic(kernel, batch, tree=False):
             continue
         args = d.get("bench_args", "").split()
         b = int(args[args.index('--batch') + 1]) if '--batch' in args else 65536
+        cap = int(args[args.index('--eta-cap') + 1]) if '--eta-cap' in args else PFI_DEFAULT
+        if b != batch or cap != eta_cap:
+            continue
         for key in keys:
             k = d.get("kernels", {}).get(key)
-            if b == batch and k and k.get("hbm_bytes_per_launch"):
-                return k["hbm_bytes_per_launch"], os.path.basename(f)
-    return None, None
+            if k and k.get("hbm_bytes_per_launch"):
+                dig = d.get("source_digest")
+                return (k["hbm_bytes_per_launch"], os.path.basename(f),
+                        None if dig is None else dig == source_digest())
+    return None, None, None
 
 
 def host_cpu():
@@ -1304,12 +1314,15 @@ def main():
         kernels = h["kernels"]
         dom = max(("fbbt", "lp_pfi"), key=lambda k: kernels[k]["ms"])
         kd = kernels[dom]
-        traffic, tsrc = pmc_traffic(dom, B, tree=True)
+        traffic, tsrc, fresh = pmc_traffic(dom, B, args.eta_cap, tree=True)
         roofline = {"kernel": dom, "bound": "hbm" if dom == "fbbt" else "fp64",
                     "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
                     "frac": kd["frac"], "traffic": traffic}
         if tsrc:
-            roofline["traffic_source"] = f"profiles/{tsrc} (PMC, bytes per launch)"
+            roofline["traffic_source"] = (f"profiles/{tsrc} (PMC, bytes per launch; " +
+                                          {True: "same engine sources)",
+                                           False: "STALE: measured on other engine sources)",
+                                           None: "engine sources not recorded)"}[fresh])
         if dom != "fbbt":
             roofline["note"] = ("FP64 VALU (no MFMA: per-node pivots); achieved = SURVEY 8(d) "
                                 "2m(n+m) flops per pivot K3P ran / its HIP-event time")

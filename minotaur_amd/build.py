@@ -28,6 +28,22 @@ def lib_path():
     return os.path.join(HERE, 'libmgpu.so')
 
 
+def source_digest():
+    """sha256 (first 16 hex digits) over the engine's sources and headers:
+    tools/pmc_summary.py stores it with a PMC summary and bench.py compares
+    it, so counters measured on other code are reported as stale."""
+    import hashlib
+    h = hashlib.sha256()
+    names = sorted(SOURCES + [f for f in os.listdir(CSRC) if f.endswith('.h')])
+    for name in names:
+        h.update(name.encode())
+        with open(os.path.join(CSRC, name), 'rb') as fh:
+            h.update(fh.read())
+    with open(os.path.join(ROOT, 'include', 'mgpu.h'), 'rb') as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def build(verbose=False, jobs=None):
     """Compile every translation unit to an object (in parallel, objects
     under build/) and link libmgpu.so; no-op when it is up to date."""

@@ -50,7 +50,10 @@ def main(src, tag, bench_args):
                 ctr[k][r['Counter_Name']].append(float(r['Counter_Value']))
     # the bench's headline since round 3 is the tree round (bench.py
     # tree_rounds); bench.pmc_traffic matches summaries by this key
-    res = {"bench_args": bench_args, "workload": "tree_rounds", "kernels": {}}
+    sys.path.insert(0, ROOT)
+    from minotaur_amd.build import source_digest
+    res = {"bench_args": bench_args, "workload": "tree_rounds",
+           "source_digest": source_digest(), "kernels": {}}
     for k in sorted(set(dur) | set(ctr)):
         d = dur.get(k, [])
         fe = ctr[k].get('FETCH_SIZE', [])
