@@ -110,6 +110,7 @@ constexpr int kRelMinDist = 50;
 constexpr double kRelETol = 1e-6;
 constexpr int kRelMaxDepth = 1000;   // maxDepth_: deeper nodes are not strong-branched (:105)
 constexpr int kRelEvents = 1 + 2 * kRelMaxCands;   // pseudocost observations per node
+static_assert(2 * kRelMaxCands <= 64, "rel_decide: one lane per strong-branching LP");
 struct RelIO {
   int nb, n;
   const uint8_t *vtype;         // [n]

@@ -163,7 +163,13 @@ __device__ __forceinline__ void wave_max_key(double &v, double &u, int &j) {
 
 // One wave per node: the candidates are spread over the lanes (column j of
 // lane j % 64); every selection is a wave reduction over (score, index) keys,
-// the same keys and the same order as the reference's serial scans.
+// the same keys and the same order as the reference's serial scans.  The keys
+// are computed once into registers (kPrepSlots columns per lane; the
+// repeated selection then reads no memory) and the owner lane of each chosen
+// column writes it: the selection loop is register work and DPP reductions,
+// not up to 20 rounds of dependent global loads.
+constexpr int kPrepSlots = 4;   // n <= 256 keeps the keys in registers
+
 __global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -181,31 +187,82 @@ __global__ __launch_bounds__(256) void rel_prepare(RelIO io) {
     const int maxcnt = io.depth[b] > kRelMaxDepth ? 0 : kRelMaxCands;
     double ps = -INFINITY;
     int pj = -1;
-    for (int k = 0; k < maxcnt; ++k) {
-      double bs = INFINITY;
-      int bj = INT_MAX;
-      for (int j = lane; j < io.n; j += 64) {
-        if (!is_int(io.vtype[j])) continue;
-        const double v = x[j];
-        if (!fractional(v)) continue;
-        const PcView pv = pc_view(io, j, own, ov, os, oc);
-        if (reliable(io, j, calls, pv)) continue;
-        const double sc = unrel_score(pv, v - floor(v), ceil(v) - v);
-        const bool after = sc > ps || (sc == ps && j > pj);
-        if (after && (sc < bs || (sc == bs && j < bj))) {
-          bs = sc;
-          bj = j;
+    if (io.n <= 64 * kPrepSlots) {
+      bool cand[kPrepSlots];
+      double key[kPrepSlots], xv[kPrepSlots];
+#pragma unroll
+      for (int t = 0; t < kPrepSlots; ++t) {
+        const int j = lane + 64 * t;
+        cand[t] = false;
+        key[t] = 0.0;
+        xv[t] = 0.0;
+        if (j < io.n && maxcnt > 0 && is_int(io.vtype[j])) {
+          const double v = x[j];
+          if (fractional(v)) {
+            const PcView pv = pc_view(io, j, own, ov, os, oc);
+            if (!reliable(io, j, calls, pv)) {
+              cand[t] = true;
+              key[t] = unrel_score(pv, v - floor(v), ceil(v) - v);
+              xv[t] = v;
+            }
+          }
         }
       }
-      wave_min_key(bs, bj);
-      if (bj == INT_MAX) break;
-      if (lane == 0) {
-        io.sb_var[(size_t)b * kRelMaxCands + k] = bj;
-        io.sb_val[(size_t)b * kRelMaxCands + k] = x[bj];
+      for (int k = 0; k < maxcnt; ++k) {
+        double bs = INFINITY;
+        int bj = INT_MAX;
+#pragma unroll
+        for (int t = 0; t < kPrepSlots; ++t) {
+          const int j = lane + 64 * t;
+          const double sc = key[t];
+          const bool after = sc > ps || (sc == ps && j > pj);
+          if (cand[t] && after && (sc < bs || (sc == bs && j < bj))) {
+            bs = sc;
+            bj = j;
+          }
+        }
+        wave_min_key(bs, bj);
+        if (bj == INT_MAX) break;
+        if ((bj & 63) == lane) {   // the column's own lane holds its value
+          const int t = bj >> 6;
+          double v = xv[0];
+#pragma unroll
+          for (int u = 1; u < kPrepSlots; ++u)
+            if (u == t) v = xv[u];
+          io.sb_var[(size_t)b * kRelMaxCands + k] = bj;
+          io.sb_val[(size_t)b * kRelMaxCands + k] = v;
+        }
+        ++nsb;
+        ps = bs;
+        pj = bj;
       }
-      ++nsb;
-      ps = bs;
-      pj = bj;
+    } else {
+      for (int k = 0; k < maxcnt; ++k) {
+        double bs = INFINITY;
+        int bj = INT_MAX;
+        for (int j = lane; j < io.n; j += 64) {
+          if (!is_int(io.vtype[j])) continue;
+          const double v = x[j];
+          if (!fractional(v)) continue;
+          const PcView pv = pc_view(io, j, own, ov, os, oc);
+          if (reliable(io, j, calls, pv)) continue;
+          const double sc = unrel_score(pv, v - floor(v), ceil(v) - v);
+          const bool after = sc > ps || (sc == ps && j > pj);
+          if (after && (sc < bs || (sc == bs && j < bj))) {
+            bs = sc;
+            bj = j;
+          }
+        }
+        wave_min_key(bs, bj);
+        if (bj == INT_MAX) break;
+        if (lane == 0) {
+          io.sb_var[(size_t)b * kRelMaxCands + k] = bj;
+          io.sb_val[(size_t)b * kRelMaxCands + k] = x[bj];
+        }
+        ++nsb;
+        ps = bs;
+        pj = bj;
+      }
     }
   }
   if (lane == 0) {
@@ -347,12 +404,21 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
     int status = 0;   // 0 NotModified, 1 Pruned, 2 Modified
     int mvar = -1, mup = 0;
     int ran = 0;       // candidates strong-branched (the loop stops at a verdict)
+    // lane k holds candidate k's column, value and verdict (loaded together,
+    // not one dependent round trip per candidate)
+    int lj = 0, loc = 0;
+    double lv = 0.0, lcd = 0.0, lcu = 0.0;
+    if (lane < nsb) {
+      lj = io.sb_var[(size_t)b * kRelMaxCands + lane];
+      lv = io.sb_val[(size_t)b * kRelMaxCands + lane];
+      loc = sb_outcome(io, off, lane, objval, maxchange, lcd, lcu);
+    }
     for (int k = 0; k < nsb; ++k) {
-      const int j = io.sb_var[(size_t)b * kRelMaxCands + k];
-      const double v = io.sb_val[(size_t)b * kRelMaxCands + k];
+      const int j = rl(lj, k);
+      const double v = rld(lv, k);
       const double dd = v - floor(v), ud = ceil(v) - v;
-      double cd, cu;
-      const int oc2 = sb_outcome(io, off, k, objval, maxchange, cd, cu);
+      const double cd = rld(lcd, k), cu = rld(lcu, k);
+      const int oc2 = rl(loc, k);
       ran = k + 1;
       if (oc2 < 0) {
         // an unreliable side: no verdict, no observation
@@ -447,11 +513,14 @@ __global__ __launch_bounds__(256) void rel_decide(RelIO io) {
         atomicAdd(&io.counters[2], 1ull);
       }
     }
-    if (ran > 0 && lane == 0) {  // the LPs the reference solves: up to the verdict
-      unsigned long long piv = 0;
-      for (int c = 0; c < 2 * ran; ++c) piv += (unsigned long long)io.c_iters[off + c];
-      atomicAdd(&io.counters[0], (unsigned long long)(2 * ran));
-      atomicAdd(&io.counters[3], piv);
+    if (ran > 0) {  // the LPs the reference solves: up to the verdict
+      unsigned long long piv = lane < 2 * ran ? (unsigned long long)io.c_iters[off + lane] : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) piv += __shfl_xor(piv, o, 64);
+      if (lane == 0) {
+        atomicAdd(&io.counters[0], (unsigned long long)(2 * ran));
+        atomicAdd(&io.counters[3], piv);
+      }
     }
   }
   if (lane == 0) {
