@@ -561,4 +561,126 @@ int integ_obbt(int device, const QSpecI *sp, int has_inc, double inc, double *ou
   return 0;
 }
 
+
+// ---- the reference's own spatial branch-and-bound (Glob's tree) -----------
+// QuadHandler whose fixNodeErr (PCBProcessor.cpp:311-314, NoCandToBranch)
+// does what the batched glob tree does there -- closes the node without a
+// solution -- and counts it: the reference calls an NLP engine here
+// (QuadHandler.cpp:356-420), and none is in the image.
+class NoNlpQuadHandler : public QuadHandler {
+ public:
+  NoNlpQuadHandler(EnvPtr env, ProblemPtr p, ProblemPtr orig) : QuadHandler(env, p, orig) {}
+  int fixNodeErr(RelaxationPtr, ConstSolutionPtr, SolutionPoolPtr, bool &sol_found) {
+    sol_found = false;
+    ++closed;
+    return 0;
+  }
+  long long closed = 0;
+};
+
+// Glob::createBab_ (Glob.cpp:134-220) over the QCQP's auxiliary form: the
+// original rows with every product replaced by its aux y (LinearHandler),
+// y = x0 x1 for each product (QuadHandler: McCormick rows, presolveNode,
+// isFeasible, spatial candidates), IntVarHandler; PCBProcessor, NodeIncRelaxer
+// (parent warm starts), MaxVioBrancher, HipLPEngine for the LPs (Clp is
+// absent; device < 0: CpuLPEngine).  Root OBBT off (the batched tree does none; "OBBT",
+// Environment.cpp:326), tree_search as given (0 dfs, 1 bfs), every other
+// option at its default (obj_gap_percent 0: the tree runs to completion).
+// res[0] UB, res[1] LB, res[2] seconds; cnt[0] nodes processed, cnt[1]
+// nodes created, cnt[2] LP solves, cnt[3] nodes closed at NoCandToBranch.
+int integ_glob_tree(int device, const QSpecI *sp, int bfs, double *res, long long *cnt) {
+  const QSpecI &s = *sp;
+  EnvPtr env = (EnvPtr) new Environment();
+  int err = 0;
+  env->startTimer(err);
+  env->getOptions()->findString("tree_search")->setValue(bfs ? "bfs" : "dfs");
+  env->getOptions()->findBool("OBBT")->setValue(false);
+  ProblemPtr orig = (ProblemPtr) new Problem(env);
+  for (int j = 0; j < s.nv0; ++j) orig->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
+  for (int c = 0; c < s.ncon; ++c) orig->newConstraint(qfun(s, orig, c), s.clb[c], s.cub[c]);
+  if (s.has_obj) orig->newObjective(qfun(s, orig, s.ncon), s.obj_const, Minimize);
+  else orig->newObjective((FunctionPtr) new Function((LinearFunctionPtr) new LinearFunction()),
+                          s.obj_const, Minimize);
+  orig->calculateSize();
+  ProbeBranchAndBound *bab = nullptr;
+  ProblemPtr p = (ProblemPtr) new Problem(env);
+  for (int j = 0; j < s.nv; ++j) p->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
+  auto yof = [&](int a, int b) {
+    for (int k = 0; k < s.nsq; ++k)
+      if (a == s.sq_x[k] && b == s.sq_x[k]) return s.sq_y[k];
+    for (int k = 0; k < s.nbil; ++k)
+      if (a == s.bil_x0[k] && b == s.bil_x1[k]) return s.bil_y[k];
+    return -1;
+  };
+  auto ylin = [&](int c) {
+    LinearFunctionPtr lf = (LinearFunctionPtr) new LinearFunction();
+    for (int k = s.lptr[c]; k < s.lptr[c + 1]; ++k) lf->incTerm(p->getVariable(s.lvar[k]), s.lval[k]);
+    for (int k = s.qptr[c]; k < s.qptr[c + 1]; ++k)
+      lf->incTerm(p->getVariable(yof(s.qv1[k], s.qv2[k])), s.qval[k]);
+    return lf;
+  };
+  for (int c = 0; c < s.ncon; ++c)
+    p->newConstraint((FunctionPtr) new Function(ylin(c)), s.clb[c], s.cub[c]);
+  if (s.has_obj) p->newObjective((FunctionPtr) new Function(ylin(s.ncon)), s.obj_const, Minimize);
+  else p->newObjective((FunctionPtr) new Function((LinearFunctionPtr) new LinearFunction()),
+                       s.obj_const, Minimize);
+  NoNlpQuadHandler *qh = new NoNlpQuadHandler(env, p, orig);
+  auto add_aux = [&](int x0, int x1, int y) {
+    LinearFunctionPtr lf = (LinearFunctionPtr) new LinearFunction();
+    lf->addTerm(p->getVariable(y), -1.0);
+    QuadraticFunctionPtr qf = (QuadraticFunctionPtr) new QuadraticFunction();
+    qf->addTerm(p->getVariable(x0), p->getVariable(x1), 1.0);
+    qh->addConstraint(p->newConstraint((FunctionPtr) new Function(lf, qf), 0.0, 0.0));
+  };
+  for (int k = 0; k < s.nsq; ++k) add_aux(s.sq_x[k], s.sq_x[k], s.sq_y[k]);
+  for (int k = 0; k < s.nbil; ++k) add_aux(s.bil_x0[k], s.bil_x1[k], s.bil_y[k]);
+  p->calculateSize();
+  bab = new ProbeBranchAndBound(env, p);
+  HandlerVector handlers;
+  IntVarHandlerPtr v_hand = (IntVarHandlerPtr) new IntVarHandler(env, p);
+  LinearHandlerPtr l_hand = (LinearHandlerPtr) new LinearHandler(env, p);
+  handlers.push_back(v_hand);
+  handlers.push_back(l_hand);
+  handlers.push_back(qh);
+  v_hand->setModFlags(false, true);
+  l_hand->setModFlags(false, true);
+  qh->setModFlags(false, true);
+  // device < 0: CpuLPEngine (the C restatement of the dual simplex), for CPU runs
+  LPEnginePtr e = device < 0 ? (LPEnginePtr) new CpuLPEngine(env)
+                             : (LPEnginePtr) new HipLPEngine(env, device);
+  PCBProcessorPtr nproc = (PCBProcessorPtr) new PCBProcessor(env, e, handlers);
+  MaxVioBrancherPtr br = (MaxVioBrancherPtr) new MaxVioBrancher(env, handlers);
+  nproc->setBrancher(br);
+  bab->setNodeProcessor(nproc);
+  NodeIncRelaxerPtr nr = (NodeIncRelaxerPtr) new NodeIncRelaxer(env, handlers);
+  nr->setProblem(p);
+  nr->setEngine(e);
+  nr->setModFlag(false);
+  bab->setNodeRelaxer(nr);
+  bab->shouldCreateRoot(true);
+  bab->setLogLevel(LogNone);
+  const auto t0 = std::chrono::steady_clock::now();
+  bab->solve();
+  res[2] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  res[0] = bab->getUb();
+  res[1] = bab->getLb();
+  cnt[0] = bab->nodesProcessed();
+  cnt[1] = (long long)bab->getTreeManager()->getSize();
+  std::vector<double> lps(6, 0.0);
+  e->fillStats(lps);
+  cnt[2] = (long long)lps[0];
+  cnt[3] = qh->closed;
+  delete v_hand;
+  delete l_hand;
+  delete qh;
+  delete e;
+  delete nproc;
+  delete nr;
+  delete bab;
+  delete p;
+  delete orig;
+  delete env;
+  return 0;
+}
+
 }  // extern "C"
