@@ -578,6 +578,16 @@ class NoNlpQuadHandler : public QuadHandler {
   long long closed = 0;
 };
 
+// LinearHandler without node presolve (flags bit 1): the batched glob
+// round runs no linear FBBT at its nodes
+class NoPresolveLinearHandler : public LinearHandler {
+ public:
+  NoPresolveLinearHandler(EnvPtr env, ProblemPtr p) : LinearHandler(env, p) {}
+  bool presolveNode(RelaxationPtr, NodePtr, SolutionPoolPtr, ModVector &, ModVector &) {
+    return false;
+  }
+};
+
 // Glob::createBab_ (Glob.cpp:134-220) over the QCQP's auxiliary form: the
 // original rows with every product replaced by its aux y (LinearHandler),
 // y = x0 x1 for each product (QuadHandler: McCormick rows, presolveNode,
@@ -588,13 +598,18 @@ class NoNlpQuadHandler : public QuadHandler {
 // option at its default (obj_gap_percent 0: the tree runs to completion).
 // res[0] UB, res[1] LB, res[2] seconds; cnt[0] nodes processed, cnt[1]
 // nodes created, cnt[2] LP solves, cnt[3] nodes closed at NoCandToBranch.
-int integ_glob_tree(int device, const QSpecI *sp, int bfs, double *res, long long *cnt) {
+// bfs: tree_search bfs (else dfs); flags bit 1: LinearHandler without node
+// presolve.  pres_freq: PCBProcessor's node-presolve frequency (reference
+// default 5, Environment.cpp:364).
+int integ_glob_tree2(int device, const QSpecI *sp, int bfs, int flags, int pres_freq, double *res,
+                     long long *cnt) {
   const QSpecI &s = *sp;
   EnvPtr env = (EnvPtr) new Environment();
   int err = 0;
   env->startTimer(err);
   env->getOptions()->findString("tree_search")->setValue(bfs ? "bfs" : "dfs");
   env->getOptions()->findBool("OBBT")->setValue(false);
+  env->getOptions()->findInt("pres_freq")->setValue(pres_freq);
   ProblemPtr orig = (ProblemPtr) new Problem(env);
   for (int j = 0; j < s.nv0; ++j) orig->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
   for (int c = 0; c < s.ncon; ++c) orig->newConstraint(qfun(s, orig, c), s.clb[c], s.cub[c]);
@@ -638,7 +653,8 @@ int integ_glob_tree(int device, const QSpecI *sp, int bfs, double *res, long lon
   bab = new ProbeBranchAndBound(env, p);
   HandlerVector handlers;
   IntVarHandlerPtr v_hand = (IntVarHandlerPtr) new IntVarHandler(env, p);
-  LinearHandlerPtr l_hand = (LinearHandlerPtr) new LinearHandler(env, p);
+  LinearHandlerPtr l_hand = (flags & 2) ? (LinearHandlerPtr) new NoPresolveLinearHandler(env, p)
+                                        : (LinearHandlerPtr) new LinearHandler(env, p);
   handlers.push_back(v_hand);
   handlers.push_back(l_hand);
   handlers.push_back(qh);
@@ -681,6 +697,11 @@ int integ_glob_tree(int device, const QSpecI *sp, int bfs, double *res, long lon
   delete orig;
   delete env;
   return 0;
+}
+
+// Glob's defaults: LinearHandler presolve, pres_freq 5
+int integ_glob_tree(int device, const QSpecI *sp, int bfs, double *res, long long *cnt) {
+  return integ_glob_tree2(device, sp, bfs, 0, 5, res, cnt);
 }
 
 }  // extern "C"

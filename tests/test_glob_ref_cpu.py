@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from minotaur_amd.quad import random_qcqp
-from test_glob_ref_gpu import CASES
+from test_glob_ref_gpu import ALIGNED, CASES
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), '..'))
 LIB = os.path.join(ROOT, 'oracle', '_ref', 'libminotaur_hip_integ.so')
@@ -25,25 +25,26 @@ def integ():
     if not os.path.exists(LIB):
         pytest.skip("integration library not built (needs /root/reference at build time)")
     lib = ctypes.CDLL(LIB, mode=os.RTLD_LAZY | os.RTLD_GLOBAL)
-    lib.integ_glob_tree.argtypes = [ctypes.c_int, P, ctypes.c_int, P, P]
+    lib.integ_glob_tree2.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     P, P]
     return lib
 
 
-@pytest.mark.parametrize('seed,nv0,ncon', CASES)
-def test_glob_restatement_optimum_equals_reference_tree(integ, seed, nv0, ncon):
-    import oracle
+CPU_CASES = [(c, 1, False) for c in CASES] + [(c, b[-1], True) for c, b in ALIGNED]
+
+
+@pytest.mark.parametrize('case,batch,aligned', CPU_CASES)
+def test_glob_restatement_optimum_equals_reference_tree(integ, case, batch, aligned):
     from glob_tree import CpuGlobContext
+    from test_glob_ref_gpu import ref_glob_tree
+    seed, nv0, ncon = case
     qp = random_qcqp(seed, nv0=nv0, ncon=ncon, squares=False)
-    spec = oracle.qspec(qp)
-    res = np.zeros(3)
-    cnt = np.zeros(4, dtype=np.int64)
-    assert integ.integ_glob_tree(-1, ctypes.byref(spec), 1, res.ctypes.data_as(P),
-                                 cnt.ctypes.data_as(P)) == 0
+    res, cnt = ref_glob_tree(integ, qp, aligned, device=-1)
     ub, proc, closed = res[0], int(cnt[0]), int(cnt[3])
     cpu = CpuGlobContext(qp)
     cpu.glob_init(1 << 16)
     for _ in range(100000):
-        st = cpu.glob_round(1)
+        st = cpu.glob_round(batch)
         if st.open == 0:
             break
     obj, x = cpu.glob_best()
