@@ -280,6 +280,40 @@ __device__ __forceinline__ bool tighten_row_(const RowRec &R, const TermRec *tre
   return true;
 }
 
+// A row of at most H terms in two phases, for the paired-row walk below:
+// phase 1 loads it into the slots and takes its activity bounds, and returns
+// its verdict (false: the row proves the node infeasible) before any bound
+// moves; phase 2 is the rest of linBndTighten_ (tighten_row_<H, true>'s
+// operations in its order).
+template <int H>
+__device__ __forceinline__ bool row_phase1(const RowRec &R, const TermRec *trec, GNode &s, int gl,
+                                           int g, Slot &sl, double &ll, double &uu, double &sll,
+                                           double &suu) {
+  const TermRec *t0 = trec + R.k0;
+  sl = slot_load(t0, 0, R.nt, gl, s);
+  activity<H, true>(t0, R.nt, s, gl, g, sl, ll, uu, sll, suu);
+  return !(ll > R.hi + kETol) && !(uu < R.lo - kETol);
+}
+
+template <int H>
+__device__ __forceinline__ void row_phase2(const RowRec &R, const TermRec *trec, GNode &s, int gl,
+                                           int g, Slot &sl, double ll, double uu, double sll,
+                                           double suu) {
+  const TermRec *t0 = trec + R.k0;
+  bool ch = false;
+  if (R.lo > -kInfty) {
+    if (uu < kInfty) ch = update_pass<H, true>(t0, R.nt, s, sl, true, R.lo, uu, false, true, gl, g);
+    else if (suu < kInfty) ch = update_pass<H, true>(t0, R.nt, s, sl, true, R.lo, suu, true, true, gl, g);
+  }
+  if (ch) activity<H, true>(t0, R.nt, s, gl, g, sl, ll, uu, sll, suu);
+  bool ch2 = false;
+  if (R.hi < kInfty) {
+    if (ll > -kInfty) ch2 = update_pass<H, true>(t0, R.nt, s, sl, false, R.hi, ll, false, true, gl, g);
+    else if (sll > -kInfty) ch2 = update_pass<H, true>(t0, R.nt, s, sl, false, R.hi, sll, true, true, gl, g);
+  }
+  if (ch || ch2) s.changed = true;
+}
+
 template <int G>
 __device__ __forceinline__ bool tighten_row(const RowRec &R, const TermRec *trec, GNode &s,
                                             int gl, int g) {
@@ -388,6 +422,24 @@ __global__ __launch_bounds__(64 * kMaxW) void fbbt_group_kernel(DevLP lp, FbbtIO
   __syncthreads();
   const GTab T{s_rows, s_trec, s_orec, s_irec, s_ccont};
 
+  // Rows r and r + 1 that can be tightened at once, one per half of a
+  // node's lanes (G = 16): both of at most G / 2 terms, no column in common.
+  // Row r then cannot flag row r + 1, and their bound updates touch
+  // different columns, so the pair gives the sequential walk's result.
+  uint64_t pairs = 0ull;
+  if constexpr (G == 16) {
+    bool ok = false;
+    if (lane + 1 < m) {
+      const RowRec ra = s_rows[lane], rb = s_rows[lane + 1];
+      if (ra.nt <= G / 2 && rb.nt <= G / 2) {
+        uint64_t cols = 0ull;
+        for (int k = 0; k < ra.nt; ++k) cols |= s_trec[ra.k0 + k].cmask;
+        ok = ((cols >> (lane + 1)) & 1ull) == 0ull;
+      }
+    }
+    pairs = __ballot(ok);
+  }
+
   // ---- this lane's node ----
   double2 *nb = (double2 *)(p + (size_t)(wave * kNG + g) * node_bytes(n, G));
   const long b = ((long)blockIdx.x * W + wave) * kNG + g;
@@ -425,7 +477,46 @@ __global__ __launch_bounds__(64 * kMaxW) void fbbt_group_kernel(DevLP lp, FbbtIO
       un &= r >= 63 ? 0ull : (~0ull << (r + 1));
       if (un == 0ull) break;
       r = __builtin_ctzll(un);
-      if (!cut && ((s.flags >> r) & 1ull)) {
+      if (G == 16 && ((pairs >> r) & 1ull) && ((un >> (r + 1)) & 1ull)) {
+        // rows r (lanes 0..7 of each node) and r + 1 (lanes 8..15) at once;
+        // each half works on a copy of the node's state, merged after
+        constexpr int H = G / 2;
+        const int hg = lane / H, hl = lane & (H - 1);
+        const bool inB = gl >= H;
+        const bool fA = !cut && ((s.flags >> r) & 1ull);
+        const bool fB = !cut && ((s.flags >> (r + 1)) & 1ull);
+        if (fA) s.flags &= ~(1ull << r);
+        if (fB) s.flags &= ~(1ull << (r + 1));
+        GNode h = s;
+        if (inB) h.P = s.P + H;   // the upper half's product slots
+        const RowRec &R = T.rows[inB ? r + 1 : r];
+        const bool act = inB ? fB : fA;
+        Slot sl{0.0, 0ull, 0, false, false, {0.0, 0.0}};
+        double ll = 0.0, uu = 0.0, sll = 0.0, suu = 0.0;
+        bool feas = true;
+        if (act) feas = row_phase1<H>(R, T.trec, h, hl, hg, sl, ll, uu, sll, suu);
+        wave_sync();
+        // row r's verdict (lane 0 of the node): an infeasible row r ends the
+        // node's walk before row r + 1, as in the sequential walk
+        const int a_inf = __shfl((act && !feas) ? 1 : 0, lane & ~(G - 1), 64);
+        if (act && feas && !(inB && a_inf))
+          row_phase2<H>(R, T.trec, h, hl, hg, sl, ll, uu, sll, suu);
+        wave_sync();
+        const int b_inf = __shfl((act && !feas) ? 1 : 0, (lane & ~(G - 1)) + H, 64);
+        const int dm = h.nmods - s.nmods, dn = (int)(h.nint - s.nint);
+        const int om = __shfl_xor(dm, H, 64), on = __shfl_xor(dn, H, 64);
+        const int oc = __shfl_xor(h.changed ? 1 : 0, H, 64);
+        s.flags = group_or<G>(h.flags);
+        // row r proved the node infeasible: row r + 1 was not visited and
+        // keeps its flag (simplePresolve ignores the verdict, :1620-1650, so
+        // the next sweep visits it)
+        if (a_inf && fB) s.flags |= 1ull << (r + 1);
+        s.nmods += dm + om;
+        s.nint += (unsigned)(dn + on);
+        s.changed = h.changed || oc != 0;
+        if (a_inf || (b_inf && fB)) cut = true;
+        r = r + 1;
+      } else if (!cut && ((s.flags >> r) & 1ull)) {
         s.flags &= ~(1ull << r);
         if (!tighten_row<G>(T.rows[r], T.trec, s, gl, g)) cut = true;
       }
