@@ -269,7 +269,8 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
     // runs them: every LP from the node's chain slot (its optimal basis, then
     // whatever basis the last optimal / iteration-limited LP left) and back
     // into it; ReliabilityBrancher's iteration cap; after each candidate's
-    // pair the nodes with a verdict stop
+    // pair the nodes with a verdict stop (the next step's list kernel takes
+    // the verdict before it lists the step's LPs)
     const LpWarm node_ws{s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), s.wo_d.as<double>(),
                          s.wo_binv.as<double>(), m, N, N, (long)m * m};
     HIPCHK(c, launch_rel_chain_init(r, node_ws, s.ch_head.as<int32_t>(), s.ch_st.as<int8_t>(),
@@ -306,8 +307,6 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
                                       s.sbcnt.as<int32_t>() + step, c->stream));
       const int lrc = launch_lp_nodes(c, io);
       if (lrc != MGPU_OK) return lrc;
-      if (step & 1)
-        HIPCHK(c, launch_rel_chain_stop(r, step >> 1, s.sbstop.as<uint8_t>(), c->stream));
     }
   }
   HIPCHK(c, launch_rel_decide(r, c->stream));

@@ -157,9 +157,8 @@ struct RelIO {
 hipError_t launch_rel_chain_init(const RelIO &io, const LpWarm &node_ws, int32_t *ch_head,
                                  int8_t *ch_st, double *ch_d, double *ch_binv, uint8_t *stopped,
                                  int m, hipStream_t stream);
-hipError_t launch_rel_chain_list(const RelIO &io, int s, const uint8_t *stopped, int32_t *list,
+hipError_t launch_rel_chain_list(const RelIO &io, int s, uint8_t *stopped, int32_t *list,
                                  int32_t *count, hipStream_t stream);
-hipError_t launch_rel_chain_stop(const RelIO &io, int c, uint8_t *stopped, hipStream_t stream);
 hipError_t launch_rel_rank(const RelIO &io, int32_t *flag, int32_t *rank, int32_t *total,
                            hipStream_t stream);
 hipError_t launch_rel_prepare(const RelIO &io, int32_t *sb_off, int32_t *total,

@@ -556,20 +556,26 @@ __global__ __launch_bounds__(256) void rel_chain_init(RelIO io, LpWarm w, int32_
   for (size_t k = lane; k < mm; k += 64) ch_binv[(size_t)b * mm + k] = w.binv[b * w.s_binv + k];
 }
 
-__global__ __launch_bounds__(256) void rel_chain_list(RelIO io, int s, const uint8_t *stopped,
+// step s's list; at an even step s >= 2 first the verdict of candidate
+// s / 2 - 1, whose pair of LPs the two previous steps ran (findBestCandidate_
+// stops strong-branching there, ReliabilityBrancher.cpp:111-118).  The
+// verdict after the last pair is not needed: rel_decide stops at it itself.
+__global__ __launch_bounds__(256) void rel_chain_list(RelIO io, int s, uint8_t *stopped,
                                                       int32_t *list, int32_t *count) {
   const int b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= io.nb || stopped[b] || s >= 2 * io.nsb[b]) return;
+  if (b >= io.nb) return;
+  bool stop = stopped[b] != 0;
+  const int c = (s >> 1) - 1;
+  if (!stop && s >= 2 && (s & 1) == 0 && c < io.nsb[b]) {
+    const double objval = io.obj[b];
+    double cd, cu;
+    if (sb_outcome(io, 2 * (size_t)io.sb_off[b], c, objval, io.cutoff - objval, cd, cu) > 0) {
+      stopped[b] = 1;
+      stop = true;
+    }
+  }
+  if (stop || s >= 2 * io.nsb[b]) return;
   list[atomicAdd(count, 1)] = 2 * io.sb_off[b] + s;
-}
-
-__global__ __launch_bounds__(256) void rel_chain_stop(RelIO io, int c, uint8_t *stopped) {
-  const int b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= io.nb || stopped[b] || c >= io.nsb[b]) return;
-  const double objval = io.obj[b];
-  double cd, cu;
-  if (sb_outcome(io, 2 * (size_t)io.sb_off[b], c, objval, io.cutoff - objval, cd, cu) > 0)
-    stopped[b] = 1;
 }
 
 // the round's observations packed in node order (offsets: excl_scan of nev)
@@ -658,18 +664,11 @@ hipError_t launch_rel_chain_init(const RelIO &io, const LpWarm &node_ws, int32_t
   return hipGetLastError();
 }
 
-hipError_t launch_rel_chain_list(const RelIO &io, int s, const uint8_t *stopped, int32_t *list,
+hipError_t launch_rel_chain_list(const RelIO &io, int s, uint8_t *stopped, int32_t *list,
                                  int32_t *count, hipStream_t stream) {
   if (io.nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(rel_chain_list, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io, s,
                      stopped, list, count);
-  return hipGetLastError();
-}
-
-hipError_t launch_rel_chain_stop(const RelIO &io, int c, uint8_t *stopped, hipStream_t stream) {
-  if (io.nb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rel_chain_stop, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io, c,
-                     stopped);
   return hipGetLastError();
 }
 
