@@ -86,6 +86,9 @@ struct BnbState {
   long long next_id = 0;
   bool guided = true;          // IntVarHandler guided_dive (Environment.cpp:160-163)
   DevBuf cslots;               // [2 nb] child slots
+  // grow-only workspaces of the migration path (shard, export, import), so a
+  // rebalance inside a timed multi-GPU run allocates nothing once warm
+  DevBuf mw_slots, mw_ft, mw_tmp, mw_tlb, mw_tub, mw_tnlb, mw_tdep;
   std::vector<int> pick;       // mgpu_bnb_pick: pool slots of the picked nodes, in pick order
   std::vector<DevBuf *> bufs() {
     return {&plb, &pub, &pnlb, &pdepth, &wlb, &wub, &inf, &nm, &st, &obj, &it, &x,
@@ -98,7 +101,8 @@ struct BnbState {
                       &nsb, &sb_off, &sb_var, &sb_val, &dec2, &nev, &ev_var, &ev_side, &ev_cost,
                       &rcnt, &clb, &cub, &cnode, &cst, &cobj, &cit, &ev_off, &cv_var, &cv_side,
                       &cv_cost, &ppk, &ppath, &ppst, &bpk, &bppath, &bpst, &opk, &oppath, &opst,
-                      &cslots, &ch_head, &ch_st, &ch_d, &ch_binv, &sbstop, &sblist, &sbcnt};
+                      &cslots, &ch_head, &ch_st, &ch_d, &ch_binv, &sbstop, &sblist, &sbcnt,
+                      &mw_slots, &mw_ft, &mw_tmp, &mw_tlb, &mw_tub, &mw_tnlb, &mw_tdep};
   }
   void release() {
     for (DevBuf *b : bufs()) b->release();
@@ -952,7 +956,7 @@ int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
     return MGPU_OK;
   }
   const size_t cnt = (size_t)(s.count > 0 ? s.count : 1);
-  DevBuf tlb, tub, tnlb, tdep;  // scratch for this call only
+  DevBuf &tlb = s.mw_tlb, &tub = s.mw_tub, &tnlb = s.mw_tnlb, &tdep = s.mw_tdep;
   HIPCHK(c, tlb.ensure(cnt * s.n * 8));
   HIPCHK(c, tub.ensure(cnt * s.n * 8));
   HIPCHK(c, tnlb.ensure(cnt * 8));
@@ -978,21 +982,16 @@ int mgpu_bnb_shard(mgpu_ctx *c, int rank, int world, int *kept) {
     }
     size_t most = 0;
     for (auto &r : rows) most = r.second > most ? r.second : most;
-    DevBuf tmp;
+    DevBuf &tmp = s.mw_tmp;
     if (most > 0) e = tmp.ensure((size_t)k * most);
     for (auto &r : rows)
       if (e == hipSuccess)
         e = launch_bnb_shard_rows(r.first->as<unsigned char>(), tmp.as<unsigned char>(), r.second,
                                   k, rank, world, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    tmp.release();
   } else if (e == hipSuccess) {
     e = hipStreamSynchronize(c->stream);
   }
-  tlb.release();
-  tub.release();
-  tnlb.release();
-  tdep.release();
   HIPCHK(c, e);
   s.count = k;
   s.tot.open = k;
@@ -1135,7 +1134,7 @@ int take_nodes(mgpu_ctx *c, BnbState &s, const std::vector<int32_t> &slots, int 
                double *buf) {
   const int k = (int)slots.size();
   if (k == 0) return MGPU_OK;
-  DevBuf dsl;
+  DevBuf &dsl = s.mw_slots;
   HIPCHK(c, dsl.ensure((size_t)k * 4));
   HIPCHK(c, hipMemcpyAsync(dsl.p, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice,
                            c->stream));
@@ -1175,7 +1174,7 @@ int take_nodes(mgpu_ctx *c, BnbState &s, const std::vector<int32_t> &slots, int 
     }
     if (!f2.empty()) {
       const int km = (int)f2.size();
-      DevBuf ft, tmp;
+      DevBuf &ft = s.mw_ft, &tmp = s.mw_tmp;
       HIPCHK(c, ft.ensure((size_t)km * 8));
       HIPCHK(c, hipMemcpyAsync(ft.p, f2.data(), (size_t)km * 4, hipMemcpyHostToDevice,
                                c->stream));
@@ -1222,7 +1221,7 @@ int place_nodes(mgpu_ctx *c, BnbState &s, int k, const double *buf) {
     for (int t = 0; t < extra; ++t) slots.push_back(s.hw + t);
     s.hw += extra;
   }
-  DevBuf dsl;
+  DevBuf &dsl = s.mw_slots;
   HIPCHK(c, dsl.ensure((size_t)k * 4));
   HIPCHK(c, hipMemcpyAsync(dsl.p, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice,
                            c->stream));
