@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05zt
+O=$R/gpurun_out/r05zw
 mkdir -p $O
 timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -30 $O/gpu_tests.txt; exit 1; }
 tail -2 $O/gpu_tests.txt
@@ -11,4 +11,4 @@ tail -1 $O/smoke.txt
 timeout -k 10 900 python -u bench.py --supp-out $O/bench_supplementary.json > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 tail -c 400 $O/bench.json
 OUT=$O/prof timeout -k 10 1000 bash tools/prof_run.sh || { echo "prof failed"; exit 1; }
-echo "r05zt done"
+echo "r05zw done"
