@@ -315,7 +315,7 @@ def tree_cpu_baseline(p, brancher, seconds):
             "solved": done, "ub": float(res[0])}
 
 
-TIMED_ALLOCS = {}   # per tree: device allocations / bytes inside its timed solve (rank's own)
+TIMED_ALLOCS = {}   # per tree: device allocations / bytes inside its timed solve (all ranks)
 
 
 def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None, growth=0):
@@ -360,15 +360,17 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=No
                                                      growth=growth)
     torch.cuda.synchronize()
     a1 = alloc_stats()
-    if a1 != a0:
-        msg = (f"run_tree {p.name}: {a1[0] - a0[0]} device allocation(s) "
-               f"({a1[1] - a0[1]} bytes) inside the timed tree")
+    # summed over the ranks (rank 0 writes the line)
+    na = [int(v) for v in comm.allreduce([float(a1[0] - a0[0]), float(a1[1] - a0[1])], OP_SUM)]
+    if na[0] != 0:
+        msg = (f"run_tree {p.name}: {na[0]} device allocation(s) ({na[1]} bytes, all ranks) "
+               f"inside the timed tree")
         if world == 1:
             raise RuntimeError(msg)
-        # N > 1: reported (timed_allocations in the result), not fatal, so
-        # that a multi-GPU run still measures
+        # N > 1: reported (timed_device_allocations in the result), not fatal,
+        # so that a multi-GPU run still measures
         progress(rank, msg)
-    TIMED_ALLOCS[p.name] = [a1[0] - a0[0], a1[1] - a0[1]]
+    TIMED_ALLOCS[p.name] = na
     if trace is not None:
         trace.extend((t - t0, v) for t, v in tr)
     comm.barrier()
@@ -440,6 +442,7 @@ def tree_search(ctx, dev, rank, world, B, args):
                     "nodes_migrated": moved,
                     "nodes_per_s": nodes / el, "relaxations_per_s": (lps + sbl) / el,
                     "batch_per_gpu": B, "optimum": inc, "optimum_highs": opt,
+                    "timed_device_allocations": TIMED_ALLOCS.get(p.name),
                     "optimum_matches_highs": bool(abs(inc - opt) <= 1e-6 * max(1.0, abs(opt)))})
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             key = (p.name, br)
@@ -942,8 +945,14 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
         state["prev"] = cur
         return most
 
+    lb_pick = B if args.lb_pick == 'batch' else 0
     for _ in range(max(1, args.warmup)):
         step(None)
+    if world > 1 and args.lb_every > 0:
+        # one rebalance at the timed pick size: the exchange's workspaces are
+        # sized here (mgpu_bnb_rebalance reserves its worst case for that
+        # size), so the timed loop's rebalances allocate nothing
+        mdist.rebalance(ctx, comm, lb_pick)
     acc = {k: 0 for k in keys}
     acc.update({"fbbt_ms": [], "lp_ms": [], "lp_main_ms": [], "lp_tail_ms": [], "batch": [],
                 "rccl_ms": [], "open": 0})
@@ -961,7 +970,7 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
             # --lb-pick reference: each rank offers the reference's 50 P next
             # candidates (:80-105); batch: max(50 P, B), the globally best
             # P * B nodes dealt (~(P-1)/P of a batch crosses xGMI)
-            _, mv, _, _ = mdist.rebalance(ctx, comm, B if args.lb_pick == 'batch' else 0)
+            _, mv, _, _ = mdist.rebalance(ctx, comm, lb_pick)
             moved += mv
     torch.cuda.synchronize()
     comm.barrier()
@@ -983,9 +992,13 @@ def tree_rounds(ctx, dev, rank, world, p, LB, UB, args):
                           "(K3P)" if args.warm == 2 else "root-basis warm start (K3P)"),
                "incumbent": state["inc"]}
     summary["nodes_migrated"] = moved
-    # device allocations inside the timed loop (0 at N = 1; at N > 1 the first
-    # rebalance sizes its row buffers)
-    summary["device_allocs_timed"] = int(a1[0] - a0[0])
+    # device allocations inside the timed loop, summed over the ranks: none
+    # at any N (the warm-up sized every buffer, the rebalance's included)
+    na = comm.allreduce([float(a1[0] - a0[0]), float(a1[1] - a0[1])], OP_SUM)
+    summary["device_allocs_timed"] = int(na[0])
+    if na[0] != 0:
+        raise RuntimeError(f"headline: {int(na[0])} device allocation(s) ({int(na[1])} bytes, "
+                           f"all ranks) inside the timed rounds")
     # after the timed rounds: the next nodes of this pool, with the parent
     # bases they carry, for the CPU baseline (exported and imported back)
     pool_sample = None

@@ -68,7 +68,8 @@ int mgpu_set_stream(mgpu_ctx *ctx, void *hip_stream);
 void *mgpu_get_stream(mgpu_ctx *ctx);
 int mgpu_sync(mgpu_ctx *ctx);
 /* Device allocations the engine has made in this process (count and bytes,
- * every context; buffers grow on demand and are then reused).  A host that
+ * every context, pinned host staging included; buffers grow on demand and
+ * are then reused).  A host that
  * times a region checks that the count did not move inside it. */
 int mgpu_alloc_stats(long long *count, long long *bytes);
 
@@ -627,7 +628,9 @@ int mgpu_bnb_rebalance(mgpu_ctx *ctx, int S, double *picked, int *npicked, doubl
  * replaced, then QuadHandler::relax_'s secant / McCormick rows at the root
  * box; columns = the quadratic problem's variables), the quadratic problem
  * (mgpu_load_quad) and the node-rows map of the rewritten entries
- * (mgpu_set_node_rows, record stride = its row-state length R).
+ * (mgpu_set_node_rows, record stride = its row-state length R, plus 2 S
+ * values per square when the LP carries S tangent-cut rows per square:
+ * minotaur_amd/quad.py relaxation_lp(tan_slots=S)).
  *   mgpu_glob_init:  the root (the loaded column bounds, its rows from
  *                    mgpu_quad_rows) on an HBM stack of `capacity` nodes; the
  *                    root LP from the slack basis gives the basis every node
@@ -640,6 +643,13 @@ int mgpu_bnb_rebalance(mgpu_ctx *ctx, int S, double *picked, int *npicked, doubl
  *                    branching at the LP value on a continuous variable,
  *                    floor / ceil on an integer one), two children per
  *                    branched node (the preferred one on top).
+ *                    With tangent slots (S > 0): the squares' separation of
+ *                    QuadHandler::separate (QuadHandler.cpp:1658-1689) for
+ *                    the nodes that would branch -- a tangent of y = x^2 at
+ *                    findLinPt_'s point into the square's next free slot,
+ *                    the node re-solved and decided again, until no node
+ *                    adds a cut (PCBProcessor.cpp:267-280); children inherit
+ *                    the node's cuts.
  *   mgpu_glob_best:  the incumbent value and point (NaN: none).
  * Decision codes of ndec: 0 branched, 1 infeasible (K2 or LP), 2 pruned by
  * bound, 3 feasible (incumbent candidate), 4 engine problem (the round
@@ -649,10 +659,12 @@ int mgpu_bnb_rebalance(mgpu_ctx *ctx, int S, double *picked, int *npicked, doubl
 typedef struct {
   long long rounds, nodes;
   long long ndec[6];
-  long long lps, pivots;       /* LPs solved (nodes not K2-infeasible), their pivots */
+  long long lps, pivots;       /* LPs solved (nodes not K2-infeasible, and the
+                                  re-solves of the separation loop), their pivots */
   long long br_int, br_cont;   /* branchings at floor / ceil, at the LP value */
   int open, last_batch;
   double incumbent;
+  long long cuts, resolves;    /* tangent cuts added, node LPs re-solved for them */
 } mgpu_glob_stats;
 int mgpu_glob_init(mgpu_ctx *ctx, int capacity, double incumbent);
 int mgpu_glob_round(mgpu_ctx *ctx, int batch, double incumbent, mgpu_glob_stats *stats);

@@ -78,7 +78,9 @@ HipLPEngine::HipLPEngine(EnvPtr env, int device)
       maxIterLimit_(10000),
       iterLimit_(10000),
       lastIters_(0),
-      strBr_(false) {
+      strBr_(false),
+      tabOn_(false),
+      tabSite_(-1) {
   logger_ = env_->getLogger();
   stats_ = new HipLPStats();
   std::memset(stats_, 0, sizeof(HipLPStats));
@@ -199,52 +201,11 @@ void HipLPEngine::refactor_() {
       return;
     }
   }
-  std::vector<double> B((size_t)m * m, 0.0), I((size_t)m * m, 0.0);
-  for (int i = 0; i < m; ++i) {
-    const int h = ws_.head[i];
-    if (h >= n) {
-      B[(size_t)(h - n) * m + i] = -1.0;
-    } else {
-      for (int r = 0; r < m; ++r)
-        for (int k = rowptr_[r]; k < rowptr_[r + 1]; ++k)
-          if (colidx_[k] == h) B[(size_t)r * m + i] = val_[k];
-    }
-    I[(size_t)i * m + i] = 1.0;
+  if (!lptab::invert(n, m, rowptr_.data(), colidx_.data(), val_.data(), ws_.head.data(),
+                     ws_.binv)) {
+    wsValid_ = false;
+    return;
   }
-  for (int c = 0; c < m; ++c) {
-    int piv = -1;
-    double best = 0;
-    for (int r = c; r < m; ++r)
-      if (std::fabs(B[(size_t)r * m + c]) > best) {
-        best = std::fabs(B[(size_t)r * m + c]);
-        piv = r;
-      }
-    if (piv < 0 || best < 1e-12) {
-      wsValid_ = false;
-      return;
-    }
-    for (int k = 0; k < m; ++k) {
-      std::swap(B[(size_t)c * m + k], B[(size_t)piv * m + k]);
-      std::swap(I[(size_t)c * m + k], I[(size_t)piv * m + k]);
-    }
-    const double inv = 1.0 / B[(size_t)c * m + c];
-    for (int k = 0; k < m; ++k) {
-      B[(size_t)c * m + k] *= inv;
-      I[(size_t)c * m + k] *= inv;
-    }
-    for (int r = 0; r < m; ++r) {
-      if (r == c) continue;
-      const double f = B[(size_t)r * m + c];
-      if (f == 0.0) continue;
-      for (int k = 0; k < m; ++k) {
-        B[(size_t)r * m + k] -= f * B[(size_t)c * m + k];
-        I[(size_t)r * m + k] -= f * I[(size_t)c * m + k];
-      }
-    }
-  }
-  ws_.binv.assign((size_t)m * m, 0.0);  // column-major (mgpu.h)
-  for (int i = 0; i < m; ++i)
-    for (int k = 0; k < m; ++k) ws_.binv[(size_t)k * m + i] = I[(size_t)i * m + k];
   recomputeDuals_();
 }
 
@@ -521,9 +482,90 @@ int HipLPEngine::devWs_() {
 }
 
 void HipLPEngine::getBasics(int *index) {
+  if (tabOn_ && (int)tabHead_.size() == m_) {
+    for (int i = 0; i < m_; ++i) index[i] = tabHead_[i];
+    return;
+  }
   if (wsValid_ && !ws_.fetch()) return;
   for (int i = 0; i < m_ && wsValid_; ++i) index[i] = ws_.head[i];
 }
+
+bool HipLPEngine::IsOptimalBasisAvailable() { return status_ == ProvenOptimal && wsValid_; }
+
+// The optimal basis of the last solve, refactored from scratch (as Clp's
+// factorization is fresh after an optimal resolve): the device's K3R when the
+// loaded matrix is the current one, else the host Gauss-Jordan.
+bool HipLPEngine::tableau_() {
+  tabHead_.clear();
+  tabBinv_.clear();
+  tabSite_ = -1;
+  if (consChanged_) syncRows_();
+  if (!IsOptimalBasisAvailable() || !ws_.fetch() || (int)ws_.head.size() != m_) return false;
+  const int n = n_, m = m_;
+  if (ctx_ && !consChanged_ && !needUpload_ && m > 0 && m <= 64) {
+    std::vector<int32_t> h((size_t)m);
+    std::vector<int8_t> st((size_t)(n + m));
+    std::vector<double> d((size_t)(n + m)), b((size_t)m * m);
+    int sing = 1;
+    if (mgpu_lp_refactor(ctx_, ws_.head.data(), ws_.st.data(), h.data(), st.data(), d.data(),
+                         b.data(), &sing) == MGPU_OK &&
+        !sing) {
+      tabHead_ = h;
+      tabBinv_ = b;
+      tabSite_ = 1;
+      return true;
+    }
+  }
+  tabHead_ = ws_.head;
+  if (!lptab::invert(n, m, rowptr_.data(), colidx_.data(), val_.data(), tabHead_.data(),
+                     tabBinv_)) {
+    tabHead_.clear();
+    return false;
+  }
+  tabSite_ = 0;
+  return true;
+}
+
+void HipLPEngine::enableFactorization() { tabOn_ = tableau_(); }
+
+void HipLPEngine::disableFactorization() {
+  tabOn_ = false;
+  tabHead_.clear();
+  tabBinv_.clear();
+}
+
+void HipLPEngine::getBInvARow(int row, double *z, double *slack) {
+  if (!tabOn_ && !(tabOn_ = tableau_())) return;
+  if (row < 0 || row >= m_) return;
+  lptab::binv_a_row(n_, m_, rowptr_.data(), colidx_.data(), val_.data(), tabHead_.data(),
+                    tabBinv_.data(), row, z, slack);
+}
+
+void HipLPEngine::views_() {
+  if (consChanged_) syncRows_();
+  tab_.fill(n_, m_, rowptr_.data(), colidx_.data(), val_.data(), clo_.data(), chi_.data(),
+            rlo_.data(), rhi_.data(), (int)x_.size() == n_ ? x_.data() : nullptr);
+}
+
+const double *HipLPEngine::getColLower() { views_(); return tab_.clo.data(); }
+const double *HipLPEngine::getColUpper() { views_(); return tab_.chi.data(); }
+const double *HipLPEngine::getRowLower() { views_(); return tab_.rlo.data(); }
+const double *HipLPEngine::getRowUpper() { views_(); return tab_.rhi.data(); }
+const double *HipLPEngine::getRightHandSide() { views_(); return tab_.rhs.data(); }
+const double *HipLPEngine::getRowActivity() { views_(); return tab_.act.data(); }
+const double *HipLPEngine::getOriginalTableau() {
+  if (consChanged_) syncRows_();
+  return val_.data();
+}
+const int *HipLPEngine::getRowStarts() {
+  if (consChanged_) syncRows_();
+  return rowptr_.data();
+}
+const int *HipLPEngine::getIndicesofVars() {
+  if (consChanged_) syncRows_();
+  return colidx_.data();
+}
+const int *HipLPEngine::getRowLength() { views_(); return tab_.rowlen.data(); }
 
 void HipLPEngine::resetIterationLimit() { iterLimit_ = maxIterLimit_; }
 void HipLPEngine::setIterationLimit(int limit) { iterLimit_ = limit; }

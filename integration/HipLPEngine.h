@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "LPEngine.h"
+#include "LPTableau.h"
 #include "WarmStart.h"
 
 struct mgpu_ctx;
@@ -130,11 +131,34 @@ class HipLPEngine : public LPEngine {
   };
   const std::vector<SolveRec> &solveLog() const { return log_; }
 
-  // LPEngine extras used by drivers
+  // LPEngine extras (LPEngine.h:39-73), answered as OsiLPEngine answers them
+  // from Clp (OsiLPEngine.cpp:314-360; conventions in LPTableau.h).  The
+  // arrays are borrowed views into the engine's host mirrors, valid until the
+  // next edit or solve.  enableFactorization refactors the optimal basis of
+  // the last solve (K3R on the device, mgpu_lp_refactor, for m <= 64; else
+  // the same Gauss-Jordan on the host); getBasics / getBInvARow then read
+  // that factorization (SimplexQuadCutGen.cpp:285-345, 366-418, 593-629).
+  void enableFactorization();
+  void disableFactorization();
+  bool IsOptimalBasisAvailable();
   void getBasics(int *index);
+  void getBInvARow(int row, double *z, double *slack);
   int getNumCols() { return n_; }
   int getNumRows() { return m_; }
+  const double *getColLower();
+  const double *getColUpper();
+  const double *getRowLower();
+  const double *getRowUpper();
+  const double *getRightHandSide();
+  const double *getRowActivity();
+  const double *getOriginalTableau();
+  const int *getRowStarts();
+  const int *getIndicesofVars();
+  const int *getRowLength();
   int getIterationCount() { return lastIters_; }
+  /// where the last enableFactorization factored the basis: 1 device (K3R),
+  /// 0 host, -1 no optimal basis
+  int factorSite() const { return tabSite_; }
 
  private:
   void syncRows_();            // re-read every row of problem_ (after edits)
@@ -163,6 +187,13 @@ class HipLPEngine : public LPEngine {
   Timer *timer_;
   std::vector<double> x_, y_, rc_, rcAll_;
   std::vector<SolveRec> log_;
+  bool tableau_();             // factor the optimal basis into tabHead_ / tabBinv_
+  void views_();               // Osi views of the mirrors (tab_)
+  bool tabOn_;                 // enableFactorization ... disableFactorization
+  int tabSite_;
+  std::vector<int32_t> tabHead_;
+  std::vector<double> tabBinv_;  // column-major
+  lptab::Views tab_;
   static const std::string me_;
 };
 typedef HipLPEngine *HipLPEnginePtr;

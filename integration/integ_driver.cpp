@@ -34,6 +34,8 @@
 #include "PCBProcessor.h"
 #include "Problem.h"
 #include "ReliabilityBrancher.h"
+#include "SimplexQuadCutGen.h"
+#include "StrongBrancher.h"
 #include "Variable.h"
 
 using namespace Minotaur;
@@ -576,6 +578,22 @@ class NoNlpQuadHandler : public QuadHandler {
     return 0;
   }
   long long closed = 0;
+  void separate(ConstSolutionPtr sol, NodePtr node, RelaxationPtr rel, CutManager *cm,
+                SolutionPoolPtr s_pool, ModVector &p_mods, ModVector &r_mods, bool *sol_found,
+                SeparationStatus *status) {
+    ++sepa_;
+    const long long m0 = (long long)rel->getNumCons();
+    QuadHandler::separate(sol, node, rel, cm, s_pool, p_mods, r_mods, sol_found, status);
+    const long long add = (long long)rel->getNumCons() - m0;
+    rows_ += add;
+    if (!node->getParent()) rootRows_ += add;
+  }
+  long long sepaRounds() const { return sepa_; }
+  long long sepaRows() const { return rows_; }        // rows added by separate()
+  long long rootSepaRows() const { return rootRows_; }  // ... at the root (simplex cuts there)
+
+ private:
+  long long sepa_ = 0, rows_ = 0, rootRows_ = 0;
 };
 
 // LinearHandler without node presolve (flags bit 1): the batched glob
@@ -588,37 +606,23 @@ class NoPresolveLinearHandler : public LinearHandler {
   }
 };
 
-// Glob::createBab_ (Glob.cpp:134-220) over the QCQP's auxiliary form: the
-// original rows with every product replaced by its aux y (LinearHandler),
-// y = x0 x1 for each product (QuadHandler: McCormick rows, presolveNode,
-// isFeasible, spatial candidates), IntVarHandler; PCBProcessor, NodeIncRelaxer
-// (parent warm starts), MaxVioBrancher, HipLPEngine for the LPs (Clp is
-// absent; device < 0: CpuLPEngine).  Root OBBT off (the batched tree does none; "OBBT",
-// Environment.cpp:326), tree_search as given (0 dfs, 1 bfs), every other
-// option at its default (obj_gap_percent 0: the tree runs to completion).
-// res[0] UB, res[1] LB, res[2] seconds; cnt[0] nodes processed, cnt[1]
-// nodes created, cnt[2] LP solves, cnt[3] nodes closed at NoCandToBranch.
-// bfs: tree_search bfs (else dfs); flags bit 1: LinearHandler without node
-// presolve.  pres_freq: PCBProcessor's node-presolve frequency (reference
-// default 5, Environment.cpp:364).
-int integ_glob_tree2(int device, const QSpecI *sp, int bfs, int flags, int pres_freq, double *res,
-                     long long *cnt) {
-  const QSpecI &s = *sp;
-  EnvPtr env = (EnvPtr) new Environment();
-  int err = 0;
-  env->startTimer(err);
-  env->getOptions()->findString("tree_search")->setValue(bfs ? "bfs" : "dfs");
-  env->getOptions()->findBool("OBBT")->setValue(false);
-  env->getOptions()->findInt("pres_freq")->setValue(pres_freq);
-  ProblemPtr orig = (ProblemPtr) new Problem(env);
+}  // extern "C"
+
+// The QCQP's auxiliary form, as SimpleTransformer builds it for Glob: the
+// original rows with every product replaced by its aux y (LinearHandler's
+// rows), and y = x0 x1 / y = x^2 for each product (QuadHandler's
+// constraints: McCormick / secant rows, presolveNode, isFeasible, spatial
+// candidates).  qh is constructed by the caller's factory.
+template <class QH>
+static QH *glob_model(EnvPtr env, const QSpecI &s, ProblemPtr &orig, ProblemPtr &p) {
+  orig = (ProblemPtr) new Problem(env);
   for (int j = 0; j < s.nv0; ++j) orig->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
   for (int c = 0; c < s.ncon; ++c) orig->newConstraint(qfun(s, orig, c), s.clb[c], s.cub[c]);
   if (s.has_obj) orig->newObjective(qfun(s, orig, s.ncon), s.obj_const, Minimize);
   else orig->newObjective((FunctionPtr) new Function((LinearFunctionPtr) new LinearFunction()),
                           s.obj_const, Minimize);
   orig->calculateSize();
-  ProbeBranchAndBound *bab = nullptr;
-  ProblemPtr p = (ProblemPtr) new Problem(env);
+  p = (ProblemPtr) new Problem(env);
   for (int j = 0; j < s.nv; ++j) p->newVariable(s.vlb[j], s.vub[j], (VariableType)s.vtype[j]);
   auto yof = [&](int a, int b) {
     for (int k = 0; k < s.nsq; ++k)
@@ -639,7 +643,7 @@ int integ_glob_tree2(int device, const QSpecI *sp, int bfs, int flags, int pres_
   if (s.has_obj) p->newObjective((FunctionPtr) new Function(ylin(s.ncon)), s.obj_const, Minimize);
   else p->newObjective((FunctionPtr) new Function((LinearFunctionPtr) new LinearFunction()),
                        s.obj_const, Minimize);
-  NoNlpQuadHandler *qh = new NoNlpQuadHandler(env, p, orig);
+  QH *qh = new QH(env, p, orig);
   auto add_aux = [&](int x0, int x1, int y) {
     LinearFunctionPtr lf = (LinearFunctionPtr) new LinearFunction();
     lf->addTerm(p->getVariable(y), -1.0);
@@ -650,22 +654,79 @@ int integ_glob_tree2(int device, const QSpecI *sp, int bfs, int flags, int pres_
   for (int k = 0; k < s.nsq; ++k) add_aux(s.sq_x[k], s.sq_x[k], s.sq_y[k]);
   for (int k = 0; k < s.nbil; ++k) add_aux(s.bil_x0[k], s.bil_x1[k], s.bil_y[k]);
   p->calculateSize();
-  bab = new ProbeBranchAndBound(env, p);
+  return qh;
+}
+
+static LPEnginePtr new_engine(EnvPtr env, int device) {
+  // device < 0: CpuLPEngine (the C restatement of the dual simplex), for CPU runs
+  return device < 0 ? (LPEnginePtr) new CpuLPEngine(env) : (LPEnginePtr) new HipLPEngine(env, device);
+}
+
+extern "C" {
+
+// Glob::createBab_ (Glob.cpp:134-220) over the QCQP's auxiliary form
+// (glob_model): IntVarHandler, LinearHandler, QuadHandler; PCBProcessor,
+// NodeIncRelaxer (parent warm starts), HipLPEngine for the LPs (Clp is
+// absent; device < 0: CpuLPEngine).  opts bits:
+//   1  tree_search bfs (else dfs)
+//   2  LinearHandler without node presolve (the batched glob round's shape)
+//   4  simplex_cut on (Glob.cpp:311): QuadHandler's cute_ is the main engine,
+//      as SimpleTransformer.cpp:953-954 wires it, so the root separation runs
+//      SimplexQuadCutGen on this engine's tableau (QuadHandler.cpp:1691-1703)
+//   8  root OBBT on (Environment.cpp:325-326 default; PCBProcessor.cpp:256-262
+//      -> QuadHandler::postSolveRootNode) with a second engine of the same
+//      kind as bte_ (SimpleTransformer.cpp:948-951)
+//  16  brancher relstronger (Glob.cpp:308): StrongBrancher::reliabilitySetup
+//      (20, 50, 5) (Glob.cpp:171-181), else MaxVioBrancher
+// Every other option keeps its default (obj_gap_percent 0: the tree runs to
+// completion).  res[0] UB, res[1] LB, res[2] seconds; cnt[0] nodes processed,
+// cnt[1] nodes created, cnt[2] LP solves of the main engine, cnt[3] nodes
+// closed at NoCandToBranch, cnt[4] rows QuadHandler::separate added at the
+// root (the simplex cuts, and tangents of violated squares), cnt[5] bound
+// LPs of OBBT, cnt[6] QuadHandler::separate calls, cnt[7] rows it added in
+// the whole tree; x (nullable, nv) the
+// incumbent of the auxiliary form.
+int integ_glob_tree3(int device, const QSpecI *sp, int opts, int pres_freq, double *res,
+                     long long *cnt, double *x) {
+  const QSpecI &s = *sp;
+  EnvPtr env = (EnvPtr) new Environment();
+  int err = 0;
+  env->startTimer(err);
+  env->getOptions()->findString("tree_search")->setValue((opts & 1) ? "bfs" : "dfs");
+  env->getOptions()->findBool("OBBT")->setValue((opts & 8) != 0);
+  env->getOptions()->findBool("simplex_cut")->setValue((opts & 4) != 0);
+  env->getOptions()->findInt("pres_freq")->setValue(pres_freq);
+  ProblemPtr orig = 0, p = 0;
+  NoNlpQuadHandler *qh = glob_model<NoNlpQuadHandler>(env, s, orig, p);
+  ProbeBranchAndBound *bab = new ProbeBranchAndBound(env, p);
   HandlerVector handlers;
   IntVarHandlerPtr v_hand = (IntVarHandlerPtr) new IntVarHandler(env, p);
-  LinearHandlerPtr l_hand = (flags & 2) ? (LinearHandlerPtr) new NoPresolveLinearHandler(env, p)
-                                        : (LinearHandlerPtr) new LinearHandler(env, p);
+  LinearHandlerPtr l_hand = (opts & 2) ? (LinearHandlerPtr) new NoPresolveLinearHandler(env, p)
+                                       : (LinearHandlerPtr) new LinearHandler(env, p);
   handlers.push_back(v_hand);
   handlers.push_back(l_hand);
   handlers.push_back(qh);
   v_hand->setModFlags(false, true);
   l_hand->setModFlags(false, true);
   qh->setModFlags(false, true);
-  // device < 0: CpuLPEngine (the C restatement of the dual simplex), for CPU runs
-  LPEnginePtr e = device < 0 ? (LPEnginePtr) new CpuLPEngine(env)
-                             : (LPEnginePtr) new HipLPEngine(env, device);
+  LPEnginePtr e = new_engine(env, device);
+  LPEnginePtr bte = 0;
+  if (opts & 8) {
+    bte = new_engine(env, device);
+    qh->setBTEngine(bte);     // owned by the handler (QuadHandler.cpp:118-120)
+  }
+  if (opts & 4) qh->setCutEngine(e);
   PCBProcessorPtr nproc = (PCBProcessorPtr) new PCBProcessor(env, e, handlers);
-  MaxVioBrancherPtr br = (MaxVioBrancherPtr) new MaxVioBrancher(env, handlers);
+  BrancherPtr br;
+  if (opts & 16) {
+    StrongBrancherPtr sb = (StrongBrancherPtr) new StrongBrancher(env, handlers);
+    sb->setEngine(e);
+    sb->reliabilitySetup(20, 50, 5);
+    sb->setProblem(p);
+    br = sb;
+  } else {
+    br = (BrancherPtr) new MaxVioBrancher(env, handlers);
+  }
   nproc->setBrancher(br);
   bab->setNodeProcessor(nproc);
   NodeIncRelaxerPtr nr = (NodeIncRelaxerPtr) new NodeIncRelaxer(env, handlers);
@@ -686,6 +747,19 @@ int integ_glob_tree2(int device, const QSpecI *sp, int bfs, int flags, int pres_
   e->fillStats(lps);
   cnt[2] = (long long)lps[0];
   cnt[3] = qh->closed;
+  cnt[4] = qh->rootSepaRows();
+  cnt[5] = 0;
+  if (bte) {
+    std::vector<double> bl(6, 0.0);
+    bte->fillStats(bl);
+    cnt[5] = (long long)bl[0];
+  }
+  cnt[6] = qh->sepaRounds();
+  cnt[7] = qh->sepaRows();
+  if (x) {
+    SolutionPtr sol = bab->getSolution();
+    for (int j = 0; j < s.nv; ++j) x[j] = sol ? sol->getPrimal()[j] : NAN;
+  }
   delete v_hand;
   delete l_hand;
   delete qh;
@@ -699,9 +773,164 @@ int integ_glob_tree2(int device, const QSpecI *sp, int bfs, int flags, int pres_
   return 0;
 }
 
+// flags bit 1: LinearHandler without node presolve; pres_freq: PCBProcessor's
+// node-presolve frequency (reference default 5, Environment.cpp:364); bfs:
+// tree_search bfs (else dfs).  Root OBBT and simplex cuts off, MaxVio.
+int integ_glob_tree2(int device, const QSpecI *sp, int bfs, int flags, int pres_freq, double *res,
+                     long long *cnt) {
+  long long c8[8];
+  int rc = integ_glob_tree3(device, sp, (bfs ? 1 : 0) | (flags & 2), pres_freq, res, c8, nullptr);
+  for (int k = 0; k < 4; ++k) cnt[k] = c8[k];
+  return rc;
+}
+
 // Glob's defaults: LinearHandler presolve, pres_freq 5
 int integ_glob_tree(int device, const QSpecI *sp, int bfs, double *res, long long *cnt) {
   return integ_glob_tree2(device, sp, bfs, 0, 5, res, cnt);
+}
+
+// The root of Glob's tree through the LPEngine tableau extras: the root
+// relaxation (NodeIncRelaxer::createRootRelaxation over IntVar / Linear /
+// Quad handlers, NodeIncRelaxer.cpp:49-67) solved by the engine (device < 0:
+// CpuLPEngine), then
+//   1. the engine's views as SimplexQuadCutGen::getBasicInfo_ reads them
+//      (SimplexQuadCutGen.cpp:285-304): dims[0] n, dims[1] m, dims[2] nnz,
+//      dims[3] root LP status, dims[4] IsOptimalBasisAvailable, dims[5] the
+//      factorization site (HipLPEngine: 1 device K3R, 0 host); rowstart
+//      [m+1], rowlen [m], ind [nnz], val [nnz], clo / chi [n], rlo / rhi /
+//      rhs / act [m]; the relaxation's own rows for comparison: rrow [nnz],
+//      rcol [nnz], rval [nnz] in iteration order, rlb / rub [m], vlb / vub [n];
+//   2. enableFactorization, getBasics -> basics [m], getBInvARow for every
+//      basis position -> z [m][n], slack [m][m], disableFactorization;
+//   3. SimplexQuadCutGen(env, p, engine, +inf)::generateCuts(rel, sol) -- the
+//      reference's own cut generator on this engine -> dims[6] cuts added;
+//      each cut's dense coefficients [cap][n] and its lb / ub.  The generator
+//      keeps maxCuts_ = min(max(ceil(0.2 n), ceil(0.05 m)), 20) of its
+//      candidates (SimplexQuadCutGen.cpp:58-60) after std::sort on the vector
+//      of SimplexCut POINTERS (:204): which ones depends on heap addresses.
+//      lift != 0 gives the generator's problem 400 extra empty rows after the
+//      relaxation is built, so maxCuts_ is its cap 20 and every candidate of
+//      depth >= minDepth_ is added (two engines then compare as sets).
+// x [n]: the root LP's primal point.  cap bounds n, m, nnz and the cuts.
+int integ_simplex_cuts(int device, const QSpecI *sp, int cap, int lift, long long *dims,
+                       int *rowstart,
+                       int *rowlen, int *ind, double *val, double *clo, double *chi, double *rlo,
+                       double *rhi, double *rhs, double *act, int *rrow, int *rcol, double *rval,
+                       double *rlb, double *rub, double *vlb, double *vub, int *basics, double *z,
+                       double *slack, double *x, double *cut_coef, double *cut_lb,
+                       double *cut_ub) {
+  const QSpecI &s = *sp;
+  EnvPtr env = (EnvPtr) new Environment();
+  int err = 0;
+  env->startTimer(err);
+  env->getOptions()->findBool("simplex_cut")->setValue(true);
+  ProblemPtr orig = 0, p = 0;
+  NoNlpQuadHandler *qh = glob_model<NoNlpQuadHandler>(env, s, orig, p);
+  HandlerVector handlers;
+  IntVarHandlerPtr v_hand = (IntVarHandlerPtr) new IntVarHandler(env, p);
+  LinearHandlerPtr l_hand = (LinearHandlerPtr) new LinearHandler(env, p);
+  handlers.push_back(v_hand);
+  handlers.push_back(l_hand);
+  handlers.push_back(qh);
+  LPEnginePtr e = new_engine(env, device);
+  NodeIncRelaxerPtr nr = (NodeIncRelaxerPtr) new NodeIncRelaxer(env, handlers);
+  nr->setProblem(p);
+  nr->setEngine(e);
+  bool prune = false;
+  RelaxationPtr rel = nr->createRootRelaxation(NodePtr(), prune);
+  int rc = 0;
+  for (int k = 0; k < 7; ++k) dims[k] = 0;
+  const int n = (int)rel->getNumVars(), m = (int)rel->getNumCons();
+  dims[0] = n;
+  dims[1] = m;
+  if (prune || n > cap || m > cap) {
+    rc = -1;
+  } else {
+    dims[3] = (long long)e->solve();
+    dims[4] = e->IsOptimalBasisAvailable() ? 1 : 0;
+    const int *rs = e->getRowStarts();
+    const int nnz = rs ? rs[m] : 0;
+    dims[2] = nnz;
+    if (!rs || nnz > cap * cap) {
+      rc = -2;
+    } else {
+      const double *v;
+      std::copy(rs, rs + m + 1, rowstart);
+      std::copy(e->getRowLength(), e->getRowLength() + m, rowlen);
+      std::copy(e->getIndicesofVars(), e->getIndicesofVars() + nnz, ind);
+      std::copy(e->getOriginalTableau(), e->getOriginalTableau() + nnz, val);
+      v = e->getColLower(); std::copy(v, v + n, clo);
+      v = e->getColUpper(); std::copy(v, v + n, chi);
+      v = e->getRowLower(); std::copy(v, v + m, rlo);
+      v = e->getRowUpper(); std::copy(v, v + m, rhi);
+      v = e->getRightHandSide(); std::copy(v, v + m, rhs);
+      v = e->getRowActivity(); std::copy(v, v + m, act);
+      int t = 0;
+      for (int i = 0; i < m; ++i) {
+        ConstraintPtr c = rel->getConstraint(i);
+        rlb[i] = c->getLb();
+        rub[i] = c->getUb();
+        LinearFunctionPtr lf = c->getLinearFunction();
+        if (lf)
+          for (VariableGroupConstIterator it = lf->termsBegin(); it != lf->termsEnd(); ++it) {
+            if (t < nnz) {
+              rrow[t] = i;
+              rcol[t] = (int)it->first->getIndex();
+              rval[t] = it->second;
+            }
+            ++t;
+          }
+      }
+      if (t != nnz) rc = -3;
+      for (int j = 0; j < n; ++j) {
+        vlb[j] = rel->getVariable(j)->getLb();
+        vub[j] = rel->getVariable(j)->getUb();
+      }
+      if (dims[3] == ProvenOptimal) {
+        const double *xp = e->getSolution()->getPrimal();
+        std::copy(xp, xp + n, x);
+        e->enableFactorization();
+        if (HipLPEngine *he = dynamic_cast<HipLPEngine *>(e)) dims[5] = he->factorSite();
+        e->getBasics(basics);
+        for (int r = 0; r < m; ++r)
+          e->getBInvARow(r, z + (size_t)r * n, slack + (size_t)r * m);
+        e->disableFactorization();
+        // the reference's cut generator on this engine (generateCuts enables
+        // and disables the factorization itself, :179-190)
+        if (lift) {
+          LinearFunctionPtr lf0 = (LinearFunctionPtr) new LinearFunction();
+          lf0->addTerm(p->getVariable(0), 1.0);
+          for (int k = 0; k < 400; ++k)
+            p->newConstraint((FunctionPtr) new Function(lf0->clone()), -INFINITY, INFINITY);
+          delete lf0;
+        }
+        SimplexQuadCutGen cg(env, p, e, INFINITY);
+        const int ncuts = cg.generateCuts(rel, e->getSolution());
+        dims[6] = ncuts;
+        for (int k = 0; k < ncuts && k < cap; ++k) {
+          ConstraintPtr c = rel->getConstraint(m + k);
+          cut_lb[k] = c->getLb();
+          cut_ub[k] = c->getUb();
+          double *row = cut_coef + (size_t)k * n;
+          for (int j = 0; j < n; ++j) row[j] = 0.0;
+          LinearFunctionPtr lf = c->getLinearFunction();
+          if (lf)
+            for (VariableGroupConstIterator it = lf->termsBegin(); it != lf->termsEnd(); ++it)
+              row[it->first->getIndex()] = it->second;
+        }
+      }
+    }
+  }
+  e->clear();
+  delete nr;   // deletes the relaxation (NodeIncRelaxer.cpp:38-44)
+  delete v_hand;
+  delete l_hand;
+  delete qh;
+  delete e;
+  delete p;
+  delete orig;
+  delete env;
+  return rc;
 }
 
 }  // extern "C"

@@ -1273,6 +1273,23 @@ int check_migrate(mgpu_ctx *c, const char *what) {
 
 extern "C" {
 
+// The pool-side migration workspaces for an exchange of up to S rows (a
+// pick of S, then an export of k <= S rows from those S slots and an import
+// of k <= S rows): sized once for that worst case, so a rebalance inside a
+// timed region never allocates (mgpu_bnb_rebalance calls this first).
+extern "C++" int bnb_reserve_migration(mgpu_ctx *c, int S) {
+  int rc = check_migrate(c, "mgpu_bnb_rebalance");
+  if (rc != MGPU_OK) return rc;
+  BnbState &s = *c->bnb;
+  const size_t k = (size_t)(S > 0 ? S : 1);
+  size_t most = 0;
+  for (auto &r : slot_rows(s, c->lp.m)) most = r.second > most ? r.second : most;
+  HIPCHK(c, s.mw_slots.ensure(k * 4));
+  HIPCHK(c, s.mw_ft.ensure(k * 8));
+  HIPCHK(c, s.mw_tmp.ensure(k * most));
+  return MGPU_OK;
+}
+
 int mgpu_bnb_pick(mgpu_ctx *c, int S, double *lbs, int *got) {
   int rc = check_migrate(c, "mgpu_bnb_pick");
   if (rc != MGPU_OK) return rc;

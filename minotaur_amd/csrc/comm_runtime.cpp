@@ -74,6 +74,7 @@ int ensure_pin(mgpu_ctx *c, CommState &s, size_t bytes) {
   s.pin_bytes = 0;
   void *p = nullptr;
   HIPCHK(c, hipHostMalloc(&p, bytes, hipHostMallocDefault));
+  note_dev_alloc(bytes);   // pinned host memory counts too (mgpu_alloc_stats)
   s.pin = static_cast<double *>(p);
   s.pin_bytes = bytes;
   return MGPU_OK;
@@ -309,6 +310,27 @@ int mgpu_bnb_rebalance(mgpu_ctx *c, int S, double *picked, int *npicked, double 
     return MGPU_OK;
   }
   vec[(size_t)S] = (double)spare;
+  // every workspace of this exchange at its worst case for S (this rank
+  // sends at most the S nodes it picked and, dealt round-robin, receives at
+  // most S): sized by the first rebalance, never again for the same S
+  const int W = mgpu_bnb_row_width(c);
+  if (W < 0) return W;
+  {
+    CommState &s = *c->comm;   // P > 1: a communicator is set
+    const size_t rowb = (size_t)W * 8, gat = (size_t)P * (S + 1) * 8;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, s.send_rows.ensure((size_t)S * rowb));
+    HIPCHK(c, s.recv_rows.ensure((size_t)S * rowb));
+    HIPCHK(c, s.ord_rows.ensure((size_t)S * rowb));
+    HIPCHK(c, s.perm.ensure((size_t)S * 4));
+    if (!s.host) {
+      HIPCHK(c, s.dbuf.ensure(gat + (size_t)(S + 1) * 8));
+      rc = ensure_pin(c, s, gat);
+      if (rc != MGPU_OK) return rc;
+    }
+    rc = bnb_reserve_migration(c, S);
+    if (rc != MGPU_OK) return rc;
+  }
   // 2. one all-gather of the bounds and the pool room (:107)
   std::vector<double> g((size_t)P * (S + 1));
   rc = mgpu_allgather_f64(c, vec.data(), S + 1, g.data());
@@ -359,16 +381,11 @@ int mgpu_bnb_rebalance(mgpu_ctx *c, int S, double *picked, int *npicked, double 
       received[j] = lbs[(size_t)owner[i] * S + local[i]];
     }
   if (nreceived) *nreceived = (int)got_at.size();
-  const int W = mgpu_bnb_row_width(c);
-  if (W < 0) return W;
-  CommState &s = *c->comm;   // P > 1: a communicator is set
+  CommState &s = *c->comm;
   const size_t rowb = (size_t)W * 8;
   const int ks = (int)idx.size(), kr = (int)got_at.size();
-  HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, s.send_rows.ensure((size_t)(ks > 0 ? ks : 1) * rowb));
-  HIPCHK(c, s.recv_rows.ensure((size_t)(kr > 0 ? kr : 1) * rowb));
-  HIPCHK(c, s.ord_rows.ensure((size_t)(kr > 0 ? kr : 1) * rowb));
-  HIPCHK(c, s.perm.ensure((size_t)(kr > 0 ? kr : 1) * 4));
+  if (ks > S || kr > S)   // the deal hands each rank at most S nodes
+    return fail(c, MGPU_ERR_STATE, "mgpu_bnb_rebalance: %d sent / %d received > S = %d", ks, kr, S);
   rc = mgpu_bnb_export_dev(c, ks, ks ? idx.data() : nullptr, s.send_rows.as<double>());
   if (rc != MGPU_OK) return rc;
   rc = mgpu_alltoall_rows_dev(c, W, s.send_rows.as<double>(), sc.data(), s.recv_rows.as<double>(),

@@ -169,6 +169,8 @@ int qp_solve_nodes(mgpu_ctx *c, int batch, const double *lb, const double *ub,
                    double *x);
 void glob_state_free(mgpu_ctx *c);  // glob_runtime.cpp
 void comm_state_free(mgpu_ctx *c);  // comm_runtime.cpp
+// the pool's migration workspaces for exchanges of up to S rows (bnb.cpp)
+int bnb_reserve_migration(mgpu_ctx *c, int S);
 // an LP batch with per-node warm starts through the K3 / K3L selection of
 // mgpu_lp_solve (mgpu_runtime.cpp); io.next is set here
 int launch_lp_nodes(mgpu_ctx *c, const LpIO &io);

@@ -30,8 +30,8 @@ struct GlobIO {
   const int32_t *kinf;          // [nb] K2 infeasible (1) / failure (2, 3)
   const double *wlb, *wub;      // [nb][nv]
   const double *wrows;          // [nb][R]
-  const int32_t *status, *iters;
-  const double *obj, *x;        // [nb], [nb][nv]
+  int32_t *status, *iters;      // (the separation loop merges re-solves in)
+  double *obj, *x;              // [nb], [nb][nv]
   double *cand;                 // [nb][4][nv] scratch
   int32_t *dec, *bvar, *pos, *depth_in;
   double *bval;
@@ -40,8 +40,24 @@ struct GlobIO {
   // the pool (stack): children go to base + pos
   double *plb, *pub, *prows, *pnlb;
   int32_t *pdepth;
+  // tangent cuts of the squares (QuadHandler::separate): S slots per square,
+  // T = 2 nsq S record values [2 xl, xl^2] (inactive [0, +inf]) after the R
+  // row-state values of the node record wvals [nb][R + T]; pool copy ptan
+  // [cap][T].  The separation loop re-solves the flagged nodes into st2 /
+  // obj2 / it2 / x2 and merges them back.
+  int S, T;
+  double *wvals, *ptan;
+  int32_t *flag, *skip2;
+  const int32_t *st2, *it2;
+  const double *obj2, *x2;
+  unsigned long long *acc;      // [2] tangent cuts, re-solved nodes (this pass)
+  const int32_t *only;          // glob_decide: only the nodes with only[b] != 0
 };
 
 hipError_t launch_glob_round_tail(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_decide(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_pack(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_separate(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_merge(const GlobIO &io, hipStream_t stream);
 
 }  // namespace mgpu

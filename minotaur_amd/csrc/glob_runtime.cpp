@@ -30,22 +30,23 @@
 #include "quad_state.h"
 
 struct GlobState {
-  int nv = 0, R = 0, cap = 0, count = 0, maxb = 0;
+  int nv = 0, R = 0, S = 0, T = 0, cap = 0, count = 0, maxb = 0;
   double inc = INFINITY;
   bool root_ws = false;
   std::vector<double> best_x;
   mgpu_glob_stats tot{};
-  DevBuf plb, pub, prows, pnlb, pdepth;
+  DevBuf plb, pub, prows, pnlb, pdepth, ptan;
   DevBuf wlb, wub, wrows, kinf, knm, st, obj, it, x, cand, dec, bvar, bval, bup, bint, pos,
       depth_in, out;
+  DevBuf wvals, flag, skip2, st2, obj2, it2, x2, acc;   // the separation loop
   DevBuf ws_head, ws_st, ws_d, ws_binv, r_st, r_obj, r_it;
   DevBuf fvtype, fsq, fbil, flptr, flvar, flval, fqptr, fqv1, fqv2, fqval, fclb, fcub;
   void release() {
-    for (DevBuf *b : {&plb, &pub, &prows, &pnlb, &pdepth, &wlb, &wub, &wrows, &kinf, &knm, &st,
-                      &obj, &it, &x, &cand, &dec, &bvar, &bval, &bup, &bint, &pos, &depth_in,
-                      &out, &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj, &r_it, &fvtype,
-                      &fsq, &fbil, &flptr, &flvar, &flval, &fqptr, &fqv1, &fqv2, &fqval, &fclb,
-                      &fcub})
+    for (DevBuf *b : {&plb, &pub, &prows, &pnlb, &pdepth, &ptan, &wlb, &wub, &wrows, &kinf,
+                      &knm, &st, &obj, &it, &x, &cand, &dec, &bvar, &bval, &bup, &bint, &pos,
+                      &depth_in, &out, &wvals, &flag, &skip2, &st2, &obj2, &it2, &x2, &acc,
+                      &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj, &r_it, &fvtype, &fsq,
+                      &fbil, &flptr, &flvar, &flval, &fqptr, &fqv1, &fqv2, &fqval, &fclb, &fcub})
       b->release();
   }
 };
@@ -73,6 +74,13 @@ int ensure_glob_batch(mgpu_ctx *c, GlobState &s, int B) {
   for (DevBuf *b : {&s.obj, &s.bval}) HIPCHK(c, b->ensure((size_t)B * 8));
   for (DevBuf *b : {&s.bup, &s.bint}) HIPCHK(c, b->ensure((size_t)B));
   HIPCHK(c, s.out.ensure(sizeof(GlobOut)));
+  if (s.T > 0) {
+    HIPCHK(c, s.wvals.ensure((size_t)B * (R + s.T) * 8));
+    for (DevBuf *b : {&s.flag, &s.skip2, &s.st2, &s.it2}) HIPCHK(c, b->ensure((size_t)B * 4));
+    HIPCHK(c, s.obj2.ensure((size_t)B * 8));
+    HIPCHK(c, s.x2.ensure((size_t)B * nv * 8));
+    HIPCHK(c, s.acc.ensure(16));
+  }
   s.maxb = B;
   return MGPU_OK;
 }
@@ -87,10 +95,13 @@ int mgpu_glob_init(mgpu_ctx *c, int capacity, double incumbent) {
     return fail(c, MGPU_ERR_STATE, "mgpu_glob_init: load the relaxation LP (mgpu_load_lp), the "
                 "quadratic problem (mgpu_load_quad) and the node-rows map first");
   const QuadState &q = *c->quad;
-  if (c->lp.n != q.nv || c->nr_stride != q.R)
+  const int nsq = (int)q.sq_x.size();
+  // record = R row-state values, then 2 S tangent values per square
+  const int extra = c->nr_stride - q.R;
+  if (c->lp.n != q.nv || extra < 0 || (extra > 0 && (nsq == 0 || extra % (2 * nsq) != 0)))
     return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: LP columns (%d) / row-record stride (%d) do "
-                "not match the quadratic problem (%d vars, %d row values)", c->lp.n,
-                c->nr_stride, q.nv, q.R);
+                "not match the quadratic problem (%d vars, %d row values, %d squares)", c->lp.n,
+                c->nr_stride, q.nv, q.R, nsq);
   if (capacity < 1) return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: capacity < 1");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -100,6 +111,8 @@ int mgpu_glob_init(mgpu_ctx *c, int capacity, double incumbent) {
   const int nv = q.nv, R = q.R, m = c->lp.m, N = nv + m;
   s->nv = nv;
   s->R = R;
+  s->T = extra;
+  s->S = nsq > 0 ? extra / (2 * nsq) : 0;
   s->cap = capacity;
   s->inc = incumbent;
   s->best_x.assign((size_t)nv, NAN);
@@ -135,6 +148,12 @@ int mgpu_glob_init(mgpu_ctx *c, int capacity, double incumbent) {
   if (R > 0) HIPCHK(c, hipMemcpy(s->prows.p, rows.data(), (size_t)R * 8, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(s->pnlb.p, &ninf, 8, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(s->pdepth.p, &zero, 4, hipMemcpyHostToDevice));
+  if (s->T > 0) {   // the root's tangent slots, all free: [0, +inf]
+    HIPCHK(c, s->ptan.ensure((size_t)capacity * s->T * 8));
+    std::vector<double> t0((size_t)s->T, 0.0);
+    for (int k = 1; k < s->T; k += 2) t0[(size_t)k] = INFINITY;
+    HIPCHK(c, hipMemcpy(s->ptan.p, t0.data(), (size_t)s->T * 8, hipMemcpyHostToDevice));
+  }
   s->count = 1;
   // the root basis every node LP refactors for its own rows: the loaded LP
   // (the root's rows) from the slack basis
@@ -187,15 +206,6 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
                           s.wub.as<double>(), s.wrows.as<double>(), s.kinf.as<int32_t>(),
                           s.knm.as<int32_t>(), 0, nullptr, nullptr, nullptr, nullptr);
   if (rc != MGPU_OK) return rc;
-  // the node LPs with their own rows (K3R + K3), K2-infeasible nodes skipped
-  rc = mgpu_lp_solve_rows_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(),
-                              s.kinf.as<int32_t>(), s.wrows.as<double>(),
-                              s.root_ws ? s.ws_head.as<int32_t>() : nullptr,
-                              s.root_ws ? s.ws_st.as<int8_t>() : nullptr, 1, 0,
-                              s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
-                              s.x.as<double>(),
-                              s.root_ws ? s.ws_binv.as<double>() : nullptr);
-  if (rc != MGPU_OK) return rc;
   GlobIO io{};
   io.nb = nb;
   io.base = base;
@@ -243,6 +253,50 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
   io.prows = s.prows.as<double>();
   io.pnlb = s.pnlb.as<double>();
   io.pdepth = s.pdepth.as<int32_t>();
+  io.S = s.S;
+  io.T = s.T;
+  io.ptan = s.T > 0 ? s.ptan.as<double>() : nullptr;
+  io.wvals = s.T > 0 ? s.wvals.as<double>() : s.wrows.as<double>();
+  io.flag = s.flag.as<int32_t>();
+  io.skip2 = s.skip2.as<int32_t>();
+  io.st2 = s.st2.as<int32_t>();
+  io.it2 = s.it2.as<int32_t>();
+  io.obj2 = s.obj2.as<double>();
+  io.x2 = s.x2.as<double>();
+  io.acc = s.acc.as<unsigned long long>();
+  // the node records: K2's rows and the node's tangent slots
+  if (s.T > 0) HIPCHK(c, launch_glob_pack(io, c->stream));
+  // the node LPs with their own rows (K3R + K3), K2-infeasible nodes skipped
+  auto solve = [&](const int32_t *skip, int32_t *st, double *obj, int32_t *it, double *x) {
+    return mgpu_lp_solve_rows_dev(c, nb, s.wlb.as<double>(), s.wub.as<double>(), skip, io.wvals,
+                                  s.root_ws ? s.ws_head.as<int32_t>() : nullptr,
+                                  s.root_ws ? s.ws_st.as<int8_t>() : nullptr, 1, 0, st, obj, it,
+                                  x, s.root_ws ? s.ws_binv.as<double>() : nullptr);
+  };
+  rc = solve(s.kinf.as<int32_t>(), s.st.as<int32_t>(), s.obj.as<double>(), s.it.as<int32_t>(),
+             s.x.as<double>());
+  if (rc != MGPU_OK) return rc;
+  HIPCHK(c, launch_glob_decide(io, c->stream));
+  // the separation loop (PCBProcessor.cpp:267-280): every pass adds at least
+  // one cut to a free slot, so it ends within nsq S passes
+  long long cuts = 0, resolves = 0;
+  for (int pass = 0; s.T > 0 && pass <= s.T / 2; ++pass) {
+    HIPCHK(c, hipMemsetAsync(s.acc.p, 0, 16, c->stream));
+    HIPCHK(c, launch_glob_separate(io, c->stream));
+    unsigned long long a[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(a, s.acc.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (a[1] == 0) break;
+    cuts += (long long)a[0];
+    resolves += (long long)a[1];
+    rc = solve(io.skip2, s.st2.as<int32_t>(), s.obj2.as<double>(), s.it2.as<int32_t>(),
+               s.x2.as<double>());
+    if (rc != MGPU_OK) return rc;
+    HIPCHK(c, launch_glob_merge(io, c->stream));
+    GlobIO again = io;
+    again.only = io.flag;
+    HIPCHK(c, launch_glob_decide(again, c->stream));
+  }
   HIPCHK(c, launch_glob_round_tail(io, c->stream));
   GlobOut o;
   HIPCHK(c, hipMemcpyAsync(&o, s.out.p, sizeof o, hipMemcpyDeviceToHost, c->stream));
@@ -256,8 +310,10 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
   s.tot.rounds += 1;
   s.tot.nodes += nb;
   for (int k = 0; k < 6; ++k) s.tot.ndec[k] += o.ndec[k];
-  s.tot.lps += o.lps;
+  s.tot.lps += o.lps + resolves;
   s.tot.pivots += o.pivots;
+  s.tot.cuts += cuts;
+  s.tot.resolves += resolves;
   s.tot.br_int += o.br_int;
   s.tot.br_cont += o.ndec[0] - o.br_int;
   s.tot.open = s.count;

@@ -47,6 +47,7 @@ __device__ __forceinline__ bool at_bnds(double v, double l, double u) {
 __global__ __launch_bounds__(256) void glob_decide(GlobIO io) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b >= io.nb) return;
+  if (io.only != nullptr && io.only[b] == 0) return;
   const int nv = io.nv;
   const double *x = io.x + (size_t)b * nv;
   const double *lb = io.wlb + (size_t)b * nv;
@@ -299,6 +300,9 @@ __global__ __launch_bounds__(256) void glob_children(GlobIO io) {
       io.pub[s * nv + k] = u;
     }
     for (int k = lane; k < R; k += 64) io.prows[s * R + k] = io.wrows[(size_t)b * R + k];
+    // the node's tangent cuts go down to both children
+    for (int k = lane; k < io.T; k += 64)
+      io.ptan[s * io.T + k] = io.wvals[(size_t)b * (R + io.T) + R + k];
     if (lane == 0) {
       io.pnlb[s] = io.obj[b];
       io.pdepth[s] = io.depth_in[b] + 1;
@@ -306,11 +310,139 @@ __global__ __launch_bounds__(256) void glob_children(GlobIO io) {
   }
 }
 
+// One wave per node: the LP record [R row state | T tangent values] from
+// K2's rows and the tangent slots the node inherited.
+__global__ __launch_bounds__(256) void glob_pack(GlobIO io) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= io.nb) return;
+  const int R = io.R, T = io.T;
+  double *w = io.wvals + (size_t)b * (R + T);
+  for (int k = lane; k < R; k += 64) w[k] = io.wrows[(size_t)b * R + k];
+  for (int k = lane; k < T; k += 64) w[R + k] = io.ptan[(size_t)(io.base + b) * T + k];
+}
+
+constexpr double kInf = __builtin_inf();
+
+// QuadHandler::findLinPt_ (QuadHandler.cpp:238-285): golden-section search
+// for the point of y = x^2 nearest to (xv, yv), the reference's operations
+// in its order (sqrt of a negative y is NaN: the loop does not run and
+// addCut_'s tests fail, as there).
+__device__ double find_lin_pt(double xv, double yv) {
+  const double alfa = 0.618, errlim = 1e-4;
+  double a, b;
+  if (xv > 0) {
+    a = sqrt(yv);
+    b = xv;
+  } else {
+    a = xv;
+    b = -sqrt(yv);
+  }
+  double mu = a + alfa * (b - a);
+  double la = b - alfa * (b - a);
+  double mu_val = (mu - xv) * (mu - xv) + (mu * mu - yv) * (mu * mu - yv);
+  double la_val = (la - xv) * (la - xv) + (la * la - yv) * (la * la - yv);
+  while ((b - a) > errlim) {
+    if (mu_val < la_val) {
+      a = la;
+      la = mu;
+      la_val = mu_val;
+      mu = a + alfa * (b - a);
+      mu_val = (mu - xv) * (mu - xv) + (mu * mu - yv) * (mu * mu - yv);
+    } else {
+      b = mu;
+      mu = la;
+      mu_val = la_val;
+      la = b - alfa * (b - a);
+      la_val = (la - xv) * (la - xv) + (la * la - yv) * (la * la - yv);
+    }
+  }
+  return la;
+}
+
+// QuadHandler::separate's squares (QuadHandler.cpp:1671-1689) for the nodes
+// PCBProcessor would branch (decision 0) or hand to the NLP engine (5): for
+// each square whose LP point lies below y = x^2 (x^2 - y > rTol |y| and >
+// aTol), the tangent at findLinPt_'s point when addCut_ accepts it
+// (2 xl x - y - xl^2 > 1e-5 and 2 xl x - y > xl^2 (1 + 1e-4), :819-840),
+// into the square's first free slot.  flag[b]: cuts added (the node is
+// re-solved, SepaResolve); skip2 = !flag for that LP call.  One thread per
+// node (the search is sequential).
+__global__ __launch_bounds__(256) void glob_separate(GlobIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb) return;
+  int cuts = 0;
+  const int d = io.dec[b];
+  if (d == 0 || d == 5) {
+    const double *x = io.x + (size_t)b * io.nv;
+    double *tan = io.wvals + (size_t)b * (io.R + io.T) + io.R;
+    for (int k = 0; k < io.nsq; ++k) {
+      const double xv = x[io.sq[2 * k]], yv = x[io.sq[2 * k + 1]];
+      if (!(xv * xv - yv > kQRTol * fabs(yv) && fabs(xv * xv - yv) > kQATol)) continue;
+      const double xl = find_lin_pt(xv, yv), yl = xl * xl;
+      if (!(2 * xl * xv - yv - yl > 1e-5 && 2 * xl * xv - yv > yl * (1 + 1e-4))) continue;
+      for (int t = 0; t < io.S; ++t) {
+        double *slot = tan + 2 * (k * io.S + t);
+        if (slot[1] == kInf) {
+          slot[0] = 2 * xl;
+          slot[1] = xl * xl;
+          ++cuts;
+          break;
+        }
+      }
+    }
+  }
+  io.flag[b] = cuts > 0 ? 1 : 0;
+  io.skip2[b] = cuts > 0 ? 0 : 1;
+  if (cuts > 0) {
+    atomicAdd(io.acc, (unsigned long long)cuts);
+    atomicAdd(io.acc + 1, 1ull);
+  }
+}
+
+// The re-solved nodes' LP results replace the earlier ones (iterations add
+// up); one wave per node.
+__global__ __launch_bounds__(256) void glob_merge(GlobIO io) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= io.nb || io.flag[b] == 0) return;
+  double *x = io.x + (size_t)b * io.nv;
+  for (int k = lane; k < io.nv; k += 64) x[k] = io.x2[(size_t)b * io.nv + k];
+  if (lane == 0) {
+    io.status[b] = io.st2[b];
+    io.obj[b] = io.obj2[b];
+    io.iters[b] += io.it2[b];
+  }
+}
+
 }  // namespace
+
+hipError_t launch_glob_decide(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_decide, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_pack(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_pack, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_separate(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_separate, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_merge(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_merge, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
 
 hipError_t launch_glob_round_tail(const GlobIO &io, hipStream_t stream) {
   if (io.nb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(glob_decide, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
   hipLaunchKernelGGL(glob_summary, dim3(1), dim3(1024), 0, stream, io);
   hipLaunchKernelGGL(glob_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
   return hipGetLastError();

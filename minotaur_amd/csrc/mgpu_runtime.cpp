@@ -507,6 +507,7 @@ int mgpu_fbbt(mgpu_ctx *c, int batch, const double *lb_in, const double *ub_in,
       c->fb1_pin_bytes = 0;
       HIPCHK(c, hipHostMalloc((void **)&c->fb1_pin, bytes, hipHostMallocDefault));
       c->fb1_pin_bytes = bytes;
+      note_dev_alloc(bytes);   // pinned host memory counts too
     }
     char *hp = c->fb1_pin, *dp = nullptr;
     HIPCHK(c, hipHostGetDevicePointer((void **)&dp, hp, 0));
@@ -960,6 +961,7 @@ int mgpu_lp_solve1(mgpu_ctx *c, const double *lb, const double *ub, int ws_in, i
     c->lp1_pin_bytes = 0;
     HIPCHK(c, hipHostMalloc((void **)&c->lp1_pin, bytes, hipHostMallocDefault));
     c->lp1_pin_bytes = bytes;
+    note_dev_alloc(bytes);   // pinned host memory counts too
   }
   // (a staged variant, one H2D of the box and one D2H of the results, measured
   // 46 vs 44 us per LP through Python: the copy commands cost more than the

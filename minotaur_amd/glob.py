@@ -6,8 +6,9 @@ BranchAndBound with NodeIncRelaxer, PCBProcessor, the handlers IntVarHandler
 / LinearHandler / QuadHandler of SimpleTransformer and (option
 brancher=maxvio) MaxVioBrancher.  Here one round evaluates the top ``batch``
 nodes of an HBM stack at once: K2 (QuadHandler::presolveNode, rows rewritten
-from the parent's), K3R + K3 (each node's LP with its own rows), the decision
-and MaxVio branching, children pushed.
+from the parent's), K3R + K3 (each node's LP with its own rows), the decision,
+the squares' separation loop (tangent cuts, re-solve), MaxVio branching,
+children pushed.
 """
 from __future__ import annotations
 
@@ -17,24 +18,30 @@ import time
 from .quad import relaxation_lp
 
 
-def setup(ctx, qp):
+TAN_SLOTS = 8   # tangent-cut rows per square (QuadHandler::separate's cuts)
+
+
+def setup(ctx, qp, tan_slots=None):
     """Load a QuadProblem for the glob tree: the quadratic problem, the LP
     relaxation at the root box (QuadHandler::relax_'s rows) and the map of
-    the per-node rewritten entries.  Returns (LinProblem, NodeRows)."""
+    the per-node rewritten entries; with squares, ``tan_slots`` tangent-cut
+    rows per square for the separation loop (default TAN_SLOTS; 0: none).
+    Returns (LinProblem, NodeRows)."""
     ctx.load_quad(qp)
     rows0 = ctx.quad_rows()
-    p, nr = relaxation_lp(qp, rows0)
+    S = (TAN_SLOTS if tan_slots is None else int(tan_slots)) if qp.nsq > 0 else 0
+    p, nr = relaxation_lp(qp, rows0, S)
     ctx.load(p)
     ctx.set_node_rows(nr)
     return p, nr
 
 
 def solve(ctx, qp, batch=1024, capacity=None, max_rounds=10**9, incumbent=math.inf,
-          loaded=False):
+          loaded=False, tan_slots=None):
     """Runs the tree until the stack is empty (or max_rounds): returns
     (incumbent, x or None, stats, seconds)."""
     if not loaded:
-        setup(ctx, qp)
+        setup(ctx, qp, tan_slots)
     cap = capacity or 64 * batch
     t0 = time.perf_counter()
     ctx.glob_init(cap, incumbent)

@@ -362,7 +362,17 @@ class NodeRows:
         return q
 
 
-def relaxation_lp(qp: QuadProblem, rows=None):
+def tangent_record(qp: QuadProblem, slots: int) -> np.ndarray:
+    """The tangent part of a node record with every slot inactive: per square
+    k and slot s the pair [2 xl, xl^2] of the cut 2 xl x - y <= xl^2
+    (QuadHandler::addTangent_, QuadHandler.cpp:805-817); inactive = [0, +inf],
+    the row 0 x - y <= +inf."""
+    rec = np.zeros(2 * qp.nsq * slots)
+    rec[1::2] = np.inf
+    return rec
+
+
+def relaxation_lp(qp: QuadProblem, rows=None, tan_slots: int = 0):
     """The LP relaxation of ``p_`` that mglob's engine solves at a node
     (QuadHandler::relax_, QuadHandler.cpp:1549-1592, plus the linear rows):
 
@@ -372,6 +382,11 @@ def relaxation_lp(qp: QuadProblem, rows=None):
       and rhs), then four McCormick rows per bilinear, ``-y + a0 x0 + a1 x1
       <= rhs`` (types 0, 1) and ``y + a0 x0 + a1 x1 <= rhs`` (types 2, 3)
       (upBilCon_ rewrites a0, a1, rhs);
+    * ``tan_slots`` > 0: per square, that many tangent-cut rows
+      ``2 xl x - y <= xl^2`` (QuadHandler::separate's cuts, addTangent_,
+      QuadHandler.cpp:805-817), coefficient and bound from the node record
+      after the row state (``tangent_record``: inactive slots are 0 x - y <=
+      +inf); the record stride becomes R + 2 nsq tan_slots;
     * objective: the original objective with products replaced (0 if none).
 
     ``rows``: the row state at the root (``Context.quad_rows()`` layout,
@@ -426,6 +441,15 @@ def relaxation_lp(qp: QuadProblem, rows=None):
             hi_src.append(o + 2)
             add_row([(x0, rows[o]), (x1, rows[o + 1]), (y, -1.0 if t < 2 else 1.0)],
                     -np.inf, rows[o + 2], {x0: o, x1: o + 1})
+    R = qp.nrow_state
+    for k in range(nsq):
+        x, y = int(qp.sq_x[k]), int(qp.sq_y[k])
+        for t in range(tan_slots):
+            o = R + 2 * (k * tan_slots + t)
+            row_idx.append(len(rlo))
+            hi_src.append(o + 1)
+            terms = sorted([(x, 0.0), (y, -1.0)])
+            add_row(terms, -np.inf, np.inf, {x: o})
     obj = np.zeros(qp.nv)
     if qp.has_obj:
         for j, a in linearize(qp.ncon):
@@ -436,6 +460,6 @@ def relaxation_lp(qp: QuadProblem, rows=None):
                    rlo=np.asarray(rlo, dtype=np.float64), rhi=np.asarray(rhi, dtype=np.float64),
                    vlb=qp.vlb.copy(), vub=qp.vub.copy(), vtype=qp.vtype.copy(), obj=obj,
                    obj_const=float(qp.obj_const) if qp.has_obj else 0.0).validate()
-    nr = NodeRows(stride=qp.nrow_state, coef_pos=i32(coef_pos), coef_src=i32(coef_src),
+    nr = NodeRows(stride=R + 2 * nsq * tan_slots, coef_pos=i32(coef_pos), coef_src=i32(coef_src),
                   row_idx=i32(row_idx), lo_src=i32([-1] * len(row_idx)), hi_src=i32(hi_src))
     return p, nr

@@ -84,7 +84,8 @@ class GlobStats(ctypes.Structure):
                 ('ndec', ctypes.c_longlong * 6), ('lps', ctypes.c_longlong),
                 ('pivots', ctypes.c_longlong), ('br_int', ctypes.c_longlong),
                 ('br_cont', ctypes.c_longlong), ('open', ctypes.c_int),
-                ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double)]
+                ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double),
+                ('cuts', ctypes.c_longlong), ('resolves', ctypes.c_longlong)]
 
 
 _lib = None

@@ -21,7 +21,17 @@ Reference semantics restated (file:line under /root/reference/src/base):
   merge per variable, score 0.1 (0.8 min + 0.2 max), first maximum, up
   first when dd > ud);
 * children: IntVarHandler::getBranches at floor / ceil, QuadHandler::
-  getBranches at the value (QuadHandler.cpp:422-471).
+  getBranches at the value (QuadHandler.cpp:422-471);
+* separation of the squares (QuadHandler::separate, QuadHandler.cpp:
+  1658-1689; findLinPt_ :238-285, addCut_ / addTangent_ :805-840): a node
+  that would branch (or has no candidate) and whose LP point lies below
+  y = x^2 (x^2 - y > rTol |y| and > aTol) gets the tangent at the nearest
+  point of the parabola when it cuts the point off by the margins of addCut_;
+  the node is then re-solved (PCBProcessor.cpp:267-280, SepaResolve) and
+  decided again, until no cut is added.  The cuts go into the node's
+  tangent slots (``tan_slots`` per square, quad.relaxation_lp) and are
+  inherited by its children; the reference adds them to the one global
+  relaxation.
 Parity with the reference's own glob solver is unpinned (it needs Ipopt /
 filterSQP and its cut loop); the GPU tree is pinned against this
 restatement and its incumbents against the QCQP itself.
@@ -44,6 +54,7 @@ class _GStats:
         self.ndec = [0] * 6
         self.lps = self.pivots = 0
         self.br_int = self.br_cont = 0
+        self.cuts = self.resolves = 0
         self.open = self.last_batch = 0
         self.incumbent = math.inf
 
@@ -158,14 +169,72 @@ def decide(qp, kinf, st, val, x, lb, ub, inc):
     return 0, bvar, float(x[bvar]), bup, bint
 
 
+QA_TOL, QR_TOL = 1e-6, 1e-7   # QuadHandler aTol_, rTol_ (QuadHandler.cpp:60-67)
+
+
+def find_lin_pt(xval, yval):
+    """QuadHandler::findLinPt_ (QuadHandler.cpp:238-285): the point of y = x^2
+    nearest to (xval, yval) by golden-section search, in the reference's
+    operation order (sqrt of a negative y is NaN there: no cut follows)."""
+    alfa, errlim = 0.618, 1e-4
+    sy = math.sqrt(yval) if yval >= 0.0 else math.nan
+    if xval > 0:
+        a, b = sy, xval
+    else:
+        a, b = xval, -sy
+    mu = a + alfa * (b - a)
+    la = b - alfa * (b - a)
+    mu_val = (mu - xval) * (mu - xval) + (mu * mu - yval) * (mu * mu - yval)
+    la_val = (la - xval) * (la - xval) + (la * la - yval) * (la * la - yval)
+    while (b - a) > errlim:
+        if mu_val < la_val:
+            a = la
+            la = mu
+            la_val = mu_val
+            mu = a + alfa * (b - a)
+            mu_val = (mu - xval) * (mu - xval) + (mu * mu - yval) * (mu * mu - yval)
+        else:
+            b = mu
+            mu = la
+            mu_val = la_val
+            la = b - alfa * (b - a)
+            la_val = (la - xval) * (la - xval) + (la * la - yval) * (la * la - yval)
+    return la, la * la
+
+
+def separate(qp, x, tan, R, S):
+    """The squares part of QuadHandler::separate on one node: fills the first
+    free tangent slot of each square whose cut addCut_ accepts (record
+    ``tan`` = the node's full row record, tangent part at R); returns the
+    number of cuts added."""
+    cuts = 0
+    for k in range(qp.nsq):
+        j, y = int(qp.sq_x[k]), int(qp.sq_y[k])
+        xval, yval = float(x[j]), float(x[y])
+        if xval * xval - yval > QR_TOL * abs(yval) and abs(xval * xval - yval) > QA_TOL:
+            xl, yl = find_lin_pt(xval, yval)
+            if 2 * xl * xval - yval - yl > 1e-5 and 2 * xl * xval - yval > yl * (1 + 1e-4):
+                for t in range(S):
+                    o = R + 2 * (k * S + t)
+                    if tan[o + 1] == math.inf:
+                        tan[o] = 2 * xl
+                        tan[o + 1] = xl * xl
+                        cuts += 1
+                        break
+    return cuts
+
+
 class CpuGlobContext:
     """mgpu_glob_init / mgpu_glob_round / mgpu_glob_best on the CPU."""
 
-    def __init__(self, qp):
-        from minotaur_amd.quad import relaxation_lp
+    def __init__(self, qp, tan_slots=0):
+        from minotaur_amd.quad import relaxation_lp, tangent_record
         self.qp = qp
+        self.S = tan_slots if qp.nsq > 0 else 0
+        self.R = qp.nrow_state
         self.rows0 = oracle.quad_root_rows(qp)
-        self.p, self.nr = relaxation_lp(qp, self.rows0)
+        self.p, self.nr = relaxation_lp(qp, self.rows0, self.S)
+        self.tan0 = tangent_record(qp, self.S)
 
     def glob_init(self, capacity, incumbent=math.inf):
         qp = self.qp
@@ -174,7 +243,7 @@ class CpuGlobContext:
         # the root inverse: nodes refactor by column replacement (K3R / K3L)
         self.ws = WarmStart(ws.head, ws.st, ws.binv, None) if st == 0 else None
         self.pool = [(qp.vlb.astype(np.float64).copy(), qp.vub.astype(np.float64).copy(),
-                      self.rows0.copy(), -math.inf, 0)]
+                      np.concatenate([self.rows0, self.tan0]), -math.inf, 0)]
         self.inc = incumbent
         self.best_x = np.full(qp.nv, np.nan)
         self.tot = _GStats()
@@ -198,20 +267,51 @@ class CpuGlobContext:
         del self.pool[base:]
         LB = np.stack([nd[0] for nd in nodes])
         UB = np.stack([nd[1] for nd in nodes])
-        RW = np.stack([nd[2] for nd in nodes])
+        R = self.R
+        RW = np.stack([nd[2][:R] for nd in nodes])
         o = oracle.quad_fbbt(qp, LB, UB, self.inc, 1, RW)
-        st, obj, it, x = oracle.dual_simplex_rows(self.p, o.lb, o.ub, self.nr, o.rows,
+        # the node records: K2's rows, then the tangent slots the node inherited
+        vals = np.concatenate([o.rows, np.stack([nd[2][R:] for nd in nodes])], axis=1)
+        st, obj, it, x = oracle.dual_simplex_rows(self.p, o.lb, o.ub, self.nr, vals,
                                                   ws=self.ws, want_x=True)
+        st, obj, it, x = st.copy(), obj.copy(), it.copy(), x.copy()
         best, bidx = math.inf, -1
         children = []
         ndec = [0] * 6
+        decs = []
         for b in range(nb):
             kinf = int(o.infeas[b])
             if kinf == 0:
                 self.tot.lps += 1
+            decs.append(decide(qp, kinf, int(st[b]), float(obj[b]), x[b], o.lb[b], o.ub[b],
+                               self.inc))
+        # the separation loop (PCBProcessor.cpp:267-280): tangents for the
+        # squares of the nodes that would branch, re-solve, decide again
+        while self.S > 0:
+            flagged = []
+            for b in range(nb):
+                if decs[b][0] in (0, 5):
+                    c = separate(qp, x[b], vals[b], R, self.S)
+                    if c:
+                        self.tot.cuts += c
+                        flagged.append(b)
+            if not flagged:
+                break
+            f = np.asarray(flagged)
+            s2, o2, i2, x2 = oracle.dual_simplex_rows(self.p, o.lb[f], o.ub[f], self.nr, vals[f],
+                                                      ws=self.ws, want_x=True)
+            for t, b in enumerate(flagged):
+                st[b], obj[b], x[b] = s2[t], o2[t], x2[t]
+                it[b] += i2[t]
+                self.tot.lps += 1
+                self.tot.resolves += 1
+                decs[b] = decide(qp, 0, int(st[b]), float(obj[b]), x[b], o.lb[b], o.ub[b],
+                                 self.inc)
+        for b in range(nb):
+            kinf = int(o.infeas[b])
+            if kinf == 0:
                 self.tot.pivots += int(it[b])
-            dec, bv, bval, bup, bint = decide(qp, kinf, int(st[b]), float(obj[b]), x[b],
-                                              o.lb[b], o.ub[b], self.inc)
+            dec, bv, bval, bup, bint = decs[b]
             ndec[dec] += 1
             if dec == 3 and obj[b] < best:
                 best, bidx = float(obj[b]), b
@@ -229,7 +329,7 @@ class CpuGlobContext:
                         lb[bv] = up
                     else:
                         ub[bv] = dn
-                    children.append((lb, ub, o.rows[b].copy(), float(obj[b]),
+                    children.append((lb, ub, vals[b].copy(), float(obj[b]),
                                      nodes[b][4] + 1))
         self.pool.extend(children)
         if bidx >= 0 and best < self.inc:

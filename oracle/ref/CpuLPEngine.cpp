@@ -70,8 +70,11 @@ CpuLPEngine::~CpuLPEngine() {
 void CpuLPEngine::syncRows_() {
   n_ = (int)problem_->getNumVars();
   m_ = (int)problem_->getNumCons();
-  std::vector<int> rowptr(1, 0), colidx;
-  std::vector<double> val;
+  std::vector<int32_t> &rowptr = rowptr_, &colidx = colidx_;
+  std::vector<double> &val = val_;
+  rowptr.assign(1, 0);
+  colidx.clear();
+  val.clear();
   rlo_.resize(m_);
   rhi_.resize(m_);
   int i = 0;
@@ -293,8 +296,64 @@ void CpuLPEngine::loadFromWarmStart(const WarmStartPtr ws) {
 }
 
 void CpuLPEngine::getBasics(int *index) {
-  for (int i = 0; i < m_ && wsValid_; ++i) index[i] = ws_.head[i];
+  const std::vector<int> &h = tabOn_ ? tabHead_ : ws_.head;
+  for (int i = 0; i < m_ && (tabOn_ || wsValid_); ++i) index[i] = h[i];
 }
+
+bool CpuLPEngine::tableau_() {
+  tabHead_.clear();
+  tabBinv_.clear();
+  if (consChanged_) syncRows_();
+  if (!IsOptimalBasisAvailable() || (int)ws_.head.size() != m_) return false;
+  tabHead_.assign(ws_.head.begin(), ws_.head.end());
+  if (!lptab::invert(n_, m_, rowptr_.data(), colidx_.data(), val_.data(), tabHead_.data(),
+                     tabBinv_)) {
+    tabHead_.clear();
+    return false;
+  }
+  return true;
+}
+
+void CpuLPEngine::enableFactorization() { tabOn_ = tableau_(); }
+
+void CpuLPEngine::disableFactorization() {
+  tabOn_ = false;
+  tabHead_.clear();
+  tabBinv_.clear();
+}
+
+void CpuLPEngine::getBInvARow(int row, double *z, double *slack) {
+  if (!tabOn_ && !(tabOn_ = tableau_())) return;
+  if (row < 0 || row >= m_) return;
+  lptab::binv_a_row(n_, m_, rowptr_.data(), colidx_.data(), val_.data(), tabHead_.data(),
+                    tabBinv_.data(), row, z, slack);
+}
+
+void CpuLPEngine::views_() {
+  if (consChanged_) syncRows_();
+  tab_.fill(n_, m_, rowptr_.data(), colidx_.data(), val_.data(), clo_.data(), chi_.data(),
+            rlo_.data(), rhi_.data(), (int)x_.size() == n_ ? x_.data() : nullptr);
+}
+
+const double *CpuLPEngine::getColLower() { views_(); return tab_.clo.data(); }
+const double *CpuLPEngine::getColUpper() { views_(); return tab_.chi.data(); }
+const double *CpuLPEngine::getRowLower() { views_(); return tab_.rlo.data(); }
+const double *CpuLPEngine::getRowUpper() { views_(); return tab_.rhi.data(); }
+const double *CpuLPEngine::getRightHandSide() { views_(); return tab_.rhs.data(); }
+const double *CpuLPEngine::getRowActivity() { views_(); return tab_.act.data(); }
+const double *CpuLPEngine::getOriginalTableau() {
+  if (consChanged_) syncRows_();
+  return val_.data();
+}
+const int *CpuLPEngine::getRowStarts() {
+  if (consChanged_) syncRows_();
+  return rowptr_.data();
+}
+const int *CpuLPEngine::getIndicesofVars() {
+  if (consChanged_) syncRows_();
+  return colidx_.data();
+}
+const int *CpuLPEngine::getRowLength() { views_(); return tab_.rowlen.data(); }
 
 void CpuLPEngine::fillStats(std::vector<double> &s) {
   if (s.size() >= 6) {

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "LPEngine.h"
+#include "LPTableau.h"
 #include "WarmStart.h"
 
 namespace Minotaur {
@@ -73,9 +74,25 @@ class CpuLPEngine : public LPEngine {
   void setIterationLimit(int limit) { iterLimit_ = limit; }
   void writeStats(std::ostream &out) const;
   void fillStats(std::vector<double> &lpStats);
+  // LPEngine extras (LPEngine.h:39-73) with OsiLPEngine's conventions
+  // (integration/LPTableau.h): the host Gauss-Jordan of the optimal basis
+  void enableFactorization();
+  void disableFactorization();
+  bool IsOptimalBasisAvailable() { return status_ == ProvenOptimal && wsValid_; }
   void getBasics(int *index);
+  void getBInvARow(int row, double *z, double *slack);
   int getNumCols() { return n_; }
   int getNumRows() { return m_; }
+  const double *getColLower();
+  const double *getColUpper();
+  const double *getRowLower();
+  const double *getRowUpper();
+  const double *getRightHandSide();
+  const double *getRowActivity();
+  const double *getOriginalTableau();
+  const int *getRowStarts();
+  const int *getIndicesofVars();
+  const int *getRowLength();
   int getIterationCount() { return lastIters_; }
 
  private:
@@ -97,6 +114,14 @@ class CpuLPEngine : public LPEngine {
   double calls_, strCalls_, time_, strTime_, iters_, strIters_;
   Timer *timer_;
   std::vector<double> x_, y_, rc_;
+  std::vector<int32_t> rowptr_, colidx_;   // the rows as read (row-major)
+  std::vector<double> val_;
+  bool tableau_();
+  void views_();
+  bool tabOn_ = false;
+  std::vector<int32_t> tabHead_;
+  std::vector<double> tabBinv_;
+  lptab::Views tab_;
 };
 
 }  // namespace Minotaur

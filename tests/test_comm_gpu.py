@@ -147,3 +147,62 @@ def test_world2_host_transport_rebalance(order, warm):
     for (p0, gt0), (p1, gt1) in zip(log0, log1):
         e0, e1 = _expected_receipts([p0, p1], world)
         assert gt0 == e0 and gt1 == e1
+
+
+def _alloc_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from minotaur_amd import dist as mdist
+    from minotaur_amd.runtime import Context, alloc_stats
+    try:
+        p = random_mkp(6, 26, 3)
+        ctx = Context(0)
+        mdist.NativeComm(ctx, rank, world, 'host')
+        ctx.load(p)
+        ctx.bnb_config(1, 2)
+        ctx.bnb_brancher(0)
+        ctx.bnb_init(1 << 14)
+        if rank > 0:
+            ctx.bnb_export(1)          # the root belongs to rank 0
+        for _ in range(6):
+            ctx.bnb_round(8)
+        S = 100
+        ctx.bnb_rebalance(S)           # sizes the exchange for S
+        a1 = alloc_stats()
+        moved = [ctx.bnb_rebalance(S)[1] for _ in range(2)]
+        a2 = alloc_stats()
+        # a warm export / import round trip of equal size allocates nothing
+        trips = []
+        for _ in range(2):
+            got = len(ctx.bnb_pick(S))
+            k = min(4, got)
+            rows = ctx.bnb_export_rows(np.arange(k))
+            ctx.bnb_import_rows(rows)
+            torch.cuda.synchronize()
+            trips.append(alloc_stats())
+        out[rank] = (a1, a2, moved, trips)
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_warm_rebalance_allocates_nothing():
+    """after the first mgpu_bnb_rebalance at a pick size S (which
+    reserves the exchange's worst case for S: rows sent / received, the
+    gather staging, the pool's pack and move workspaces), further rebalances
+    at S and equal-size export / import round trips make no device (or
+    pinned host) allocation -- what lets bench.py assert a timed multi-GPU
+    headline allocation-free."""
+    import torch.multiprocessing as mp
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_alloc_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        a1, a2, moved, trips = out[r]
+        assert a2 == a1, (r, a1, a2)
+        assert trips[1] == trips[0], (r, trips)
