@@ -719,15 +719,20 @@ def glob_tree(ctx, dev, rank, world, args, B=8192, max_rounds=400):
     from minotaur_amd import glob as mglob
     from minotaur_amd.quad import random_qcqp
     out = []
-    for seed, nv0, ncon in ((17, 10, 6), (9, 12, 7), (19, 12, 7), (2, 16, 10)):
-        qp = random_qcqp(seed + rank, nv0=nv0, ncon=ncon, squares=False)
+    # bilinear QCQPs, and one with squares (y >= x^2 by the separation loop's
+    # tangent cuts, S slots per square: round 6)
+    for seed, nv0, ncon, sq in ((17, 10, 6, False), (9, 12, 7, False), (19, 12, 7, False),
+                                (2, 16, 10, False), (2, 16, 10, True)):
+        qp = random_qcqp(seed + rank, nv0=nv0, ncon=ncon, squares=sq)
         p, nr = mglob.setup(ctx, qp)
         mglob.solve(ctx, qp, batch=64, capacity=1 << 14, max_rounds=2, loaded=True)  # warm-up
         torch.cuda.synchronize()
         obj, x, st, secs = mglob.solve(ctx, qp, batch=B, capacity=64 * B,
                                        max_rounds=max_rounds, loaded=True)
         torch.cuda.synchronize()
-        e = {"instance": f"{qp.name} bilinear QCQP ({qp.nv0} vars, {qp.nbil} products, "
+        kind = (f"QCQP with {qp.nsq} squares and {qp.nbil} products" if sq else
+                f"bilinear QCQP ({qp.nbil} products")
+        e = {"instance": f"{qp.name} {kind}, {qp.nv0} vars, "
                          f"{qp.ncon} rows -> LP {p.n} cols x {p.m} rows)",
              "batch_per_gpu": B, "rounds": int(st.rounds), "nodes": int(st.nodes),
              "open": int(st.open), "solved": st.open == 0,
@@ -736,12 +741,13 @@ def glob_tree(ctx, dev, rank, world, args, B=8192, max_rounds=400):
                            "no_candidate": int(st.ndec[5])},
              "branchings_int": int(st.br_int), "branchings_spatial": int(st.br_cont),
              "lp_solves": int(st.lps), "pivots_per_lp": st.pivots / max(st.lps, 1),
+             "tangent_cuts": int(st.cuts), "resolves": int(st.resolves),
              "incumbent": obj, "seconds": secs, "nodes_per_s": st.nodes / secs,
              "relaxations_per_s": st.lps / secs}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, 'oracle'))
             from glob_tree import CpuGlobContext
-            c = CpuGlobContext(qp)
+            c = CpuGlobContext(qp, tan_slots=mglob.TAN_SLOTS if sq else 0)
             c.glob_init(1 << 22)
             t0 = time.perf_counter()
             cs = None

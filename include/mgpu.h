@@ -666,6 +666,23 @@ typedef struct {
   double incumbent;
   long long cuts, resolves;    /* tangent cuts added, node LPs re-solved for them */
 } mgpu_glob_stats;
+/* Search order, warm starts and the tightenQuad_ rule of the next
+ * mgpu_glob_init (defaults 0, 0, 1):
+ *   order 0  depth-first over batches (an HBM stack, the preferred child on top);
+ *         2  the reference's node order: TreeManager's "bfs" NodeHeap
+ *            (NodeHeap.cpp:24-47), node ids as TreeManager assigns them, the
+ *            children in QuadHandler / IntVarHandler::getBranches order;
+ *   warm  0  every node LP from the root basis refactored for its rows;
+ *         1  from its parent's optimal basis refactored for its rows, as
+ *            HipLPEngine / OsiLPEngine refactor the kept basis after
+ *            NodeIncRelaxer replays the node's rows; the root from the slack
+ *            basis;
+ *   qt    1  tightenQuad_ at every node (doQT_ set, as Glob's presolve sets
+ *            it on QCQPs it can tighten); 0 only at the first presolveNode
+ *            call (QuadHandler.cpp:1215, 1241; doQT_ false).
+ * At batch 1 with order 2, warm 1 the tree is the reference's own glob tree
+ * node for node (tests/test_glob_pin_gpu.py). */
+int mgpu_glob_config(mgpu_ctx *ctx, int order, int warm, int qt);
 int mgpu_glob_init(mgpu_ctx *ctx, int capacity, double incumbent);
 int mgpu_glob_round(mgpu_ctx *ctx, int batch, double incumbent, mgpu_glob_stats *stats);
 int mgpu_glob_best(mgpu_ctx *ctx, double *obj, double *x);

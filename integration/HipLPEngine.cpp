@@ -243,7 +243,10 @@ EngineStatus HipLPEngine::solve() {
       return status_;
     }
     needUpload_ = false;
-    if (wsValid_ && consChanged_) refactor_();
+    if (wsValid_ && consChanged_) {
+      refactor_();
+      ++nRefactor_;
+    }
     // new objective, same basis: the kernel rebuilds the reduced costs (d = NULL)
     else if (wsValid_ && objChanged_) dStale_ = true;
   }
@@ -255,6 +258,7 @@ EngineStatus HipLPEngine::solve() {
   x_.resize(n);
   rcAll_.resize(N);
   int in = -1;
+  if (!wsValid_) ++nCold_;
   if (wsValid_) {
     in = devWs_();
     if (in < 0) wsValid_ = false;

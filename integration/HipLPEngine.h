@@ -159,6 +159,10 @@ class HipLPEngine : public LPEngine {
   /// where the last enableFactorization factored the basis: 1 device (K3R),
   /// 0 host, -1 no optimal basis
   int factorSite() const { return tabSite_; }
+  /// solves that refactored the kept basis (rows edited since the basis was
+  /// made) and solves that started from the slack basis
+  long long refactors() const { return nRefactor_; }
+  long long coldSolves() const { return nCold_; }
 
  private:
   void syncRows_();            // re-read every row of problem_ (after edits)
@@ -189,6 +193,7 @@ class HipLPEngine : public LPEngine {
   std::vector<SolveRec> log_;
   bool tableau_();             // factor the optimal basis into tabHead_ / tabBinv_
   void views_();               // Osi views of the mirrors (tab_)
+  long long nRefactor_ = 0, nCold_ = 0;
   bool tabOn_;                 // enableFactorization ... disableFactorization
   int tabSite_;
   std::vector<int32_t> tabHead_;

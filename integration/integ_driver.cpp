@@ -35,6 +35,8 @@
 #include "Problem.h"
 #include "ReliabilityBrancher.h"
 #include "SimplexQuadCutGen.h"
+#include "BrVarCand.h"
+#include "Branch.h"
 #include "StrongBrancher.h"
 #include "Variable.h"
 
@@ -130,6 +132,34 @@ int integ_lp_eg0(int device) {
   delete inst;
   delete env;
   return s;
+}
+
+// the main HipLPEngine of the last integ_glob_tree3: solves that refactored
+// the kept basis, solves from the slack basis (integ_last_engine_stats)
+static long long g_last_engine[2] = {0, 0};
+
+int integ_last_engine_stats(long long *out) {
+  out[0] = g_last_engine[0];
+  out[1] = g_last_engine[1];
+  return 0;
+}
+
+// the main engine's solves in order (status, value incl. constant, pivots)
+// of the last integ_glob_tree3; returns their count (at most cap written)
+struct LogRec {
+  int status;
+  double value;
+  int iters;
+};
+static std::vector<LogRec> g_last_log;
+
+int integ_last_solve_log(int cap, int *status, double *value, int *iters) {
+  for (size_t k = 0; k < g_last_log.size() && (int)k < cap; ++k) {
+    status[k] = g_last_log[k].status;
+    value[k] = g_last_log[k].value;
+    iters[k] = g_last_log[k].iters;
+  }
+  return (int)g_last_log.size();
 }
 
 // HipLPEngine::fillStats of the engine of the last integ_bnb / integ_bnb_tree
@@ -596,6 +626,35 @@ class NoNlpQuadHandler : public QuadHandler {
   long long sepa_ = 0, rows_ = 0, rootRows_ = 0;
 };
 
+// MaxVioBrancher that logs each branching (variable, its LP value) in order:
+// the pin tests compare it with the batched tree's branching sequence
+static std::vector<std::pair<int, double>> g_last_branch;
+
+class LogMaxVioBrancher : public MaxVioBrancher {
+ public:
+  LogMaxVioBrancher(EnvPtr env, HandlerVector &h) : MaxVioBrancher(env, h) {}
+  Branches findBranches(RelaxationPtr rel, NodePtr node, ConstSolutionPtr sol,
+                        SolutionPoolPtr s_pool, BrancherStatus &br_status, ModVector &mods) {
+    Branches br = MaxVioBrancher::findBranches(rel, node, sol, s_pool, br_status, mods);
+    if (br && !br->empty()) {
+      BrVarCandPtr vc = dynamic_cast<BrVarCand *>((*br->begin())->getBrCand());
+      if (vc) {
+        const int j = (int)vc->getVar()->getIndex();
+        g_last_branch.push_back({j, sol->getPrimal()[j]});
+      }
+    }
+    return br;
+  }
+};
+
+int integ_last_branch_log(int cap, int *var, double *val) {
+  for (size_t k = 0; k < g_last_branch.size() && (int)k < cap; ++k) {
+    var[k] = g_last_branch[k].first;
+    val[k] = g_last_branch[k].second;
+  }
+  return (int)g_last_branch.size();
+}
+
 // LinearHandler without node presolve (flags bit 1): the batched glob
 // round runs no linear FBBT at its nodes
 class NoPresolveLinearHandler : public LinearHandler {
@@ -706,9 +765,15 @@ int integ_glob_tree3(int device, const QSpecI *sp, int opts, int pres_freq, doub
   handlers.push_back(v_hand);
   handlers.push_back(l_hand);
   handlers.push_back(qh);
-  v_hand->setModFlags(false, true);
-  l_hand->setModFlags(false, true);
-  qh->setModFlags(false, true);
+  // SimpleTransformer's flags (SimpleTransformer.cpp:936-949): every handler
+  // modifies the problem and the relaxation, and NodeIncRelaxer replays both
+  // (modProb_ true by default, NodeIncRelaxer.cpp:28-35).  QuadHandler's
+  // updatePBounds_ tightens p_ whatever its flags (QuadHandler.cpp:3268-
+  // 3275) and reads p_'s bounds, so with the problem's mods not replayed the
+  // tree would depend on the order nodes ran in.
+  v_hand->setModFlags(true, true);
+  l_hand->setModFlags(true, true);
+  qh->setModFlags(true, true);
   LPEnginePtr e = new_engine(env, device);
   LPEnginePtr bte = 0;
   if (opts & 8) {
@@ -725,14 +790,14 @@ int integ_glob_tree3(int device, const QSpecI *sp, int opts, int pres_freq, doub
     sb->setProblem(p);
     br = sb;
   } else {
-    br = (BrancherPtr) new MaxVioBrancher(env, handlers);
+    g_last_branch.clear();
+    br = (BrancherPtr) new LogMaxVioBrancher(env, handlers);
   }
   nproc->setBrancher(br);
   bab->setNodeProcessor(nproc);
   NodeIncRelaxerPtr nr = (NodeIncRelaxerPtr) new NodeIncRelaxer(env, handlers);
   nr->setProblem(p);
   nr->setEngine(e);
-  nr->setModFlag(false);
   bab->setNodeRelaxer(nr);
   bab->shouldCreateRoot(true);
   bab->setLogLevel(LogNone);
@@ -756,6 +821,16 @@ int integ_glob_tree3(int device, const QSpecI *sp, int opts, int pres_freq, doub
   }
   cnt[6] = qh->sepaRounds();
   cnt[7] = qh->sepaRows();
+  g_last_log.clear();
+  if (HipLPEngine *he = dynamic_cast<HipLPEngine *>(e)) {
+    g_last_engine[0] = he->refactors();
+    g_last_engine[1] = he->coldSolves();
+    for (const auto &r : he->solveLog()) g_last_log.push_back({r.status, r.value, r.iters});
+  } else if (CpuLPEngine *ce = dynamic_cast<CpuLPEngine *>(e)) {
+    g_last_engine[0] = ce->refactors();
+    g_last_engine[1] = ce->coldSolves();
+    for (const auto &r : ce->solveLog()) g_last_log.push_back({r.status, r.value, r.iters});
+  }
   if (x) {
     SolutionPtr sol = bab->getSolution();
     for (int j = 0; j < s.nv; ++j) x[j] = sol ? sol->getPrimal()[j] : NAN;

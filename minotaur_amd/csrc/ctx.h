@@ -123,6 +123,7 @@ struct mgpu_ctx {
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
   QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)
   GlobState *glob = nullptr;   // batched spatial B&B (mgpu_glob_init)
+  int glob_order = 0, glob_warm = 0, glob_qt = 1;   // mgpu_glob_config
   CommState *comm = nullptr;   // round collectives (mgpu_comm_init[_host])
 };
 
@@ -171,6 +172,17 @@ void glob_state_free(mgpu_ctx *c);  // glob_runtime.cpp
 void comm_state_free(mgpu_ctx *c);  // comm_runtime.cpp
 // the pool's migration workspaces for exchanges of up to S rows (bnb.cpp)
 int bnb_reserve_migration(mgpu_ctx *c, int S);
+// a solve's optimal basis out (rows_runtime.cpp lp_solve_rows_wo)
+struct LpWarmOut {
+  int32_t *head;
+  int8_t *st;
+  double *d, *binv;
+};
+int lp_solve_rows_wo(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                     const int32_t *skip, const double *vals, const int32_t *ws_head,
+                     const int8_t *ws_st, int ws_shared, int iter_limit, int32_t *status,
+                     double *obj, int32_t *iters, double *x, const double *ws_binv,
+                     const LpWarmOut *wo);
 // an LP batch with per-node warm starts through the K3 / K3L selection of
 // mgpu_lp_solve (mgpu_runtime.cpp); io.next is set here
 int launch_lp_nodes(mgpu_ctx *c, const LpIO &io);

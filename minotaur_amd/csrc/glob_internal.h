@@ -52,6 +52,25 @@ struct GlobIO {
   const double *obj2, *x2;
   unsigned long long *acc;      // [2] tangent cuts, re-solved nodes (this pass)
   const int32_t *only;          // glob_decide: only the nodes with only[b] != 0
+  // the round's input nodes: depth [nb] and tangent slots [nb][T] (stack
+  // order: the pool at base; reference order: gathered from pool slots)
+  const int32_t *in_depth;
+  const double *in_tan;
+  // reference order (mgpu_glob_config order 2): the pool slots of the round
+  // (gather) and of the children (2 per branched node at pos: down, up)
+  const int32_t *sel, *child_slots;
+  double *glb, *gub, *grows, *gtan;   // gathered boxes, rows, tangent slots
+  int32_t *gdepth;
+  // parent-basis warm starts (warm 1): per pool slot the parent's optimal
+  // basis (head [m], statuses [n+m], has-basis flag); gathered per node;
+  // the round's optimal bases (wo) go to the children
+  int m, N;
+  int32_t *pws_head, *ghead;
+  int8_t *pws_st, *gst;
+  uint8_t *pws_ok, *gok;
+  const int32_t *wo_head;
+  const int8_t *wo_st;
+  int32_t *skip_a;              // kinf or no basis: the warm call skips the node
 };
 
 hipError_t launch_glob_round_tail(const GlobIO &io, hipStream_t stream);
@@ -59,5 +78,9 @@ hipError_t launch_glob_decide(const GlobIO &io, hipStream_t stream);
 hipError_t launch_glob_pack(const GlobIO &io, hipStream_t stream);
 hipError_t launch_glob_separate(const GlobIO &io, hipStream_t stream);
 hipError_t launch_glob_merge(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_gather(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_skips(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_summary(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_children(const GlobIO &io, hipStream_t stream);
 
 }  // namespace mgpu

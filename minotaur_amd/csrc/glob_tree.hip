@@ -17,9 +17,10 @@
 //     from IntVarHandler (IntVarHandler.cpp:86-110: dd = x - floor x,
 //     ud = ceil x - x) then QuadHandler (QuadHandler.cpp:473-614: y = x^2
 //     violated from above, y = x0 x1 violated per LinBil::isViolated, a
-//     variable at its bounds is not a candidate), merged per variable by
-//     adding the distances (the later handler takes over when its distance
-//     sum is >= the earlier one's), score 0.8 min + 0.2 max (x 0.1 for the
+//     variable at its bounds is not a candidate), merged per variable (the
+//     later handler takes over when its distance sum is >= the earlier
+//     one's; the distances stay the earlier handler's, because the merge's
+//     setDist resolves to the empty BrCand::setDist), score 0.8 min + 0.2 max (x 0.1 for the
 //     original variables: every candidate here), the first maximum in
 //     variable order; up branch first when dd > ud.  IntVarHandler branches
 //     at floor / ceil (IntVarHandler.cpp:133-175), QuadHandler at the value
@@ -52,7 +53,7 @@ __global__ __launch_bounds__(256) void glob_decide(GlobIO io) {
   const double *x = io.x + (size_t)b * nv;
   const double *lb = io.wlb + (size_t)b * nv;
   const double *ub = io.wub + (size_t)b * nv;
-  io.depth_in[b] = io.pdepth[io.base + b];
+  io.depth_in[b] = io.in_depth[b];
   const int st = io.status[b];
   const double val = io.obj[b];
   int dec = 0;
@@ -164,10 +165,13 @@ __global__ __launch_bounds__(256) void glob_decide(GlobIO io) {
         int isint;
         if (hi && hq) {
           // the later handler (QuadHandler) takes the candidate when its
-          // distance sum is >= IntVarHandler's (MaxVioBrancher.cpp:109-113)
+          // distance sum is >= IntVarHandler's (MaxVioBrancher.cpp:129-133);
+          // the distances stay IntVarHandler's: the merge calls setDist
+          // through a BrCandPtr, and BrCand::setDist is an empty non-virtual
+          // (BrCand.cpp:44-46; a reference quirk, kept)
           isint = (id[j] + iu[j] <= qd[j] + qu[j]) ? 0 : 1;
-          d = id[j] + qd[j];
-          u = iu[j] + qu[j];
+          d = id[j];
+          u = iu[j];
         } else if (hi) {
           isint = 1;
           d = id[j];
@@ -287,9 +291,12 @@ __global__ __launch_bounds__(256) void glob_children(GlobIO io) {
   const bool isint = io.bint[b] != 0;
   const double dn = isint ? floor(v) : v, up = isint ? ceil(v) : v;
   for (int c = 0; c < 2; ++c) {
-    // c = 0: the other branch, c = 1: the preferred one (on top)
-    const bool upc = (c == 1) == (io.bup[b] != 0);
-    const size_t s = (size_t)io.base + io.pos[b] + c;
+    // stack: c = 0 the other branch, c = 1 the preferred one (on top);
+    // reference order: c = 0 the down child, c = 1 the up child, at the
+    // slots the host assigned
+    const bool upc = io.child_slots != nullptr ? c == 1 : (c == 1) == (io.bup[b] != 0);
+    const size_t s = io.child_slots != nullptr ? (size_t)io.child_slots[io.pos[b] + c]
+                                               : (size_t)io.base + io.pos[b] + c;
     for (int k = lane; k < nv; k += 64) {
       double l = io.wlb[(size_t)b * nv + k], u = io.wub[(size_t)b * nv + k];
       if (k == j) {
@@ -303,11 +310,51 @@ __global__ __launch_bounds__(256) void glob_children(GlobIO io) {
     // the node's tangent cuts go down to both children
     for (int k = lane; k < io.T; k += 64)
       io.ptan[s * io.T + k] = io.wvals[(size_t)b * (R + io.T) + R + k];
+    if (io.pws_head != nullptr) {   // the node's optimal basis for both children
+      for (int k = lane; k < io.m; k += 64)
+        io.pws_head[s * io.m + k] = io.wo_head[(size_t)b * io.m + k];
+      for (int k = lane; k < io.N; k += 64)
+        io.pws_st[s * io.N + k] = io.wo_st[(size_t)b * io.N + k];
+      if (lane == 0) io.pws_ok[s] = 1;
+    }
     if (lane == 0) {
       io.pnlb[s] = io.obj[b];
       io.pdepth[s] = io.depth_in[b] + 1;
     }
   }
+}
+
+// reference order: the round's nodes from their pool slots (one wave per node)
+__global__ __launch_bounds__(256) void glob_gather(GlobIO io) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= io.nb) return;
+  const size_t sl = (size_t)io.sel[b];
+  const int nv = io.nv, R = io.R, T = io.T;
+  for (int k = lane; k < nv; k += 64) {
+    io.glb[(size_t)b * nv + k] = io.plb[sl * nv + k];
+    io.gub[(size_t)b * nv + k] = io.pub[sl * nv + k];
+  }
+  for (int k = lane; k < R; k += 64) io.grows[(size_t)b * R + k] = io.prows[sl * R + k];
+  for (int k = lane; k < T; k += 64) io.gtan[(size_t)b * T + k] = io.ptan[sl * T + k];
+  if (io.pws_head != nullptr) {
+    for (int k = lane; k < io.m; k += 64) io.ghead[(size_t)b * io.m + k] = io.pws_head[sl * io.m + k];
+    for (int k = lane; k < io.N; k += 64) io.gst[(size_t)b * io.N + k] = io.pws_st[sl * io.N + k];
+    if (lane == 0) io.gok[b] = io.pws_ok[sl];
+  }
+  if (lane == 0) io.gdepth[b] = io.pdepth[sl];
+}
+
+// parent-basis warm starts: the warm call solves the nodes with a basis
+// (skip_a), the cold call (slack basis) the others (skip2; flag marks them
+// for glob_merge)
+__global__ __launch_bounds__(256) void glob_skips(GlobIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= io.nb) return;
+  const bool inf = io.kinf[b] != 0, ok = io.gok[b] != 0;
+  io.skip_a[b] = inf || !ok ? 1 : 0;
+  io.skip2[b] = inf || ok ? 1 : 0;
+  io.flag[b] = !inf && !ok ? 1 : 0;
 }
 
 // One wave per node: the LP record [R row state | T tangent values] from
@@ -319,7 +366,7 @@ __global__ __launch_bounds__(256) void glob_pack(GlobIO io) {
   const int R = io.R, T = io.T;
   double *w = io.wvals + (size_t)b * (R + T);
   for (int k = lane; k < R; k += 64) w[k] = io.wrows[(size_t)b * R + k];
-  for (int k = lane; k < T; k += 64) w[R + k] = io.ptan[(size_t)(io.base + b) * T + k];
+  for (int k = lane; k < T; k += 64) w[R + k] = io.in_tan[(size_t)b * T + k];
 }
 
 constexpr double kInf = __builtin_inf();
@@ -438,6 +485,30 @@ hipError_t launch_glob_separate(const GlobIO &io, hipStream_t stream) {
 hipError_t launch_glob_merge(const GlobIO &io, hipStream_t stream) {
   if (io.nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(glob_merge, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_gather(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_gather, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_skips(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_skips, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_children(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_children, dim3((io.nb + 3) / 4), dim3(256), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_summary(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_summary, dim3(1), dim3(1024), 0, stream, io);
   return hipGetLastError();
 }
 

@@ -94,6 +94,20 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
                            const int32_t *skip, const double *vals, const int32_t *ws_head,
                            const int8_t *ws_st, int ws_shared, int iter_limit, int32_t *status,
                            double *obj, int32_t *iters, double *x, const double *ws_binv) {
+  return lp_solve_rows_wo(c, batch, lb, ub, skip, vals, ws_head, ws_st, ws_shared, iter_limit,
+                          status, obj, iters, x, ws_binv, nullptr);
+}
+
+}  // extern "C"
+
+// mgpu_lp_solve_rows_dev plus the optimal basis of every solved node written
+// out (wo: head [B][m], st [B][n+m], d [B][n+m], B^-1 [B][m][m]; null: none):
+// the glob tree's parent-basis warm starts (glob_runtime.cpp)
+int lp_solve_rows_wo(mgpu_ctx *c, int batch, const double *lb, const double *ub,
+                     const int32_t *skip, const double *vals, const int32_t *ws_head,
+                     const int8_t *ws_st, int ws_shared, int iter_limit, int32_t *status,
+                     double *obj, int32_t *iters, double *x, const double *ws_binv,
+                     const LpWarmOut *wo) {
   if (!c) return MGPU_ERR_ARG;
   if (!c->loaded) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_rows: no problem loaded");
   if (!c->nr_set) return fail(c, MGPU_ERR_STATE, "mgpu_lp_solve_rows: no node rows set");
@@ -140,6 +154,12 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
   io.obj = obj;
   io.iters = iters;
   io.x = x;
+  if (wo != nullptr) {
+    io.wo_head = wo->head;
+    io.wo_st = wo->st;
+    io.wo_d = wo->d;
+    io.wo_binv = wo->binv;
+  }
   HIPCHK(c, hipEventRecord(c->ev9, c->stream));
   if (large) {
     const int grid = lp_large_grid(batch, n, m, c->num_cus);
@@ -197,6 +217,8 @@ int mgpu_lp_solve_rows_dev(mgpu_ctx *c, int batch, const double *lb, const doubl
   HIPCHK(c, hipEventRecord(c->ev3, c->stream));
   return MGPU_OK;
 }
+
+extern "C" {
 
 int mgpu_lp_solve_rows(mgpu_ctx *c, int batch, const double *lb, const double *ub,
                        const int32_t *skip, const double *vals, const int32_t *ws_head,

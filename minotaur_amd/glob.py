@@ -37,13 +37,16 @@ def setup(ctx, qp, tan_slots=None):
 
 
 def solve(ctx, qp, batch=1024, capacity=None, max_rounds=10**9, incumbent=math.inf,
-          loaded=False, tan_slots=None):
+          loaded=False, tan_slots=None, order=0, warm=0, qt=1):
     """Runs the tree until the stack is empty (or max_rounds): returns
-    (incumbent, x or None, stats, seconds)."""
+    (incumbent, x or None, stats, seconds).  order / warm / qt:
+    mgpu_glob_config (order 2, warm 1 at batch 1: the reference's own glob
+    tree node for node)."""
     if not loaded:
         setup(ctx, qp, tan_slots)
     cap = capacity or 64 * batch
     t0 = time.perf_counter()
+    ctx.glob_config(order, warm, qt)
     ctx.glob_init(cap, incumbent)
     st = None
     for _ in range(max_rounds):

@@ -42,7 +42,7 @@ EXPORTS = [
     'mgpu_lp_refactor', 'mgpu_set_lp_pfi_wide', 'mgpu_lp_pfi_cap', 'mgpu_lp_solve_path',
     'mgpu_lp_solve_path_dev', 'mgpu_bnb_guided_dive', 'mgpu_ws_alloc', 'mgpu_ws_free',
     'mgpu_ws_read', 'mgpu_ws_write', 'mgpu_lp_solve1', 'mgpu_bnb_pick', 'mgpu_bnb_export_dev',
-    'mgpu_bnb_import_dev', 'mgpu_bnb_row_width', 'mgpu_bnb_count', 'mgpu_glob_init', 'mgpu_glob_round', 'mgpu_glob_best',
+    'mgpu_bnb_import_dev', 'mgpu_bnb_row_width', 'mgpu_bnb_count', 'mgpu_glob_config', 'mgpu_glob_init', 'mgpu_glob_round', 'mgpu_glob_best',
     'mgpu_comm_unique_id', 'mgpu_comm_init', 'mgpu_comm_init_host', 'mgpu_comm_info',
     'mgpu_allreduce_f64', 'mgpu_allreduce_min', 'mgpu_round_reduce', 'mgpu_allgather_f64',
     'mgpu_alltoall_rows_dev', 'mgpu_lb_deal', 'mgpu_bnb_rebalance', 'mgpu_alloc_stats',
@@ -163,6 +163,7 @@ def load_library():
     lib.mgpu_alltoall_rows_dev.argtypes = [_P, _I, _P, _P, _P, _P]
     lib.mgpu_lb_deal.argtypes = [_I, _I, _P, _P, _P, _P]
     lib.mgpu_bnb_rebalance.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P]
+    lib.mgpu_glob_config.argtypes = [_P, _I, _I, _I]
     lib.mgpu_glob_init.argtypes = [_P, _I, _D]
     lib.mgpu_glob_round.argtypes = [_P, _I, _D, ctypes.POINTER(GlobStats)]
     lib.mgpu_glob_best.argtypes = [_P, _P, _P]
@@ -950,6 +951,13 @@ class Context:
         return op.value, int(mv.value), picked[:npk.value].copy(), got[:ngot.value].copy()
 
     # -- batched spatial B&B (mgpu_glob_*) ------------------------------------
+    def glob_config(self, order=0, warm=0, qt=1):
+        """mgpu_glob_config: the next glob_init's node order (0 stack, 2 the
+        reference's heap), warm starts (0 root basis, 1 parent basis) and
+        tightenQuad_ rule (1 every node, 0 the first call only)."""
+        self._chk(self.lib.mgpu_glob_config(self.h, int(order), int(warm), int(qt)),
+                  'mgpu_glob_config')
+
     def glob_init(self, capacity, incumbent=math.inf):
         self._chk(self.lib.mgpu_glob_init(self.h, int(capacity), float(incumbent)),
                   'mgpu_glob_init')

@@ -18,8 +18,11 @@ Reference semantics restated (file:line under /root/reference/src/base):
   LinBil::isViolated, LinBil.cpp:64-82, aTol 1e-5, rTol 1e-4; isAtBnds_
   bTol_ 1e-8, :897-902);
 * MaxVioBrancher::findCandidates_ / findBestCandidate_ (MaxVioBrancher.cpp:
-  merge per variable, score 0.1 (0.8 min + 0.2 max), first maximum, up
-  first when dd > ud);
+  merge per variable -- the later handler takes the candidate when its
+  distance sum is >= the earlier one's, but the distances stay the earlier
+  handler's: the merge calls setDist through a BrCandPtr, and
+  BrCand::setDist is an empty non-virtual (BrCand.cpp:44-46) -- score
+  0.1 (0.8 min + 0.2 max), first maximum, up first when dd > ud);
 * children: IntVarHandler::getBranches at floor / ceil, QuadHandler::
   getBranches at the value (QuadHandler.cpp:422-471);
 * separation of the squares (QuadHandler::separate, QuadHandler.cpp:
@@ -154,8 +157,11 @@ def decide(qp, kinf, st, val, x, lb, ub, inc):
         if not hi and not hq:
             continue
         if hi and hq:
+            # the later handler takes the candidate, the distances stay the
+            # earlier one's (MaxVioBrancher's merge calls the empty
+            # BrCand::setDist through a BrCandPtr, BrCand.cpp:44-46)
             isint = 0 if idd[j] + iud[j] <= qd[j] + qu[j] else 1
-            d, u = idd[j] + qd[j], iud[j] + qu[j]
+            d, u = idd[j], iud[j]
         elif hi:
             isint, d, u = 1, idd[j], iud[j]
         else:
@@ -224,8 +230,42 @@ def separate(qp, x, tan, R, S):
     return cuts
 
 
+class _Heap:
+    """TreeManager's bfs NodeHeap order (NodeHeap.cpp:24-47, as
+    glob_runtime.cpp's gheap_greater): the smallest bound within 1e-6 on top,
+    then the shallower node, then the larger id."""
+
+    def __init__(self):
+        self.items = []
+
+    @staticmethod
+    def _key(n):
+        return n
+
+    def push(self, node):
+        self.items.append(node)
+
+    def pop(self):
+        def better(a, b):   # a comes out before b
+            if a['lb'] > b['lb'] + 1e-6:
+                return False
+            if a['lb'] < b['lb'] - 1e-6:
+                return True
+            if a['depth'] != b['depth']:
+                return a['depth'] < b['depth']
+            return a['id'] > b['id']
+        best = 0
+        for i in range(1, len(self.items)):
+            if better(self.items[i], self.items[best]):
+                best = i
+        return self.items.pop(best)
+
+    def __len__(self):
+        return len(self.items)
+
+
 class CpuGlobContext:
-    """mgpu_glob_init / mgpu_glob_round / mgpu_glob_best on the CPU."""
+    """mgpu_glob_config / _init / _round / _best on the CPU."""
 
     def __init__(self, qp, tan_slots=0):
         from minotaur_amd.quad import relaxation_lp, tangent_record
@@ -235,6 +275,10 @@ class CpuGlobContext:
         self.rows0 = oracle.quad_root_rows(qp)
         self.p, self.nr = relaxation_lp(qp, self.rows0, self.S)
         self.tan0 = tangent_record(qp, self.S)
+        self.order, self.warm, self.qt = 0, 0, 1
+
+    def glob_config(self, order=0, warm=0, qt=1):
+        self.order, self.warm, self.qt = order, warm, qt
 
     def glob_init(self, capacity, incumbent=math.inf):
         qp = self.qp
@@ -242,39 +286,104 @@ class CpuGlobContext:
         st, obj, x, y, it, ws = oracle.dual_simplex_root(self.p)
         # the root inverse: nodes refactor by column replacement (K3R / K3L)
         self.ws = WarmStart(ws.head, ws.st, ws.binv, None) if st == 0 else None
-        self.pool = [(qp.vlb.astype(np.float64).copy(), qp.vub.astype(np.float64).copy(),
-                      np.concatenate([self.rows0, self.tan0]), -math.inf, 0)]
+        root = (qp.vlb.astype(np.float64).copy(), qp.vub.astype(np.float64).copy(),
+                np.concatenate([self.rows0, self.tan0]), -math.inf, 0)
+        # a node: (lb, ub, record, bound, depth[, basis head, statuses])
+        self.pool = [root + (None, None)]
+        self.heap = _Heap()
+        if self.order == 2:
+            self.heap.push({'lb': -math.inf, 'depth': 0, 'id': 0, 'node': self.pool.pop()})
+            self.next_id = 1
         self.inc = incumbent
         self.best_x = np.full(qp.nv, np.nan)
+        self.lplog = []        # (status, value, pivots) of every node LP in order
+        self.brlog = []        # (variable, value) of every branching in order
         self.tot = _GStats()
         self.tot.incumbent = incumbent
         self.tot.open = 1
+
+    def _lp(self, lb, ub, vals, heads, sts):
+        """The node LPs: warm 0 from the root basis; warm 1 from each node's
+        parent basis refactored for its rows (None: the slack basis).
+        Returns status, obj, iters, x and the final bases (warm 1)."""
+        B = lb.shape[0]
+        if self.warm != 1:
+            st, obj, it, x = oracle.dual_simplex_rows(self.p, lb, ub, self.nr, vals,
+                                                      ws=self.ws, want_x=True)
+            return st.copy(), obj.copy(), it.copy(), x.copy(), None, None
+        m, N = self.p.m, self.p.n + self.p.m
+        st = np.zeros(B, dtype=np.int32)
+        obj = np.zeros(B)
+        it = np.zeros(B, dtype=np.int32)
+        x = np.zeros((B, self.p.n))
+        ho = np.zeros((B, m), dtype=np.int32)
+        so = np.zeros((B, N), dtype=np.int8)
+        warm = [b for b in range(B) if heads[b] is not None]
+        cold = [b for b in range(B) if heads[b] is None]
+        for idx, w in ((warm, True), (cold, False)):
+            if not idx:
+                continue
+            f = np.asarray(idx)
+            ws = WarmStart(np.stack([heads[b] for b in idx]), np.stack([sts[b] for b in idx]),
+                           None, None) if w else None
+            r = oracle.dual_simplex_rows(self.p, lb[f], ub[f], self.nr, vals[f], ws=ws,
+                                         want_x=True, want_ws=True)
+            st[f], obj[f], it[f], x[f], ho[f], so[f] = r
+        return st, obj, it, x, ho, so
 
     def glob_round(self, batch, incumbent=math.inf):
         qp = self.qp
         if incumbent < self.inc:
             self.inc = incumbent
-        nb = min(batch, len(self.pool))
-        if len(self.pool) + nb > self.cap:
-            nb = self.cap - len(self.pool)
-        if nb <= 0:
-            if self.pool:
+        heap = self.order == 2
+        if heap:
+            nodes, ids = [], []
+            while len(nodes) < batch and len(self.heap):
+                top = self.heap.pop()
+                if top['lb'] > self.inc - 1e-6 or \
+                        abs(self.inc - top['lb']) / (abs(self.inc) + 1e-6) * 100.0 < 1e-6:
+                    continue
+                nodes.append(top['node'])
+                ids.append(top['id'])
+            nb = len(nodes)
+        else:
+            nb = min(batch, len(self.pool))
+            if len(self.pool) + nb > self.cap:
+                nb = self.cap - len(self.pool)
+            if nb <= 0 and self.pool:
                 raise RuntimeError('glob pool full')
+            base = len(self.pool) - nb
+            nodes = self.pool[base:]
+            del self.pool[base:]
+        if nb <= 0:
             self.tot.open = 0
             return self.tot
-        base = len(self.pool) - nb
-        nodes = self.pool[base:]
-        del self.pool[base:]
+        R = self.R
         LB = np.stack([nd[0] for nd in nodes])
         UB = np.stack([nd[1] for nd in nodes])
-        R = self.R
         RW = np.stack([nd[2][:R] for nd in nodes])
-        o = oracle.quad_fbbt(qp, LB, UB, self.inc, 1, RW)
+        qt = 1 if (self.qt or self.tot.nodes == 0) else 0
+        o = oracle.quad_fbbt(qp, LB, UB, self.inc, qt, RW)
         # the node records: K2's rows, then the tangent slots the node inherited
         vals = np.concatenate([o.rows, np.stack([nd[2][R:] for nd in nodes])], axis=1)
-        st, obj, it, x = oracle.dual_simplex_rows(self.p, o.lb, o.ub, self.nr, vals,
-                                                  ws=self.ws, want_x=True)
-        st, obj, it, x = st.copy(), obj.copy(), it.copy(), x.copy()
+        heads = [nd[5] if self.warm == 1 else None for nd in nodes]
+        sts = [nd[6] if self.warm == 1 else None for nd in nodes]
+        live = [b for b in range(nb) if int(o.infeas[b]) == 0]
+        st = np.full(nb, 12, dtype=np.int32)
+        obj = np.full(nb, math.inf)
+        it = np.zeros(nb, dtype=np.int32)
+        x = np.zeros((nb, qp.nv))
+        wh, wst = [None] * nb, [None] * nb
+        if live:
+            f = np.asarray(live)
+            r = self._lp(o.lb[f], o.ub[f], vals[f], [heads[b] for b in live],
+                         [sts[b] for b in live])
+            st[f], obj[f], it[f], x[f] = r[0], r[1], r[2], r[3]
+            for b in live:
+                self.lplog.append((int(st[b]), float(obj[b]), int(it[b])))
+            if self.warm == 1:
+                for t, b in enumerate(live):
+                    wh[b], wst[b] = r[4][t], r[5][t]
         best, bidx = math.inf, -1
         children = []
         ndec = [0] * 6
@@ -286,7 +395,8 @@ class CpuGlobContext:
             decs.append(decide(qp, kinf, int(st[b]), float(obj[b]), x[b], o.lb[b], o.ub[b],
                                self.inc))
         # the separation loop (PCBProcessor.cpp:267-280): tangents for the
-        # squares of the nodes that would branch, re-solve, decide again
+        # squares of the nodes that would branch, re-solve (warm 1: from the
+        # node's last basis), decide again
         while self.S > 0:
             flagged = []
             for b in range(nb):
@@ -298,15 +408,19 @@ class CpuGlobContext:
             if not flagged:
                 break
             f = np.asarray(flagged)
-            s2, o2, i2, x2 = oracle.dual_simplex_rows(self.p, o.lb[f], o.ub[f], self.nr, vals[f],
-                                                      ws=self.ws, want_x=True)
+            r = self._lp(o.lb[f], o.ub[f], vals[f],
+                         [wh[b] if self.warm == 1 else None for b in flagged],
+                         [wst[b] if self.warm == 1 else None for b in flagged])
             for t, b in enumerate(flagged):
-                st[b], obj[b], x[b] = s2[t], o2[t], x2[t]
-                it[b] += i2[t]
+                st[b], obj[b], x[b] = r[0][t], r[1][t], r[3][t]
+                it[b] += r[2][t]
+                if self.warm == 1:
+                    wh[b], wst[b] = r[4][t], r[5][t]
                 self.tot.lps += 1
                 self.tot.resolves += 1
                 decs[b] = decide(qp, 0, int(st[b]), float(obj[b]), x[b], o.lb[b], o.ub[b],
                                  self.inc)
+        kids = []
         for b in range(nb):
             kinf = int(o.infeas[b])
             if kinf == 0:
@@ -316,22 +430,44 @@ class CpuGlobContext:
             if dec == 3 and obj[b] < best:
                 best, bidx = float(obj[b]), b
             if dec == 0:
+                self.brlog.append((int(bv), float(bval)))
                 if bint:
                     self.tot.br_int += 1
                 else:
                     self.tot.br_cont += 1
                 dn = math.floor(bval) if bint else bval
                 up = math.ceil(bval) if bint else bval
-                for c in range(2):
-                    upc = (c == 1) == (bup != 0)
+                made = {}
+                for upc in (False, True):
                     lb, ub = o.lb[b].copy(), o.ub[b].copy()
                     if upc:
                         lb[bv] = up
                     else:
                         ub[bv] = dn
-                    children.append((lb, ub, vals[b].copy(), float(obj[b]),
-                                     nodes[b][4] + 1))
-        self.pool.extend(children)
+                    made[upc] = (lb, ub, vals[b].copy(), float(obj[b]), nodes[b][4] + 1,
+                                 wh[b], wst[b])
+                if heap:
+                    # QuadHandler::getBranches: down, up; IntVarHandler: the
+                    # guided dive's side first with an incumbent, else the
+                    # candidate's preferred direction
+                    down_first = True
+                    if bint:
+                        down_first = bup == 0
+                        if math.isfinite(self.inc) and not math.isnan(self.best_x[bv]):
+                            down_first = self.best_x[bv] < bval
+                    order = (False, True) if down_first else (True, False)
+                    for upc in order:
+                        kids.append(made[upc])
+                else:
+                    for c in range(2):
+                        upc = (c == 1) == (bup != 0)
+                        children.append(made[upc])
+        if heap:
+            for k in kids:
+                self.heap.push({'lb': k[3], 'depth': k[4], 'id': self.next_id, 'node': k})
+                self.next_id += 1
+        else:
+            self.pool.extend(children)
         if bidx >= 0 and best < self.inc:
             self.inc = best
             self.best_x = x[bidx].copy()
@@ -339,7 +475,7 @@ class CpuGlobContext:
         self.tot.nodes += nb
         for k in range(6):
             self.tot.ndec[k] += ndec[k]
-        self.tot.open = len(self.pool)
+        self.tot.open = len(self.heap) if heap else len(self.pool)
         self.tot.last_batch = nb
         self.tot.incumbent = self.inc
         if ndec[4]:

@@ -1027,7 +1027,8 @@ int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
                           const int *coef_src, int nrow, const int *row, const int *lo_src,
                           const int *hi_src, const int *ws_head, const signed char *ws_st,
                           int ws_shared, int iter_limit, int *status, double *obj, double *x,
-                          int *iters, int nthreads, const double *ws_binv0)
+                          int *iters, int nthreads, const double *ws_binv0, int *head_out,
+                          signed char *st_out)
 {
   const int nnz = colptr[n];
   const size_t N = (size_t) (n + m);
@@ -1078,6 +1079,9 @@ int orc_dual_simplex_rows(int n, int m, const int *colptr, const int *rowidx,
                                     have ? ws_head + wb * m : 0, have ? ws_st + wb * N : 0, 0, 0,
                                     have, 0, iter_limit, obj + b, x ? x + (size_t) b * n : 0,
                                     iters + b, 0, h, s, bi, 0, 0);
+      /* the final basis (the glob tree's parent-basis warm starts) */
+      if (head_out) memcpy(head_out + (size_t) b * m, h, sizeof(int) * (size_t) m);
+      if (st_out) memcpy(st_out + (size_t) b * N, s, N);
     }
     free(cv); free(lo); free(hi); free(h); free(s); free(bi); free(al);
   }

@@ -619,7 +619,7 @@ def node_decide(vtype, status, obj, x, incumbent=math.inf, fbbt_infeas=None, abs
 
 
 def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1,
-                      want_x=False):
+                      want_x=False, want_ws=False):
     """Per-node rows (mgpu_lp_solve_rows): node b solves ``p`` with the entries
     and row bounds of ``nr`` (a quad.NodeRows) taken from ``vals[b]``, from
     the warm basis ``ws`` (head/st; 1-D shared or per node) refactored for
@@ -630,7 +630,7 @@ def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1
     l.orc_dual_simplex_rows.restype = _I
     l.orc_dual_simplex_rows.argtypes = ([_I, _I] + [_P] * 6 + [_I] + [_P] * 3 + [_I, _I]
                                         + [_P] * 2 + [_I] + [_P] * 5 + [_I, _I] + [_P] * 4
-                                        + [_I, _P])
+                                        + [_I, _P, _P, _P])
     LB = np.ascontiguousarray(LB, dtype=np.float64)
     UB = np.ascontiguousarray(UB, dtype=np.float64)
     vals = np.ascontiguousarray(vals, dtype=np.float64)
@@ -662,9 +662,14 @@ def dual_simplex_rows(p, LB, UB, nr, vals, ws=None, iter_limit=10000, nthreads=1
     obj = np.zeros(B)
     it = np.zeros(B, dtype=np.int32)
     x = np.zeros((B, p.n)) if want_x else None
+    ho = np.zeros((B, p.m), dtype=np.int32) if want_ws else None
+    so = np.zeros((B, p.n + p.m), dtype=np.int8) if want_ws else None
     l.orc_dual_simplex_rows(p.n, p.m, _ptr(colptr), _ptr(rowidx), _ptr(cval), _ptr(p.obj),
                             _ptr(p.rlo), _ptr(p.rhi), B, _ptr(LB), _ptr(UB), _ptr(vals),
                             int(nr.stride), int(cpos.size), _ptr(cpos), _ptr(csrc), int(row.size),
                             _ptr(row), _ptr(lo), _ptr(hi), _ptr(h), _ptr(s), shared, iter_limit,
-                            _ptr(st), _ptr(obj), _ptr(x), _ptr(it), nthreads, _ptr(b0))
+                            _ptr(st), _ptr(obj), _ptr(x), _ptr(it), nthreads, _ptr(b0),
+                            _ptr(ho), _ptr(so))
+    if want_ws:   # the final bases (head [B][m], statuses [B][n+m]; status 0 / 6)
+        return st, obj + p.obj_const, it, x, ho, so
     return st, obj + p.obj_const, it, x

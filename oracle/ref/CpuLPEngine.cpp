@@ -163,6 +163,8 @@ EngineStatus CpuLPEngine::solve() {
   // have_binv: 1 inverse and reduced costs given, 2 inverse given and the
   // reduced costs rebuilt for this objective, 0 re-invert the basis
   const int have_binv = !wsValid_ ? 0 : binvStale_ ? 0 : dStale_ ? 2 : 1;
+  if (!wsValid_) ++nCold_;
+  else if (binvStale_) ++nRefactor_;
   x_.assign(n, 0.0);
   y_.assign(m, 0.0);
   double obj = 0.0;
@@ -189,6 +191,7 @@ EngineStatus CpuLPEngine::solve() {
     sol_->setObjValue(INFINITY);
   }
   lastIters_ = it;
+  log_.push_back({(int)status_, sol_->getObjValue(), it});
   iters_ += it;
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   time_ += dt;

@@ -94,6 +94,14 @@ class CpuLPEngine : public LPEngine {
   const int *getIndicesofVars();
   const int *getRowLength();
   int getIterationCount() { return lastIters_; }
+  struct SolveRec {
+    int status;
+    double value;
+    int iters;
+  };
+  const std::vector<SolveRec> &solveLog() const { return log_; }
+  long long refactors() const { return nRefactor_; }
+  long long coldSolves() const { return nCold_; }
 
  private:
   void syncRows_();  // re-read every row of problem_, rebuild the CSC
@@ -118,6 +126,8 @@ class CpuLPEngine : public LPEngine {
   std::vector<double> val_;
   bool tableau_();
   void views_();
+  long long nRefactor_ = 0, nCold_ = 0;
+  std::vector<SolveRec> log_;
   bool tabOn_ = false;
   std::vector<int32_t> tabHead_;
   std::vector<double> tabBinv_;
