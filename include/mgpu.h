@@ -665,9 +665,10 @@ typedef struct {
   int open, last_batch;
   double incumbent;
   long long cuts, resolves;    /* tangent cuts added, node LPs re-solved for them */
+  long long obbt_lps;          /* root OBBT's bound LPs (its root re-solve counts in lps) */
 } mgpu_glob_stats;
-/* Search order, warm starts and the tightenQuad_ rule of the next
- * mgpu_glob_init (defaults 0, 0, 1):
+/* Search order, warm starts, the tightenQuad_ rule, the linear node
+ * presolve and root OBBT of the next mgpu_glob_init (defaults 0, 0, 1, 0, 0):
  *   order 0  depth-first over batches (an HBM stack, the preferred child on top);
  *         2  the reference's node order: TreeManager's "bfs" NodeHeap
  *            (NodeHeap.cpp:24-47), node ids as TreeManager assigns them, the
@@ -679,10 +680,30 @@ typedef struct {
  *            basis;
  *   qt    1  tightenQuad_ at every node (doQT_ set, as Glob's presolve sets
  *            it on QCQPs it can tighten); 0 only at the first presolveNode
- *            call (QuadHandler.cpp:1215, 1241; doQT_ false).
+ *            call (QuadHandler.cpp:1215, 1241; doQT_ false);
+ *   lin   1  LinearHandler::presolveNode before QuadHandler's at every node
+ *            (PCBProcessor::presolveNode_, PCBProcessor.cpp:134-175; Glob sets
+ *            pres_freq 1, Glob.cpp:404): simplePresolve in node mode
+ *            (LinearHandler.cpp:1592-1653) over the node's relaxation rows --
+ *            the linear rows, the secant / McCormick rows as the node
+ *            inherited them, the tangent cuts -- with the incumbent's
+ *            objective bound once one is known; a node it proves infeasible
+ *            is pruned before its LP (decision 1, no LP counted); 0 none;
+ *   obbt  1  root OBBT (OBBT option, Environment.cpp:325-326, on in Glob):
+ *            QuadHandler::postSolveRootNode (QuadHandler.cpp:1397-1547) when
+ *            the root's first LP neither prunes nor is feasible
+ *            (PCBProcessor.cpp:256-262) -- the variables of violated products
+ *            marked, tightenLP_'s bound LPs chained one after the other on a
+ *            bound-tightening context of the round's own (bte_: each from the
+ *            previous optimal basis, the first from the slack basis),
+ *            setItmpFromSol_ after each, updatePBounds_, then the secant /
+ *            McCormick rows rewritten for the new box; the root is re-solved
+ *            when its point violates the tightened relaxation (SepaResolve)
+ *            and decided again either way; 0 none.
  * At batch 1 with order 2, warm 1 the tree is the reference's own glob tree
- * node for node (tests/test_glob_pin_gpu.py). */
-int mgpu_glob_config(mgpu_ctx *ctx, int order, int warm, int qt);
+ * node for node, with or without the linear presolve and root OBBT
+ * (tests/test_glob_pin_{cpu,gpu}.py). */
+int mgpu_glob_config(mgpu_ctx *ctx, int order, int warm, int qt, int lin, int obbt);
 int mgpu_glob_init(mgpu_ctx *ctx, int capacity, double incumbent);
 int mgpu_glob_round(mgpu_ctx *ctx, int batch, double incumbent, mgpu_glob_stats *stats);
 int mgpu_glob_best(mgpu_ctx *ctx, double *obj, double *x);

@@ -123,7 +123,7 @@ struct mgpu_ctx {
   BnbState *bnb = nullptr;     // batched B&B tree (mgpu_bnb_init)
   QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)
   GlobState *glob = nullptr;   // batched spatial B&B (mgpu_glob_init)
-  int glob_order = 0, glob_warm = 0, glob_qt = 1;   // mgpu_glob_config
+  int glob_order = 0, glob_warm = 0, glob_qt = 1, glob_lin = 0, glob_obbt = 0;  // mgpu_glob_config
   CommState *comm = nullptr;   // round collectives (mgpu_comm_init[_host])
 };
 

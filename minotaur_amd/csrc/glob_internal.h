@@ -71,6 +71,21 @@ struct GlobIO {
   const int32_t *wo_head;
   const int8_t *wo_st;
   int32_t *skip_a;              // kinf or no basis: the warm call skips the node
+  // LinearHandler::presolveNode on the node's relaxation (mgpu_glob_config
+  // lin 1; glob_linear): the M rows of the relaxation as a term table, rows
+  // ascending, each row's terms ascending by variable.  A term's weight is
+  // ltval (ltsrc < 0) or the node record's value ltsrc (< R: the rows frows,
+  // else the tangent slots ftan); a row's upper side likewise (lrhsrc).
+  // Column incidence lcptr / lcterm (term indices).  Objective loidx /
+  // loval; has_inc: the incumbent bound inc_ub = incumbent - constant.
+  int M, nobj, cons_bad, has_inc;
+  double inc_ub;
+  const int32_t *lrptr, *ltvar, *ltsrc, *ltrow, *lrhsrc, *lcptr, *lcterm, *loidx;
+  const double *ltval, *lrlo, *lrhi, *loval;
+  const double *flb_in, *fub_in, *frows, *ftan;   // the round's nodes as they come
+  double *flb, *fub;            // [nb][nv] the presolved boxes (K2's input)
+  int32_t *finf;                // [nb] checkBounds_ found the node infeasible
+  uint8_t *fflag;               // [nb][M] the rows' BFlag
 };
 
 hipError_t launch_glob_round_tail(const GlobIO &io, hipStream_t stream);
@@ -82,5 +97,7 @@ hipError_t launch_glob_gather(const GlobIO &io, hipStream_t stream);
 hipError_t launch_glob_skips(const GlobIO &io, hipStream_t stream);
 hipError_t launch_glob_summary(const GlobIO &io, hipStream_t stream);
 hipError_t launch_glob_children(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_linear(const GlobIO &io, hipStream_t stream);
+hipError_t launch_glob_linear_verdict(const GlobIO &io, hipStream_t stream);
 
 }  // namespace mgpu

@@ -5,6 +5,8 @@
 // MaxVioBrancher; BranchAndBound.cpp:424-514) for a QCQP after
 // SimpleTransformer: one round pops the top B open nodes of an HBM stack and
 // runs, all on the device,
+//   lin  (mgpu_glob_config lin 1) LinearHandler::presolveNode: simplePresolve
+//        in node mode over the node's relaxation rows (glob_linear);
 //   K2   QuadHandler::presolveNode (QuadHandler.cpp:1204-1269): bound
 //        propagation over the products and tightenQuad_, then the rewrite of
 //        the node's secant / McCormick rows (upSqCon_ / upBilCon_,
@@ -17,12 +19,18 @@
 //   decide     shouldPrune_, IntVarHandler + QuadHandler isFeasible, and
 //        MaxVioBrancher over both handlers' candidates (glob_tree.hip),
 //        spatial branching at the LP value on a continuous variable;
+//   OBBT (mgpu_glob_config obbt 1, the root only) QuadHandler::
+//        postSolveRootNode's bound LPs, chained on a bound-tightening
+//        context of its own (bte_), then the root re-solved when its point
+//        left the tightened relaxation (PCBProcessor.cpp:256-280);
 //   children   two per branched node, each with the node's tightened box,
 //        the branching bound and the node's rows.
 // One small record comes back per round (counts, best feasible node).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <utility>
 #include <vector>
 
 #include "ctx.h"
@@ -54,7 +62,8 @@ struct GlobState {
   // mgpu_glob_config at init: order 0 stack / 2 reference heap; warm 0 the
   // root basis / 1 the parent's basis; qt 1 tightenQuad_ at every node / 0 at
   // the first presolveNode call only
-  int order = 0, warm = 0, qt = 1;
+  int order = 0, warm = 0, qt = 1, lin = 0, obbt = 0;
+  mgpu_ctx *bte = nullptr;       // root OBBT's bound-tightening engine (bte_)
   std::vector<GHeap> heap;
   std::vector<int> free_slots;
   long long next_id = 1;
@@ -72,6 +81,12 @@ struct GlobState {
   DevBuf wvals, flag, skip2, st2, obj2, it2, x2, acc;   // the separation loop
   DevBuf ws_head, ws_st, ws_d, ws_binv, r_st, r_obj, r_it;
   DevBuf fvtype, fsq, fbil, flptr, flvar, flval, fqptr, fqv1, fqv2, fqval, fclb, fcub;
+  // the linear presolve (lin 1): the relaxation's term table and its scratch
+  int M = 0, nobj = 0, cons_bad = 0;
+  std::vector<int32_t> h_rptr, h_tvar, h_tsrc, h_rhsrc, h_oidx;
+  std::vector<double> h_tval, h_rlo, h_rhi, h_oval;
+  DevBuf lrptr, ltvar, ltsrc, ltrow, lrhsrc, lcptr, lcterm, loidx, ltval, lrlo, lrhi, loval;
+  DevBuf flb, fub, finf, fflag;
   void release() {
     for (DevBuf *b : {&plb, &pub, &prows, &pnlb, &pdepth, &ptan, &wlb, &wub, &wrows, &kinf,
                       &knm, &st, &obj, &it, &x, &cand, &dec, &bvar, &bval, &bup, &bint, &pos,
@@ -79,8 +94,12 @@ struct GlobState {
                       &ws_head, &ws_st, &ws_d, &ws_binv, &r_st, &r_obj, &r_it, &fvtype, &fsq,
                       &fbil, &flptr, &flvar, &flval, &fqptr, &fqv1, &fqv2, &fqval, &fclb, &fcub,
                       &pws_head, &pws_st, &pws_ok, &gsel, &cslots, &glb, &gub, &grows, &gtan,
-                      &gdepth, &ghead, &gst, &gok, &skip_a, &wo_head, &wo_st, &wo_d, &wo_binv})
+                      &gdepth, &ghead, &gst, &gok, &skip_a, &wo_head, &wo_st, &wo_d, &wo_binv,
+                      &lrptr, &ltvar, &ltsrc, &ltrow, &lrhsrc, &lcptr, &lcterm, &loidx, &ltval,
+                      &lrlo, &lrhi, &loval, &flb, &fub, &finf, &fflag})
       b->release();
+    if (bte) mgpu_destroy(bte);
+    bte = nullptr;
   }
 };
 
@@ -131,7 +150,394 @@ int ensure_glob_batch(mgpu_ctx *c, GlobState &s, int B) {
     HIPCHK(c, s.wo_d.ensure((size_t)B * N * 8));
     HIPCHK(c, s.wo_binv.ensure((size_t)B * m * m * 8));
   }
+  if (s.lin) {
+    HIPCHK(c, s.flb.ensure((size_t)B * nv * 8));
+    HIPCHK(c, s.fub.ensure((size_t)B * nv * 8));
+    HIPCHK(c, s.finf.ensure((size_t)B * 4));
+    HIPCHK(c, s.fflag.ensure((size_t)B * (s.M > 0 ? s.M : 1)));
+  }
   s.maxb = B;
+  return MGPU_OK;
+}
+
+// The relaxation's rows as LinearHandler sees them (the rows of
+// quad.relaxation_lp, in its order): the linear rows with every product
+// replaced by its auxiliary (duplicates summed, |a| <= 1e-9 dropped, terms
+// ascending), one secant row per square, four McCormick rows per bilinear,
+// S tangent rows per square.  Record offsets: the secant [a_x, rhs] at 2k,
+// bilinear k's row t [a0, a1, rhs] at 2 nsq + 12 k + 3 t, tangent slot t of
+// square k [2 xl, xl^2] at R + 2 (k S + t).
+int build_linear_table(mgpu_ctx *c, GlobState &s) {
+  const QuadState &q = *c->quad;
+  const int nsq = (int)q.sq_x.size(), nbil = (int)q.bil_x0.size(), R = q.R, S = s.S;
+  std::map<std::pair<int, int>, int> aux;
+  for (int k = 0; k < nsq; ++k) aux[{q.sq_x[k], q.sq_x[k]}] = q.sq_y[k];
+  for (int k = 0; k < nbil; ++k) aux[{q.bil_x0[k], q.bil_x1[k]}] = q.bil_y[k];
+  struct T {
+    int var, src;
+    double val;
+  };
+  std::vector<int32_t> rptr{0}, tvar, tsrc, trow, rhsrc;
+  std::vector<double> tval, rlo, rhi;
+  auto add_row = [&](std::vector<T> terms, double lo, double hi, int hsrc) {
+    std::sort(terms.begin(), terms.end(), [](const T &a, const T &b) { return a.var < b.var; });
+    const int r = (int)rlo.size();
+    for (const T &t : terms) {
+      tvar.push_back(t.var);
+      tsrc.push_back(t.src);
+      tval.push_back(t.val);
+      trow.push_back(r);
+    }
+    rptr.push_back((int32_t)tvar.size());
+    rlo.push_back(lo);
+    rhi.push_back(hi);
+    rhsrc.push_back(hsrc);
+  };
+  auto linearize = [&](int f, std::vector<T> &out) -> int {
+    std::map<int, double> d;
+    for (int t = q.h_lptr[f]; t < q.h_lptr[f + 1]; ++t) d[q.h_lvar[t]] += q.h_lval[t];
+    for (int t = q.h_qptr[f]; t < q.h_qptr[f + 1]; ++t) {
+      auto it = aux.find({q.h_qv1[t], q.h_qv2[t]});
+      if (it == aux.end()) it = aux.find({q.h_qv2[t], q.h_qv1[t]});
+      if (it == aux.end()) return -1;
+      d[it->second] += q.h_qval[t];
+    }
+    for (const auto &e : d)
+      if (std::fabs(e.second) > 1e-9) out.push_back({e.first, -1, e.second});
+    return 0;
+  };
+  int bad = 0;
+  for (int f = 0; f < q.ncon; ++f) {
+    std::vector<T> terms;
+    if (linearize(f, terms) != 0)
+      return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: a product of function %d has no auxiliary", f);
+    add_row(terms, q.h_clb[f], q.h_cub[f], -1);
+    if (q.h_clb[f] > q.h_cub[f] + 1e-8) bad = 1;
+  }
+  for (int k = 0; k < nsq; ++k)
+    add_row({{q.sq_x[k], 2 * k, 0.0}, {q.sq_y[k], -1, 1.0}}, -INFINITY, 0.0, 2 * k + 1);
+  for (int k = 0; k < nbil; ++k)
+    for (int t = 0; t < 4; ++t) {
+      const int o = 2 * nsq + 12 * k + 3 * t;
+      add_row({{q.bil_x0[k], o, 0.0}, {q.bil_x1[k], o + 1, 0.0},
+               {q.bil_y[k], -1, t < 2 ? -1.0 : 1.0}}, -INFINITY, 0.0, o + 2);
+    }
+  for (int k = 0; k < nsq; ++k)
+    for (int t = 0; t < S; ++t) {
+      const int o = R + 2 * (k * S + t);
+      add_row({{q.sq_x[k], o, 0.0}, {q.sq_y[k], -1, -1.0}}, -INFINITY, 0.0, o + 1);
+    }
+  std::vector<T> ob;
+  if (q.has_obj && linearize(q.ncon, ob) != 0)
+    return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: a product of the objective has no auxiliary");
+  std::vector<int32_t> oidx;
+  std::vector<double> oval;
+  for (const T &t : ob) {
+    oidx.push_back(t.var);
+    oval.push_back(t.val);
+  }
+  // column incidence (term indices)
+  const int nv = s.nv, nt = (int)tvar.size();
+  std::vector<int32_t> cptr((size_t)nv + 1, 0), cterm((size_t)nt);
+  for (int t = 0; t < nt; ++t) ++cptr[(size_t)tvar[t] + 1];
+  for (int j = 0; j < nv; ++j) cptr[(size_t)j + 1] += cptr[(size_t)j];
+  std::vector<int32_t> fill(cptr.begin(), cptr.end() - 1);
+  for (int t = 0; t < nt; ++t) cterm[(size_t)fill[(size_t)tvar[t]]++] = t;
+  s.M = (int)rlo.size();
+  s.nobj = (int)oidx.size();
+  s.cons_bad = bad;
+  s.h_rptr = rptr;
+  s.h_tvar = tvar;
+  s.h_tsrc = tsrc;
+  s.h_tval = tval;
+  s.h_rlo = rlo;
+  s.h_rhi = rhi;
+  s.h_rhsrc = rhsrc;
+  s.h_oidx = oidx;
+  s.h_oval = oval;
+  if (!s.lin) return MGPU_OK;
+  HIPCHK(c, upload(s.lrptr, rptr.data(), rptr.size()));
+  HIPCHK(c, upload(s.ltvar, tvar.data(), tvar.size()));
+  HIPCHK(c, upload(s.ltsrc, tsrc.data(), tsrc.size()));
+  HIPCHK(c, upload(s.ltrow, trow.data(), trow.size()));
+  HIPCHK(c, upload(s.ltval, tval.data(), tval.size()));
+  HIPCHK(c, upload(s.lrlo, rlo.data(), rlo.size()));
+  HIPCHK(c, upload(s.lrhi, rhi.data(), rhi.size()));
+  HIPCHK(c, upload(s.lrhsrc, rhsrc.data(), rhsrc.size()));
+  HIPCHK(c, upload(s.lcptr, cptr.data(), cptr.size()));
+  HIPCHK(c, upload(s.lcterm, cterm.data(), cterm.size()));
+  HIPCHK(c, upload(s.loidx, oidx.data(), oidx.size()));
+  HIPCHK(c, upload(s.loval, oval.data(), oval.size()));
+  return MGPU_OK;
+}
+
+// ---- root OBBT: QuadHandler::postSolveRootNode (QuadHandler.cpp:1397-1547)
+// with tightenLP_ (:2218-2297), on the host around device LPs -- the same
+// restatement as minotaur_amd/obbt.py obbt_chained (pinned bit for bit
+// against the reference's postSolveRootNode), here inside the glob round.
+constexpr double kObbtMaxVio = 1e-3, kObbtGap = 0.01, kObbtBTol = 1e-8, kObbtRTol = 1e-7;
+
+// the itmp marks of postSolveRootNode (:1410-1517): 1 lower, 2 upper, 3 both
+void obbt_marks(const QuadState &q, const double *x, const double *lb, const double *ub,
+                std::vector<int> &itmp) {
+  itmp.assign((size_t)q.nv, 0);
+  for (size_t k = 0; k < q.sq_x.size(); ++k) {
+    const int y = q.sq_y[k], x0 = q.sq_x[k];
+    const double yv = x[y], xv = x[x0];
+    double vio1 = std::fabs(xv * xv - yv);
+    if (vio1 > kObbtMaxVio && vio1 > 0.1 * std::fabs(yv)) {
+      if (ub[x0] - lb[x0] >= 2) itmp[(size_t)x0] = 3;
+      if (ub[y] - lb[y] >= 2) {
+        vio1 = yv - lb[y];
+        itmp[(size_t)y] = (vio1 > kObbtMaxVio && vio1 > 0.1 * lb[y]) ? 3 : 2;
+      }
+    }
+  }
+  auto mark = [&](int v) {
+    int &t = itmp[(size_t)v];
+    if (!(ub[v] - lb[v] >= 2 && t != 3)) return;
+    const double vio1 = x[v] - lb[v], vio2 = ub[v] - x[v];
+    if (vio1 > kObbtMaxVio && vio1 > 0.1 * std::fabs(lb[v])) {
+      if (vio2 > kObbtMaxVio && vio2 > 0.1 * std::fabs(ub[v])) t = 3;
+      else t = t == 2 ? 3 : 1;
+    } else if (vio2 > kObbtMaxVio && vio2 > std::fabs(ub[v])) {
+      t = t == 1 ? 3 : 2;
+    }
+  };
+  for (size_t k = 0; k < q.bil_x0.size(); ++k) {
+    const int y = q.bil_y[k], x0 = q.bil_x0[k], x1 = q.bil_x1[k];
+    const double yv = x[y];
+    const double vio1 = std::fabs(x[x0] * x[x1] - yv);
+    if (vio1 > kObbtMaxVio && vio1 > 0.1 * std::fabs(yv)) {
+      mark(x0);
+      mark(x1);
+      mark(y);
+    }
+  }
+}
+
+// setItmpFromSol_ (:2173-2216) with p_'s current bounds
+void obbt_itmp_from_sol(std::vector<int> &itmp, const double *xs, const double *lb,
+                        const double *ub) {
+  for (size_t v = 0; v < itmp.size(); ++v) {
+    const int t = itmp[v];
+    if (t == 0) continue;
+    const double l = lb[v], u = ub[v], xv = xs[v];
+    if (t == 1) {
+      if ((xv - l) / (u - l) <= kObbtGap) itmp[v] = 0;
+    } else if (t == 2) {
+      if ((u - xv) / (u - l) <= kObbtGap) itmp[v] = 0;
+    } else {
+      if ((xv - l) / (u - l) <= kObbtGap) itmp[v] = 2;
+      if ((u - xv) / (u - l) <= kObbtGap) itmp[v] = 1;
+    }
+  }
+}
+
+// updatePBounds_ (:3248-3320): -1 infeasible, 1 a bound moved, 0 none
+int obbt_update_bounds(int v, double nlb, double nub, int vtype, double *lb, double *ub) {
+  if (vtype <= 3) {
+    nub = std::floor(nub);
+    nlb = std::ceil(nlb);
+  }
+  const double L = lb[v], U = ub[v];
+  if (nlb > U + kObbtBTol || nub < L - kObbtBTol) return -1;
+  const bool lo = nlb > L + kObbtBTol && (L == -INFINITY || nlb > L + kObbtRTol * std::fabs(L));
+  const bool up = nub < U - kObbtBTol && (U == INFINITY || nub < U - kObbtRTol * std::fabs(U));
+  if (lo && up) {
+    lb[v] = nlb;
+    ub[v] = nub;
+    return 1;
+  }
+  if (lo) {
+    lb[v] = nlb;
+    return 1;
+  }
+  if (up) {
+    ub[v] = nub;
+    return 1;
+  }
+  return 0;
+}
+
+// upSqCon_ / upBilCon_ (:3322-3419) over every square, then every bilinear,
+// on the row state rows[R] with the box lb / ub
+void obbt_update_rows(const QuadState &q, const double *lb, const double *ub, double *rows) {
+  const double eps = 1e-6 / 10.0;
+  auto keep = [](double a) { return std::fabs(a) > 1e-9 ? a : 0.0; };
+  const int nsq = (int)q.sq_x.size();
+  for (int k = 0; k < nsq; ++k) {
+    double *r = rows + 2 * k;
+    const double l = lb[q.sq_x[k]], u = ub[q.sq_x[k]], ax = r[0];
+    if ((l * l + ax * l < r[1] - eps) || (u * u + ax * u < r[1] - eps)) {
+      r[1] = -u * l;
+      r[0] = std::fabs(u + l) > 1e-5 ? keep(-1. * (u + l)) : 0.0;
+    }
+  }
+  for (size_t k = 0; k < q.bil_x0.size(); ++k) {
+    const int x0 = q.bil_x0[k], x1 = q.bil_x1[k];
+    const double l0 = lb[x0], u0 = ub[x0], l1 = lb[x1], u1 = ub[x1];
+    double *r = rows + 2 * nsq + 12 * k;
+    if (r[0] * l0 + r[1] * l1 - l0 * l1 < r[2] - eps || r[0] * l0 + r[1] * u1 - l0 * u1 < r[2] - eps ||
+        r[0] * u0 + r[1] * l1 - u0 * l1 < r[2] - eps) {
+      r[0] = keep(l1);
+      r[1] = keep(l0);
+      r[2] = l0 * l1;
+    }
+    r += 3;
+    if (r[0] * l0 + r[1] * u1 - l0 * u1 < r[2] - eps || r[0] * u0 + r[1] * l1 - u0 * l1 < r[2] - eps ||
+        r[0] * u0 + r[1] * u1 - u0 * u1 < r[2] - eps) {
+      r[0] = keep(u1);
+      r[1] = keep(u0);
+      r[2] = u0 * u1;
+    }
+    r += 3;
+    if (r[0] * l0 + r[1] * l1 + l0 * l1 < r[2] - eps || r[0] * l0 + r[1] * u1 + l0 * u1 < r[2] - eps ||
+        r[0] * u0 + r[1] * u1 + u0 * u1 < r[2] - eps) {
+      r[0] = keep(-1.0 * u1);
+      r[1] = keep(-1.0 * l0);
+      r[2] = -l0 * u1;
+    }
+    r += 3;
+    if (r[0] * l0 + r[1] * l1 + l0 * l1 < r[2] - eps || r[0] * u0 + r[1] * l1 + u0 * l1 < r[2] - eps ||
+        r[0] * u0 + r[1] * u1 + u0 * u1 < r[2] - eps) {
+      r[0] = keep(-1.0 * l1);
+      r[1] = keep(-1.0 * u0);
+      r[2] = -u0 * l1;
+    }
+  }
+}
+
+// a row's weight / upper side with the node record rec [R + T]
+inline double tab_w(const GlobState &s, const double *rec, int t) {
+  return s.h_tsrc[(size_t)t] < 0 ? s.h_tval[(size_t)t] : rec[s.h_tsrc[(size_t)t]];
+}
+inline double tab_hi(const GlobState &s, const double *rec, int r) {
+  return s.h_rhsrc[(size_t)r] < 0 ? s.h_rhi[(size_t)r] : rec[s.h_rhsrc[(size_t)r]];
+}
+
+// isFeasibleToRelaxation_ (:955-981): x against every relaxation row
+bool obbt_rel_feasible(const GlobState &s, const double *rec, const double *x) {
+  for (int r = 0; r < s.M; ++r) {
+    double act = 0.0;
+    for (int t = s.h_rptr[(size_t)r]; t < s.h_rptr[(size_t)r + 1]; ++t) {
+      const double a = tab_w(s, rec, t);
+      if (std::fabs(a) > 1e-9) act += a * x[s.h_tvar[(size_t)t]];
+    }
+    const double cub = tab_hi(s, rec, r), clb = s.h_rlo[(size_t)r];
+    if ((act > cub + 1e-6) && (cub == 0 || act > cub + std::fabs(cub) * 1e-7)) return false;
+    if ((act < clb - 1e-6) && (clb == 0 || act < clb - std::fabs(clb) * 1e-7)) return false;
+  }
+  return true;
+}
+
+// postSolveRootNode on the root (batch index 0 of the first round): x its LP
+// point, lb / ub its box, rec its record; tightens lb / ub / rec in place.
+// *changed: a bound moved (rows rewritten); *feasible: x still satisfies
+// the tightened relaxation.  *nlps: bound LPs solved.
+int glob_root_obbt(mgpu_ctx *c, GlobState &s, const double *x, std::vector<double> &lb,
+                   std::vector<double> &ub, std::vector<double> &rec, bool *changed,
+                   bool *feasible, long long *nlps) {
+  const QuadState &q = *c->quad;
+  const int nv = s.nv;
+  *changed = false;
+  *feasible = true;
+  std::vector<int> itmp;
+  obbt_marks(q, x, lb.data(), ub.data(), itmp);
+  // tightenLP_: the relaxation cloned with the root's bounds and rows (the
+  // free rows of unused tangent slots left out: the reference has no such
+  // row), plus the objective cutoff row with an incumbent (:2232-2244)
+  std::vector<int32_t> rptr{0}, cidx, ctype((size_t)nv);
+  std::vector<double> val, rlo, rhi;
+  const int R = s.R;
+  for (int r = 0; r < s.M; ++r) {
+    const double hi = tab_hi(s, rec.data(), r);
+    if (s.h_rhsrc[(size_t)r] >= R && hi == INFINITY) continue;
+    for (int t = s.h_rptr[(size_t)r]; t < s.h_rptr[(size_t)r + 1]; ++t) {
+      const double a = tab_w(s, rec.data(), t);
+      if (std::fabs(a) <= 1e-9) continue;
+      cidx.push_back(s.h_tvar[(size_t)t]);
+      val.push_back(a);
+    }
+    rptr.push_back((int32_t)cidx.size());
+    rlo.push_back(s.h_rlo[(size_t)r]);
+    rhi.push_back(hi);
+  }
+  if (std::isfinite(s.inc) && q.has_obj) {
+    for (size_t k = 0; k < s.h_oidx.size(); ++k) {
+      cidx.push_back(s.h_oidx[k]);
+      val.push_back(s.h_oval[k]);
+    }
+    rptr.push_back((int32_t)cidx.size());
+    rlo.push_back(-INFINITY);
+    rhi.push_back(s.inc - q.obj_const);
+  }
+  for (int j = 0; j < nv; ++j) ctype[(size_t)j] = q.h_vtype[(size_t)j];
+  const int m = (int)rlo.size(), N = nv + m;
+  const std::vector<double> lb0 = lb, ub0 = ub;   // the clone's bounds stay as loaded
+  if (!s.bte) {
+    int rc = mgpu_create(c->device, &s.bte);
+    if (rc != MGPU_OK) return fail(c, rc, "mgpu_glob_round: the OBBT engine: mgpu_create failed");
+    mgpu_set_stream(s.bte, c->stream);
+  }
+  std::vector<double> obj((size_t)nv, 0.0), xs((size_t)nv), wd((size_t)N), wb((size_t)m * m),
+      ib((size_t)m * m);
+  std::vector<int32_t> wh((size_t)m), ih((size_t)m);
+  std::vector<int8_t> wst((size_t)N), ist((size_t)N);
+  bool have_ws = false;   // bte_->load drops the warm start: the first LP from the slack basis
+  // getBndByLP_ (:2080-2109): the bound LP min sign x_v from the last
+  // optimal basis (HipLPEngine keeps a basis after ProvenOptimal /
+  // EngineIterationLimit), its reduced costs rebuilt for the new objective
+  auto bound_lp = [&](int v, double sign, double *b, bool *inf) -> int {
+    std::fill(obj.begin(), obj.end(), 0.0);
+    obj[(size_t)v] = sign;
+    int rc = mgpu_load_lp(s.bte, nv, m, rptr.data(), cidx.data(), val.data(), rlo.data(),
+                          rhi.data(), lb0.data(), ub0.data(), ctype.data(), obj.data(), 0.0);
+    if (rc != MGPU_OK) return fail(c, rc, "mgpu_glob_round: OBBT load: %s", mgpu_last_error(s.bte));
+    int32_t st = 0, it = 0;
+    double ov = 0.0;
+    rc = mgpu_lp_solve(s.bte, 1, lb0.data(), ub0.data(), nullptr, have_ws ? ih.data() : nullptr,
+                       have_ws ? ist.data() : nullptr, nullptr, have_ws ? ib.data() : nullptr, 1, 0,
+                       &st, &ov, &it, xs.data(), wh.data(), wst.data(), wd.data(), wb.data());
+    if (rc != MGPU_OK) return fail(c, rc, "mgpu_glob_round: OBBT solve: %s", mgpu_last_error(s.bte));
+    ++*nlps;
+    if (st == 0 || st == 6) {
+      ih.swap(wh);
+      ist.swap(wst);
+      ib.swap(wb);
+      have_ws = true;
+    }
+    *inf = !(st == 0 || st == 6 || st == 4);
+    *b = *inf ? INFINITY : ov;
+    return MGPU_OK;
+  };
+  for (int v = 0; v < nv; ++v) {
+    const int t = itmp[(size_t)v];
+    if (t == 0) continue;
+    double nlb = -INFINITY, nub = INFINITY, b = 0.0;
+    bool inf = false;
+    if (t == 1 || t == 3) {
+      int rc = bound_lp(v, 1.0, &b, &inf);
+      if (rc != MGPU_OK) return rc;
+      if (inf) continue;
+      nlb = b;
+      obbt_itmp_from_sol(itmp, xs.data(), lb.data(), ub.data());
+    }
+    if (t == 2) {
+      int rc = bound_lp(v, -1.0, &b, &inf);
+      if (rc != MGPU_OK) return rc;
+      if (inf) continue;
+      nub = -b;
+      obbt_itmp_from_sol(itmp, xs.data(), lb.data(), ub.data());
+    }
+    const int u = obbt_update_bounds(v, nlb, nub, q.h_vtype[(size_t)v], lb.data(), ub.data());
+    if (u < 0) break;   // tightenLP_ returns "infeasible" (only logged, :1519-1524)
+    if (u > 0) *changed = true;
+  }
+  if (*changed) {
+    obbt_update_rows(q, lb.data(), ub.data(), rec.data());
+    *feasible = obbt_rel_feasible(s, rec.data(), x);
+  }
   return MGPU_OK;
 }
 
@@ -139,14 +545,17 @@ int ensure_glob_batch(mgpu_ctx *c, GlobState &s, int B) {
 
 extern "C" {
 
-int mgpu_glob_config(mgpu_ctx *c, int order, int warm, int qt) {
+int mgpu_glob_config(mgpu_ctx *c, int order, int warm, int qt, int lin, int obbt) {
   if (!c) return MGPU_ERR_ARG;
-  if ((order != 0 && order != 2) || warm < 0 || warm > 1 || qt < 0 || qt > 1)
-    return fail(c, MGPU_ERR_ARG, "mgpu_glob_config: order %d (0, 2), warm %d (0, 1), qt %d (0, 1)",
-                order, warm, qt);
+  if ((order != 0 && order != 2) || warm < 0 || warm > 1 || qt < 0 || qt > 1 || lin < 0 ||
+      lin > 1 || obbt < 0 || obbt > 1)
+    return fail(c, MGPU_ERR_ARG, "mgpu_glob_config: order %d (0, 2), warm %d (0, 1), qt %d (0, 1), "
+                "lin %d (0, 1), obbt %d (0, 1)", order, warm, qt, lin, obbt);
   c->glob_order = order;
   c->glob_warm = warm;
   c->glob_qt = qt;
+  c->glob_lin = lin;
+  c->glob_obbt = obbt;
   return MGPU_OK;
 }
 
@@ -175,8 +584,14 @@ int mgpu_glob_init(mgpu_ctx *c, int capacity, double incumbent) {
   s->order = c->glob_order;
   s->warm = c->glob_warm;
   s->qt = c->glob_qt;
+  s->lin = c->glob_lin;
+  s->obbt = c->glob_obbt;
   s->T = extra;
   s->S = nsq > 0 ? extra / (2 * nsq) : 0;
+  if (s->lin || s->obbt) {
+    const int rc0 = build_linear_table(c, *s);
+    if (rc0 != MGPU_OK) return rc0;
+  }
   s->cap = capacity;
   s->inc = incumbent;
   s->best_x.assign((size_t)nv, NAN);
@@ -403,6 +818,40 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
     io.in_depth = s.pdepth.as<int32_t>() + base;
     io.in_tan = s.T > 0 ? s.ptan.as<double>() + (size_t)base * s.T : nullptr;
   }
+  // the handlers' presolveNode in order (PCBProcessor.cpp:148-167):
+  // LinearHandler's over the node's relaxation rows as the node inherited
+  // them, then QuadHandler's on the box that leaves
+  if (s.lin) {
+    io.M = s.M;
+    io.nobj = s.nobj;
+    io.cons_bad = s.cons_bad;
+    // a solution in the pool (LinearHandler.cpp:1636-1640)
+    io.has_inc = std::isfinite(s.inc) ? 1 : 0;
+    io.inc_ub = s.inc - q.obj_const;
+    io.lrptr = s.lrptr.as<int32_t>();
+    io.ltvar = s.ltvar.as<int32_t>();
+    io.ltsrc = s.ltsrc.as<int32_t>();
+    io.ltrow = s.ltrow.as<int32_t>();
+    io.lrhsrc = s.lrhsrc.as<int32_t>();
+    io.lcptr = s.lcptr.as<int32_t>();
+    io.lcterm = s.lcterm.as<int32_t>();
+    io.loidx = s.loidx.as<int32_t>();
+    io.ltval = s.ltval.as<double>();
+    io.lrlo = s.lrlo.as<double>();
+    io.lrhi = s.lrhi.as<double>();
+    io.loval = s.loval.as<double>();
+    io.flb_in = in_lb;
+    io.fub_in = in_ub;
+    io.frows = in_rows;
+    io.ftan = io.in_tan;
+    io.flb = s.flb.as<double>();
+    io.fub = s.fub.as<double>();
+    io.finf = s.finf.as<int32_t>();
+    io.fflag = s.fflag.as<uint8_t>();
+    HIPCHK(c, launch_glob_linear(io, c->stream));
+    in_lb = io.flb;
+    in_ub = io.fub;
+  }
   // K2 from the parents' rows; tightenQuad_ at every node (doQT_, set by
   // Glob's presolve) or only at the first presolveNode call (QuadHandler.cpp:
   // 1215, 1241: niters <= 1)
@@ -411,6 +860,7 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
                           s.wub.as<double>(), s.wrows.as<double>(), s.kinf.as<int32_t>(),
                           s.knm.as<int32_t>(), 0, nullptr, nullptr, nullptr, nullptr);
   if (rc != MGPU_OK) return rc;
+  if (s.lin) HIPCHK(c, launch_glob_linear_verdict(io, c->stream));
   // the node records: K2's rows and the node's tangent slots
   if (s.T > 0) HIPCHK(c, launch_glob_pack(io, c->stream));
   // the node LPs with their own rows (K3R + K3), K2-infeasible nodes skipped.
@@ -452,9 +902,68 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
     if (rc != MGPU_OK) return rc;
   }
   HIPCHK(c, launch_glob_decide(io, c->stream));
+  // the flagged nodes (flag / skip2) re-solved -- from the root basis (warm
+  // 0) or the node's last basis refactored for its rows (warm 1) -- merged
+  // back and decided again
+  auto resolve_flagged = [&]() -> int {
+    int r;
+    if (s.warm == 1)
+      r = solve(io.skip2, s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), 0, nullptr,
+                s.st2.as<int32_t>(), s.obj2.as<double>(), s.it2.as<int32_t>(), s.x2.as<double>());
+    else
+      r = solve(io.skip2, s.root_ws ? s.ws_head.as<int32_t>() : nullptr,
+                s.root_ws ? s.ws_st.as<int8_t>() : nullptr, 1,
+                s.root_ws ? s.ws_binv.as<double>() : nullptr, s.st2.as<int32_t>(),
+                s.obj2.as<double>(), s.it2.as<int32_t>(), s.x2.as<double>());
+    if (r != MGPU_OK) return r;
+    HIPCHK(c, launch_glob_merge(io, c->stream));
+    GlobIO again = io;
+    again.only = io.flag;
+    HIPCHK(c, launch_glob_decide(again, c->stream));
+    return MGPU_OK;
+  };
+  // root OBBT (PCBProcessor::process, :256-280): at the root's first solve,
+  // when it is neither pruned nor feasible, QuadHandler::postSolveRootNode;
+  // if its point leaves the tightened relaxation the root is re-solved
+  // (SepaResolve, no separation in between), else it is decided again on the
+  // same point with the tightened box
+  long long obbt_lps = 0, obbt_resolves = 0;
+  if (s.obbt && s.tot.nodes == 0 && nb == 1) {
+    int32_t d0 = -1;
+    HIPCHK(c, hipMemcpyAsync(&d0, io.dec, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (d0 == 0 || d0 == 5) {
+      const int RT = R + s.T;
+      std::vector<double> x0((size_t)nv), lb0((size_t)nv), ub0((size_t)nv), rec((size_t)RT);
+      HIPCHK(c, hipMemcpy(x0.data(), io.x, (size_t)nv * 8, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(lb0.data(), io.wlb, (size_t)nv * 8, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(ub0.data(), io.wub, (size_t)nv * 8, hipMemcpyDeviceToHost));
+      if (RT > 0) HIPCHK(c, hipMemcpy(rec.data(), io.wvals, (size_t)RT * 8, hipMemcpyDeviceToHost));
+      bool changed = false, feasible = true;
+      rc = glob_root_obbt(c, s, x0.data(), lb0, ub0, rec, &changed, &feasible, &obbt_lps);
+      if (rc != MGPU_OK) return rc;
+      if (changed) {
+        HIPCHK(c, hipMemcpy(s.wlb.p, lb0.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(s.wub.p, ub0.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+        if (R > 0) HIPCHK(c, hipMemcpy(s.wrows.p, rec.data(), (size_t)R * 8, hipMemcpyHostToDevice));
+        if (s.T > 0) HIPCHK(c, hipMemcpy(io.wvals, rec.data(), (size_t)RT * 8, hipMemcpyHostToDevice));
+        const int32_t one = 1, zero = 0;
+        HIPCHK(c, hipMemcpy(io.flag, &one, 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(io.skip2, &zero, 4, hipMemcpyHostToDevice));
+        if (!feasible) {
+          rc = resolve_flagged();
+          if (rc != MGPU_OK) return rc;
+          obbt_resolves = 1;
+        } else {
+          GlobIO again = io;
+          again.only = io.flag;
+          HIPCHK(c, launch_glob_decide(again, c->stream));
+        }
+      }
+    }
+  }
   // the separation loop (PCBProcessor.cpp:267-280): every pass adds at least
-  // one cut to a free slot, so it ends within nsq S passes; a re-solve starts
-  // from the root basis (warm 0) or the node's last basis (warm 1)
+  // one cut to a free slot, so it ends within nsq S passes
   long long cuts = 0, resolves = 0;
   for (int pass = 0; s.T > 0 && pass <= s.T / 2; ++pass) {
     HIPCHK(c, hipMemsetAsync(s.acc.p, 0, 16, c->stream));
@@ -465,20 +974,8 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
     if (a[1] == 0) break;
     cuts += (long long)a[0];
     resolves += (long long)a[1];
-    if (s.warm == 1)
-      rc = solve(io.skip2, s.wo_head.as<int32_t>(), s.wo_st.as<int8_t>(), 0, nullptr,
-                 s.st2.as<int32_t>(), s.obj2.as<double>(), s.it2.as<int32_t>(),
-                 s.x2.as<double>());
-    else
-      rc = solve(io.skip2, s.root_ws ? s.ws_head.as<int32_t>() : nullptr,
-                 s.root_ws ? s.ws_st.as<int8_t>() : nullptr, 1,
-                 s.root_ws ? s.ws_binv.as<double>() : nullptr, s.st2.as<int32_t>(),
-                 s.obj2.as<double>(), s.it2.as<int32_t>(), s.x2.as<double>());
+    rc = resolve_flagged();
     if (rc != MGPU_OK) return rc;
-    HIPCHK(c, launch_glob_merge(io, c->stream));
-    GlobIO again = io;
-    again.only = io.flag;
-    HIPCHK(c, launch_glob_decide(again, c->stream));
   }
   HIPCHK(c, launch_glob_summary(io, c->stream));
   GlobOut o;
@@ -555,7 +1052,8 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
   s.tot.rounds += 1;
   s.tot.nodes += nb;
   for (int k = 0; k < 6; ++k) s.tot.ndec[k] += o.ndec[k];
-  s.tot.lps += o.lps + resolves;
+  s.tot.lps += o.lps + resolves + obbt_resolves;
+  s.tot.obbt_lps += obbt_lps;
   s.tot.pivots += o.pivots;
   s.tot.cuts += cuts;
   s.tot.resolves += resolves;

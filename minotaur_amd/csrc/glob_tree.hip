@@ -462,6 +462,234 @@ __global__ __launch_bounds__(256) void glob_merge(GlobIO io) {
   }
 }
 
+// ---- LinearHandler::presolveNode on the node's relaxation -----------------
+// PCBProcessor::presolveNode_ (PCBProcessor.cpp:134-175) runs the handlers'
+// presolveNode in order; LinearHandler's (LinearHandler.cpp:1592-1602) is
+// simplePresolve in node mode over EVERY row of the relaxation (:1605-1653):
+// the linear rows and QuadHandler's secant / McCormick rows as the node
+// inherited them, and the tangent cuts.  Weights of |a| <= 1e-9 are absent
+// (LinearFunction::addTerm, LinearFunction.cpp:89-95): they neither count in
+// the sums nor put their row in the variable's constraint set
+// (Problem::changeConstraint keeps that set, Problem.cpp:273-303, which
+// changeBFlag_ walks, LinearHandler.cpp:1229-1234).  One thread per node,
+// the reference's operations in its order (-ffp-contract=off).
+constexpr double kLfTol = 1e-9, kLinETol = 1e-8, kLinInfty = 1e20, kLinIntTol = 1e-6;
+
+struct LinNode {
+  const GlobIO *io;
+  double *lb, *ub;
+  uint8_t *flag;
+  const double *rows, *tan;
+  unsigned nintmods;
+  __device__ double rec(int src) const { return src < io->R ? rows[src] : tan[src - io->R]; }
+  __device__ double w(int t) const {
+    const int s = io->ltsrc[t];
+    return s < 0 ? io->ltval[t] : rec(s);
+  }
+  __device__ bool is_int(int j) const { return io->vtype[j] <= 1; }
+  // changeBFlag_
+  __device__ void change_bflag(int j) {
+    for (int p = io->lcptr[j]; p < io->lcptr[j + 1]; ++p) {
+      const int t = io->lcterm[p];
+      if (fabs(w(t)) > kLfTol) flag[io->ltrow[t]] = 1;
+    }
+  }
+};
+
+// getLfBnds_ (LinearHandler.cpp:1237-1258) over terms [t0, t1) (obj: loidx)
+template <bool OBJ>
+__device__ void lin_lf_bnds(const LinNode &s, int t0, int t1, double *lo, double *up) {
+  double l = 0, u = 0;
+  for (int t = t0; t < t1; ++t) {
+    const double c = OBJ ? s.io->loval[t] : s.w(t);
+    if (!OBJ && fabs(c) <= kLfTol) continue;
+    const int j = OBJ ? s.io->loidx[t] : s.io->ltvar[t];
+    const double vl = s.lb[j], vu = s.ub[j];
+    if (c > 0) {
+      l += c * vl;
+      u += c * vu;
+    } else {
+      l += c * vu;
+      u += c * vl;
+    }
+  }
+  *lo = l;
+  *up = u;
+}
+
+// getSingLfBnds_ (LinearHandler.cpp:1261-1319)
+template <bool OBJ>
+__device__ void lin_sing_bnds(const LinNode &s, int t0, int t1, double *lo, double *up) {
+  double l = 0, u = 0;
+  bool lo_sing = false, up_sing = false, lo_fin = true, up_fin = true;
+  for (int t = t0; t < t1; ++t) {
+    const double c = OBJ ? s.io->loval[t] : s.w(t);
+    if (!OBJ && fabs(c) <= kLfTol) continue;
+    const int j = OBJ ? s.io->loidx[t] : s.io->ltvar[t];
+    const double vl = s.lb[j], vu = s.ub[j];
+    if (c > kLinETol) {
+      if (vu < kLinInfty && up_fin) u += c * vu;
+      else if (up_sing) { up_sing = false; u = kInf; up_fin = false; }
+      else up_sing = true;
+      if (vl > -kLinInfty && lo_fin) l += c * vl;
+      else if (lo_sing) { lo_sing = false; l = -kInf; lo_fin = false; }
+      else lo_sing = true;
+    } else if (c < -kLinETol) {
+      if (vu < kLinInfty && lo_fin) l += c * vu;
+      else if (lo_sing) { lo_sing = false; l = -kInf; lo_fin = false; }
+      else lo_sing = true;
+      if (vl > -kLinInfty && up_fin) u += c * vl;
+      else if (up_sing) { up_sing = false; u = kInf; up_fin = false; }
+      else up_sing = true;
+    }
+  }
+  *lo = l;
+  *up = u;
+}
+
+// updateLfBoundsFromLb_ (FROM_LB, LinearHandler.cpp:1048-1134) and
+// updateLfBoundsFromUb_ (:1137-1226); side = the row's lb (ub), act = uu (ll)
+template <bool OBJ, bool FROM_LB>
+__device__ void lin_update(LinNode &s, int t0, int t1, double side, double act, bool sing,
+                           bool *changed, bool count_int) {
+  for (int t = t0; t < t1; ++t) {
+    const double c = OBJ ? s.io->loval[t] : s.w(t);
+    const int j = OBJ ? s.io->loidx[t] : s.io->ltvar[t];
+    double vlb = s.lb[j], vub = s.ub[j];
+    // FROM_LB: c > 0 raises the lower bound, c < 0 lowers the upper one;
+    // from the upper side the other way round
+    const bool raise = FROM_LB ? c > kLinETol : c < -kLinETol;
+    const bool lower = FROM_LB ? c < -kLinETol : c > kLinETol;
+    if (raise && (!sing || vub >= kLinInfty)) {
+      if (vub >= kLinInfty) vub = 0.;
+      double nlb = (side - act) / c + vub;
+      if (nlb > vlb + kLinETol) {
+        if (nlb > s.ub[j] - kLinETol) nlb = s.ub[j];
+        s.change_bflag(j);
+        s.lb[j] = nlb;
+        if (count_int && s.is_int(j)) s.nintmods++;
+        *changed = true;
+      }
+    } else if (lower && (!sing || vlb <= -kLinInfty)) {
+      if (vlb <= -kLinInfty) vlb = 0.;
+      double nub = (side - act) / c + vlb;
+      if (nub < vub - kLinETol) {
+        if (nub < s.lb[j] + kLinETol) nub = s.lb[j];
+        s.change_bflag(j);
+        s.ub[j] = nub;
+        if (count_int && s.is_int(j)) s.nintmods++;
+        *changed = true;
+      }
+    }
+  }
+}
+
+// linBndTighten_ (LinearHandler.cpp:952-1045, node mode); true: infeasible
+__device__ bool lin_row(LinNode &s, int i, bool *changed) {
+  const GlobIO &io = *s.io;
+  const int t0 = io.lrptr[i], t1 = io.lrptr[i + 1];
+  const double lb = io.lrlo[i];
+  const double ub = io.lrhsrc[i] < 0 ? io.lrhi[i] : s.rec(io.lrhsrc[i]);
+  double ll, uu, sll = -kInf, suu = kInf;
+  *changed = false;
+  lin_lf_bnds<false>(s, t0, t1, &ll, &uu);
+  if (ll < -kLinInfty || uu > kLinInfty) lin_sing_bnds<false>(s, t0, t1, &sll, &suu);
+  if (ll > ub + kLinETol) return true;
+  if (uu < lb - kLinETol) return true;
+  if (lb > -kLinInfty) {
+    if (uu < kLinInfty) lin_update<false, true>(s, t0, t1, lb, uu, false, changed, true);
+    else if (suu < kLinInfty) lin_update<false, true>(s, t0, t1, lb, suu, true, changed, true);
+  }
+  if (*changed) {
+    lin_lf_bnds<false>(s, t0, t1, &ll, &uu);
+    if (ll < -kLinInfty || uu > kLinInfty) lin_sing_bnds<false>(s, t0, t1, &sll, &suu);
+  }
+  if (ub < kLinInfty) {
+    if (ll > -kLinInfty) lin_update<false, false>(s, t0, t1, ub, ll, false, changed, true);
+    else if (sll > -kLinInfty) lin_update<false, false>(s, t0, t1, ub, sll, true, changed, true);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(64) void glob_linear(GlobIO io) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= io.nb) return;
+  const int nv = io.nv, M = io.M;
+  LinNode s;
+  s.io = &io;
+  s.lb = io.flb + (size_t)b * nv;
+  s.ub = io.fub + (size_t)b * nv;
+  s.flag = io.fflag + (size_t)b * M;
+  s.rows = io.frows + (size_t)b * io.R;
+  s.tan = io.T > 0 ? io.ftan + (size_t)b * io.T : nullptr;
+  s.nintmods = 0;
+  for (int j = 0; j < nv; ++j) {
+    s.lb[j] = io.flb_in[(size_t)b * nv + j];
+    s.ub[j] = io.fub_in[(size_t)b * nv + j];
+  }
+  for (int i = 0; i < M; ++i) s.flag[i] = 1;
+  // simplePresolve: sweeps while changed, at most 10, past the second only
+  // while an integer bound moved; varBndsFromCons_ / varBndsFromObj_'s
+  // verdicts are dropped there (:1630-1640), checkBounds_ decides
+  bool changed = true, infeas = false;
+  unsigned iters = 1;
+  while (changed && iters <= 10 && (iters <= 2 || s.nintmods > 0) && !infeas) {
+    s.nintmods = 0;
+    changed = false;
+    ++iters;
+    // varBndsFromCons_ (:493-541): each flagged row once per sweep
+    for (int i = 0; i < M; ++i) {
+      if (!s.flag[i]) continue;
+      s.flag[i] = 0;
+      bool tch;
+      if (lin_row(s, i, &tch)) break;
+      if (tch) changed = true;
+    }
+    // varBndsFromObj_ (:544-597) with a solution in the pool
+    if (io.has_inc && io.nobj > 0) {
+      bool tch = true;
+      for (long guard = 0; tch && guard <= 100000; ++guard) {
+        double ll, uu, sll = kInf, suu = kInf;
+        tch = false;
+        lin_lf_bnds<true>(s, 0, io.nobj, &ll, &uu);
+        if (ll < -kLinInfty || uu > kLinInfty) lin_sing_bnds<true>(s, 0, io.nobj, &sll, &suu);
+        if (ll > io.inc_ub + kLinETol) break;
+        if (ll > -kLinInfty)
+          lin_update<true, false>(s, 0, io.nobj, io.inc_ub, ll, false, &tch, false);
+        else if (sll > -kLinInfty)
+          lin_update<true, false>(s, 0, io.nobj, io.inc_ub, sll, true, &tch, false);
+        if (tch) changed = true;
+      }
+    }
+    // tightenInts_ (:415-490)
+    for (int j = 0; j < nv; ++j) {
+      if (!s.is_int(j)) continue;
+      const double l = s.lb[j], u = s.ub[j];
+      if (l > -kLinInfty && fabs(l - floor(l + 0.5)) > kLinIntTol) {
+        s.change_bflag(j);
+        s.lb[j] = ceil(l);
+        changed = true;
+      }
+      if (u < kLinInfty && fabs(u - floor(u + 0.5)) > kLinIntTol) {
+        s.ub[j] = floor(u);
+        s.change_bflag(j);
+        changed = true;
+      }
+    }
+    // checkBounds_ (:328-359)
+    infeas = io.cons_bad != 0;
+    for (int j = 0; j < nv && !infeas; ++j) infeas = s.lb[j] > s.ub[j] + kLinETol;
+  }
+  io.finf[b] = infeas ? 1 : 0;
+}
+
+// a node the linear presolve found infeasible is pruned before the LP
+// (PCBProcessor::process, :208-213): K2's verdict for it becomes infeasible
+__global__ __launch_bounds__(256) void glob_linear_verdict(GlobIO io) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b < io.nb && io.finf[b] != 0) const_cast<int32_t *>(io.kinf)[b] = 1;
+}
+
 }  // namespace
 
 hipError_t launch_glob_decide(const GlobIO &io, hipStream_t stream) {
@@ -509,6 +737,18 @@ hipError_t launch_glob_children(const GlobIO &io, hipStream_t stream) {
 hipError_t launch_glob_summary(const GlobIO &io, hipStream_t stream) {
   if (io.nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(glob_summary, dim3(1), dim3(1024), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_linear(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_linear, dim3((io.nb + 63) / 64), dim3(64), 0, stream, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_glob_linear_verdict(const GlobIO &io, hipStream_t stream) {
+  if (io.nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(glob_linear_verdict, dim3((io.nb + 255) / 256), dim3(256), 0, stream, io);
   return hipGetLastError();
 }
 

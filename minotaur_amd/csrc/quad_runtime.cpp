@@ -161,8 +161,10 @@ int mgpu_load_quad(mgpu_ctx *c, int nv0, int nv, const int32_t *vtype, int nsq,
   q->nv = nv;
   q->R = 2 * nsq + 12 * nbil;
   q->sq_x.assign(sq_x, sq_x + nsq);
+  q->sq_y.assign(sq_y, sq_y + nsq);
   q->bil_x0.assign(bil_x0, bil_x0 + nbil);
   q->bil_x1.assign(bil_x1, bil_x1 + nbil);
+  q->bil_y.assign(bil_y, bil_y + nbil);
   q->obj_const = obj_const;
   // the original functions as given (the glob tree's QuadHandler::isFeasible)
   q->ncon = ncon;

@@ -7,7 +7,7 @@
 struct QuadState {
   DevQuad dq{};
   int nv0 = 0, nv = 0, R = 0;
-  std::vector<int32_t> sq_x, bil_x0, bil_x1;
+  std::vector<int32_t> sq_x, sq_y, bil_x0, bil_x1, bil_y;
   // the original functions as loaded (function ncon = the objective when
   // has_obj) and the variable types, host copies
   int ncon = 0;

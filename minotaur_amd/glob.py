@@ -5,8 +5,9 @@ The reference's glob solver (src/solvers/Glob.cpp:134-220) runs
 BranchAndBound with NodeIncRelaxer, PCBProcessor, the handlers IntVarHandler
 / LinearHandler / QuadHandler of SimpleTransformer and (option
 brancher=maxvio) MaxVioBrancher.  Here one round evaluates the top ``batch``
-nodes of an HBM stack at once: K2 (QuadHandler::presolveNode, rows rewritten
-from the parent's), K3R + K3 (each node's LP with its own rows), the decision,
+nodes of an HBM stack at once: optionally LinearHandler::presolveNode on the
+node's relaxation rows (glob_linear), K2 (QuadHandler::presolveNode, rows
+rewritten from the parent's), K3R + K3 (each node's LP with its own rows), the decision,
 the squares' separation loop (tangent cuts, re-solve), MaxVio branching,
 children pushed.
 """
@@ -37,16 +38,17 @@ def setup(ctx, qp, tan_slots=None):
 
 
 def solve(ctx, qp, batch=1024, capacity=None, max_rounds=10**9, incumbent=math.inf,
-          loaded=False, tan_slots=None, order=0, warm=0, qt=1):
+          loaded=False, tan_slots=None, order=0, warm=0, qt=1, lin=0, obbt=0):
     """Runs the tree until the stack is empty (or max_rounds): returns
-    (incumbent, x or None, stats, seconds).  order / warm / qt:
+    (incumbent, x or None, stats, seconds).  order / warm / qt / lin / obbt:
     mgpu_glob_config (order 2, warm 1 at batch 1: the reference's own glob
-    tree node for node)."""
+    tree node for node; lin 1: LinearHandler's node presolve too; obbt 1:
+    root OBBT)."""
     if not loaded:
         setup(ctx, qp, tan_slots)
     cap = capacity or 64 * batch
     t0 = time.perf_counter()
-    ctx.glob_config(order, warm, qt)
+    ctx.glob_config(order, warm, qt, lin, obbt)
     ctx.glob_init(cap, incumbent)
     st = None
     for _ in range(max_rounds):

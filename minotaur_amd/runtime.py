@@ -85,7 +85,8 @@ class GlobStats(ctypes.Structure):
                 ('pivots', ctypes.c_longlong), ('br_int', ctypes.c_longlong),
                 ('br_cont', ctypes.c_longlong), ('open', ctypes.c_int),
                 ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double),
-                ('cuts', ctypes.c_longlong), ('resolves', ctypes.c_longlong)]
+                ('cuts', ctypes.c_longlong), ('resolves', ctypes.c_longlong),
+                ('obbt_lps', ctypes.c_longlong)]
 
 
 _lib = None
@@ -163,7 +164,7 @@ def load_library():
     lib.mgpu_alltoall_rows_dev.argtypes = [_P, _I, _P, _P, _P, _P]
     lib.mgpu_lb_deal.argtypes = [_I, _I, _P, _P, _P, _P]
     lib.mgpu_bnb_rebalance.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P]
-    lib.mgpu_glob_config.argtypes = [_P, _I, _I, _I]
+    lib.mgpu_glob_config.argtypes = [_P, _I, _I, _I, _I, _I]
     lib.mgpu_glob_init.argtypes = [_P, _I, _D]
     lib.mgpu_glob_round.argtypes = [_P, _I, _D, ctypes.POINTER(GlobStats)]
     lib.mgpu_glob_best.argtypes = [_P, _P, _P]
@@ -951,12 +952,14 @@ class Context:
         return op.value, int(mv.value), picked[:npk.value].copy(), got[:ngot.value].copy()
 
     # -- batched spatial B&B (mgpu_glob_*) ------------------------------------
-    def glob_config(self, order=0, warm=0, qt=1):
+    def glob_config(self, order=0, warm=0, qt=1, lin=0, obbt=0):
         """mgpu_glob_config: the next glob_init's node order (0 stack, 2 the
-        reference's heap), warm starts (0 root basis, 1 parent basis) and
-        tightenQuad_ rule (1 every node, 0 the first call only)."""
-        self._chk(self.lib.mgpu_glob_config(self.h, int(order), int(warm), int(qt)),
-                  'mgpu_glob_config')
+        reference's heap), warm starts (0 root basis, 1 parent basis),
+        tightenQuad_ rule (1 every node, 0 the first call only), linear node
+        presolve (1 LinearHandler::presolveNode at every node, 0 none) and
+        root OBBT (1 QuadHandler::postSolveRootNode, 0 none)."""
+        self._chk(self.lib.mgpu_glob_config(self.h, int(order), int(warm), int(qt), int(lin),
+                                            int(obbt)), 'mgpu_glob_config')
 
     def glob_init(self, capacity, incumbent=math.inf):
         self._chk(self.lib.mgpu_glob_init(self.h, int(capacity), float(incumbent)),

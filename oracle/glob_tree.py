@@ -58,6 +58,7 @@ class _GStats:
         self.lps = self.pivots = 0
         self.br_int = self.br_cont = 0
         self.cuts = self.resolves = 0
+        self.obbt_lps = 0
         self.open = self.last_batch = 0
         self.incumbent = math.inf
 
@@ -275,10 +276,66 @@ class CpuGlobContext:
         self.rows0 = oracle.quad_root_rows(qp)
         self.p, self.nr = relaxation_lp(qp, self.rows0, self.S)
         self.tan0 = tangent_record(qp, self.S)
-        self.order, self.warm, self.qt = 0, 0, 1
+        self.order, self.warm, self.qt, self.lin, self.obbt = 0, 0, 1, 0, 0
 
-    def glob_config(self, order=0, warm=0, qt=1):
-        self.order, self.warm, self.qt = order, warm, qt
+    def glob_config(self, order=0, warm=0, qt=1, lin=0, obbt=0):
+        self.order, self.warm, self.qt, self.lin, self.obbt = order, warm, qt, lin, obbt
+
+    def _rel_feasible(self, rec, x):
+        """QuadHandler::isFeasibleToRelaxation_ (QuadHandler.cpp:955-981):
+        x against every row of the relaxation with record rec (weights of
+        |a| <= 1e-9 absent, terms ascending), aTol 1e-6 / rTol 1e-7."""
+        q = self.nr.node_problem(self.p, rec)
+        for i in range(q.m):
+            act = 0.0
+            for k in range(q.rowptr[i], q.rowptr[i + 1]):
+                a = float(q.val[k])
+                if abs(a) > 1e-9:
+                    act += a * x[q.colidx[k]]
+            cub, clb = float(q.rhi[i]), float(q.rlo[i])
+            if act > cub + 1e-6 and (cub == 0 or act > cub + abs(cub) * 1e-7):
+                return False
+            if act < clb - 1e-6 and (clb == 0 or act < clb - abs(clb) * 1e-7):
+                return False
+        return True
+
+    def _root_obbt(self, lb, ub, rec, x):
+        """QuadHandler::postSolveRootNode (QuadHandler.cpp:1397-1547): the
+        chained bound LPs of tightenLP_ (minotaur_amd/obbt.py obbt_chained,
+        pinned bit for bit against the reference, over this module's CPU
+        chain step oracle.chain_solve), then the rows rewritten for the new
+        box.  Returns (changed, feasible, lb, ub, rec, bound LPs)."""
+        from minotaur_amd import obbt
+        R = self.R
+        _, nlb, nub, mods, log = obbt.obbt_chained(oracle.chain_solve, self.qp, rec[:R], x,
+                                                   lb=lb, ub=ub, incumbent=self.inc)
+        if not mods:
+            return False, True, lb, ub, rec, len(log)
+        rec = rec.copy()
+        rec[:R] = oracle.quad_update_rows(self.qp, nlb, nub, rec[:R])
+        return True, self._rel_feasible(rec, x), nlb, nub, rec, len(log)
+
+    def _linear(self, LB, UB, recs):
+        """LinearHandler::presolveNode (LinearHandler.cpp:1592-1653) on each
+        node's relaxation: the C restatement of simplePresolve (node mode,
+        pinned bit for bit against the reference's LinearHandler) over the
+        rows with the node's record applied, |a| <= 1e-9 dropped and terms
+        ascending (LinearFunction::addTerm), the incumbent's objective bound
+        once one is known.  Tightens LB / UB in place; returns infeasible."""
+        from minotaur_amd.problem import from_rows
+        nb = LB.shape[0]
+        linf = np.zeros(nb, dtype=np.int32)
+        for b in range(nb):
+            q = self.nr.node_problem(self.p, recs[b])
+            rows = [[(int(q.colidx[k]), float(q.val[k])) for k in range(q.rowptr[i], q.rowptr[i + 1])]
+                    for i in range(q.m)]
+            qn = from_rows(q.name, q.n, rows, q.rlo, q.rhi, q.vlb, q.vub, q.vtype, q.obj,
+                           q.obj_const)
+            r = oracle.linear_fbbt(qn, LB[b:b + 1], UB[b:b + 1],
+                                   self.inc if math.isfinite(self.inc) else None)
+            LB[b], UB[b] = r.lb[0], r.ub[0]
+            linf[b] = int(r.infeas[0])
+        return linf
 
     def glob_init(self, capacity, incumbent=math.inf):
         qp = self.qp
@@ -362,13 +419,17 @@ class CpuGlobContext:
         LB = np.stack([nd[0] for nd in nodes])
         UB = np.stack([nd[1] for nd in nodes])
         RW = np.stack([nd[2][:R] for nd in nodes])
+        # the handlers' presolveNode in order (PCBProcessor.cpp:148-167):
+        # LinearHandler's on the node's relaxation rows, then QuadHandler's
+        linf = self._linear(LB, UB, [nd[2] for nd in nodes]) if self.lin else np.zeros(nb, np.int32)
         qt = 1 if (self.qt or self.tot.nodes == 0) else 0
         o = oracle.quad_fbbt(qp, LB, UB, self.inc, qt, RW)
+        kinf_all = np.where(linf != 0, 1, o.infeas).astype(np.int32)
         # the node records: K2's rows, then the tangent slots the node inherited
         vals = np.concatenate([o.rows, np.stack([nd[2][R:] for nd in nodes])], axis=1)
         heads = [nd[5] if self.warm == 1 else None for nd in nodes]
         sts = [nd[6] if self.warm == 1 else None for nd in nodes]
-        live = [b for b in range(nb) if int(o.infeas[b]) == 0]
+        live = [b for b in range(nb) if int(kinf_all[b]) == 0]
         st = np.full(nb, 12, dtype=np.int32)
         obj = np.full(nb, math.inf)
         it = np.zeros(nb, dtype=np.int32)
@@ -389,11 +450,32 @@ class CpuGlobContext:
         ndec = [0] * 6
         decs = []
         for b in range(nb):
-            kinf = int(o.infeas[b])
+            kinf = int(kinf_all[b])
             if kinf == 0:
                 self.tot.lps += 1
             decs.append(decide(qp, kinf, int(st[b]), float(obj[b]), x[b], o.lb[b], o.ub[b],
                                self.inc))
+        # root OBBT (PCBProcessor.cpp:256-280): the root neither pruned nor
+        # feasible at its first solve; re-solved when its point leaves the
+        # tightened relaxation, decided again either way
+        if self.obbt and self.tot.nodes == 0 and nb == 1 and decs[0][0] in (0, 5):
+            ch, feas, nlb, nub, rec, nl = self._root_obbt(o.lb[0].copy(), o.ub[0].copy(),
+                                                          vals[0], x[0])
+            self.tot.obbt_lps += nl
+            if ch:
+                o.lb[0], o.ub[0], vals[0] = nlb, nub, rec
+                if not feas:
+                    r = self._lp(o.lb[:1], o.ub[:1], vals[:1],
+                                 [wh[0] if self.warm == 1 else None],
+                                 [wst[0] if self.warm == 1 else None])
+                    st[0], obj[0], x[0] = r[0][0], r[1][0], r[3][0]
+                    it[0] += r[2][0]
+                    if self.warm == 1:
+                        wh[0], wst[0] = r[4][0], r[5][0]
+                    self.tot.lps += 1
+                    self.lplog.append((int(st[0]), float(obj[0]), int(r[2][0])))
+                decs[0] = decide(qp, 0, int(st[0]), float(obj[0]), x[0], o.lb[0], o.ub[0],
+                                 self.inc)
         # the separation loop (PCBProcessor.cpp:267-280): tangents for the
         # squares of the nodes that would branch, re-solve (warm 1: from the
         # node's last basis), decide again
@@ -422,7 +504,7 @@ class CpuGlobContext:
                                  self.inc)
         kids = []
         for b in range(nb):
-            kinf = int(o.infeas[b])
+            kinf = int(kinf_all[b])
             if kinf == 0:
                 self.tot.pivots += int(it[b])
             dec, bv, bval, bup, bint = decs[b]

@@ -78,6 +78,7 @@ typedef struct {
 } orc_qspec;
 
 void orc_quad_rows(const orc_qspec *S, const double *lb, const double *ub, double *rows);
+void orc_quad_update_rows(const orc_qspec *S, double *lb, double *ub, double *rows);
 int orc_quad_fbbt_batch(const orc_qspec *S, int B, const double *lb_in, const double *ub_in,
                         double best, int qt, const double *rows_in, long rows_stride,
                         double *lb_out, double *ub_out, int *infeas, int *nmods,

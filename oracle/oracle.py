@@ -420,6 +420,20 @@ def quad_root_rows(qp, lb=None, ub=None):
     return rows
 
 
+def quad_update_rows(qp, lb, ub, rows):
+    """upSqCon_ / upBilCon_ over every product at box lb/ub on a copy of the
+    row state rows (C); postSolveRootNode's rewrite after OBBT."""
+    L = lib()
+    L.orc_quad_update_rows.restype = None
+    L.orc_quad_update_rows.argtypes = [ctypes.POINTER(_QSpec), _P, _P, _P]
+    lb = np.ascontiguousarray(lb, dtype=np.float64).copy()
+    ub = np.ascontiguousarray(ub, dtype=np.float64).copy()
+    out = np.ascontiguousarray(rows, dtype=np.float64).copy()
+    s = qspec(qp)
+    L.orc_quad_update_rows(ctypes.byref(s), _ptr(lb), _ptr(ub), _ptr(out))
+    return out
+
+
 def quad_fbbt(qp, lb, ub, incumbent=None, qt=1, rows=None, mod_cap=0):
     """C restatement of QuadHandler::presolveNode over a batch of boxes.
     rows: [R] shared or [B, R] per node (default: root rows)."""

@@ -604,6 +604,16 @@ void orc_quad_rows(const orc_qspec *S, const double *lb, const double *ub, doubl
   }
 }
 
+/* upSqCon_ / upBilCon_ over every square, then every bilinear, on the row
+ * state rows[R] with box lb/ub: QuadHandler::postSolveRootNode's rewrite
+ * after OBBT moved a bound (QuadHandler.cpp:1527-1533). */
+void orc_quad_update_rows(const orc_qspec *S, double *lb, double *ub, double *rows)
+{
+  qnode s = {S, lb, ub, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < S->nsq; ++k) up_sq_con(&s, k, rows + 2 * k);
+  for (int k = 0; k < S->nbil; ++k) up_bil_con(&s, k, rows + 2 * S->nsq + 12 * k);
+}
+
 /* QuadHandler::presolveNode, QuadHandler.cpp:1204-1269, on one node box
  * (lb/ub updated in place, rows = row state updated in place).  Returns 1
  * when the node is infeasible, -1 when the propagation loop hit PROP_CAP. */

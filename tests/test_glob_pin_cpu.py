@@ -7,11 +7,19 @@ CpuLPEngine, device -1): Glob::createBab_'s objects compiled from
 /root/reference -- BranchAndBound with tree_search bfs, PCBProcessor,
 NodeIncRelaxer (parent-basis warm starts; the problem's and relaxation's mods
 replayed, SimpleTransformer's flags), MaxVioBrancher, IntVarHandler /
-LinearHandler without node presolve / QuadHandler.
+LinearHandler / QuadHandler.
 
-Restatement side: glob_config(order 2, warm 1, qt 0), batch 1.  Seeds are
-every seed of a fixed range (no selection).  Bar: nodes processed and created,
-LP solves, closures, the incumbent's bits, the branching sequence (variable
+Restatement side: glob_config(order 2, warm 1, qt 0, lin, obbt), batch 1.
+lin 0 pairs with the reference's LinearHandler without node presolve; lin 1
+with its real LinearHandler, whose presolveNode (simplePresolve on the node's
+relaxation rows) runs at every node as Glob sets pres_freq 1 (Glob.cpp:404).
+obbt 1 turns on the reference's root OBBT (the OBBT option, on in Glob;
+QuadHandler::postSolveRootNode with CpuLPEngine as bte_) and the
+restatement's (obbt_chained, the rows rewritten, the root re-solved when its
+point leaves the tightened relaxation); the bound LPs are counted on both
+sides.
+Seeds are every seed of a fixed range (no selection).  Bar: nodes processed
+and created, LP solves, closures, the incumbent's bits, the branching sequence (variable
 and its LP value, 1e-9) and each node LP's pivot count and value (1e-9)."""
 import ctypes
 import math
@@ -48,18 +56,30 @@ def _logs(integ):
     return (bv, bx), (ls, lv, li)
 
 
+# (lin, obbt): Glob's configuration is (1, 1)
+CONFIGS = [(0, 0), (1, 0), (0, 1), (1, 1)]
+
+
+def ref_opts(lin, obbt):
+    """integ_glob_tree3 bits: bfs (1), LinearHandler without node presolve
+    (2) unless lin, root OBBT (8) with obbt."""
+    return 1 | (0 if lin else 2) | (8 if obbt else 0)
+
+
+@pytest.mark.parametrize('config', CONFIGS)
 @pytest.mark.parametrize('case', PIN_CASES)
-def test_restated_glob_tree_is_the_reference_tree(integ, case):
+def test_restated_glob_tree_is_the_reference_tree(integ, case, config):
+    lin, obbt = config
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'oracle'))
     from glob_tree import CpuGlobContext
     from test_simplex_cuts_cpu import glob_tree3
     seed, nv0, ncon = case
     qp = random_qcqp(seed, nv0=nv0, ncon=ncon, squares=False)
-    ub, cnt, _ = glob_tree3(integ, qp, 1 | 2, -1, 1)   # bfs, no linear presolve, pres_freq 1
+    ub, cnt, _ = glob_tree3(integ, qp, ref_opts(lin, obbt), -1, 1)   # pres_freq 1
     (bv, bx), (ls, lv, li) = _logs(integ)
     c = CpuGlobContext(qp)
-    c.glob_config(2, 1, 0)
+    c.glob_config(2, 1, 0, lin, obbt)
     c.glob_init(1 << 16)
     for _ in range(20000):
         st = c.glob_round(1)
@@ -67,8 +87,8 @@ def test_restated_glob_tree_is_the_reference_tree(integ, case):
             break
     obj, _ = c.glob_best()
     assert st.open == 0
-    assert (st.nodes, 1 + 2 * int(st.ndec[0]), st.lps, int(st.ndec[5])) == \
-        (int(cnt[0]), int(cnt[1]), int(cnt[2]), int(cnt[3]))
+    assert (st.nodes, 1 + 2 * int(st.ndec[0]), st.lps, int(st.ndec[5]), st.obbt_lps) == \
+        (int(cnt[0]), int(cnt[1]), int(cnt[2]), int(cnt[3]), int(cnt[5]))
     assert obj == ub or (math.isinf(obj) and math.isinf(ub))
     mb = np.array([v for v, _ in c.brlog], np.int32)
     mx = np.array([x for _, x in c.brlog])

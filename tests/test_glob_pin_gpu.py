@@ -13,7 +13,14 @@ false and tightenQuad_ runs at the first presolveNode call only.
 
 Batched side: mgpu_glob_config(order 2 = TreeManager's bfs NodeHeap with the
 reference's node ids and branch order, warm 1 = parent-basis warm starts
-refactored for the node's rows, qt 0), batch 1.
+refactored for the node's rows, qt 0, lin, obbt), batch 1.  lin 1 adds
+LinearHandler::presolveNode on the node's relaxation rows (glob_linear),
+paired with the reference's real LinearHandler at pres_freq 1 (Glob.cpp:404);
+lin 0 with the LinearHandler that skips node presolve.  obbt 1 adds root
+OBBT (QuadHandler::postSolveRootNode: the bound LPs chained on the round's
+own bound-tightening context, the rows rewritten, the root re-solved when
+its point leaves the tightened relaxation), paired with the reference's
+OBBT on HipLPEngine as bte_; (1, 1) is Glob's configuration.
 
 Seeds are drawn without filtering: nodes the reference hands to an NLP
 engine at NoCandToBranch (none in the image: closed and counted) are counted
@@ -31,7 +38,7 @@ from minotaur_amd.quad import random_qcqp
 pytestmark = pytest.mark.gpu
 
 # every seed of a fixed range, three shapes (no selection): the CPU pin's cases
-from test_glob_pin_cpu import PIN_CASES  # noqa: E402
+from test_glob_pin_cpu import CONFIGS, PIN_CASES, ref_opts  # noqa: E402
 
 
 @pytest.fixture(scope='module')
@@ -53,26 +60,28 @@ def ctx():
     c.close()
 
 
-def _pair(integ, ctx, seed, nv0, ncon):
+def _pair(integ, ctx, seed, nv0, ncon, lin, obbt):
     from test_simplex_cuts_cpu import glob_tree3
     qp = random_qcqp(seed, nv0=nv0, ncon=ncon, squares=False)
-    ub, cnt, _ = glob_tree3(integ, qp, 1 | 2, 0, 1)   # bfs, no linear presolve, pres_freq 1
+    ub, cnt, _ = glob_tree3(integ, qp, ref_opts(lin, obbt), 0, 1)   # pres_freq 1
     obj, x, st, _ = mglob.solve(ctx, qp, batch=1, capacity=1 << 14, order=2, warm=1, qt=0,
-                                max_rounds=20000)
+                                lin=lin, obbt=obbt, max_rounds=20000)
     return qp, (ub, cnt), (obj, st)
 
 
+@pytest.mark.parametrize('config', CONFIGS)
 @pytest.mark.parametrize('case', PIN_CASES)
-def test_glob_tree_is_the_reference_tree_node_for_node(integ, ctx, case):
+def test_glob_tree_is_the_reference_tree_node_for_node(integ, ctx, case, config):
+    lin, obbt = config
     seed, nv0, ncon = case
-    qp, (ub, cnt), (obj, st) = _pair(integ, ctx, seed, nv0, ncon)
+    qp, (ub, cnt), (obj, st) = _pair(integ, ctx, seed, nv0, ncon, lin, obbt)
     created = 1 + 2 * int(st.ndec[0])
     print(f"seed {seed} ({nv0}, {ncon}): reference nodes {cnt[0]} created {cnt[1]} LPs {cnt[2]} "
           f"closed {cnt[3]} ub {ub!r}; batched nodes {st.nodes} created {created} LPs "
-          f"{st.lps} closed {st.ndec[5]} ub {obj!r}")
+          f"{st.lps} closed {st.ndec[5]} ub {obj!r}; OBBT LPs {cnt[5]} / {st.obbt_lps}")
     assert st.open == 0
-    assert (st.nodes, created, st.lps, int(st.ndec[5])) == (int(cnt[0]), int(cnt[1]),
-                                                            int(cnt[2]), int(cnt[3]))
+    assert (st.nodes, created, st.lps, int(st.ndec[5]), st.obbt_lps) == \
+        (int(cnt[0]), int(cnt[1]), int(cnt[2]), int(cnt[3]), int(cnt[5]))
     assert obj == ub or (math.isinf(obj) and math.isinf(ub))
 
 
