@@ -461,6 +461,14 @@ int mgpu_bnb_brancher(mgpu_ctx *ctx, int kind);
  * reference's.  tls4-OA with reliability branching: 12 977 nodes at a fixed
  * batch, 3 371 with div 2 (the reference's own tree: 2 626). */
 int mgpu_bnb_growth(mgpu_ctx *ctx, int div);
+/* How the reliability brancher runs a round's strong-branching LPs (default
+ * 1): 1 every node's chain in one K3 launch, one wave per node, each LP from
+ * the basis the previous optimal / iteration-limited one left and the chain
+ * ended after the first candidate with a verdict (ReliabilityBrancher::
+ * strongBranch_ / findBestCandidate_, :469-506, :111-118); 0 one launch per
+ * chain position over every node still strong-branching.  The same LPs, the
+ * same results; K3L problems (m > 64) always take the per-position launches. */
+int mgpu_set_sb_chain(mgpu_ctx *ctx, int on);
 
 int mgpu_bnb_init(mgpu_ctx *ctx, int capacity, const double *root_lb, const double *root_ub,
                   double incumbent);

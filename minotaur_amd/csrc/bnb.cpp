@@ -300,6 +300,22 @@ int rel_round(mgpu_ctx *c, BnbState &s, int nb, int base, bool bfs) {
     io.status = s.cst.as<int32_t>();
     io.obj = s.cobj.as<double>();
     io.iters = s.cit.as<int32_t>();
+    if (c->sb_chain && lp_chain_ok(c)) {
+      // every node's whole chain in ONE K3 launch, one wave per node: no
+      // launch, matrix staging or list kernel per step, and a node no longer
+      // waits for the slowest LP of each step (LpIO::chain_*)
+      io.batch = nb;
+      io.node_list = nullptr;
+      io.chain_off = r.sb_off;
+      io.chain_n = r.nsb;
+      io.chain_nobj = r.obj;
+      io.chain_cutoff = r.cutoff;
+      const int lrc = launch_lp_nodes(c, io);
+      if (lrc != MGPU_OK) return lrc;
+      HIPCHK(c, launch_rel_decide(r, c->stream));
+      s.calls += h_tot[0];
+      return MGPU_OK;
+    }
     // one list counter per chain step, zeroed together (one fill per round
     // instead of one per step: the rounds of a reliability tree are short)
     const int nsteps = 2 * h_tot[3];

@@ -38,6 +38,7 @@
 // (score, index) keys, which took the per-round latency of the two kernels
 // from ~90 us each on a tree's narrow rounds.
 #include "bnb_internal.h"
+#include "sb_rule.h"
 #include "wave.h"
 
 #include <climits>
@@ -298,47 +299,13 @@ __global__ __launch_bounds__(256) void rel_children(RelIO io, const double *wlb,
   }
 }
 
-// ReliabilityBrancher::shouldPrune_ (:430-467) for one strong-branching LP
-__device__ __forceinline__ bool sb_prune(double chcutoff, double change, int st, bool &is_rel) {
-  switch (st) {
-    case 3:   // ProvenLocalInfeasible
-    case 2:   // ProvenInfeasible
-    case 5:   // ProvenObjectiveCutOff
-      return true;
-    case 1:   // ProvenLocalOptimal
-    case 0:   // ProvenOptimal (trustCutoff_)
-      return change > chcutoff - kRelETol;
-    case 6:   // EngineIterationLimit
-      return false;
-    case 7:   // ProvenFailedCQFeas / Infeas
-    case 8:
-      is_rel = false;
-      return false;
-    default:  // unexpected status (engProbs)
-      is_rel = false;
-      return false;
-  }
-}
+static_assert(kSbETol == kRelETol, "one eTol_ for the strong-branching verdict");
 
-// candidate k of node b after both strong-branching LPs: the changes
-// (max(obj - objval, 0), zeroed when a side is unreliable) and
-// useStrongBranchInfo_'s verdict: -1 a side unreliable (no observation),
-// 0 none, 1 both sides pruned, 2 the up side pruned (the down branch's bound
-// change), 3 the down side pruned (the up branch's)
+// candidate k of node b after both strong-branching LPs (sb_verdict)
 __device__ __forceinline__ int sb_outcome(const RelIO &io, size_t off, int k, double objval,
                                           double maxchange, double &cd, double &cu) {
-  const int sd = io.c_status[off + 2 * k], su = io.c_status[off + 2 * k + 1];
-  cd = fmax(io.c_obj[off + 2 * k] - objval, 0.0);
-  cu = fmax(io.c_obj[off + 2 * k + 1] - objval, 0.0);
-  bool is_rel = true;
-  const bool pd = sb_prune(maxchange, cd, sd, is_rel);
-  const bool pu = sb_prune(maxchange, cu, su, is_rel);
-  if (!is_rel) {
-    cu = 0.0;
-    cd = 0.0;
-    return -1;
-  }
-  return (pu && pd) ? 1 : pu ? 2 : pd ? 3 : 0;
+  return sb_verdict(io.c_status[off + 2 * k], io.c_obj[off + 2 * k], io.c_status[off + 2 * k + 1],
+                    io.c_obj[off + 2 * k + 1], objval, maxchange, cd, cu);
 }
 
 // One wave per node (as rel_prepare): the candidate scans are wave

@@ -79,6 +79,7 @@ struct mgpu_ctx {
   int bnb_brancher = 0;        // mgpu_bnb_brancher: 0 MaxVio, 1 reliability
   int bnb_guided = 1;          // mgpu_bnb_guided_dive (order 2: child order by the incumbent)
   int bnb_grow = 0;            // mgpu_bnb_growth: batch <= nodes so far / div (0: off)
+  bool sb_chain = true;        // mgpu_set_sb_chain: strong-branching chains in one K3 launch
   DevBuf lp_slots;             // K3L: one B^-1 [m][m] per resident workgroup
   DevBuf lp_next;              // K3L: node counter of the dynamic schedule
   DevBuf pfi_ovf;              // K3P: overflow counter + node list
@@ -186,3 +187,4 @@ int lp_solve_rows_wo(mgpu_ctx *c, int batch, const double *lb, const double *ub,
 // an LP batch with per-node warm starts through the K3 / K3L selection of
 // mgpu_lp_solve (mgpu_runtime.cpp); io.next is set here
 int launch_lp_nodes(mgpu_ctx *c, const LpIO &io);
+bool lp_chain_ok(const mgpu_ctx *c);

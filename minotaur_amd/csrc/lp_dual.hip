@@ -24,6 +24,7 @@
 //  * Pivots: B^{-1} row r is published to LDS once and read back as a
 //    broadcast for both the pivot row and the rank-1 update.
 #include "mgpu_internal.h"
+#include "sb_rule.h"
 #include "wave.h"
 
 namespace mgpu {
@@ -33,7 +34,7 @@ namespace mgpu {
 // cycles per section summed over all waves; never compiled into the product.
 __device__ unsigned long long g_lp_stamps[16];
 #define STAMP_KSTART const unsigned long long st_k0 = __builtin_amdgcn_s_memtime();
-#define STAMP_DECL unsigned long long st_acc[10] = {0}, st_t = __builtin_amdgcn_s_memtime(); \
+#define STAMP_DECL unsigned long long st_acc[16] = {0}, st_t = __builtin_amdgcn_s_memtime(); \
   const unsigned long long st_pro = st_t - st_k0;
 #define STAMP(i)                                              \
   do {                                                        \
@@ -43,7 +44,8 @@ __device__ unsigned long long g_lp_stamps[16];
   } while (0)
 #define STAMP_FLUSH                                            \
   if ((threadIdx.x & 63) == 0)                                \
-    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_lp_stamps[i_], st_acc[i_]); \
+    for (int i_ = 0; i_ < 16; ++i_)                            \
+      if (i_ < 10 || i_ > 11) atomicAdd(&g_lp_stamps[i_], st_acc[i_]); \
   if ((threadIdx.x & 63) == 0) {                               \
     atomicAdd(&g_lp_stamps[10], __builtin_amdgcn_s_memtime() - st_k0); \
     atomicAdd(&g_lp_stamps[11], st_pro);                       \
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
   double *s_rhi = (double *)p;  p += al16((size_t)m * 8);
   double *s_blb = (double *)p;  p += al16((size_t)n * 8);
   double *s_bub = (double *)p;  p += al16((size_t)n * 8);
-  const bool box1 = io.batch == 1 && io.node_list == nullptr;
+  const bool box1 = io.batch == 1 && io.node_list == nullptr && io.chain_n == nullptr;
   for (int t = threadIdx.x; t < n; t += 64 * W) {
     s_c[t] = lp.objd[t];
     if (box1) {
@@ -329,7 +331,35 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       bi = lo + __builtin_amdgcn_readfirstlane(t);
     }
     if (bi >= nsolve) break;
-    const int b = io.node_list != nullptr ? io.node_list[bi] : bi;
+    const int unit = io.node_list != nullptr ? io.node_list[bi] : bi;
+    // chained mode: the unit's LPs one after the other (one LP otherwise)
+    const bool chained = io.chain_n != nullptr;
+    const int c0 = chained ? 2 * io.chain_off[unit] : unit;
+    const int cn = chained ? 2 * io.chain_n[unit] : 1;
+    int pst0 = 0, pst1 = 0;        // the chain's last pair: statuses, values
+    double pob0 = 0.0, pob1 = 0.0;
+    // the basis: B^-1 rows, basic column per lane; in chained mode `held`
+    // says the wave still holds the chain slot's basis (the last LP kept its
+    // basis and wrote it there), so the next LP need not read it back
+    double binv[M];
+    int h = -1;
+    bool held = false;
+    for (int cs = 0; cs < cn; ++cs) {
+    if (chained && cs >= 2 && (cs & 1) == 0) {
+      const double ov = io.chain_nobj[unit];
+      double cd, cu;
+      if (sb_verdict(pst0, pob0, pst1, pob1, ov, io.chain_cutoff - ov, cd, cu) > 0) break;
+    }
+    auto note = [&](int st, double ob) {
+      if (cs & 1) {
+        pst1 = st;
+        pob1 = ob;
+      } else {
+        pst0 = st;
+        pob0 = ob;
+      }
+    };
+    const int b = chained ? c0 + cs : unit;
     // pivots already made by K3P / K3PW (continuation): counted by the
     // iteration limit, the Bland switch and the reported total
     const int ib = io.iter_base_list != nullptr ? io.iter_base_list[bi] : io.iter_base;
@@ -369,6 +399,8 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         io.obj[b] = INFINITY;
         io.iters[b] = 0;
       }
+      note(kUnknownStatus, INFINITY);
+      held = false;
       continue;
     }
     if (nrows) {
@@ -420,14 +452,18 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
         io.obj[b] = INFINITY;
         io.iters[b] = 0;
       }
+      note(2, INFINITY);
+      held = false;
       continue;
     }
 
     // ---- basis: warm start (parent / root optimum) or slack basis ----
     const bool warm = io.ws.head != nullptr;
-    double binv[M];
-    int h = -1;
-    if (warm) {
+    if (warm && chained && held) {
+      // the chain slot is this wave's own last basis: statuses, reduced
+      // costs (0 on basic columns) in LDS and B^-1 / h in registers are what
+      // the load below would produce
+    } else if (warm) {
       const int32_t *wh = kSharedWs ? s_whead : io.ws.head + (size_t)bw * io.ws.s_head;
       const int8_t *wst = kSharedWs ? s_wst : io.ws.st + (size_t)bw * io.ws.s_st;
       const double *wd = kSharedWs ? s_wd : io.ws.d + (size_t)bw * io.ws.s_d;
@@ -494,6 +530,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       for (int k = 0; k < M; ++k) binv[k] = (k == lane && lane < m) ? -1.0 : 0.0;
     }
     wave_sync();
+    STAMP(12);
     double art_bound = kArt0;
     for (int j = lane; j < N; j += 64) {
       if (C.st[j] == ST_BASIC) continue;
@@ -516,6 +553,7 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       if (!keep) place_nonbasic(C, j, art_bound);
     }
     wave_sync();
+    STAMP(13);
     double lbB = 0.0, ubB = 0.0;
     if (lane < m) {
       lbB = C.blo[h];
@@ -745,17 +783,25 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
     // ---- outputs ----
     STAMP(8);
     wave_sync();
+    double objv = status == 2 ? INFINITY : -INFINITY;
     if (status == 0 || status == 6) {
       if (lane < m) C.z[h] = zB;
       wave_sync();
       // objective as the oracle sums it: sequentially over the columns, so
       // the value is the oracle's bit for bit (the batched tree's reliability
       // branching compares strong-branching values and pseudocosts exactly)
-      if (lane == 0) {
-        double s = 0.0;
-        for (int j = 0; j < n; ++j) s += C.cj(j) * C.z[j];
-        io.obj[b] = C.ocol < 0 ? s + lp.objoff : s;
+      // the products lane-parallel (the same roundings: no contraction),
+      // then summed in column order through lane reads
+      double s = 0.0;
+      for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        const double pj = j < n ? C.cj(j) * C.z[j] : 0.0;
+        const int cnt = n - j0 < 64 ? n - j0 : 64;
+        for (int l = 0; l < cnt; ++l) s += rld(pj, l);
       }
+      objv = C.ocol < 0 ? s + lp.objoff : s;
+      if (lane == 0) io.obj[b] = objv;
+      STAMP(14);
       if (io.x != nullptr)
         for (int j = lane; j < n; j += 64) io.x[(size_t)b * n + j] = C.z[j];
       if (io.rc != nullptr)
@@ -775,14 +821,20 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
             if (k < m) dst[(size_t)k * m] = binv[k];   // column-major: coalesced
         }
       }
+      STAMP(15);
     } else if (lane == 0) {
-      io.obj[b] = status == 2 ? INFINITY : -INFINITY;
+      io.obj[b] = objv;
     }
     if (lane == 0) {
       io.status[b] = status;
       io.iters[b] = iters + ib;
     }
+    if (chained) {
+      note(status, objv);
+      held = status == 0 || status == 6;
+    }
     STAMP(9);
+    }  // the unit's LPs
   }
   leave();
   STAMP_FLUSH

@@ -160,6 +160,17 @@ struct LpIO {
     int8_t *st_out;
     int inherit;
   } path;
+  // Chained LPs (K3 only; chain_n == null: none), ReliabilityBrancher::
+  // strongBranch_ through one engine (:469-506): unit u of the batch is node
+  // u, whose LPs 2 chain_off[u] .. 2 (chain_off[u] + chain_n[u]) - 1 (down,
+  // up per candidate) run one after the other in ONE wave, each from the
+  // warm start the previous optimal / iteration-limited one left (ws_index /
+  // wo_index: the node's chain slot); after each pair the verdict of
+  // sb_verdict against the node's value chain_nobj[u] and the incumbent
+  // chain_cutoff ends the chain (findBestCandidate_, :111-118).
+  const int32_t *chain_off, *chain_n;
+  const double *chain_nobj;
+  double chain_cutoff;
 };
 constexpr int kPathMax = 32;    // pivots per path warm start (MGPU_PATH_MAX)
 constexpr int kPathInherit = 32; // longest basis difference the batched tree hands to children (= the eta cap: profiles/r04q)

@@ -773,6 +773,15 @@ extern "C++" int launch_lp_nodes(mgpu_ctx *c, const LpIO &io) {
   return launch_lp(c, io, "lp batch");
 }
 
+// chained LPs (LpIO::chain_*) run on K3 only
+extern "C++" bool lp_chain_ok(const mgpu_ctx *c) { return !use_large_lp(c); }
+
+int mgpu_set_sb_chain(mgpu_ctx *c, int on) {
+  if (!c) return MGPU_ERR_ARG;
+  c->sb_chain = on != 0;
+  return MGPU_OK;
+}
+
 int mgpu_lp_pfi_cap(mgpu_ctx *c) {
   if (!c) return MGPU_ERR_ARG;
   bool wide;

@@ -46,7 +46,7 @@ EXPORTS = [
     'mgpu_comm_unique_id', 'mgpu_comm_init', 'mgpu_comm_init_host', 'mgpu_comm_info',
     'mgpu_allreduce_f64', 'mgpu_allreduce_min', 'mgpu_round_reduce', 'mgpu_allgather_f64',
     'mgpu_alltoall_rows_dev', 'mgpu_lb_deal', 'mgpu_bnb_rebalance', 'mgpu_alloc_stats',
-    'mgpu_bnb_growth',
+    'mgpu_bnb_growth', 'mgpu_set_sb_chain',
 ]
 
 COMM_ID_BYTES = 128            # MGPU_COMM_ID_BYTES
@@ -143,6 +143,7 @@ def load_library():
     lib.mgpu_bnb_config.argtypes = [_P, _I, _I]
     lib.mgpu_bnb_brancher.argtypes = [_P, _I]
     lib.mgpu_bnb_growth.argtypes = [_P, _I]
+    lib.mgpu_set_sb_chain.argtypes = [_P, _I]
     lib.mgpu_bnb_relaxation.argtypes = [_P, _I]
     lib.mgpu_bnb_guided_dive.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
@@ -709,6 +710,12 @@ class Context:
         """Next tree's batch growth (mgpu_bnb_growth): a round evaluates at most
         max(1, nodes so far // div) nodes; 0 = off."""
         self._chk(self.lib.mgpu_bnb_growth(self.h, int(div)), 'mgpu_bnb_growth')
+
+    def set_sb_chain(self, on):
+        """mgpu_set_sb_chain: the reliability brancher's strong-branching
+        chains in one K3 launch (1, default) or one launch per chain position
+        (0); the same results."""
+        self._chk(self.lib.mgpu_set_sb_chain(self.h, int(on)), 'mgpu_set_sb_chain')
 
     def bnb_relaxation(self, kind):
         """Next tree's relaxation: 0 the loaded LP, 1 the loaded QP by K5

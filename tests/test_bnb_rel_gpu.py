@@ -6,7 +6,9 @@ pseudocosts, pruning and one-sided bound changes by the brancher.
 Bar: the GPU tree equals the CPU restatement (oracle/bnb.py, brancher 1)
 round for round: rounds, nodes, decision counts, strong-branching LP counts,
 nodes pruned / modified by the brancher; the optimum is HiGHS' MILP optimum
-(1e-6) and the same bit for bit as the restatement's."""
+(1e-6) and the same bit for bit as the restatement's.  The strong-branching
+chains run in one K3 launch per round (mgpu_set_sb_chain 1, the default) or
+one launch per chain position (0): both equal the restatement."""
 import math
 
 import pytest
@@ -81,8 +83,9 @@ def test_rel_tls4_lin_tree(ctx):
     assert abs(og - hobj) <= 1e-6 * max(1.0, abs(hobj))
 
 
+@pytest.mark.parametrize('chain', [1, 0])
 @pytest.mark.parametrize('warm', [0, 1])
-def test_rel_tree_growth_tls4_oa(ctx, warm):
+def test_rel_tree_growth_tls4_oa(ctx, warm, chain):
     """with a fixed batch the round's nodes share one
     pseudocost state and config 2's reliability tree grows to 4.9x the
     reference's.  mgpu_bnb_growth 2 (a round evaluates at most half the
@@ -97,8 +100,12 @@ def test_rel_tree_growth_tls4_oa(ctx, warm):
     p = LinProblem.load(os.path.join(root, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
     hs, hobj = oracle.highs_milp(p)
     ctx.load(p)
-    og, _, sg, _ = bnb.solve(ctx, batch=131072, capacity=1 << 20, order=1, warm=warm,
-                             brancher=1, growth=2)
+    ctx.set_sb_chain(chain)
+    try:
+        og, _, sg, _ = bnb.solve(ctx, batch=131072, capacity=1 << 20, order=1, warm=warm,
+                                 brancher=1, growth=2)
+    finally:
+        ctx.set_sb_chain(1)
     oc, _, sc, _ = bnb.solve(CpuBnbContext(p), batch=131072, capacity=1 << 20, order=1,
                              warm=warm, brancher=1, growth=2)
     assert sg.open == sc.open == 0

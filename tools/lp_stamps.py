@@ -97,9 +97,46 @@ def b1():
     print(f"  {'kernel total':14s} {buf[10] / L:9.0f}   (prologue {buf[11] / L:.0f}; 4 waves summed)")
 
 
+def rel():
+    """--rel: K3's sections over config 2's whole reliability tree (tls4-oa,
+    best-first, parent warm starts, growth 2; node LPs and chained strong
+    branching): wave-cycles per LP and per pivot per section."""
+    if not os.path.exists(OUT):
+        build()
+    os.environ['MGPU_LIB'] = OUT
+    from minotaur_amd import bnb
+    from minotaur_amd.problem import LinProblem
+    from minotaur_amd.runtime import Context, load_library
+    lib = load_library()
+    p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
+    ctx = Context(0)
+    ctx.load(p)
+    bnb.solve(ctx, batch=131072, capacity=1 << 20, order=1, warm=1, brancher=1, growth=2)
+    buf = (ctypes.c_ulonglong * 16)()
+    lib.mgpu_debug_lp_stamps(buf, 1)
+    _, _, st, _ = bnb.solve(ctx, batch=131072, capacity=1 << 20, order=1, warm=1, brancher=1,
+                            growth=2)
+    lib.mgpu_debug_lp_stamps(buf, 1)
+    lps = st.lps + st.sb_lps
+    piv = st.pivots + st.sb_pivots
+    tot = sum(buf[i] for i in range(10))
+    print(f"{lps} LPs, {piv} pivots ({piv / max(lps, 1):.2f} per LP); section wave-cycles "
+          f"{tot:.3e}; kernel total {buf[10]:.3e}, prologue {buf[11]:.3e}")
+    names = NAMES[:10] + ['', '', 'setup:basis', 'setup:place', 'out:objective', 'out:x+ws']
+    tot += sum(buf[i] for i in range(12, 16))
+    for i, nme in enumerate(names):
+        if not nme:
+            continue
+        print(f"  {nme:14s} {100.0 * buf[i] / tot:6.2f} %   {buf[i] / max(lps, 1):9.0f} cyc/LP"
+              f"   {buf[i] / max(piv, 1):9.0f} cyc/pivot")
+
+
 def main():
     if '--tree' in sys.argv:
         tree()
+        return
+    if '--rel' in sys.argv:
+        rel()
         return
     if '--b1' in sys.argv:
         b1()
