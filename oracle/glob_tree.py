@@ -59,6 +59,7 @@ class _GStats:
         self.br_int = self.br_cont = 0
         self.cuts = self.resolves = 0
         self.obbt_lps = 0
+        self.sb_lps = 0
         self.open = self.last_batch = 0
         self.incumbent = math.inf
 
@@ -110,6 +111,30 @@ def decide(qp, kinf, st, val, x, lb, ub, inc):
         c += 1
     if feas:
         return 3, -1, 0.0, 0, 0
+    # MaxVio over the merged candidates: score 0.1 (0.8 min + 0.2 max), the
+    # first maximum, up first when dd > ud
+    best, bvar, bup, bint = -math.inf, -1, 0, 0
+    for j, isint, d, u in candidates(qp, x, lb, ub):
+        lo, hv = (d, u) if d < u else (u, d)
+        sc = 0.1 * (0.8 * lo + 0.2 * hv)
+        if sc > best:
+            best, bvar, bint, bup = sc, j, isint, (1 if d > u else 0)
+    if bvar < 0:
+        return 5, -1, 0.0, 0, 0
+    return 0, bvar, float(x[bvar]), bup, bint
+
+
+QA_TOL, QR_TOL = 1e-6, 1e-7   # QuadHandler aTol_, rTol_ (QuadHandler.cpp:60-67)
+
+
+def candidates(qp, x, lb, ub):
+    """The branching candidates of IntVarHandler and QuadHandler merged per
+    variable as MaxVioBrancher / StrongBrancher::findCandidates_ merge them
+    (the later handler takes a candidate when its distance sum is >=, the
+    distances stay the earlier handler's: BrCand::setDist is an empty
+    non-virtual): [(var, isint, ddist, udist)] ascending by variable (the
+    candidate sets' order, CompareVarBrCand, Types.cpp:23-27)."""
+    nv, vt = qp.nv, qp.vtype
     idd, iud, qd, qu = {}, {}, {}, {}
     for j in range(nv):
         v = x[j]
@@ -152,31 +177,104 @@ def decide(qp, kinf, st, val, x, lb, ub, inc):
                 dd = (yv - v1 * v0) / math.sqrt(1.0 + v1 * v1 + lb[j0] * lb[j0])
                 ud = (yv - v1 * v0) / math.sqrt(1.0 + v1 * v1 + ub[j0] * ub[j0])
             add_q(j1, dd, ud)
-    best, bvar, bup, bint = -math.inf, -1, 0, 0
+    out = []
     for j in range(nv):
         hi, hq = j in idd, j in qd
-        if not hi and not hq:
-            continue
         if hi and hq:
-            # the later handler takes the candidate, the distances stay the
-            # earlier one's (MaxVioBrancher's merge calls the empty
-            # BrCand::setDist through a BrCandPtr, BrCand.cpp:44-46)
-            isint = 0 if idd[j] + iud[j] <= qd[j] + qu[j] else 1
-            d, u = idd[j], iud[j]
+            out.append((j, 0 if idd[j] + iud[j] <= qd[j] + qu[j] else 1, idd[j], iud[j]))
         elif hi:
-            isint, d, u = 1, idd[j], iud[j]
+            out.append((j, 1, idd[j], iud[j]))
+        elif hq:
+            out.append((j, 0, qd[j], qu[j]))
+    return out
+
+
+def _keep(a):
+    return a if abs(a) > 1e-9 else 0.0   # LinearFunction::addTerm (LinearFunction.cpp:89-95)
+
+
+def br_mod(qp, rec, lb, ub, x, j, isint, down):
+    """Handler::getBrMod of candidate j on copies of the node's box and row
+    record: IntVarHandler (IntVarHandler.cpp:113-130) floor / ceil of x_j;
+    QuadHandler (QuadHandler.cpp:616-692) x_j itself, plus the rows of the
+    violated terms of x_j rebuilt for the branch's box: the secant of its
+    square (getNewSqLf_ over [lb, x_j] or [x_j, ub]) and, per violated
+    bilinear holding x_j, rows 1 and 3 (down) or 0 and 2 (up) from
+    getNewBilLf_ with x_j's bound at its value -- with x_j the bilinear's
+    second factor the arguments come swapped, so row 3 / 2 then carries the
+    other upper-envelope formula, as in the reference."""
+    lb, ub, rec = lb.copy(), ub.copy(), np.array(rec, dtype=np.float64)
+    v = float(x[j])
+    if isint:
+        if down:
+            ub[j] = math.floor(v)
         else:
-            isint, d, u = 0, qd[j], qu[j]
-        lo, hv = (d, u) if d < u else (u, d)
-        sc = 0.1 * (0.8 * lo + 0.2 * hv)
-        if sc > best:
-            best, bvar, bint, bup = sc, j, isint, (1 if d > u else 0)
-    if bvar < 0:
-        return 5, -1, 0.0, 0, 0
-    return 0, bvar, float(x[bvar]), bup, bint
+            lb[j] = math.ceil(v)
+        return lb, ub, rec
+    nsq = qp.nsq
+    for k in range(nsq):
+        if int(qp.sq_x[k]) != j:
+            continue
+        y = int(qp.sq_y[k])
+        vio = v * v - x[y]
+        if vio > QA_TOL and vio > abs(x[y]) * QR_TOL:
+            lo_, hi_ = (lb[j], v) if down else (v, ub[j])
+            rec[2 * k + 1] = -hi_ * lo_
+            rec[2 * k] = _keep(-1. * (hi_ + lo_)) if abs(hi_ + lo_) > 1e-5 else 0.0
+    for k in range(qp.nbil):
+        X0, X1 = int(qp.bil_x0[k]), int(qp.bil_x1[k])
+        if j != X0 and j != X1:
+            continue
+        y = int(qp.bil_y[k])
+        xv = x[X0] * x[X1]
+        vio = abs(xv - x[y])
+        if not (vio > 1e-5 and vio > abs(x[y]) * 1e-4):
+            continue
+        a, b = (X0, X1) if j == X0 else (X1, X0)    # getNewBilLf_'s x0, x1
+        xa = x[a]
+        if down:
+            lb0, ub0 = lb[a], xa
+        else:
+            lb0, ub0 = xa, ub[a]
+        lb1, ub1 = lb[b], ub[b]
+
+        def row(t):
+            # getNewBilLf_ (QuadHandler.cpp:730-763): coefficients of a, b, rhs
+            if t == 0:
+                return lb1, lb0, lb0 * lb1
+            if t == 1:
+                return ub1, ub0, ub0 * ub1
+            if t == 2:
+                return -1.0 * ub1, -1.0 * lb0, -lb0 * ub1
+            return -1.0 * lb1, -1.0 * ub0, -ub0 * lb1
+        o0 = 2 * nsq + 12 * k
+        for t in ((1, 3) if down else (0, 2)):
+            ca, cb, rhs = row(t)
+            cx0, cx1 = (ca, cb) if a == X0 else (cb, ca)
+            o = o0 + 3 * t
+            rec[o], rec[o + 1], rec[o + 2] = _keep(cx0), _keep(cx1), rhs
+    lb[j] = v if not down else lb[j]
+    ub[j] = v if down else ub[j]
+    return lb, ub, rec
 
 
-QA_TOL, QR_TOL = 1e-6, 1e-7   # QuadHandler aTol_, rTol_ (QuadHandler.cpp:60-67)
+SB_CANDS, SB_ITER, SB_THRESH, SB_ETOL = 20, 50, 5, 1e-6   # reliabilitySetup(20, 50, 5), Glob.cpp:171-181
+
+
+def _sb_prune(chcutoff, change, st):
+    """StrongBrancher::shouldPrune_ (StrongBrancher.cpp:461-497): (prune, reliable)."""
+    if st in (3, 2, 5):
+        return True, True
+    if st in (1, 0):
+        return change > chcutoff - SB_ETOL, True
+    if st == 6:
+        return False, True
+    return False, False
+
+
+def _score(up, down):
+    """getScore_ (StrongBrancher.cpp:381-389)."""
+    return down * 0.8 + up * 0.2 if up > down else up * 0.8 + down * 0.2
 
 
 def find_lin_pt(xval, yval):
@@ -277,9 +375,243 @@ class CpuGlobContext:
         self.p, self.nr = relaxation_lp(qp, self.rows0, self.S)
         self.tan0 = tangent_record(qp, self.S)
         self.order, self.warm, self.qt, self.lin, self.obbt = 0, 0, 1, 0, 0
+        self.brancher = 0
 
     def glob_config(self, order=0, warm=0, qt=1, lin=0, obbt=0):
         self.order, self.warm, self.qt, self.lin, self.obbt = order, warm, qt, lin, obbt
+
+    def glob_brancher(self, kind=0):
+        """0 MaxVioBrancher, 1 Glob's relstronger (StrongBrancher with
+        reliabilitySetup(20, 50, 5), Glob.cpp:171-181; batch 1, order 2,
+        warm 1, lin 1)."""
+        self.brancher = kind
+
+    def _lp1(self, lb, ub, rec, ws, iter_limit=10000):
+        """One node LP from the engine's basis ws = (head, st) or the slack
+        basis: (status, value, pivots, x, basis out)."""
+        W = None if ws is None else WarmStart(ws[0][None], ws[1][None], None, None)
+        st, obj, it, x, ho, so = oracle.dual_simplex_rows(self.p, lb[None], ub[None], self.nr,
+                                                          np.asarray(rec)[None], ws=W,
+                                                          iter_limit=iter_limit, want_x=True,
+                                                          want_ws=True)
+        return int(st[0]), float(obj[0]), int(it[0]), x[0].copy(), (ho[0].copy(), so[0].copy())
+
+    def _presolve(self, lb, ub, rec, first=False):
+        """PCBProcessor::presolveNode_ / Handler::getStrongerMods: the
+        handlers' presolveNode in order (LinearHandler's when lin, then
+        QuadHandler's K2).  Returns (infeasible, lb, ub, rec)."""
+        lb, ub = lb.copy()[None], ub.copy()[None]
+        if self.lin and self._linear(lb, ub, [rec])[0]:
+            return True, lb[0], ub[0], rec
+        qt = 1 if (self.qt or first) else 0
+        o = oracle.quad_fbbt(self.qp, lb, ub, self.inc, qt, np.asarray(rec)[None, :self.R])
+        if int(o.infeas[0]) != 0:
+            if int(o.infeas[0]) != 1:
+                raise RuntimeError('glob round: engine problem in K2')
+            return True, o.lb[0], o.ub[0], rec
+        rec = np.array(rec, dtype=np.float64)
+        rec[:self.R] = o.rows[0]
+        return False, o.lb[0].copy(), o.ub[0].copy(), rec
+
+    def _after_solve(self, info, obj, x):
+        """StrongBrancher::updateAfterSolve (StrongBrancher.cpp:589-643): the
+        pseudocost of the branching that made this node."""
+        if info is None:
+            return
+        j = info['var']
+        if info['int']:
+            oldval, newval = info['act'], x[j]
+            c = (obj - info['plb']) / (abs(newval - oldval) + SB_ETOL)
+            down = newval < oldval
+        else:
+            down = info['act'] < 0
+            c = (obj - info['plb']) / ((info['dd'] if down else info['ud']) + SB_ETOL)
+        if c < 0.0 or math.isinf(c) or math.isnan(c):
+            c = 0.0
+        self._upd_pc(j, c, down)
+
+    def _upd_pc(self, j, c, down):
+        """updatePCost_ (:645-650)."""
+        if down:
+            self.pd[j] = (self.pd[j] * self.td[j] + c) / (self.td[j] + 1)
+            self.td[j] += 1
+        else:
+            self.pu[j] = (self.pu[j] * self.tu[j] + c) / (self.tu[j] + 1)
+            self.tu[j] += 1
+
+    def _strong(self, lb, ub, rec, x, objval, eng):
+        """StrongBrancher::findBranches (StrongBrancher.cpp:184-264) on one
+        node.  Returns (kind, payload, engine basis): ('branch', (var, isint,
+        dd, ud, up_first)), ('prune', None), ('mod', (lb, ub, rec)) or
+        ('nocand', None)."""
+        qp = self.qp
+        cands = candidates(qp, x, lb, ub)
+        if not cands:
+            return 'nocand', None, eng
+        rel = [c for c in cands if self.tu[c[0]] >= SB_THRESH and self.td[c[0]] >= SB_THRESH]
+        unrel = [c for c in cands if not (self.tu[c[0]] >= SB_THRESH and self.td[c[0]] >= SB_THRESH)]
+        maxchange = self.inc - objval
+        best, bc = -math.inf, None
+        dirs = {}      # setDir per candidate (BrVarCand's default: UpBranch, BrVarCand.cpp:31)
+
+        def pcscore(c):
+            j = c[0]
+            chd, chu = c[2] * self.pd[j], c[3] * self.pu[j]
+            return chd, chu, _score(chu, chd)
+
+        for c in rel:                      # findBestCandidate_ :93-108
+            chd, chu, sc = pcscore(c)
+            if sc > best:
+                best, bc = sc, c
+                dirs[c[0]] = not (chu > chd)
+        # sortUnrelCands_ (:429-459): vio = score / (max(times) + 1); the
+        # smallest of the top maxCands_
+        vio = [_score(c[3], c[2]) / (max(self.td[c[0]], self.tu[c[0]]) + 1) for c in unrel]
+        minscore = sorted(vio, reverse=True)[:SB_CANDS][-1] if unrel else 0.0
+        status, mod = 'none', None
+        cnt = i = 0
+        for c in unrel:                    # :115-145
+            if cnt >= SB_CANDS:
+                break
+            if vio[i] >= minscore:
+                cnt += 1
+                res = []
+                for down in (True, False):   # strongBranch_ :499-587: down, then up
+                    blb, bub, brec = br_mod(qp, rec, lb, ub, x, c[0], c[1], down)
+                    inf, blb, bub, brec = self._presolve(blb, bub, brec)
+                    if inf:
+                        res.append((2, self._last_val))
+                        continue
+                    st, ob, it, _, wo = self._lp1(blb, bub, brec, eng, SB_ITER)
+                    self.tot.lps += 1
+                    self.tot.sb_lps += 1
+                    self.lplog.append((st, ob, it))
+                    self._last_val = ob
+                    if st in (0, 6):
+                        eng = wo
+                    res.append((st, ob))
+                (sd, od), (su, ou) = res
+                chu, chd = max(ou - objval, 0.0), max(od - objval, 0.0)
+                # useStrongBranchInfo_ (:652-689)
+                pdn, rd = _sb_prune(maxchange, chd, sd)
+                pup, ru = _sb_prune(maxchange, chu, su)
+                if not (rd and ru):
+                    chu = chd = 0.0
+                elif pup and pdn:
+                    status = 'prune'
+                elif pup:
+                    status, mod = 'mod', br_mod(qp, rec, lb, ub, x, c[0], c[1], True)
+                elif pdn:
+                    status, mod = 'mod', br_mod(qp, rec, lb, ub, x, c[0], c[1], False)
+                else:
+                    j = c[0]
+                    self._upd_pc(j, abs(chd) / (abs(c[2]) + SB_ETOL), True)
+                    self._upd_pc(j, abs(chu) / (abs(c[3]) + SB_ETOL), False)
+                sc = _score(chu, chd)
+                if status != 'none':
+                    break
+                if sc > best:
+                    best, bc = sc, c
+                    dirs[c[0]] = not (chu > chd)
+            i += 1
+        if status == 'prune':
+            return 'prune', None, eng
+        if status == 'mod':
+            return 'mod', mod, eng
+        for jx, c in enumerate(unrel):     # :149-169
+            if vio[jx] < minscore or jx >= i:
+                chd, chu, sc = pcscore(c)
+                if sc > best:
+                    best, bc = sc, c
+                    dirs[c[0]] = not (chu > chd)
+        if best == 0 and not rel:          # :170-180
+            bc = unrel[int(np.argmax(vio))]
+        if bc is None:
+            return 'nocand', None, eng
+        return 'branch', (bc[0], bc[1], bc[2], bc[3], dirs.get(bc[0], True)), eng
+
+    def _process_rs(self, nd, nid):
+        """PCBProcessor::process (PCBProcessor.cpp:178-353) on one node with
+        the StrongBrancher: presolve, then solve / prune / updateAfterSolve /
+        feasible / root OBBT / separate / findBranches, re-solving after a
+        separation cut, OBBT or a brancher modification.  Returns (decision,
+        children as node tuples)."""
+        qp = self.qp
+        lb, ub, rec = nd[0].copy(), nd[1].copy(), np.array(nd[2], dtype=np.float64)
+        info = nd[7] if len(nd) > 7 else None
+        first = self.tot.nodes == 0
+        inf, lb, ub, rec = self._presolve(lb, ub, rec, first)
+        if inf:
+            return 1, []
+        eng = None if nd[5] is None else (nd[5], nd[6])
+        it_ = 0
+        root = nid == 0
+        while True:
+            it_ += 1
+            st, obj, piv, x, wo = self._lp1(lb, ub, rec, eng)
+            self.tot.lps += 1
+            self.tot.pivots += piv
+            self.lplog.append((st, obj, piv))
+            self._last_val = obj
+            if st in (0, 6):
+                eng = wo
+            d = decide(qp, 0, st, obj, x, lb, ub, self.inc)[0]
+            if d in (1, 2, 4):
+                if d == 4:
+                    raise RuntimeError('glob round: engine problem')
+                return d, []
+            if it_ == 1:
+                self._after_solve(info, obj, x)
+            if d == 3:
+                if obj < self.inc:
+                    self.inc = obj
+                    self.best_x = x.copy()
+                return 3, []
+            if it_ == 1 and root and self.obbt:
+                ch, feas, nlb, nub, nrec, nl = self._root_obbt(lb.copy(), ub.copy(), rec, x)
+                self.tot.obbt_lps += nl
+                if ch:
+                    lb, ub, rec = nlb, nub, nrec
+                    if not feas:
+                        continue
+            if self.S > 0 and separate(qp, x, rec, self.R, self.S):
+                self.tot.resolves += 1
+                continue
+            ws_children = eng
+            kind, pay, eng = self._strong(lb, ub, rec, x, obj, eng)
+            if kind == 'nocand':
+                return 5, []
+            if kind == 'prune':
+                return 1, []
+            if kind == 'mod':
+                lb, ub, rec = pay
+                inf, lb, ub, rec = self._presolve(lb, ub, rec)
+                if inf:
+                    return 1, []
+                continue
+            j, isint, dd, ud, up_first = pay
+            v = float(x[j])
+            self.brlog.append((j, v))
+            if isint:
+                self.tot.br_int += 1
+            else:
+                self.tot.br_cont += 1
+            kids = []
+            for upc in (False, True):
+                clb, cub = lb.copy(), ub.copy()
+                if upc:
+                    clb[j] = math.ceil(v) if isint else v
+                else:
+                    cub[j] = math.floor(v) if isint else v
+                act = v if isint else (1.0 if upc else -1.0)
+                kids.append((clb, cub, rec.copy(), obj, nd[4] + 1, ws_children[0], ws_children[1],
+                             {'var': j, 'int': isint, 'act': act, 'dd': dd, 'ud': ud, 'plb': obj}))
+            down_first = True
+            if isint:   # IntVarHandler::getBranches (:133-190): guided dive, else the direction
+                down_first = not up_first
+                if math.isfinite(self.inc) and not math.isnan(self.best_x[j]):
+                    down_first = self.best_x[j] < v
+            return 0, kids if down_first else kids[::-1]
 
     def _rel_feasible(self, rec, x):
         """QuadHandler::isFeasibleToRelaxation_ (QuadHandler.cpp:955-981):
@@ -357,6 +689,11 @@ class CpuGlobContext:
         self.brlog = []        # (variable, value) of every branching in order
         self.tot = _GStats()
         self.tot.incumbent = incumbent
+        # StrongBrancher's pseudocosts (initialize_, :391-401) and the engine's
+        # last solution value (strongBranch_ reads it after a presolve verdict)
+        self.pu, self.pd = np.zeros(qp.nv), np.zeros(qp.nv)
+        self.tu, self.td = np.zeros(qp.nv, dtype=np.int64), np.zeros(qp.nv, dtype=np.int64)
+        self._last_val = 0.0
         self.tot.open = 1
 
     def _lp(self, lb, ub, vals, heads, sts):
@@ -393,6 +730,8 @@ class CpuGlobContext:
         if incumbent < self.inc:
             self.inc = incumbent
         heap = self.order == 2
+        if self.brancher == 1:
+            return self._round_rs(batch)
         if heap:
             nodes, ids = [], []
             while len(nodes) < batch and len(self.heap):
@@ -562,6 +901,36 @@ class CpuGlobContext:
         self.tot.incumbent = self.inc
         if ndec[4]:
             raise RuntimeError('glob round: engine problem')
+        return self.tot
+
+    def _round_rs(self, batch):
+        """A round with the StrongBrancher: one node (batch 1, reference
+        order, parent-basis warm starts), processed as the reference does."""
+        # lin 1: a brancher modification reaches p_, whose box QuadHandler
+        # propagates, only through LinearHandler's copyBndsFromRel_
+        # (PCBProcessor.cpp:299-305 applies it to the relaxation), so one box
+        # per node restates the reference only with the linear presolve on
+        if batch != 1 or self.order != 2 or self.warm != 1 or self.lin != 1:
+            raise ValueError('relstronger: batch 1, order 2, warm 1, lin 1')
+        while len(self.heap):
+            top = self.heap.pop()
+            if top['lb'] > self.inc - 1e-6 or \
+                    abs(self.inc - top['lb']) / (abs(self.inc) + 1e-6) * 100.0 < 1e-6:
+                continue
+            break
+        else:
+            self.tot.open = 0
+            return self.tot
+        d, kids = self._process_rs(top['node'], top['id'])
+        self.tot.ndec[d] += 1
+        for k in kids:
+            self.heap.push({'lb': k[3], 'depth': k[4], 'id': self.next_id, 'node': k})
+            self.next_id += 1
+        self.tot.rounds += 1
+        self.tot.nodes += 1
+        self.tot.open = len(self.heap)
+        self.tot.last_batch = 1
+        self.tot.incumbent = self.inc
         return self.tot
 
     def glob_best(self):

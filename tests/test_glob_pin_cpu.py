@@ -17,7 +17,11 @@ obbt 1 turns on the reference's root OBBT (the OBBT option, on in Glob;
 QuadHandler::postSolveRootNode with CpuLPEngine as bte_) and the
 restatement's (obbt_chained, the rows rewritten, the root re-solved when its
 point leaves the tightened relaxation); the bound LPs are counted on both
-sides.
+sides.  brancher 1 is Glob's default brancher relstronger (StrongBrancher::
+reliabilitySetup(20, 50, 5), Glob.cpp:171-181) on both sides: strong-
+branching children with getBrMod's rows and every handler's node presolve,
+LPs chained through the engine with 50 pivots at most, verdicts, pseudocosts
+and updateAfterSolve; there every main-engine solve's pivots are compared.
 Seeds are every seed of a fixed range (no selection).  Bar: nodes processed
 and created, LP solves, closures, the incumbent's bits, the branching sequence (variable
 and its LP value, 1e-9) and each node LP's pivot count and value (1e-9)."""
@@ -56,30 +60,33 @@ def _logs(integ):
     return (bv, bx), (ls, lv, li)
 
 
-# (lin, obbt): Glob's configuration is (1, 1)
-CONFIGS = [(0, 0), (1, 0), (0, 1), (1, 1)]
+# (lin, obbt, brancher): brancher 0 MaxVio, 1 Glob's relstronger; Glob's
+# configuration is (1, 1, 1)
+CONFIGS = [(0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 0, 1), (1, 1, 1)]
 
 
-def ref_opts(lin, obbt):
+def ref_opts(lin, obbt, brancher=0):
     """integ_glob_tree3 bits: bfs (1), LinearHandler without node presolve
-    (2) unless lin, root OBBT (8) with obbt."""
-    return 1 | (0 if lin else 2) | (8 if obbt else 0)
+    (2) unless lin, root OBBT (8) with obbt, StrongBrancher with
+    reliabilitySetup(20, 50, 5) (16) with brancher 1."""
+    return 1 | (0 if lin else 2) | (8 if obbt else 0) | (16 if brancher else 0)
 
 
 @pytest.mark.parametrize('config', CONFIGS)
 @pytest.mark.parametrize('case', PIN_CASES)
 def test_restated_glob_tree_is_the_reference_tree(integ, case, config):
-    lin, obbt = config
+    lin, obbt, brancher = config
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'oracle'))
     from glob_tree import CpuGlobContext
     from test_simplex_cuts_cpu import glob_tree3
     seed, nv0, ncon = case
     qp = random_qcqp(seed, nv0=nv0, ncon=ncon, squares=False)
-    ub, cnt, _ = glob_tree3(integ, qp, ref_opts(lin, obbt), -1, 1)   # pres_freq 1
+    ub, cnt, _ = glob_tree3(integ, qp, ref_opts(lin, obbt, brancher), -1, 1)   # pres_freq 1
     (bv, bx), (ls, lv, li) = _logs(integ)
     c = CpuGlobContext(qp)
     c.glob_config(2, 1, 0, lin, obbt)
+    c.glob_brancher(brancher)
     c.glob_init(1 << 16)
     for _ in range(20000):
         st = c.glob_round(1)
@@ -90,6 +97,11 @@ def test_restated_glob_tree_is_the_reference_tree(integ, case, config):
     assert (st.nodes, 1 + 2 * int(st.ndec[0]), st.lps, int(st.ndec[5]), st.obbt_lps) == \
         (int(cnt[0]), int(cnt[1]), int(cnt[2]), int(cnt[3]), int(cnt[5]))
     assert obj == ub or (math.isinf(obj) and math.isinf(ub))
+    if brancher:
+        # the StrongBrancher's LPs are main-engine solves too: compare the
+        # whole solve sequence (no branch log from the reference's brancher)
+        assert [r[2] for r in c.lplog] == li.tolist()
+        return
     mb = np.array([v for v, _ in c.brlog], np.int32)
     mx = np.array([x for _, x in c.brlog])
     assert np.array_equal(mb, bv)
