@@ -674,6 +674,7 @@ typedef struct {
   double incumbent;
   long long cuts, resolves;    /* tangent cuts added, node LPs re-solved for them */
   long long obbt_lps;          /* root OBBT's bound LPs (its root re-solve counts in lps) */
+  long long sb_lps;            /* relstronger's strong-branching LPs (counted in lps too) */
 } mgpu_glob_stats;
 /* Search order, warm starts, the tightenQuad_ rule, the linear node
  * presolve and root OBBT of the next mgpu_glob_init (defaults 0, 0, 1, 0, 0):
@@ -712,9 +713,28 @@ typedef struct {
  * node for node, with or without the linear presolve and root OBBT
  * (tests/test_glob_pin_{cpu,gpu}.py). */
 int mgpu_glob_config(mgpu_ctx *ctx, int order, int warm, int qt, int lin, int obbt);
+/* The glob tree's brancher for the next mgpu_glob_init (default 0):
+ *   0  MaxVioBrancher (device decision, any batch);
+ *   1  Glob's default, relstronger: StrongBrancher with reliabilitySetup(20,
+ *      50, 5) (Glob.cpp:171-181, 308; StrongBrancher.cpp) -- pseudocosts with
+ *      reliability threshold 5, up to 20 unreliable candidates strong-
+ *      branched in the order of their violation score, each child built with
+ *      the handler's getBrMod (QuadHandler's rows for the branch's box) and
+ *      every handler's node presolve (getStrongerMods), its LP chained through
+ *      the engine with 50 pivots at most, stopping at a verdict (the node
+ *      pruned, or modified and re-solved), updateAfterSolve's pseudocost per
+ *      node.  One node per round (the reference's sequence; the host runs the
+ *      node's loop, the device every presolve, LP and decision); needs order
+ *      2, warm 1 and lin 1. */
+int mgpu_glob_brancher(mgpu_ctx *ctx, int kind);
 int mgpu_glob_init(mgpu_ctx *ctx, int capacity, double incumbent);
 int mgpu_glob_round(mgpu_ctx *ctx, int batch, double incumbent, mgpu_glob_stats *stats);
 int mgpu_glob_best(mgpu_ctx *ctx, double *obj, double *x);
+/* relstronger trees (mgpu_glob_brancher 1): the main engine's solves since
+ * mgpu_glob_init in order -- node LPs, re-solves and strong-branching LPs --
+ * as (status, value incl. constant, pivots); at most cap written (any array
+ * may be NULL); returns the count. */
+int mgpu_glob_lp_log(mgpu_ctx *ctx, int cap, int32_t *status, double *value, int32_t *iters);
 
 /* ---- QP relaxation with an MFMA KKT block (K5) ---------------
  * Replaces BqpdEngine::solve (src/interfaces/BqpdEngine.cpp:449-534) on the

@@ -158,6 +158,7 @@ void HipLPEngine::load(ProblemPtr problem) {
   delete sol_;
   sol_ = new Solution(1E20, 0, problem_);
   wsValid_ = false;
+  binvStale_ = false;
   ws_ = HipLPWarmStart();
   objChanged_ = bndChanged_ = consChanged_ = needUpload_ = true;
   problem->setEngine(this);
@@ -234,6 +235,12 @@ EngineStatus HipLPEngine::solve() {
   if (problem_->getObjective()) off = problem_->getObjective()->getConstant();
   timer_->start();
   stats_->calls += 1;
+  // the kept basis is refactored for edited rows into a working basis; a
+  // solve that ends neither optimal nor at the iteration limit keeps the
+  // basis it started from, its inverse marked stale (CpuLPEngine's wk_)
+  const bool refactor = wsValid_ && (consChanged_ || binvStale_);
+  HipLPWarmStart kept;
+  if (refactor) kept = ws_;
   if (needUpload_ || consChanged_ || objChanged_) {
     if (consChanged_) syncRows_();
     if (upload_() != MGPU_OK) {
@@ -243,12 +250,12 @@ EngineStatus HipLPEngine::solve() {
       return status_;
     }
     needUpload_ = false;
-    if (wsValid_ && consChanged_) {
-      refactor_();
-      ++nRefactor_;
-    }
     // new objective, same basis: the kernel rebuilds the reduced costs (d = NULL)
-    else if (wsValid_ && objChanged_) dStale_ = true;
+    if (!refactor && wsValid_ && objChanged_) dStale_ = true;
+  }
+  if (refactor) {
+    refactor_();
+    ++nRefactor_;
   }
   // current column bounds (edits since the last solve); the LP starts from
   // the kept basis in its device slot and leaves its basis in a fresh slot
@@ -277,7 +284,7 @@ EngineStatus HipLPEngine::solve() {
       ws_ = HipLPWarmStart();
       ws_.dev = out;
       wsValid_ = true;
-      dStale_ = false;
+      dStale_ = binvStale_ = false;
       // duals from the final basis, computed in the kernel: reduced costs of
       // the structurals, and of the logicals (d_{n+r} = y_r for the row -e_r)
       rc_.assign(rcAll_.begin(), rcAll_.begin() + n);
@@ -293,6 +300,11 @@ EngineStatus HipLPEngine::solve() {
     } else {
       sol_->setObjValue(INFINITY);
     }
+  }
+  if (refactor && !(rc == MGPU_OK && (status_ == ProvenOptimal || status_ == EngineIterationLimit))) {
+    ws_ = kept;
+    wsValid_ = true;
+    binvStale_ = true;
   }
   {
     SolveRec r{-1, 0.0, (int)status_, sol_->getObjValue(), it};

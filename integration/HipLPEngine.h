@@ -182,6 +182,10 @@ class HipLPEngine : public LPEngine {
   std::vector<double> val_, rlo_, rhi_, clo_, chi_, obj_;
   bool bndChanged_, consChanged_, objChanged_, needUpload_;
   bool dStale_;  // ws_.d is for an older objective: solve passes d = NULL
+  // ws_'s inverse is for rows edited since: refactored before the next solve
+  // (the kept basis of a solve that ended neither optimal nor at the
+  // iteration limit, as CpuLPEngine keeps it)
+  bool binvStale_ = false;
   HipLPWarmStart ws_;
   bool wsValid_;
   SolutionPtr sol_;

@@ -125,6 +125,7 @@ struct mgpu_ctx {
   QpState *qp = nullptr;       // QP relaxation (mgpu_load_qp)
   GlobState *glob = nullptr;   // batched spatial B&B (mgpu_glob_init)
   int glob_order = 0, glob_warm = 0, glob_qt = 1, glob_lin = 0, glob_obbt = 0;  // mgpu_glob_config
+  int glob_brancher = 0;                                                        // mgpu_glob_brancher
   CommState *comm = nullptr;   // round collectives (mgpu_comm_init[_host])
 };
 

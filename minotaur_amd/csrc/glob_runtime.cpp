@@ -64,6 +64,25 @@ struct GlobState {
   // the first presolveNode call only
   int order = 0, warm = 0, qt = 1, lin = 0, obbt = 0;
   mgpu_ctx *bte = nullptr;       // root OBBT's bound-tightening engine (bte_)
+  // Glob's relstronger (mgpu_glob_brancher 1): per pool slot the branching
+  // that made the node (updateAfterSolve), the pseudocosts, and the main
+  // engine's last solution value (strongBranch_ reads it after a verdict of
+  // the stronger mods)
+  int brancher = 0;
+  struct BrInfo {
+    int var = -1, isint = 0;
+    double act = 0.0, dd = 0.0, ud = 0.0, plb = 0.0;
+  };
+  std::vector<BrInfo> pinfo;
+  std::vector<double> pc_up, pc_dn;
+  std::vector<long long> tm_up, tm_dn;
+  double last_val = 0.0;
+  struct LpRec {
+    int32_t status, iters;
+    double value;
+  };
+  std::vector<LpRec> lp_log;     // relstronger: every main-engine solve in order
+  DevBuf rs_head, rs_st;         // relstronger: the node's basis for its children
   std::vector<GHeap> heap;
   std::vector<int> free_slots;
   long long next_id = 1;
@@ -96,7 +115,7 @@ struct GlobState {
                       &pws_head, &pws_st, &pws_ok, &gsel, &cslots, &glb, &gub, &grows, &gtan,
                       &gdepth, &ghead, &gst, &gok, &skip_a, &wo_head, &wo_st, &wo_d, &wo_binv,
                       &lrptr, &ltvar, &ltsrc, &ltrow, &lrhsrc, &lcptr, &lcterm, &loidx, &ltval,
-                      &lrlo, &lrhi, &loval, &flb, &fub, &finf, &fflag})
+                      &lrlo, &lrhi, &loval, &flb, &fub, &finf, &fflag, &rs_head, &rs_st})
       b->release();
     if (bte) mgpu_destroy(bte);
     bte = nullptr;
@@ -541,9 +560,566 @@ int glob_root_obbt(mgpu_ctx *c, GlobState &s, const double *x, std::vector<doubl
   return MGPU_OK;
 }
 
+// ---- Glob's relstronger: StrongBrancher with reliabilitySetup(20, 50, 5)
+// (Glob.cpp:171-181; StrongBrancher.cpp) on the reference's node at a time.
+// The host runs PCBProcessor::process's loop for the popped node (batch 1,
+// order 2, warm 1, lin 1) the way the reference does; every presolve
+// (glob_linear, K2), LP (K3R + K3 through lp_solve_rows_wo) and decision
+// (glob_decide) runs on the device.  The strong-branching children and the
+// brancher's modifications are built here from QuadHandler / IntVarHandler::
+// getBrMod (QuadHandler.cpp:616-692, IntVarHandler.cpp:113-130); the engine's
+// basis is chained through two device slots (A: the node's gathered basis,
+// B: the round's warm-start output) as the reference's one engine chains it.
+constexpr int kSbCands = 20, kSbIter = 50, kSbThresh = 5;
+constexpr double kSbEps = 1e-6;
+
+struct RsCand {
+  int var, isint;
+  double dd, ud;
+};
+
+inline bool rs_at_bnds(double v, double l, double u) {
+  return std::fabs(v - l) < 1e-8 || std::fabs(v - u) < 1e-8;
+}
+
+// IntVarHandler / QuadHandler getBranchingCandidates merged per variable
+// (the later handler takes a candidate whose distance sum is >=; the
+// distances stay the earlier one's: BrCand::setDist is an empty
+// non-virtual), ascending by variable (CompareVarBrCand, Types.cpp:23-27);
+// the arithmetic of glob_decide's candidate pass
+void rs_candidates(const QuadState &q, const double *x, const double *lb, const double *ub,
+                   std::vector<RsCand> &out) {
+  const int nv = q.nv;
+  std::vector<char> hi((size_t)nv, 0), hq((size_t)nv, 0);
+  std::vector<double> idd((size_t)nv), iud((size_t)nv), qd((size_t)nv), qu((size_t)nv);
+  for (int j = 0; j < nv; ++j) {
+    const double v = x[j];
+    if (q.h_vtype[(size_t)j] <= 1 && std::fabs(std::floor(v + 0.5) - v) > 1e-6) {
+      hi[(size_t)j] = 1;
+      idd[(size_t)j] = v - std::floor(v);
+      iud[(size_t)j] = std::ceil(v) - v;
+    }
+  }
+  auto add_q = [&](int j, double d, double u) {
+    if (!hq[(size_t)j]) {
+      hq[(size_t)j] = 1;
+      qd[(size_t)j] = d;
+      qu[(size_t)j] = u;
+    } else {
+      qd[(size_t)j] = d + qd[(size_t)j];
+      qu[(size_t)j] = u + qu[(size_t)j];
+    }
+  };
+  for (size_t k = 0; k < q.sq_x.size(); ++k) {
+    const int j = q.sq_x[k], y = q.sq_y[k];
+    const double x0 = x[j], yv = x[y];
+    if (yv - x0 * x0 > std::fabs(yv) * 1e-7 && yv - x0 * x0 > 1e-6) {
+      const double dd = (yv - x0 * x0) / std::sqrt(1.0 + (lb[j] + x0) * (lb[j] + x0));
+      const double ud = (yv - x0 * x0) / std::sqrt(1.0 + (ub[j] + x0) * (ub[j] + x0));
+      add_q(j, dd, ud);
+    }
+  }
+  for (size_t k = 0; k < q.bil_x0.size(); ++k) {
+    const int j0 = q.bil_x0[k], j1 = q.bil_x1[k], y = q.bil_y[k];
+    const double v0 = x[j0], v1 = x[j1], yv = x[y], pr = v1 * v0;
+    if (!(std::fabs(pr - yv) > 1e-5 && std::fabs(pr - yv) > std::fabs(yv) * 1e-4)) continue;
+    if (!rs_at_bnds(v0, lb[j0], ub[j0])) {
+      double dd, ud;
+      if (v0 * v1 > yv) {
+        dd = (-yv + v0 * v1) / std::sqrt(1.0 + v0 * v0 + ub[j1] * ub[j1]);
+        ud = (-yv + v0 * v1) / std::sqrt(1.0 + v0 * v0 + lb[j1] * lb[j1]);
+      } else {
+        dd = (yv - v0 * v1) / std::sqrt(1.0 + v0 * v0 + lb[j1] * lb[j1]);
+        ud = (yv - v0 * v1) / std::sqrt(1.0 + v0 * v0 + ub[j1] * ub[j1]);
+      }
+      add_q(j0, dd, ud);
+    }
+    if (!rs_at_bnds(v1, lb[j1], ub[j1])) {
+      double dd, ud;
+      if (v0 * v1 > yv) {
+        dd = (-yv + v1 * v0) / std::sqrt(1.0 + v1 * v1 + ub[j0] * ub[j0]);
+        ud = (-yv + v1 * v0) / std::sqrt(1.0 + v1 * v1 + lb[j0] * lb[j0]);
+      } else {
+        dd = (yv - v1 * v0) / std::sqrt(1.0 + v1 * v1 + lb[j0] * lb[j0]);
+        ud = (yv - v1 * v0) / std::sqrt(1.0 + v1 * v1 + ub[j0] * ub[j0]);
+      }
+      add_q(j1, dd, ud);
+    }
+  }
+  out.clear();
+  for (int j = 0; j < nv; ++j) {
+    const size_t u = (size_t)j;
+    if (hi[u] && hq[u])
+      out.push_back({j, idd[u] + iud[u] <= qd[u] + qu[u] ? 0 : 1, idd[u], iud[u]});
+    else if (hi[u])
+      out.push_back({j, 1, idd[u], iud[u]});
+    else if (hq[u])
+      out.push_back({j, 0, qd[u], qu[u]});
+  }
+}
+
+inline double rs_keep(double a) { return std::fabs(a) > 1e-9 ? a : 0.0; }
+
+// Handler::getBrMod of candidate (j, isint) in one direction on the node's
+// box and record (in place): IntVarHandler floor / ceil of x_j;
+// QuadHandler x_j itself plus the rows of x_j's violated terms rebuilt for
+// the branch's box (getNewSqLf_, getNewBilLf_; with x_j the bilinear's
+// second factor the arguments come swapped, as in the reference)
+void rs_br_mod(const QuadState &q, std::vector<double> &rec, std::vector<double> &lb,
+               std::vector<double> &ub, const double *x, int j, int isint, bool down) {
+  const double v = x[j];
+  if (isint) {
+    if (down) ub[(size_t)j] = std::floor(v);
+    else lb[(size_t)j] = std::ceil(v);
+    return;
+  }
+  const int nsq = (int)q.sq_x.size();
+  for (int k = 0; k < nsq; ++k) {
+    if (q.sq_x[(size_t)k] != j) continue;
+    const double yv = x[q.sq_y[(size_t)k]], vio = v * v - yv;
+    if (vio > 1e-6 && vio > std::fabs(yv) * 1e-7) {
+      const double lo = down ? lb[(size_t)j] : v, hi = down ? v : ub[(size_t)j];
+      rec[(size_t)(2 * k + 1)] = -hi * lo;
+      rec[(size_t)(2 * k)] = std::fabs(hi + lo) > 1e-5 ? rs_keep(-1. * (hi + lo)) : 0.0;
+    }
+  }
+  for (size_t k = 0; k < q.bil_x0.size(); ++k) {
+    const int X0 = q.bil_x0[k], X1 = q.bil_x1[k], y = q.bil_y[k];
+    if (j != X0 && j != X1) continue;
+    const double vio = std::fabs(x[X0] * x[X1] - x[y]);
+    if (!(vio > 1e-5 && vio > std::fabs(x[y]) * 1e-4)) continue;
+    const int a = j == X0 ? X0 : X1, bb = j == X0 ? X1 : X0;
+    const double xa = x[a];
+    const double lb0 = down ? lb[(size_t)a] : xa, ub0 = down ? xa : ub[(size_t)a];
+    const double lb1 = lb[(size_t)bb], ub1 = ub[(size_t)bb];
+    const size_t o0 = (size_t)(2 * nsq) + 12 * k;
+    for (int t : {down ? 1 : 0, down ? 3 : 2}) {
+      double ca, cb, rhs;   // getNewBilLf_ (QuadHandler.cpp:730-763): a's, b's coefficient
+      if (t == 0) {
+        ca = lb1; cb = lb0; rhs = lb0 * lb1;
+      } else if (t == 1) {
+        ca = ub1; cb = ub0; rhs = ub0 * ub1;
+      } else if (t == 2) {
+        ca = -1.0 * ub1; cb = -1.0 * lb0; rhs = -lb0 * ub1;
+      } else {
+        ca = -1.0 * lb1; cb = -1.0 * ub0; rhs = -ub0 * lb1;
+      }
+      const double c0 = a == X0 ? ca : cb, c1 = a == X0 ? cb : ca;
+      double *r = rec.data() + o0 + 3 * (size_t)t;
+      r[0] = rs_keep(c0);
+      r[1] = rs_keep(c1);
+      r[2] = rhs;
+    }
+  }
+  if (down) ub[(size_t)j] = v;
+  else lb[(size_t)j] = v;
+}
+
+// StrongBrancher::shouldPrune_ (:461-497): prune; *rel cleared when the
+// status makes the candidate unreliable
+inline bool rs_prune(double chcutoff, double change, int st, bool *rel) {
+  if (st == 3 || st == 2 || st == 5) return true;
+  if (st == 1 || st == 0) return change > chcutoff - kSbEps;
+  if (st == 6) return false;
+  *rel = false;
+  return false;
+}
+
+inline double rs_score(double up, double down) {   // getScore_ (:381-389)
+  return up > down ? down * 0.8 + up * 0.2 : up * 0.8 + down * 0.2;
+}
+
+int glob_node_rs(mgpu_ctx *c, GlobState &s, GlobIO &io, const GHeap &node,
+                 mgpu_glob_stats *stats) {
+  const QuadState &q = *c->quad;
+  const int nv = s.nv, R = s.R, T = s.T, RT = R + T, m = c->lp.m, N = nv + m;
+  hipStream_t stream = c->stream;
+  // every copy ordered on the context's (non-blocking) stream and waited
+  // for: the node's loop reads each kernel's result before the next step
+  auto cp = [stream](void *dst, const void *src, size_t bytes, hipMemcpyKind kind) -> hipError_t {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(stream);
+  };
+  // the engine's basis: 0 none (slack), 1 slot A (ghead / gst), 2 slot B (wo)
+  int32_t *hA = io.ghead, *hB = s.wo_head.as<int32_t>();
+  int8_t *sA = io.gst, *sB = s.wo_st.as<int8_t>();
+  LpWarmOut woA{hA, sA, s.wo_d.as<double>(), s.wo_binv.as<double>()};
+  LpWarmOut woB{hB, sB, s.wo_d.as<double>(), s.wo_binv.as<double>()};
+  const double *dvals = io.wvals;   // the node's LP record (the rows, then the tangent slots)
+  std::vector<double> x((size_t)nv), lb((size_t)nv), ub((size_t)nv), rec((size_t)(RT > 0 ? RT : 1));
+  int32_t st = 0, it = 0, kinf = 0, dec = 0;
+  double obj = 0.0;
+  long long lps = 0, pivots = 0, sb_lps = 0, obbt_lps = 0, resolves = 0;
+  // the node's first LP (the round's code ran it): results and basis
+  HIPCHK(c, hipStreamSynchronize(stream));
+  HIPCHK(c, cp(&kinf, io.kinf, 4, hipMemcpyDeviceToHost));
+  const GlobState::BrInfo info = s.pinfo[(size_t)node.slot];
+  int eng = 0;
+  auto finish = [&](int d, const std::vector<GHeap> &kids) -> int {
+    s.tot.rounds += 1;
+    s.tot.nodes += 1;
+    s.tot.ndec[d] += 1;
+    s.tot.lps += lps;
+    s.tot.pivots += pivots;
+    s.tot.obbt_lps += obbt_lps;
+    s.tot.sb_lps += sb_lps;
+    s.tot.resolves += resolves;
+    for (const GHeap &k : kids) {
+      s.heap.push_back(k);
+      std::push_heap(s.heap.begin(), s.heap.end(), gheap_greater);
+    }
+    s.count = (int)s.heap.size();
+    s.tot.open = s.count;
+    s.tot.last_batch = 1;
+    s.tot.incumbent = s.inc;
+    if (stats) *stats = s.tot;
+    if (d == 4)
+      return fail(c, MGPU_ERR_ENGINE, "mgpu_glob_round: an engine problem (K2 propagation cap / "
+                  "default bound, or an unbounded / unknown LP status)");
+    return MGPU_OK;
+  };
+  if (kinf != 0) return finish(kinf == 1 ? 1 : 4, {});
+  auto pull = [&]() -> int {   // the LP result and decision at index 0
+    HIPCHK(c, cp(&st, io.status, 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, cp(&it, io.iters, 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, cp(&obj, io.obj, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, cp(&dec, io.dec, 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, cp(x.data(), io.x, (size_t)nv * 8, hipMemcpyDeviceToHost));
+    return MGPU_OK;
+  };
+  int rc = pull();
+  if (rc != MGPU_OK) return rc;
+  HIPCHK(c, cp(lb.data(), io.wlb, (size_t)nv * 8, hipMemcpyDeviceToHost));
+  HIPCHK(c, cp(ub.data(), io.wub, (size_t)nv * 8, hipMemcpyDeviceToHost));
+  if (RT > 0) HIPCHK(c, cp(rec.data(), dvals, (size_t)RT * 8, hipMemcpyDeviceToHost));
+  lps += 1;
+  pivots += it;
+  s.last_val = obj;
+  s.lp_log.push_back({st, it, obj});
+  uint8_t gok = 0;
+  HIPCHK(c, cp(&gok, io.gok, 1, hipMemcpyDeviceToHost));
+  eng = (st == 0 || st == 6) ? 2 : (gok ? 1 : 0);
+  // one LP of the node's current device state (wlb / wub / record at index
+  // 0) from the engine's basis into the other slot
+  auto lp = [&](int iter_limit, bool decide_after) -> int {
+    const int out = eng == 2 ? 1 : 2;
+    int r = lp_solve_rows_wo(c, 1, io.wlb, io.wub, nullptr, dvals, eng == 0 ? nullptr : eng == 1 ? hA : hB,
+                             eng == 0 ? nullptr : eng == 1 ? sA : sB, 0, iter_limit, io.status, io.obj,
+                             io.iters, io.x, nullptr, out == 1 ? &woA : &woB);
+    if (r != MGPU_OK) return r;
+    if (decide_after) {
+      const int32_t zero = 0;
+      HIPCHK(c, cp(const_cast<int32_t *>(io.kinf), &zero, 4, hipMemcpyHostToDevice));
+      HIPCHK(c, launch_glob_decide(io, stream));
+      r = pull();
+      if (r != MGPU_OK) return r;
+    } else {
+      HIPCHK(c, cp(&st, io.status, 4, hipMemcpyDeviceToHost));
+      HIPCHK(c, cp(&it, io.iters, 4, hipMemcpyDeviceToHost));
+      HIPCHK(c, cp(&obj, io.obj, 8, hipMemcpyDeviceToHost));
+    }
+    lps += 1;
+    s.last_val = obj;
+    s.lp_log.push_back({st, it, obj});
+    if (st == 0 || st == 6) eng = out;
+    return MGPU_OK;
+  };
+  // a box and record through the handlers' presolveNode (glob_linear, K2)
+  // into the node's device state; *inf: proven infeasible
+  auto presolve = [&](const std::vector<double> &l, const std::vector<double> &u,
+                      const std::vector<double> &r, bool *inf) -> int {
+    HIPCHK(c, cp(io.glb, l.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, cp(io.gub, u.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+    if (R > 0) HIPCHK(c, cp(io.grows, r.data(), (size_t)R * 8, hipMemcpyHostToDevice));
+    if (T > 0) HIPCHK(c, cp(io.gtan, r.data() + R, (size_t)T * 8, hipMemcpyHostToDevice));
+    GlobIO pio = io;
+    pio.flb_in = io.glb;
+    pio.fub_in = io.gub;
+    pio.frows = io.grows;
+    pio.ftan = io.gtan;
+    pio.in_tan = io.gtan;
+    HIPCHK(c, launch_glob_linear(pio, stream));
+    int r2 = mgpu_quad_fbbt_dev(c, 1, io.flb, io.fub, s.inc, s.qt, io.grows, 0, s.wlb.as<double>(),
+                                s.wub.as<double>(), s.wrows.as<double>(), s.kinf.as<int32_t>(),
+                                s.knm.as<int32_t>(), 0, nullptr, nullptr, nullptr, nullptr);
+    if (r2 != MGPU_OK) return r2;
+    HIPCHK(c, launch_glob_linear_verdict(pio, stream));
+    if (T > 0) HIPCHK(c, launch_glob_pack(pio, stream));
+    int32_t ki = 0;
+    HIPCHK(c, cp(&ki, io.kinf, 4, hipMemcpyDeviceToHost));
+    if (ki > 1)
+      return fail(c, MGPU_ERR_ENGINE, "mgpu_glob_round: K2 failed on a strong-branching child");
+    *inf = ki != 0;
+    return MGPU_OK;
+  };
+  auto after_solve = [&]() {   // StrongBrancher::updateAfterSolve (:589-643)
+    if (info.var < 0) return;
+    const int j = info.var;
+    double cost;
+    bool down;
+    if (info.isint) {
+      cost = (obj - info.plb) / (std::fabs(x[(size_t)j] - info.act) + kSbEps);
+      down = x[(size_t)j] < info.act;
+    } else {
+      down = info.act < 0;
+      cost = (obj - info.plb) / ((down ? info.dd : info.ud) + kSbEps);
+    }
+    if (cost < 0.0 || std::isinf(cost) || std::isnan(cost)) cost = 0.0;
+    if (down) {
+      s.pc_dn[(size_t)j] = (s.pc_dn[(size_t)j] * s.tm_dn[(size_t)j] + cost) / (s.tm_dn[(size_t)j] + 1);
+      s.tm_dn[(size_t)j] += 1;
+    } else {
+      s.pc_up[(size_t)j] = (s.pc_up[(size_t)j] * s.tm_up[(size_t)j] + cost) / (s.tm_up[(size_t)j] + 1);
+      s.tm_up[(size_t)j] += 1;
+    }
+  };
+  auto upd_pc = [&](int j, double cost, bool down) {   // updatePCost_ (:645-650)
+    if (down) {
+      s.pc_dn[(size_t)j] = (s.pc_dn[(size_t)j] * s.tm_dn[(size_t)j] + cost) / (s.tm_dn[(size_t)j] + 1);
+      s.tm_dn[(size_t)j] += 1;
+    } else {
+      s.pc_up[(size_t)j] = (s.pc_up[(size_t)j] * s.tm_up[(size_t)j] + cost) / (s.tm_up[(size_t)j] + 1);
+      s.tm_up[(size_t)j] += 1;
+    }
+  };
+  std::vector<RsCand> cands;
+  for (int iter = 1;; ++iter) {
+    if (iter > 1) {   // re-solved: decide again
+      rc = lp(0, true);
+      if (rc != MGPU_OK) return rc;
+      pivots += it;
+    }
+    if (dec == 1 || dec == 2 || dec == 4) return finish(dec, {});
+    if (iter == 1) after_solve();
+    if (dec == 3) {
+      if (obj < s.inc) {
+        s.inc = obj;
+        s.best_x = x;
+      }
+      return finish(3, {});
+    }
+    if (iter == 1 && node.id == 0 && s.obbt) {   // tightenBounds_ (PCBProcessor.cpp:256-262)
+      bool changed = false, feasible = true;
+      rc = glob_root_obbt(c, s, x.data(), lb, ub, rec, &changed, &feasible, &obbt_lps);
+      if (rc != MGPU_OK) return rc;
+      if (changed) {
+        HIPCHK(c, cp(s.wlb.p, lb.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+        HIPCHK(c, cp(s.wub.p, ub.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+        if (R > 0) HIPCHK(c, cp(s.wrows.p, rec.data(), (size_t)R * 8, hipMemcpyHostToDevice));
+        if (T > 0) HIPCHK(c, cp(io.wvals, rec.data(), (size_t)RT * 8, hipMemcpyHostToDevice));
+        if (!feasible) continue;
+      }
+    }
+    if (T > 0) {   // separate_: the squares' tangents (glob_separate), then re-solve
+      HIPCHK(c, hipMemsetAsync(s.acc.p, 0, 16, stream));
+      HIPCHK(c, launch_glob_separate(io, stream));
+      unsigned long long a[2] = {0, 0};
+      HIPCHK(c, hipMemcpyAsync(a, s.acc.p, 16, hipMemcpyDeviceToHost, stream));
+      HIPCHK(c, hipStreamSynchronize(stream));
+      if (a[1] > 0) {
+        s.tot.cuts += (long long)a[0];
+        resolves += 1;
+        HIPCHK(c, cp(rec.data(), io.wvals, (size_t)RT * 8, hipMemcpyDeviceToHost));
+        continue;
+      }
+    }
+    // ---- StrongBrancher::findBranches (StrongBrancher.cpp:184-264) ----
+    // the children's warm start: the engine's basis now (PCBProcessor.cpp:
+    // 282, getWarmStartCopy before findBranches), saved before the strong-
+    // branching LPs chain through both slots
+    const int ws_children = eng;
+    int32_t *ch_head = s.rs_head.as<int32_t>();
+    int8_t *ch_st = s.rs_st.as<int8_t>();
+    if (eng != 0) {
+      HIPCHK(c, cp(ch_head, eng == 1 ? hA : hB, (size_t)m * 4, hipMemcpyDeviceToDevice));
+      HIPCHK(c, cp(ch_st, eng == 1 ? sA : sB, (size_t)N, hipMemcpyDeviceToDevice));
+    }
+    rs_candidates(q, x.data(), lb.data(), ub.data(), cands);
+    if (cands.empty()) return finish(5, {});
+    auto reliable = [&](int j) {
+      return s.tm_up[(size_t)j] >= kSbThresh && s.tm_dn[(size_t)j] >= kSbThresh;
+    };
+    std::vector<RsCand> rel, unrel;
+    for (const RsCand &cd : cands) (reliable(cd.var) ? rel : unrel).push_back(cd);
+    // the node's value (the strong-branching LPs overwrite obj): the
+    // children's bound and the pseudocosts' reference
+    const double objval = obj, maxchange = s.inc - objval;
+    const std::vector<double> xs = x;   // x_ (StrongBrancher copies x: solves overwrite it)
+    double best = -INFINITY;
+    int bc = -1;                          // the best candidate's variable
+    std::vector<signed char> dirs((size_t)nv, -1);   // setDir; default UpBranch
+    auto pick = [&](const RsCand &cd, double sc, double chu, double chd) {
+      if (sc > best) {
+        best = sc;
+        bc = cd.var;
+        dirs[(size_t)cd.var] = chu > chd ? 0 : 1;
+      }
+    };
+    auto pcscore = [&](const RsCand &cd, double *chd, double *chu) {
+      *chd = cd.dd * s.pc_dn[(size_t)cd.var];
+      *chu = cd.ud * s.pc_up[(size_t)cd.var];
+      return rs_score(*chu, *chd);
+    };
+    for (const RsCand &cd : rel) {
+      double chd, chu;
+      const double sc = pcscore(cd, &chd, &chu);
+      pick(cd, sc, chu, chd);
+    }
+    // sortUnrelCands_ (:429-459)
+    std::vector<double> vio;
+    for (const RsCand &cd : unrel)
+      vio.push_back(rs_score(cd.ud, cd.dd) /
+                    (double)(std::max(s.tm_dn[(size_t)cd.var], s.tm_up[(size_t)cd.var]) + 1));
+    double minscore = 0.0;
+    if (!unrel.empty()) {
+      std::vector<double> top = vio;
+      std::sort(top.begin(), top.end(), [](double a, double b) { return a > b; });
+      minscore = top[(size_t)std::min<size_t>(top.size(), (size_t)kSbCands) - 1];
+    }
+    int status = 0;   // 0 none, 1 pruned, 2 modified
+    std::vector<double> mlb, mub, mrec;
+    int cnt = 0;
+    size_t i = 0;
+    for (; i < unrel.size(); ++i) {
+      if (cnt >= kSbCands) break;
+      if (!(vio[i] >= minscore)) continue;
+      const RsCand &cd = unrel[i];
+      ++cnt;
+      int sres[2];
+      double ores[2];
+      for (int side = 0; side < 2; ++side) {   // strongBranch_ (:499-587): down, then up
+        std::vector<double> blb = lb, bub = ub, brec = rec;
+        rs_br_mod(q, brec, blb, bub, xs.data(), cd.var, cd.isint, side == 0);
+        bool inf = false;
+        rc = presolve(blb, bub, brec, &inf);
+        if (rc != MGPU_OK) return rc;
+        if (inf) {
+          sres[side] = 2;
+          ores[side] = s.last_val;
+          continue;
+        }
+        rc = lp(kSbIter, false);
+        if (rc != MGPU_OK) return rc;
+        sb_lps += 1;
+        sres[side] = st;
+        ores[side] = obj;
+      }
+      double chu = std::max(ores[1] - objval, 0.0), chd = std::max(ores[0] - objval, 0.0);
+      // useStrongBranchInfo_ (:652-689)
+      bool is_rel = true;
+      const bool pdn = rs_prune(maxchange, chd, sres[0], &is_rel);
+      const bool pup = rs_prune(maxchange, chu, sres[1], &is_rel);
+      if (!is_rel) {
+        chu = chd = 0.0;
+      } else if (pup && pdn) {
+        status = 1;
+      } else if (pup || pdn) {
+        status = 2;
+        mlb = lb;
+        mub = ub;
+        mrec = rec;
+        rs_br_mod(q, mrec, mlb, mub, xs.data(), cd.var, cd.isint, pup);
+      } else {
+        upd_pc(cd.var, std::fabs(chd) / (std::fabs(cd.dd) + kSbEps), true);
+        upd_pc(cd.var, std::fabs(chu) / (std::fabs(cd.ud) + kSbEps), false);
+      }
+      const double sc = rs_score(chu, chd);
+      if (status != 0) break;
+      pick(cd, sc, chu, chd);
+    }
+    if (status == 1) return finish(1, {});
+    if (status == 2) {   // ModifiedByBrancher: the mod, presolveNode_, re-solve
+      lb = mlb;
+      ub = mub;
+      rec = mrec;
+      bool inf = false;
+      rc = presolve(lb, ub, rec, &inf);
+      if (rc != MGPU_OK) return rc;
+      if (inf) return finish(1, {});
+      HIPCHK(c, cp(lb.data(), io.wlb, (size_t)nv * 8, hipMemcpyDeviceToHost));
+      HIPCHK(c, cp(ub.data(), io.wub, (size_t)nv * 8, hipMemcpyDeviceToHost));
+      if (RT > 0) HIPCHK(c, cp(rec.data(), dvals, (size_t)RT * 8, hipMemcpyDeviceToHost));
+      continue;
+    }
+    for (size_t jx = 0; jx < unrel.size(); ++jx) {   // :149-169
+      if (vio[jx] < minscore || jx >= i) {
+        double chd, chu;
+        const double sc = pcscore(unrel[jx], &chd, &chu);
+        pick(unrel[jx], sc, chu, chd);
+      }
+    }
+    if (best == 0 && rel.empty())   // :170-180: the first largest violation
+      bc = unrel[(size_t)(std::max_element(vio.begin(), vio.end()) - vio.begin())].var;
+    if (bc < 0) return finish(5, {});
+    const RsCand *bcand = nullptr;
+    for (const RsCand &cd : cands)
+      if (cd.var == bc) bcand = &cd;
+    // the children (QuadHandler::getBranches down, up; IntVarHandler's
+    // guided dive, else the candidate's direction), each with the node's box,
+    // record and basis
+    const int j = bcand->var;
+    const double v = xs[(size_t)j];
+    const bool up_first = dirs[(size_t)j] != 0;
+    bool down_first = true;
+    if (bcand->isint) {
+      down_first = !up_first;
+      if (std::isfinite(s.inc) && !std::isnan(s.best_x[(size_t)j])) down_first = s.best_x[(size_t)j] < v;
+    }
+    if (bcand->isint) s.tot.br_int += 1;
+    else s.tot.br_cont += 1;
+    std::vector<GHeap> kids;
+    for (int k = 0; k < 2; ++k) {
+      const bool upc = down_first ? k == 1 : k == 0;
+      int slot;
+      if (!s.free_slots.empty()) {
+        slot = s.free_slots.back();
+        s.free_slots.pop_back();
+      } else {
+        if (s.hw >= s.cap) return fail(c, MGPU_ERR_NOMEM, "mgpu_glob_round: node pool full (%d slots)", s.cap);
+        slot = s.hw++;
+      }
+      std::vector<double> clb = lb, cub = ub;
+      if (upc) clb[(size_t)j] = bcand->isint ? std::ceil(v) : v;
+      else cub[(size_t)j] = bcand->isint ? std::floor(v) : v;
+      const size_t so = (size_t)slot;
+      HIPCHK(c, cp(s.plb.as<double>() + so * nv, clb.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+      HIPCHK(c, cp(s.pub.as<double>() + so * nv, cub.data(), (size_t)nv * 8, hipMemcpyHostToDevice));
+      if (R > 0) HIPCHK(c, cp(s.prows.as<double>() + so * R, rec.data(), (size_t)R * 8, hipMemcpyHostToDevice));
+      if (T > 0) HIPCHK(c, cp(s.ptan.as<double>() + so * T, rec.data() + R, (size_t)T * 8, hipMemcpyHostToDevice));
+      const uint8_t ok = ws_children != 0 ? 1 : 0;
+      if (ok) {
+        HIPCHK(c, cp(s.pws_head.as<int32_t>() + so * m, ch_head, (size_t)m * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(c, cp(s.pws_st.as<int8_t>() + so * N, ch_st, (size_t)N, hipMemcpyDeviceToDevice));
+      }
+      HIPCHK(c, cp(s.pws_ok.as<uint8_t>() + so, &ok, 1, hipMemcpyHostToDevice));
+      const int32_t dep = node.depth + 1;
+      HIPCHK(c, cp(s.pnlb.as<double>() + so, &objval, 8, hipMemcpyHostToDevice));
+      HIPCHK(c, cp(s.pdepth.as<int32_t>() + so, &dep, 4, hipMemcpyHostToDevice));
+      GlobState::BrInfo bi;
+      bi.var = j;
+      bi.isint = bcand->isint;
+      bi.act = bcand->isint ? v : (upc ? 1.0 : -1.0);
+      bi.dd = bcand->dd;
+      bi.ud = bcand->ud;
+      bi.plb = objval;
+      s.pinfo[so] = bi;
+      kids.push_back(GHeap{objval, node.depth + 1, s.next_id++, slot});
+    }
+    return finish(0, kids);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int mgpu_glob_brancher(mgpu_ctx *c, int kind) {
+  if (!c) return MGPU_ERR_ARG;
+  if (kind < 0 || kind > 1)
+    return fail(c, MGPU_ERR_ARG, "mgpu_glob_brancher: kind %d (0 MaxVio, 1 relstronger)", kind);
+  c->glob_brancher = kind;
+  return MGPU_OK;
+}
 
 int mgpu_glob_config(mgpu_ctx *c, int order, int warm, int qt, int lin, int obbt) {
   if (!c) return MGPU_ERR_ARG;
@@ -586,6 +1162,20 @@ int mgpu_glob_init(mgpu_ctx *c, int capacity, double incumbent) {
   s->qt = c->glob_qt;
   s->lin = c->glob_lin;
   s->obbt = c->glob_obbt;
+  s->brancher = c->glob_brancher;
+  if (s->brancher == 1 && (s->order != 2 || s->warm != 1 || s->lin != 1))
+    return fail(c, MGPU_ERR_ARG, "mgpu_glob_init: relstronger needs order 2, warm 1 and lin 1 "
+                "(a brancher's modification reaches p_ only through LinearHandler's "
+                "copyBndsFromRel_)");
+  if (s->brancher == 1) {
+    HIPCHK(c, s->rs_head.ensure((size_t)c->lp.m * 4 + 4));
+    HIPCHK(c, s->rs_st.ensure((size_t)(nv + c->lp.m)));
+    s->pinfo.assign((size_t)capacity, GlobState::BrInfo{});
+    s->pc_up.assign((size_t)nv, 0.0);
+    s->pc_dn.assign((size_t)nv, 0.0);
+    s->tm_up.assign((size_t)nv, 0);
+    s->tm_dn.assign((size_t)nv, 0);
+  }
   s->T = extra;
   s->S = nsq > 0 ? extra / (2 * nsq) : 0;
   if (s->lin || s->obbt) {
@@ -672,6 +1262,7 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
   if (!c->glob) return fail(c, MGPU_ERR_STATE, "mgpu_glob_round: mgpu_glob_init first");
   if (batch < 1) return fail(c, MGPU_ERR_ARG, "mgpu_glob_round: batch < 1");
   GlobState &s = *c->glob;
+  if (s.brancher == 1) batch = 1;   // relstronger: the reference's node at a time
   const QuadState &q = *c->quad;
   HIPCHK(c, hipSetDevice(c->device));
   if (incumbent < s.inc) {  // an outside incumbent: no point of ours matches it
@@ -902,6 +1493,7 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
     if (rc != MGPU_OK) return rc;
   }
   HIPCHK(c, launch_glob_decide(io, c->stream));
+  if (s.brancher == 1) return glob_node_rs(c, s, io, popped[0], stats);
   // the flagged nodes (flag / skip2) re-solved -- from the root basis (warm
   // 0) or the node's last basis refactored for its rows (warm 1) -- merged
   // back and decided again
@@ -1068,6 +1660,18 @@ int mgpu_glob_round(mgpu_ctx *c, int batch, double incumbent, mgpu_glob_stats *s
                 "(K2 propagation cap / default bound, or an unbounded / unknown LP status)",
                 (long long)o.ndec[4]);
   return MGPU_OK;
+}
+
+int mgpu_glob_lp_log(mgpu_ctx *c, int cap, int32_t *status, double *value, int32_t *iters) {
+  if (!c) return MGPU_ERR_ARG;
+  if (!c->glob) return fail(c, MGPU_ERR_STATE, "mgpu_glob_lp_log: mgpu_glob_init first");
+  const auto &lg = c->glob->lp_log;
+  for (size_t k = 0; k < lg.size() && (int)k < cap; ++k) {
+    if (status) status[k] = lg[k].status;
+    if (value) value[k] = lg[k].value;
+    if (iters) iters[k] = lg[k].iters;
+  }
+  return (int)lg.size();
 }
 
 int mgpu_glob_best(mgpu_ctx *c, double *obj, double *x) {

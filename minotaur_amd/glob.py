@@ -38,17 +38,18 @@ def setup(ctx, qp, tan_slots=None):
 
 
 def solve(ctx, qp, batch=1024, capacity=None, max_rounds=10**9, incumbent=math.inf,
-          loaded=False, tan_slots=None, order=0, warm=0, qt=1, lin=0, obbt=0):
+          loaded=False, tan_slots=None, order=0, warm=0, qt=1, lin=0, obbt=0, brancher=0):
     """Runs the tree until the stack is empty (or max_rounds): returns
     (incumbent, x or None, stats, seconds).  order / warm / qt / lin / obbt:
     mgpu_glob_config (order 2, warm 1 at batch 1: the reference's own glob
     tree node for node; lin 1: LinearHandler's node presolve too; obbt 1:
-    root OBBT)."""
+    root OBBT).  brancher 1: Glob's relstronger (one node per round)."""
     if not loaded:
         setup(ctx, qp, tan_slots)
     cap = capacity or 64 * batch
     t0 = time.perf_counter()
     ctx.glob_config(order, warm, qt, lin, obbt)
+    ctx.glob_brancher(brancher)
     ctx.glob_init(cap, incumbent)
     st = None
     for _ in range(max_rounds):

@@ -46,7 +46,7 @@ EXPORTS = [
     'mgpu_comm_unique_id', 'mgpu_comm_init', 'mgpu_comm_init_host', 'mgpu_comm_info',
     'mgpu_allreduce_f64', 'mgpu_allreduce_min', 'mgpu_round_reduce', 'mgpu_allgather_f64',
     'mgpu_alltoall_rows_dev', 'mgpu_lb_deal', 'mgpu_bnb_rebalance', 'mgpu_alloc_stats',
-    'mgpu_bnb_growth', 'mgpu_set_sb_chain',
+    'mgpu_bnb_growth', 'mgpu_set_sb_chain', 'mgpu_glob_brancher', 'mgpu_glob_lp_log',
 ]
 
 COMM_ID_BYTES = 128            # MGPU_COMM_ID_BYTES
@@ -86,7 +86,7 @@ class GlobStats(ctypes.Structure):
                 ('br_cont', ctypes.c_longlong), ('open', ctypes.c_int),
                 ('last_batch', ctypes.c_int), ('incumbent', ctypes.c_double),
                 ('cuts', ctypes.c_longlong), ('resolves', ctypes.c_longlong),
-                ('obbt_lps', ctypes.c_longlong)]
+                ('obbt_lps', ctypes.c_longlong), ('sb_lps', ctypes.c_longlong)]
 
 
 _lib = None
@@ -144,6 +144,8 @@ def load_library():
     lib.mgpu_bnb_brancher.argtypes = [_P, _I]
     lib.mgpu_bnb_growth.argtypes = [_P, _I]
     lib.mgpu_set_sb_chain.argtypes = [_P, _I]
+    lib.mgpu_glob_brancher.argtypes = [_P, _I]
+    lib.mgpu_glob_lp_log.argtypes = [_P, _I, _P, _P, _P]
     lib.mgpu_bnb_relaxation.argtypes = [_P, _I]
     lib.mgpu_bnb_guided_dive.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
@@ -967,6 +969,23 @@ class Context:
         root OBBT (1 QuadHandler::postSolveRootNode, 0 none)."""
         self._chk(self.lib.mgpu_glob_config(self.h, int(order), int(warm), int(qt), int(lin),
                                             int(obbt)), 'mgpu_glob_config')
+
+    def glob_brancher(self, kind):
+        """mgpu_glob_brancher: the next glob_init's brancher (0 MaxVio, 1 Glob's
+        relstronger: one node per round, order 2, warm 1, lin 1)."""
+        self._chk(self.lib.mgpu_glob_brancher(self.h, int(kind)), 'mgpu_glob_brancher')
+
+    def glob_lp_log(self):
+        """mgpu_glob_lp_log: (status, value, pivots) of every main-engine solve
+        of a relstronger tree, in order."""
+        n = self.lib.mgpu_glob_lp_log(self.h, 0, None, None, None)
+        if n < 0:
+            self._chk(n, 'mgpu_glob_lp_log')
+        st = np.zeros(n, dtype=np.int32)
+        val = np.zeros(n)
+        it = np.zeros(n, dtype=np.int32)
+        self.lib.mgpu_glob_lp_log(self.h, n, st.ctypes.data, val.ctypes.data, it.ctypes.data)
+        return st, val, it
 
     def glob_init(self, capacity, incumbent=math.inf):
         self._chk(self.lib.mgpu_glob_init(self.h, int(capacity), float(incumbent)),

@@ -20,7 +20,9 @@ lin 0 with the LinearHandler that skips node presolve.  obbt 1 adds root
 OBBT (QuadHandler::postSolveRootNode: the bound LPs chained on the round's
 own bound-tightening context, the rows rewritten, the root re-solved when
 its point leaves the tightened relaxation), paired with the reference's
-OBBT on HipLPEngine as bte_; (1, 1) is Glob's configuration.
+OBBT on HipLPEngine as bte_.  brancher 1 (mgpu_glob_brancher) is Glob's
+default brancher relstronger, paired with the reference's StrongBrancher
+(reliabilitySetup(20, 50, 5)); (1, 1, 1) is Glob's configuration.
 
 Seeds are drawn without filtering: nodes the reference hands to an NLP
 engine at NoCandToBranch (none in the image: closed and counted) are counted
@@ -60,21 +62,21 @@ def ctx():
     c.close()
 
 
-def _pair(integ, ctx, seed, nv0, ncon, lin, obbt):
+def _pair(integ, ctx, seed, nv0, ncon, lin, obbt, brancher):
     from test_simplex_cuts_cpu import glob_tree3
     qp = random_qcqp(seed, nv0=nv0, ncon=ncon, squares=False)
-    ub, cnt, _ = glob_tree3(integ, qp, ref_opts(lin, obbt), 0, 1)   # pres_freq 1
+    ub, cnt, _ = glob_tree3(integ, qp, ref_opts(lin, obbt, brancher), 0, 1)   # pres_freq 1
     obj, x, st, _ = mglob.solve(ctx, qp, batch=1, capacity=1 << 14, order=2, warm=1, qt=0,
-                                lin=lin, obbt=obbt, max_rounds=20000)
+                                lin=lin, obbt=obbt, brancher=brancher, max_rounds=20000)
     return qp, (ub, cnt), (obj, st)
 
 
 @pytest.mark.parametrize('config', CONFIGS)
 @pytest.mark.parametrize('case', PIN_CASES)
 def test_glob_tree_is_the_reference_tree_node_for_node(integ, ctx, case, config):
-    lin, obbt = config
+    lin, obbt, brancher = config
     seed, nv0, ncon = case
-    qp, (ub, cnt), (obj, st) = _pair(integ, ctx, seed, nv0, ncon, lin, obbt)
+    qp, (ub, cnt), (obj, st) = _pair(integ, ctx, seed, nv0, ncon, lin, obbt, brancher)
     created = 1 + 2 * int(st.ndec[0])
     print(f"seed {seed} ({nv0}, {ncon}): reference nodes {cnt[0]} created {cnt[1]} LPs {cnt[2]} "
           f"closed {cnt[3]} ub {ub!r}; batched nodes {st.nodes} created {created} LPs "

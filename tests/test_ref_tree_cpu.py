@@ -69,7 +69,9 @@ def test_cpu_reference_tree_time_limit(integ):
     at it (BabOptions time_limit, read in the BranchAndBound constructor)."""
     p = random_mkp(1, 60, 8)
     r = cpu_tree(integ, p, 0, 1, time_limit=0.5)
-    assert 0.45 <= r["seconds"] <= 1.5 and r["processed"] > 100
+    # the limit is read between nodes; the upper bound only shows the tree
+    # stopped (loose: a loaded host, e.g. pytest -n, stretches one node)
+    assert 0.45 <= r["seconds"] <= 4.0 and r["processed"] > 100
 
 
 def test_growth_caps_each_round():
