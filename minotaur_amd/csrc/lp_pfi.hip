@@ -574,11 +574,8 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       }
     }
     PSTAMP(10);
-    double lbB = 0.0, ubB = 0.0;
-    if (lane < m) {
-      lbB = lo[h];
-      ubB = hi[h];
-    }
+    // the basic rows' bounds are lo[h] / hi[h] (a basic column keeps its
+    // working bounds; grow() skips basic columns), read at pricing
     double d[S];
     if (reuse) {
 #pragma unroll
@@ -747,6 +744,9 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
     bool need = true;   // recompute before pricing
     int status = kUnknownStatus;
     for (;;) {
+      // lane-derived addresses recomputed per pivot (not hoisted and spilled)
+      lane = lane0;
+      asm volatile("" : "+v"(lane));
       if (need) {
         zB = primals();
         PSTAMP(1);
@@ -755,6 +755,7 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       // ---- pricing: most infeasible basic row, lowest row on ties ----
       double inf = 0.0;
       if (lane < m) {
+        const double lbB = lo[h], ubB = hi[h];
         if (zB < lbB - kPTol) inf = zB - lbB;
         else if (zB > ubB + kPTol) inf = zB - ubB;
       }
@@ -837,10 +838,6 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
             if (colrep(kb, freem, [&](int i) { return cl[i]; },
                        std::integral_constant<int, 1>())) {
               ne = kb;
-              if (lane < m) {
-                lbB = lo[h];
-                ubB = hi[h];
-              }
               again = true;
             } else {
               // no usable pivot: the dense continuation restarts from the
@@ -988,8 +985,6 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       if (lane == r) {
         h = q;
         zB = zq;
-        lbB = bloq;
-        ubB = bhiq;
       }
       // ---- eta column of this pivot (oracle: -alpha_q/alpha_rq, 1/alpha_rq at r)
       const double inv = 1.0 / arq;
