@@ -318,14 +318,17 @@ def tree_cpu_baseline(p, brancher, seconds):
 TIMED_ALLOCS = {}   # per tree: device allocations / bytes inside its timed solve (all ranks)
 
 
-def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None, growth=0):
+def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=None, growth=0,
+             reps=1, times=None):
     """One complete tree with the batched driver (mgpu_bnb_*), node-sharded
     across ranks after the shared first rounds: one packed all-reduce per
     round (incumbent MIN + open counts), open nodes rebalanced every 8 rounds
     or when a rank runs dry (dist.rebalance).  Returns (incumbent, nodes, LP
     solves, pivots, pruned-open, rounds, seconds, nodes moved, strong-branching
     LPs, their pivots) — counts summed over ranks, seconds the max.  ``trace``
-    (a list) receives (seconds since the start, incumbent) per round."""
+    (a list) receives (seconds since the start, incumbent) per round of the
+    first timed run.  reps > 1 times that many complete solves (the same tree
+    each time) and returns the median; ``times`` (a list) receives each."""
     import torch
     from minotaur_amd import bnb
     from minotaur_amd.runtime import alloc_stats
@@ -349,16 +352,22 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=No
         grew = float(comm.allreduce([float(alloc_stats() != w0)], OP_MAX)[0])
         if not grew:
             break
-    comm.barrier()
-    torch.cuda.synchronize()
     a0 = alloc_stats()
-    t0 = time.perf_counter()
-    tr = []
-    inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=cap,
-                                                     order=order, warm=warm, comm=comm,
-                                                     lb_every=8, brancher=brancher, trace=tr,
-                                                     growth=growth)
-    torch.cuda.synchronize()
+    els = []
+    for rep in range(reps):
+        comm.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr = []
+        inc, x, st, rounds, mine = bnb.solve_distributed(ctx, B, rank, world, capacity=cap,
+                                                         order=order, warm=warm, comm=comm,
+                                                         lb_every=8, brancher=brancher, trace=tr,
+                                                         growth=growth)
+        torch.cuda.synchronize()
+        if rep == 0 and trace is not None:
+            trace.extend((t - t0, v) for t, v in tr)
+        comm.barrier()
+        els.append(float(comm.allreduce([time.perf_counter() - t0], OP_MAX)[0]))
     a1 = alloc_stats()
     # summed over the ranks (rank 0 writes the line)
     na = [int(v) for v in comm.allreduce([float(a1[0] - a0[0]), float(a1[1] - a0[1])], OP_SUM)]
@@ -371,10 +380,9 @@ def run_tree(ctx, dev, rank, world, p, B, order, warm, cap, brancher=0, trace=No
         # so that a multi-GPU run still measures
         progress(rank, msg)
     TIMED_ALLOCS[p.name] = na
-    if trace is not None:
-        trace.extend((t - t0, v) for t, v in tr)
-    comm.barrier()
-    el = float(comm.allreduce([time.perf_counter() - t0], OP_MAX)[0])
+    if times is not None:
+        times.extend(els)
+    el = sorted(els)[len(els) // 2]
     c = [float(v) for v in comm.allreduce([float(mine[k]) for k in (
         'nodes', 'lps', 'pivots', 'pruned', 'sb_lps', 'sb_pivots')], OP_SUM)]
     return inc, c[0], c[1], c[2], c[3], rounds, el, mine['moved'], c[4], c[5]
@@ -508,13 +516,17 @@ def tls4_oa_rel_tree(ctx, dev, rank, world, args):
     from minotaur_amd.problem import LinProblem
     p = LinProblem.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'tls4_oa.npz'))
     B = args.tree_batch
+    # the median of five complete solves (each ~25 ms; a single run moves by
+    # about 1 ms from process to process)
+    runs = []
     inc, nodes, lps, piv, pruned, rounds, el, moved, sbl, sbp = run_tree(
-        ctx, dev, rank, world, p, B, 1, 1, 1 << 20, 1, growth=2)
+        ctx, dev, rank, world, p, B, 1, 1, 1 << 20, 1, growth=2, reps=5, times=runs)
     out = {"instance": f"tls4-oa ({p.m} rows, {p.n} cols)", "batch_cap_per_gpu": B,
            "search": "best-first, reliability branching (strong branching + pseudocosts), "
                      "parent-basis warm starts, batch growth 2",
            "nodes": nodes, "rounds": rounds, "lp_solves": lps, "strong_branching_lps": sbl,
-           "time_to_proof_s": el, "optimum": inc,
+           "time_to_proof_s": el, "time_to_proof_runs_s": [round(t, 5) for t in runs],
+           "optimum": inc,
            "optimum_matches_highs": bool(abs(inc - 3.2) <= 1e-6 * 3.2),
            "timed_device_allocations": TIMED_ALLOCS.get(p.name)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
