@@ -791,13 +791,19 @@ __global__ __launch_bounds__(64 * W) void lp_dual_kernel(DevLP lp, LpIO io) {
       // the value is the oracle's bit for bit (the batched tree's reliability
       // branching compares strong-branching values and pseudocosts exactly)
       // the products lane-parallel (the same roundings: no contraction),
-      // then summed in column order through lane reads
+      // then summed in column order through lane reads of the nonzero ones
+      // (adding +-0 to a sum that starts at +0 never changes its bits: the
+      // sum is never -0, so the value is the full sum's)
       double s = 0.0;
       for (int j0 = 0; j0 < n; j0 += 64) {
         const int j = j0 + lane;
         const double pj = j < n ? C.cj(j) * C.z[j] : 0.0;
-        const int cnt = n - j0 < 64 ? n - j0 : 64;
-        for (int l = 0; l < cnt; ++l) s += rld(pj, l);
+        uint64_t nz = __ballot(pj != 0.0);
+        while (nz != 0ull) {
+          const int l = __builtin_ctzll(nz);
+          nz &= nz - 1ull;
+          s += rld(pj, l);
+        }
       }
       objv = C.ocol < 0 ? s + lp.objoff : s;
       if (lane == 0) io.obj[b] = objv;
