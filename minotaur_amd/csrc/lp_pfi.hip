@@ -1042,7 +1042,8 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
       // the value is the oracle's bit for bit (best-first search orders nodes
       // by these bounds; a last-bit difference reorders ties)
       // the products lane-parallel (64 nonzero columns per pass), the sum
-      // sequential in column order through readlanes
+      // sequential in column order through readlanes of the nonzero products
+      // (a zero value gives +-0, which the sum skips for the same reason)
       double sum = 0.0;
       if (P.ocol >= 0) {
         sum += P.osign * zc[P.ocol];
@@ -1051,8 +1052,12 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         for (int k0 = 0; k0 < no; k0 += 64) {
           const int k = k0 + lane;
           const double pr = k < no ? s_oval[k] * zc[s_oidx[k]] : 0.0;
-          const int cnt = no - k0 < 64 ? no - k0 : 64;
-          for (int i = 0; i < cnt; ++i) sum += rld(pr, i);
+          uint64_t nz = __ballot(pr != 0.0);
+          while (nz != 0ull) {
+            const int i = __builtin_ctzll(nz);
+            nz &= nz - 1ull;
+            sum += rld(pr, i);
+          }
         }
       }
       const double solval = P.ocol < 0 ? sum + lp.objoff : sum;
