@@ -3,7 +3,15 @@
 certificate (primal/dual residuals, duality gap) and agrees with an
 independent solver (scipy SLSQP) on small convex QPs.  BQPD itself is
 absent, so iterates are unpinned; the optimal objective of a convex QP is
-unique and is what the GPU tests compare."""
+unique and is what the GPU tests compare.
+
+dual_bound (also used by tests/test_qp_gpu.py on K5's own solutions) is an
+optimality certificate that needs no solver's multipliers: for a primal
+point x and ANY y, z = Qx + c - A'y splits into z_l, z_u >= 0 with exact
+stationarity at x, so -x'Qx/2 + b'y + l'z_l - u'z_u is a lower bound on a
+convex QP's optimum (Wolfe duality); the best y is an LP, solved by HiGHS
+(scipy.optimize.linprog).  A feasible x whose objective meets that bound
+is optimal, whatever produced it."""
 import os
 
 import numpy as np
@@ -26,6 +34,27 @@ def random_qp(seed, n=12, m=3):
                          np.full(n, 4, dtype=np.int32))
 
 
+def dual_bound(P, l, u, x):
+    """max over y of the Wolfe dual value at x (see the module docstring):
+    max b'y + sum_j min(l_j z_j, u_j z_j), z = Qx + c - A'y, as an LP."""
+    from scipy.optimize import linprog
+    n, m = P.n, P.m
+    g = P.Q @ x + P.c
+    AT = P.A.T
+    rows = np.vstack([np.hstack([l[:, None] * AT, np.eye(n)]),
+                      np.hstack([u[:, None] * AT, np.eye(n)])])
+    res = linprog(-np.concatenate([P.b, np.ones(n)]), A_ub=rows,
+                  b_ub=np.concatenate([l * g, u * g]), bounds=[(None, None)] * (m + n),
+                  method='highs')
+    assert res.status == 0, res.message
+    return -0.5 * x @ P.Q @ x - res.fun
+
+
+def assert_convex(P):
+    ev = np.linalg.eigvalsh(P.Q)
+    assert ev.min() >= -1e-9 * max(1.0, ev.max())   # the dual bound needs Q PSD
+
+
 def test_color_lab2_nodes_certified():
     P = qpm.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'color_lab2_qp.npz'))
     assert (P.n, P.m) == (300, 61)
@@ -37,6 +66,21 @@ def test_color_lab2_nodes_certified():
                                       r['zl'], r['zu'])
         assert cert['rp'] <= 1e-8 and cert['rd'] <= 1e-8 and cert['box'] == 0.0
         assert abs(cert['gap']) <= 1e-6 and cert['zmin'] >= 0.0
+
+
+def test_color_lab2_restatement_meets_the_dual_bound():
+    """The restatement's color_lab2 node optima against the multiplier-free
+    certificate (dual_bound), on boxes of another seed."""
+    P = qpm.load(os.path.join(ROOT, 'minotaur_amd', 'instances', 'color_lab2_qp.npz'))
+    assert_convex(P)
+    LB, UB = qpm.random_node_boxes(P, 4, 9)
+    for b in range(4):
+        r = qp_ipm.solve_node(P.Q, P.c, P.A, P.b, LB[b], UB[b])
+        x = r['x']
+        f = 0.5 * x @ P.Q @ x + P.c @ x
+        D = dual_bound(P, LB[b], UB[b], x)
+        tol = 1e-6 * max(1.0, abs(f))
+        assert -tol <= f - D <= tol, (b, f, D)
 
 
 @pytest.mark.parametrize('seed', range(4))

@@ -1,7 +1,10 @@
 """GPU: the batched QP relaxation solve (K5, MFMA KKT block) reaches the
 same optimal objectives as the interior-point restatement (within 1e-6,
 the north-star bar for relaxation objectives) with primal-feasible
-solutions, on color_lab2_4x0 node boxes and on small random convex QPs."""
+solutions, on color_lab2_4x0 node boxes and on small random convex QPs.
+On color_lab2, K5's own solutions are also certified optimal without the
+restatement: each meets the LP-computed Wolfe dual bound at its x
+(tests/test_qp_cpu.py dual_bound) within 1e-6."""
 import os
 
 import numpy as np
@@ -41,6 +44,15 @@ def test_color_lab2_batch(ctx):
     st, ob, it, x = ctx.qp_solve(LB, UB)
     _check(P, LB, UB, st, ob, x)              # every box against the restatement
     assert it.max() < 80 and ctx.last_kernel_ms('qp') > 0
+    # and against the multiplier-free certificate, independent of the restatement
+    from test_qp_cpu import assert_convex, dual_bound
+    assert_convex(P)
+    for b in range(LB.shape[0]):
+        f = 0.5 * x[b] @ P.Q @ x[b] + P.c @ x[b]
+        assert abs(ob[b] - (f + P.k)) <= 1e-9 * max(1.0, abs(f))
+        D = dual_bound(P, LB[b], UB[b], x[b])
+        tol = 1e-6 * max(1.0, abs(f))
+        assert -tol <= f - D <= tol, (b, f, D)
 
 
 @pytest.mark.parametrize('seed', range(3))
