@@ -32,6 +32,7 @@
 #ifndef MGPU_H
 #define MGPU_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -511,6 +512,31 @@ int mgpu_bnb_export(mgpu_ctx *ctx, int k, double *lb, double *ub, double *nlb, i
                     int *got);
 int mgpu_bnb_import(mgpu_ctx *ctx, int k, const double *lb, const double *ub, const double *nlb,
                     const int32_t *depth);
+
+/* Open nodes in Minotaur's Serializer wire format (Serializer::writeNode /
+ * writeMods, src/base/Serializer.cpp:26-112; DeSerializer::readNode /
+ * readMods / readVarBoundMod, :130-191), the format MpiBranchAndBound moves
+ * nodes in: a node exported by mgpu_bnb_export can go to a reference rank or
+ * into a checkpoint the reference's DeSerializer reads, and back through
+ * mgpu_bnb_import.  Host only (no context, no device work).
+ *   bytes: [uint32 id][double lb][size_t k], then k entries
+ *          [int var][short lu][double old][double new], packed, host byte
+ *          order, ascending (var, lu) (lu 0 Lower, 1 Upper: BoundType).
+ *   mgpu_node_serialize: the node's box against the root box: one entry per
+ *          bound that differs (old = the root's, new = the node's), which is
+ *          writeMods' merge of the path's relaxation mods (first old, last
+ *          new).  *len = the byte count; out NULL: the count only;
+ *          MGPU_ERR_ARG if cap < *len.
+ *   mgpu_node_deserialize: one node from buf[0, len): its id, lower bound
+ *          and box (the root box with each entry's new value); *used = the
+ *          bytes read.  MGPU_ERR_ARG on a short buffer, a variable outside
+ *          [0, n) or lu not 0 / 1. */
+int mgpu_node_serialize(uint32_t id, double lb, int n, const double *root_lb,
+                        const double *root_ub, const double *lb_box, const double *ub_box,
+                        uint8_t *out, size_t cap, size_t *len);
+int mgpu_node_deserialize(const uint8_t *buf, size_t len, int n, const double *root_lb,
+                          const double *root_ub, uint32_t *id, double *lb, double *lb_box,
+                          double *ub_box, size_t *used);
 
 /* Bound-aware load balancing on device rows (MpiBranchAndBound::LoadBalance_,
  * src/base/MpiBranchAndBound.cpp:78-195).  LoadBalance_ pops each rank's

@@ -7,6 +7,7 @@
 // (testOsiLP, testOsiLP2, testOsiWarmStart, testOsiBnB), with the instances
 // built programmatically from src/testing/instances/*.mod (ASL is absent).
 #include <chrono>
+#include <cstring>
 #include <cmath>
 #include <vector>
 
@@ -37,6 +38,7 @@
 #include "SimplexQuadCutGen.h"
 #include "BrVarCand.h"
 #include "Branch.h"
+#include "Serializer.h"
 #include "StrongBrancher.h"
 #include "Variable.h"
 
@@ -1006,6 +1008,83 @@ int integ_simplex_cuts(int device, const QSpecI *sp, int cap, int lift, long lon
   delete orig;
   delete env;
   return rc;
+}
+
+// The reference's own Serializer / DeSerializer (src/base/Serializer.cpp:
+// 26-191) for tests/test_serial_cpu.py.
+// integ_serialize_path: a Problem with the root box and the root Node, then
+// `steps` modifications in order: kind 0 a child whose Branch carries
+// VarBoundMod(var, lu, val) (the child becomes the current node), kind 1 a
+// relaxation mod of the current node (Node::addRMod, where presolve mods
+// live).  Each mod's old value is the bound before it (VarBoundMod reads the
+// variable; the harness then moves the bound).  Serializer::writeNode(the
+// current node) -> out; returns the byte count (-1: cap too small).
+long integ_serialize_path(int n, const double *root_lb, const double *root_ub, int steps,
+                          const int *kind, const int *var, const int *lu, const double *val,
+                          unsigned id, double nlb, unsigned char *out, long cap) {
+  EnvPtr env = (EnvPtr) new Environment();
+  ProblemPtr p = (ProblemPtr) new Problem(env);
+  std::vector<VariablePtr> vars;
+  for (int j = 0; j < n; ++j) vars.push_back(p->newVariable(root_lb[j], root_ub[j], Continuous));
+  std::vector<NodePtr> path;
+  NodePtr cur = (NodePtr) new Node();
+  path.push_back(cur);
+  for (int s = 0; s < steps; ++s) {
+    VariablePtr v = vars[var[s]];
+    const BoundType bt = lu[s] ? Upper : Lower;
+    VarBoundModPtr md = (VarBoundModPtr) new VarBoundMod(v, bt, val[s]);
+    p->changeBound(v, bt, val[s]);
+    if (kind[s] == 0) {
+      BranchPtr br = (BranchPtr) new Branch();
+      br->addRMod(md);
+      cur = (NodePtr) new Node(cur, br);
+      path.push_back(cur);
+    } else {
+      cur->addRMod(md);
+    }
+  }
+  cur->setId(id);
+  cur->setLb(nlb);
+  Serializer ser;
+  ser.writeNode(cur);
+  const std::string bytes = ser.get_string();
+  long len = (long)bytes.size();
+  if (out) {
+    if (len <= cap) std::memcpy(out, bytes.data(), bytes.size());
+    else len = -1;
+  }
+  for (size_t k = path.size(); k-- > 0;) delete path[k];
+  delete p;
+  delete env;
+  return len;
+}
+
+// integ_deserialize_node: DeSerializer::readNode on buf against a Problem with
+// the root box: the node's id, lower bound and its relaxation mods applied to
+// the root box (lb / ub); returns the mod count.
+int integ_deserialize_node(const unsigned char *buf, long len, int n, const double *root_lb,
+                           const double *root_ub, unsigned *id, double *nlb, double *lb,
+                           double *ub) {
+  EnvPtr env = (EnvPtr) new Environment();
+  ProblemPtr p = (ProblemPtr) new Problem(env);
+  for (int j = 0; j < n; ++j) p->newVariable(root_lb[j], root_ub[j], Continuous);
+  DeSerializer d(std::string((const char *)buf, (size_t)len));
+  NodePtr node = d.readNode(p);
+  *id = node->getId();
+  *nlb = node->getLb();
+  for (int j = 0; j < n; ++j) {
+    lb[j] = root_lb[j];
+    ub[j] = root_ub[j];
+  }
+  int cnt = 0;
+  for (ModificationConstIterator it = node->modsrBegin(); it != node->modsrEnd(); ++it, ++cnt) {
+    VarBoundModPtr md = (VarBoundModPtr) *it;
+    (md->getLU() == Lower ? lb : ub)[md->getVar()->getIndex()] = md->getNewVal();
+  }
+  delete node;
+  delete p;
+  delete env;
+  return cnt;
 }
 
 }  // extern "C"

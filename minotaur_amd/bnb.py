@@ -36,6 +36,46 @@ def solve(ctx, batch=4096, capacity=None, max_rounds=10**9, incumbent=math.inf,
     return obj, x, st, time.perf_counter() - t0
 
 
+def checkpoint(ctx, root_lb=None, root_ub=None) -> bytes:
+    """The open pool as Minotaur Serializer records (Serializer::writeNode,
+    src/base/Serializer.cpp:26-112; runtime.serialize_nodes): every open node
+    exported (mgpu_bnb_export), written with id = its position and lb = its
+    bound against the root box (default: the loaded problem's bounds), then
+    put back (mgpu_bnb_import; re-imported nodes warm-start from the root
+    basis, as any import).  The incumbent is not part of the format (the
+    reference sends it separately too): take it from ctx.bnb_best()."""
+    from minotaur_amd import runtime
+    p = ctx.problem
+    rl = p.vlb if root_lb is None else root_lb
+    ru = p.vub if root_ub is None else root_ub
+    k, _ = ctx.bnb_count()
+    lb, ub, nlb, depth = ctx.bnb_export(k)
+    data = runtime.serialize_nodes(rl, ru, lb, ub, nlb)
+    if len(nlb):
+        ctx.bnb_import(lb, ub, nlb, depth)
+    return data
+
+
+def restore(ctx, data, capacity, root_lb=None, root_ub=None, incumbent=math.inf):
+    """A tree from checkpoint() bytes, or any stream of the reference's
+    Serializer::writeNode records (DeSerializer::readNode, :130-191): the
+    pool initialised on the root box, the root replaced by the records' nodes
+    (their depth is not in the format: 0).  The caller has set the search
+    order, warm mode and brancher (bnb_config / bnb_brancher) as for bnb_init;
+    bnb_round continues the search."""
+    import numpy as np
+    from minotaur_amd import runtime
+    p = ctx.problem
+    rl = p.vlb if root_lb is None else root_lb
+    ru = p.vub if root_ub is None else root_ub
+    _, nlb, lb, ub = runtime.deserialize_nodes(data, rl, ru)
+    ctx.bnb_init(capacity, rl, ru, incumbent)
+    k, _ = ctx.bnb_count()
+    ctx.bnb_export(k)                        # the fresh root
+    if len(nlb):
+        ctx.bnb_import(lb, ub, nlb, np.zeros(len(nlb), dtype=np.int32))
+
+
 def solve_distributed(ctx, batch, rank, world, allreduce_min=None, allreduce_max=None,
                       capacity=None, max_rounds=10**9, shard_at=None, order=0, warm=0,
                       comm=None, lb_every=0, brancher=0, trace=None, growth=0):

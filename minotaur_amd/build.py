@@ -17,7 +17,7 @@ SOURCES = ['mgpu_runtime.cpp', 'quad_runtime.cpp', 'bnb.cpp', 'fbbt_linear.hip',
            'lp_dual.hip', 'lp_pfi.hip', 'lp_pfi_wide.hip', 'lp_large.hip', 'node_decide.hip', 'quad_fbbt.hip', 'bnb.hip',
            'bnb_select.hip', 'qp_runtime.cpp', 'rows_runtime.cpp', 'lp_rows.hip', 'bnb_rel.hip', 'bnb_migrate.hip',
            'glob_tree.hip', 'glob_runtime.cpp',
-           'qp_kkt.hip', 'comm_runtime.cpp']
+           'qp_kkt.hip', 'comm_runtime.cpp', 'serial.cpp']
 # -ffp-contract=off: no fused multiply-add anywhere (bit-exact FBBT sums,
 # SURVEY §7.3); -fno-gpu-rdc keeps one code object per TU.
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off',

@@ -47,6 +47,7 @@ EXPORTS = [
     'mgpu_allreduce_f64', 'mgpu_allreduce_min', 'mgpu_round_reduce', 'mgpu_allgather_f64',
     'mgpu_alltoall_rows_dev', 'mgpu_lb_deal', 'mgpu_bnb_rebalance', 'mgpu_alloc_stats',
     'mgpu_bnb_growth', 'mgpu_set_sb_chain', 'mgpu_glob_brancher', 'mgpu_glob_lp_log',
+    'mgpu_node_serialize', 'mgpu_node_deserialize',
 ]
 
 COMM_ID_BYTES = 128            # MGPU_COMM_ID_BYTES
@@ -146,6 +147,9 @@ def load_library():
     lib.mgpu_set_sb_chain.argtypes = [_P, _I]
     lib.mgpu_glob_brancher.argtypes = [_P, _I]
     lib.mgpu_glob_lp_log.argtypes = [_P, _I, _P, _P, _P]
+    lib.mgpu_node_serialize.argtypes = [ctypes.c_uint32, _D, _I, _P, _P, _P, _P, _P,
+                                        ctypes.c_size_t, _P]
+    lib.mgpu_node_deserialize.argtypes = [_P, ctypes.c_size_t, _I, _P, _P, _P, _P, _P, _P, _P]
     lib.mgpu_bnb_relaxation.argtypes = [_P, _I]
     lib.mgpu_bnb_guided_dive.argtypes = [_P, _I]
     lib.mgpu_bnb_export.argtypes = [_P, _I, _P, _P, _P, _P, _P]
@@ -244,6 +248,57 @@ def lb_deal(world, S, lbs):
     if nd < 0:
         raise MgpuError(f"mgpu_lb_deal failed rc={nd}")
     return o[:nd].copy(), loc[:nd].copy(), r[:nd].copy()
+
+
+def serialize_nodes(root_lb, root_ub, lb, ub, nlb, ids=None) -> bytes:
+    """mgpu_node_serialize over k nodes (boxes lb / ub [k][n], lower bounds
+    nlb [k], ids default 0..k-1): the concatenated Serializer::writeNode
+    records (src/base/Serializer.cpp:26-112), in node order."""
+    lib = load_library()
+    rl, ru = _np(root_lb, np.float64), _np(root_ub, np.float64)
+    L = _np(lb, np.float64).reshape(-1, rl.size)
+    U = _np(ub, np.float64).reshape(-1, rl.size)
+    nb = _np(nlb, np.float64).reshape(-1)
+    k, n = L.shape
+    ids = np.arange(k, dtype=np.uint32) if ids is None else _np(ids, np.uint32)
+    out = []
+    ln = ctypes.c_size_t(0)
+    for b in range(k):
+        args = (int(ids[b]), float(nb[b]), n, _hp(rl), _hp(ru), _hp(L[b]), _hp(U[b]))
+        if lib.mgpu_node_serialize(*args, None, 0, ctypes.byref(ln)) != 0:
+            raise MgpuError(f"mgpu_node_serialize failed on node {b}")
+        buf = ctypes.create_string_buffer(ln.value)
+        if lib.mgpu_node_serialize(*args, buf, ln.value, ctypes.byref(ln)) != 0:
+            raise MgpuError(f"mgpu_node_serialize failed on node {b}")
+        out.append(buf.raw[:ln.value])
+    return b''.join(out)
+
+
+def deserialize_nodes(data: bytes, root_lb, root_ub):
+    """mgpu_node_deserialize until data is used up (DeSerializer::readNode,
+    src/base/Serializer.cpp:130-191) -> (ids, lower bounds, lb, ub)."""
+    lib = load_library()
+    rl, ru = _np(root_lb, np.float64), _np(root_ub, np.float64)
+    n = rl.size
+    buf = ctypes.create_string_buffer(data, len(data))
+    base = ctypes.addressof(buf)
+    ids, nlb, L, U = [], [], [], []
+    at = 0
+    while at < len(data):
+        i, v = ctypes.c_uint32(0), ctypes.c_double(0.0)
+        lo, hi = np.empty(n), np.empty(n)
+        used = ctypes.c_size_t(0)
+        if lib.mgpu_node_deserialize(ctypes.c_void_p(base + at), len(data) - at, n, _hp(rl),
+                                     _hp(ru), ctypes.byref(i), ctypes.byref(v), _hp(lo), _hp(hi),
+                                     ctypes.byref(used)) != 0:
+            raise MgpuError(f"mgpu_node_deserialize failed at byte {at}")
+        ids.append(i.value)
+        nlb.append(v.value)
+        L.append(lo)
+        U.append(hi)
+        at += used.value
+    return (np.array(ids, dtype=np.uint32), np.array(nlb), np.array(L).reshape(-1, n),
+            np.array(U).reshape(-1, n))
 
 
 class FbbtOut:

@@ -66,6 +66,14 @@ def integ():
 
 
 def load_integ():
+    # torch (which libmgpu's loader imports) before the integration library:
+    # loaded RTLD_GLOBAL first, the reference objects' symbols would bind
+    # torch's libraries too, and the process would destroy an object twice
+    # at exit ("double free", exit 134)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB, mode=os.RTLD_LAZY | os.RTLD_GLOBAL)
     lib.integ_simplex_cuts.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P] + \
         [P] * len(_ORDER)
