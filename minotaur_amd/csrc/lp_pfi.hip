@@ -705,18 +705,28 @@ __global__ __launch_bounds__((64 * waves_for<S, K>())) void lp_pfi_kernel(DevLP 
         const double zl = zc[n + lane];
         if (zl != 0.0) w -= zl;
       }
+      // over the rows with w_k != 0 only, ascending (a zero w_k adds +-0,
+      // which never changes a sum that starts at +0): four LDS loads in
+      // flight, adds in order
       double sacc = 0.0;
       const int li = lane < m ? lane : 0;
-      int k = 0;
-      for (; k + 4 <= m; k += 4) {  // four LDS loads in flight, adds in order
-        const double b0 = P.b0[(size_t)k * ld + li], b1 = P.b0[(size_t)(k + 1) * ld + li];
-        const double b2 = P.b0[(size_t)(k + 2) * ld + li], b3 = P.b0[(size_t)(k + 3) * ld + li];
-        sacc += b0 * rld(w, k);
-        sacc += b1 * rld(w, k + 1);
-        sacc += b2 * rld(w, k + 2);
-        sacc += b3 * rld(w, k + 3);
+      uint64_t nzw = __ballot(lane < m && w != 0.0);
+      while (nzw) {
+        int ii[4];
+        int c = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          ii[t] = nzw ? __builtin_ctzll(nzw) : 0;
+          c += nzw ? 1 : 0;
+          nzw &= nzw - 1;
+        }
+        double bv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bv[t] = P.b0[(size_t)ii[t] * ld + li];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (t < c) sacc += bv[t] * rld(w, ii[t]);
       }
-      for (; k < m; ++k) sacc += P.b0[(size_t)k * ld + li] * rld(w, k);
       if (lane >= m) sacc = 0.0;
       sacc = apply_etas(sacc, eta, prow, ne, lane);
       return -sacc;
