@@ -574,9 +574,12 @@ class CpuGlobContext:
                     lb, ub, rec = nlb, nub, nrec
                     if not feas:
                         continue
-            if self.S > 0 and separate(qp, x, rec, self.R, self.S):
-                self.tot.resolves += 1
-                continue
+            if self.S > 0:
+                nc = separate(qp, x, rec, self.R, self.S)
+                if nc:
+                    self.tot.cuts += nc
+                    self.tot.resolves += 1
+                    continue
             ws_children = eng
             kind, pay, eng = self._strong(lb, ub, rec, x, obj, eng)
             if kind == 'nocand':
