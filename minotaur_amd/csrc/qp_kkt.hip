@@ -278,7 +278,10 @@ __global__ __launch_bounds__(kT) void qp_potrf(QpWork w, int np) {
 // accumulated on MFMA over all k at once (L_ik and L_jk streamed from
 // HBM / L2, each 16x16 tile read as 16 rows of 128 contiguous bytes, four
 // column blocks' loads in flight together; the LDS holds only the tiles of
-// column block j, so three workgroups share a CU), the diagonal tile is factored and the tiles
+// column block j: three workgroups fit a CU's LDS; at 5 waves per SIMD, 96
+// VGPRs without spills, two run at once, which measured faster than three
+// at 80 VGPRs with 9 spilled: 13.2 -> 11.6 ms per batch, profiles/r06aj),
+// the diagonal tile is factored and the tiles
 // below solved against it, and L_ij is written ONCE.  The right-looking
 // kernel above read and wrote the whole trailing matrix for every column
 // block (~9 MB per node at n = 304); this one reads ~2.3 MB of L and writes
@@ -292,7 +295,7 @@ size_t potrf_ll_lds(int np) {
   return sizeof(double) * (16 * 17 + (size_t)T * 256 + 2 * (size_t)np);
 }
 
-__global__ __launch_bounds__(kPT, 6) void qp_potrf_ll(DevQP q, QpWork w) {
+__global__ __launch_bounds__(kPT, 5) void qp_potrf_ll(DevQP q, QpWork w) {
   extern __shared__ double sm[];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   if (w.done[b]) return;
