@@ -3,7 +3,7 @@
 # suite, smoke(), then the default bench line.  TAG names the output dir.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-r06zh}; mkdir -p $O
+O=gpurun_out/${TAG:-r06zj}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests/ -m gpu -q --timeout 200 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -30 $O/gpu_tests.txt; exit 1; }
 tail -2 $O/gpu_tests.txt
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
